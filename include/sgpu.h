@@ -1,0 +1,132 @@
+/* sgpu.h -- C ABI of the MI355X SIFT hot path (libsiftgpu.so).
+ *
+ * Plain C types only (no torch, no C++): this is the boundary a cgo/ctypes/JNI binding or the
+ * C++ SiftGPU/SiftMatchGPU classes (include/SiftGPU.h) call.  Each entry point names the
+ * reference interface it replaces (paths relative to the reference repo root).
+ *
+ * Errors: every function returns SGPU_OK (0) or a negative SGPU_E* code; sgpu_last_error()
+ * returns a message.  There is no CPU fallback: when no gfx950 device is usable the context
+ * cannot be created and every compute call fails with SGPU_ENODEV.
+ */
+#ifndef SGPU_H
+#define SGPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SGPU_OK 0
+#define SGPU_EINVAL (-1)   /* bad argument */
+#define SGPU_ENODEV (-2)   /* no usable GPU / HIP runtime error */
+#define SGPU_ENOMEM (-3)   /* device or host allocation failed */
+#define SGPU_ERANGE (-4)   /* capacity exceeded (e.g. more matches than max_match) */
+
+/* Extraction / matching options.  Field meaning and defaults follow the reference's global
+ * parameters (SiftGPU/GlobalUtil.cpp:50-135) and ParseParam (SiftGPU/SiftGPU.cpp:801-1246). */
+typedef struct sgpu_options {
+    float filter_width_factor;         /* -f   (4.0)                                        */
+    float descriptor_window_factor;    /* -dw  (3.0)                                        */
+    float orientation_window_factor;   /* -w   (2.0)                                        */
+    float orientation_gaussian_factor; /*      (1.5)                                        */
+    float dog_threshold;               /* -t   (0 -> 0.02/dog_level_num)                    */
+    float edge_threshold;              /* -e   (0 -> 10)                                    */
+    int subpixel;                      /* -s   (1)                                          */
+    int max_orientation;               /* -m   (2)                                          */
+    int fixed_orientation;             /* -ofix (0)                                         */
+    int octave_min;                    /* -fo  (0; only 0 is implemented)                   */
+    int octave_num;                    /* -no  (-1 = floor(log2(min(w,h)))-3)                */
+    int dog_level_num;                 /* -d   (3)                                          */
+    int lowe_origin;                   /* -loweo (0)                                        */
+    int normalized;                    /* -unn clears (1)                                   */
+    int descriptors;                   /* -sd clears (1)                                    */
+    int keep_extremum_sign;            /* -sign (0)                                         */
+    int circular_window;               /* 0: square orientation window of the active
+                                          ProgramCU.cu:869-884; 1: circular window of
+                                          ProgramCU-0.cu:834 / the GLSL path                */
+    int verbose;                       /* -v   (0 here; the library prints nothing at 0)     */
+} sgpu_options;
+
+/* Defaults of GlobalUtil.cpp:50-135. */
+void sgpu_default_options(sgpu_options* opt);
+
+/* Parse reference command-line options into *opt (SiftGPU::ParseParam, SiftGPU.cpp:801-1246:
+ * first-4-character case-insensitive option hashing, same argument rules).  Options the MI355X
+ * path has no use for (-cuda, -winpos, -display, -pack, ...) are accepted and ignored; -cuda <n>
+ * sets *device when device != NULL.  Returns SGPU_OK. */
+int sgpu_parse_args(sgpu_options* opt, int argc, const char* const* argv, int* device);
+
+typedef struct sgpu_ctx sgpu_ctx;
+
+/* Create a context bound to HIP device `device` (replaces ProgramCU::CheckCudaDevice,
+ * ProgramCU.cu:1414-1448, + PyramidCU construction).  The context owns all device buffers. */
+int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out);
+int sgpu_ctx_destroy(sgpu_ctx* ctx);
+int sgpu_ctx_set_options(sgpu_ctx* ctx, const sgpu_options* opt);
+const char* sgpu_last_error(const sgpu_ctx* ctx);
+/* Number of visible HIP devices (0 when the runtime is unusable). */
+int sgpu_device_count(void);
+
+/* Input flags. */
+#define SGPU_INPUT_HOST   0   /* `images` is a host pointer                                */
+#define SGPU_INPUT_DEVICE 1   /* `images` is a device pointer on the context's device      */
+
+/* Extract SIFT features from n gray u8 images of w x h pixels, row stride `stride` bytes,
+ * image i at images + i*stride*h.  Replaces SiftGPU::RunSIFT(w, h, data, GL_LUMINANCE,
+ * GL_UNSIGNED_BYTE) (SiftGPU.h:176, SiftGPU.cpp:233-268 -> SiftPyramid::RunSIFT,
+ * SiftPyramid.cpp:58-216), batched.  Results stay valid until the next extract call. */
+int sgpu_extract(sgpu_ctx* ctx, const uint8_t* images, int n, int w, int h, int stride,
+                 int flags);
+
+/* Same with float luminance input in [0, 1] (stride in floats): the GL_FLOAT / converted-RGB
+ * input path of GLTexInput::SetImageData (GLTexImage.cpp:981-1006). */
+int sgpu_extract_f32(sgpu_ctx* ctx, const float* images, int n, int w, int h, int stride,
+                     int flags);
+
+/* Feature count of image i of the last extract (SiftGPU::GetFeatureNum, SiftGPU.cpp:1411). */
+int sgpu_feature_count(const sgpu_ctx* ctx, int image);
+/* Total over the batch. */
+int64_t sgpu_feature_total(const sgpu_ctx* ctx);
+
+/* Copy image i's keypoints (x, y, scale, orientation: 4 floats each) and descriptors (128
+ * floats each) to host memory; either pointer may be NULL (SiftGPU::GetFeatureVector,
+ * SiftGPU.cpp:1416-1428, SiftPyramid::CopyFeatureVector, SiftPyramid.cpp:287-291). */
+int sgpu_copy_features(sgpu_ctx* ctx, int image, float* keys, float* descriptors);
+
+/* Device pointers to the whole batch's keypoints [total][4] / descriptors [total][128] and the
+ * per-image start offsets [n+1] (host array).  Zero-copy access for batch consumers. */
+int sgpu_device_features(sgpu_ctx* ctx, const float** keys, const float** descriptors,
+                         const int64_t** image_offsets);
+
+/* Matcher.  d1 [n1][128], d2 [n2][128] u8 descriptors (the reference quantizes float
+ * descriptors as (unsigned char)int(512*d+0.5), SiftMatchCU.cpp:87-101: see
+ * sgpu_quantize_descriptors).  Replaces SiftMatchGPU::SetDescriptors + GetSiftMatch
+ * (SiftGPU.h:300-311; SiftMatchCU.cpp:139-179; kernels ProgramCU.cu:1466-1900).
+ * Writes pairs {i, j} in ascending i into out_pairs (max_match entries) and returns the match
+ * count (>= 0) or an error. */
+int sgpu_match(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d2, int n2,
+               float distmax, float ratiomax, int mutual_best_match, int max_match,
+               int* out_pairs, int flags);
+
+/* float -> u8 quantization of SiftMatchCU::SetDescriptors (SiftMatchCU.cpp:94-99), host side. */
+void sgpu_quantize_descriptors(const float* d, size_t count, uint8_t* out);
+
+/* Timing of the last call: stage times in milliseconds measured with HIP events
+ * (SiftGPU::_timing, SiftPyramid.cpp:48-56).  times[0..7] =
+ * {upload, pyramid, detect, orientation, expand, descriptor, download, total}. */
+int sgpu_last_timing(const sgpu_ctx* ctx, float* times, int n);
+
+/* ---- test hooks (parity tests read intermediate stages; not part of the drop-in surface) ---- */
+/* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
+int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);
+/* Gaussian level (image, octave, level 0..level_num-1) as wa*h floats. */
+int sgpu_debug_gaussian(sgpu_ctx* ctx, int image, int octave, int level, float* out);
+/* Detected (pre-orientation) keypoints of the batch in reference order: per entry
+ * {col, row, level_id, image} ints and {dx, dy, ds, pad} floats.  Returns count via *n. */
+int sgpu_debug_candidates(sgpu_ctx* ctx, int* ints, float* floats, int cap, int* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SGPU_H */

@@ -1,0 +1,107 @@
+// sift_kernels.h -- launch interface of the gfx950 SIFT kernels (sift_kernels.hip).
+//
+// All launchers are asynchronous on `stream` and take device pointers.  Images of one batch
+// share one geometry; every kernel covers the whole batch in one launch (grid.z / flat index).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sgk {
+
+constexpr int kMaxLevels = 16;     // d + 3 Gaussian levels per octave (d <= 10 in the CLI)
+constexpr int kMaxOctaves = 16;
+
+struct Taps { float k[33]; };
+
+// Per-octave geometry and buffer offsets used by the feature kernels.
+struct OctaveDesc {
+    int w, h, wa;          // wa = padded width = row stride of every level image
+    int nwords;            // bitmask words per row = ceil(wa / 32)
+    long long gauss_off;   // float offset of (octave, level 0, image 0) in the pyramid buffer
+    long long level_stride;// floats between levels of one octave = batch * wa * h
+    long long mask_off;    // uint32 offset of (octave, dog level 0, image 0) in the bitmask buffer
+    long long mask_level_stride; // words between dog levels = batch * h * nwords
+};
+
+struct FeatureParams {
+    int batch, n_octaves, d;             // d = dog_level_num
+    int rows_per_image;                  // sum over octaves of d * h
+    int row_off[kMaxOctaves];            // first row id of (octave o, level 0) inside an image
+    float level_sigma[kMaxLevels];       // GetLevelSigma(j), j = 0..d-1
+    float sigma_step;                    // 2^(1/d)
+    float t0, t, edge;                   // dog threshold * 0.8 (subpixel), dog threshold, (r+1)^2/r
+    float gaussian_factor, sample_factor;// orientation window (1.5, 3.0)
+    float window_factor;                 // descriptor (3.0)
+    int subpixel, num_orientation, keep_sign, circular, normalize;
+    float origin_offset;                 // 0.5 (or 0 with -loweo)
+    OctaveDesc oct[kMaxOctaves];
+};
+
+// Gaussian level filter: dst = V(H(src)) with the reference's clamp-to-edge semantics.
+// src_u8 != nullptr selects the ingest variant (src value = u8 / 255.0f).  src_stride is the
+// row stride in elements of whichever source is used.
+// ds_dst != nullptr additionally writes the 2x point-downsampled output (next octave level 0).
+hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
+                        long long src_img_stride, float* dst, long long dst_img_stride,
+                        int w, int h, int fw, const Taps& taps, int batch,
+                        float* ds_dst, int ds_w, int ds_h, long long ds_img_stride,
+                        hipStream_t stream);
+
+// Extremum detection for one octave, all d levels and all images: writes the keypoint bitmask
+// and adds per-row keypoint counts into row_count (rows ordered image, octave, level, row).
+hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
+                          const FeatureParams& fp, int octave, hipStream_t stream);
+
+// Exclusive scan of n uint32 values into out[0..n]; out[n] = total.  tmp needs
+// scan_tmp_words(n) words.
+size_t scan_tmp_words(size_t n);
+hipError_t launch_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
+                       hipStream_t stream);
+
+// Keypoint materialisation + orientation: one thread per detected keypoint.
+// out4: (x, y, s, packed orientations) in octave coordinates; info: (image, level id);
+// ocount: number of oriented features the keypoint expands to.
+hipError_t launch_orientation(const float* pyr, const uint32_t* mask, const uint32_t* row_base,
+                              int total_rows, const uint32_t* n_cand_dev, int n_cand_cap,
+                              const FeatureParams& fp, float4* out4, int2* info,
+                              uint32_t* ocount, hipStream_t stream);
+
+// Expansion into oriented features (+ image-coordinate keypoints).
+hipError_t launch_expand(const float4* cand, const int2* info, const uint32_t* eoff,
+                         const uint32_t* n_cand_dev, int n_cand_cap, const FeatureParams& fp,
+                         float4* feat, int2* feat_info, float4* keys, hipStream_t stream);
+
+// Descriptors (+ normalisation) of the expanded features.
+hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* feat_info,
+                             const uint32_t* n_feat_dev, int n_feat_cap, const FeatureParams& fp,
+                             float* desc, hipStream_t stream);
+
+// Per-image feature offsets: off[b] = eoff[row_base[b * rows_per_image]] for b in [0, batch].
+hipError_t launch_image_offsets(const uint32_t* row_base, const uint32_t* eoff, int batch,
+                                int rows_per_image, int total_rows, int64_t* off,
+                                hipStream_t stream);
+
+// Debug: candidates of the orientation stage back as (col, row, level id, image) + (dx,dy,ds).
+hipError_t launch_debug_candidates(const float* pyr, const uint32_t* mask,
+                                   const uint32_t* row_base, int total_rows,
+                                   const uint32_t* n_cand_dev, int n_cand_cap,
+                                   const FeatureParams& fp, int4* ints, float4* floats,
+                                   hipStream_t stream);
+
+// ---- matcher (sift_match.hip) ----
+// Distance table dist[v] = float(acos(min(v * 2^-18, 1.0))) for v in [0, 262144], built on the
+// host with the same expression as the oracle and uploaded once.
+constexpr int kDistTable = 262145;
+struct Top2 { int max, idx, second; };
+// s[i] = scale * sum_k d[i][k] + bias
+hipError_t launch_rowsums(const uint8_t* d, int n, int* s, int scale, int bias, hipStream_t stream);
+int match_chunks(int nA, int nB);
+// part[chunk][nA]: per-row top-2 of (A_i . B_j + col_term[j]) over each column chunk
+hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
+                             const int* col_term, int chunks, Top2* part, hipStream_t stream);
+// merge chunks, add row_term, apply distmax / ratiomax -> out[i] = matched index or -1
+hipError_t launch_match_finish(const Top2* part, int n, int chunks, const int* row_term,
+                               const float* dist, float distmax, float ratiomax, int* out,
+                               Top2* best, hipStream_t stream);
+
+}  // namespace sgk

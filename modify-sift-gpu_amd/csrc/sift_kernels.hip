@@ -1,0 +1,828 @@
+// sift_kernels.hip -- gfx950 (MI355X / CDNA4) kernels of the SIFT hot path.
+//
+// Reference semantics: SiftGPU/ProgramCU.cu (kernels) and SiftGPU/PyramidCU.cpp (stage order).
+// The structure is MI355X-first, not a translation:
+//   * one launch per (octave, level) covers the whole image batch (grid.z = image);
+//   * the separable Gaussian is one fused kernel (H pass into an LDS tile, V pass from LDS),
+//     8 B/px of HBM traffic per level instead of the reference's 16, with the next octave's
+//     2x downsample written from the same tile;
+//   * DoG and gradient images are never stored: the extremum kernel forms the 5 DoG planes of
+//     an octave in LDS from the 6 Gaussian planes, and the orientation / descriptor kernels
+//     evaluate gradients from the Gaussian level on the fly;
+//   * keypoint compaction is a 1-bit-per-pixel mask written with wave ballots plus per-row
+//     counts; one exclusive scan over rows gives every keypoint its slot in the reference's
+//     (image, octave, level, row, column) order -- no histogram pyramid, no host round trips.
+// Floating-point conventions are those of oracle/sift_oracle.cpp (fma contractions written
+// out, transcendentals from sift_math.h); the build uses -ffp-contract=off.
+#include "sift_kernels.h"
+#include "sift_math.h"
+
+using namespace sgm;
+
+namespace sgk {
+namespace {
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// ------------------------------------------------------------------------------------------
+// Gaussian level: FilterH<FW> then FilterV<FW> (ProgramCU.cu:115-222) fused in one tile.
+// Output tile 64 x 64, 256 threads.  The input tile (64+FW-1)^2 is loaded with the clamped
+// indices of both passes, so the H pass over the tile rows reproduces the reference's
+// per-row clamping and the V pass its row clamping.
+constexpr int GT = 64;
+
+template <int FW, bool U8>
+__global__ __launch_bounds__(256) void k_gauss(const float* __restrict__ src,
+                                               const uint8_t* __restrict__ src8, int src_stride,
+                                               long long src_img_stride, float* __restrict__ dst,
+                                               long long dst_img_stride, int W, int H, Taps taps,
+                                               float* __restrict__ ds, int dsw, int dsh,
+                                               long long ds_img_stride) {
+    constexpr int HALF = FW >> 1;
+    constexpr int IN_W = GT + FW - 1;
+    constexpr int IN_H = GT + FW - 1;
+    constexpr int NV4 = (FW + 3 + 3) / 4;          // float4 reads per H-pass thread
+    constexpr int IN_S = 60 + 4 * NV4 + 4;         // row stride (floats), multiple of 4
+    constexpr int HS = GT + 1;
+    __shared__ __attribute__((aligned(16))) float s_in[IN_H * IN_S];
+    __shared__ float s_h[IN_H * HS];
+
+    const int tid = threadIdx.x;
+    const int b = blockIdx.z;
+    const int x0 = blockIdx.x * GT, y0 = blockIdx.y * GT;
+
+    // ---- load (clamped) input tile
+    if (U8) {
+        const uint8_t* s = src8 + (long long)b * src_img_stride;
+        for (int i = tid; i < IN_H * IN_W; i += 256) {
+            int ty = i / IN_W, tx = i - ty * IN_W;
+            int gy = clampi(y0 - HALF + ty, 0, H - 1), gx = clampi(x0 - HALF + tx, 0, W - 1);
+            s_in[ty * IN_S + tx] = (float)s[(long long)gy * src_stride + gx] / 255.0f;
+        }
+    } else {
+        const float* s = src + (long long)b * src_img_stride;
+        for (int i = tid; i < IN_H * IN_W; i += 256) {
+            int ty = i / IN_W, tx = i - ty * IN_W;
+            int gy = clampi(y0 - HALF + ty, 0, H - 1), gx = clampi(x0 - HALF + tx, 0, W - 1);
+            s_in[ty * IN_S + tx] = s[(long long)gy * src_stride + gx];
+        }
+    }
+    __syncthreads();
+
+    float k[FW];
+#pragma unroll
+    for (int i = 0; i < FW; i++) k[i] = taps.k[i];
+
+    // ---- H pass: 4 consecutive outputs per thread, taps summed i = 0..FW-1 in order.
+    {
+        const int c0 = (tid & 15) * 4;
+        for (int ty = tid >> 4; ty < IN_H; ty += 16) {
+            const float4* row = reinterpret_cast<const float4*>(&s_in[ty * IN_S + c0]);
+            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+            for (int q = 0; q < NV4; q++) {
+                float4 v4 = row[q];
+                float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int m = q * 4 + e;
+                    const float v = vv[e];
+                    if (m < FW) a0 = fma_(v, k[m], a0);
+                    if (m >= 1 && m - 1 < FW) a1 = fma_(v, k[m - 1], a1);
+                    if (m >= 2 && m - 2 < FW) a2 = fma_(v, k[m - 2], a2);
+                    if (m >= 3 && m - 3 < FW) a3 = fma_(v, k[m - 3], a3);
+                }
+            }
+            float* o = &s_h[ty * HS + c0];
+            o[0] = a0; o[1] = a1; o[2] = a2; o[3] = a3;
+        }
+    }
+    __syncthreads();
+
+    // ---- V pass: column c, 8 consecutive rows per step.
+    const int c = tid & 63;
+    const int x = x0 + c;
+    float* d = dst + (long long)b * dst_img_stride;
+    float* dd = ds ? ds + (long long)b * ds_img_stride : nullptr;
+    for (int rb = (tid >> 6) * 8; rb < GT; rb += 32) {
+        float acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) acc[j] = 0.f;
+#pragma unroll
+        for (int m = 0; m < FW + 7; m++) {
+            const float v = s_h[(rb + m) * HS + c];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int i = m - j;
+                if (i >= 0 && i < FW) acc[j] = fma_(v, k[i], acc[j]);
+            }
+        }
+        if (x < W) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int y = y0 + rb + j;
+                if (y < H) {
+                    d[(long long)y * W + x] = acc[j];
+                    // DownsampleKernel<1> (ProgramCU.cu:287-298) of this level into the next
+                    // octave's level 0: dst(r, c) = src(2r, min(2c, W-1)).
+                    if (dd && !(y & 1) && (y >> 1) < dsh) {
+                        float* drow = dd + (long long)(y >> 1) * dsw;
+                        if (!(x & 1) && (x >> 1) < dsw) drow[x >> 1] = acc[j];
+                        if (x == W - 1)
+                            for (int cc = W >> 1; cc < dsw; cc++) drow[cc] = acc[j];
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <int FW>
+hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
+                          long long src_img_stride, float* dst, long long dst_img_stride, int w,
+                          int h, const Taps& taps, int batch, float* ds, int dsw, int dsh,
+                          long long ds_img_stride, hipStream_t stream) {
+    dim3 grid((w + GT - 1) / GT, (h + GT - 1) / GT, batch);
+    if (src8)
+        hipLaunchKernelGGL((k_gauss<FW, true>), grid, dim3(256), 0, stream, src, src8,
+                           src_stride, src_img_stride, dst, dst_img_stride, w, h, taps, ds, dsw,
+                           dsh, ds_img_stride);
+    else
+        hipLaunchKernelGGL((k_gauss<FW, false>), grid, dim3(256), 0, stream, src, src8,
+                           src_stride, src_img_stride, dst, dst_img_stride, w, h, taps, ds, dsw,
+                           dsh, ds_img_stride);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// ComputeKEY_Kernel (ProgramCU.cu:553-671): extremum state machine + edge test + subpixel
+// solve on 27 DoG values.  get(m, r, c): m = 0 previous / 1 current / 2 next DoG level,
+// r, c in {0,1,2} around the pixel.  The READ_CMP_DOG_DATA order (:534-550) is kept because it
+// decides ties.
+struct KeyOut { float result, dx, dy, ds; };
+
+template <class Get>
+__device__ __forceinline__ KeyOut key_test(Get get, float t0, float t, float edge, int subpixel) {
+    KeyOut o{0.f, 0.f, 0.f, 0.f};
+    const float v = get(1, 1, 1);
+    if (fabs_(v) <= t0) return o;
+    const float l = get(1, 1, 0), r = get(1, 1, 2);
+    float nmax = fmax_(l, r), nmin = fmin_(l, r);
+    if (v <= nmax && v >= nmin) return o;
+    // the 9 row-triples in reference order: cur r0, cur r2, [edge test], prev r0..2, next r0..2
+    const int seq_m[8] = {1, 1, 0, 0, 0, 2, 2, 2};
+    const int seq_r[8] = {0, 2, 0, 1, 2, 0, 1, 2};
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        if (s == 2) {
+            const float vx2 = v * 2.0f;
+            const float fxx = l + r - vx2;
+            const float fyy = get(1, 0, 1) + get(1, 2, 1) - vx2;
+            const float fxy = 0.25f * (get(1, 2, 2) + get(1, 0, 0) - get(1, 2, 0) - get(1, 0, 2));
+            const float temp1 = fma_(fxx, fyy, -(fxy * fxy));
+            const float temp2 = (fxx + fyy) * (fxx + fyy);
+            if (temp1 <= 0 || temp2 > edge * temp1) return o;
+        }
+        const float a = get(seq_m[s], seq_r[s], 0), bb = get(seq_m[s], seq_r[s], 1),
+                    cc = get(seq_m[s], seq_r[s], 2);
+        if (v > nmax) {
+            nmax = fmax_(fmax_(fmax_(nmax, a), bb), cc);
+            if (v < nmax) return o;
+        } else {
+            nmin = fmin_(fmin_(fmin_(nmin, a), bb), cc);
+            if (v > nmin) return o;
+        }
+    }
+    bool ok = true;
+    float dx = 0.f, dy = 0.f, ds = 0.f;
+    if (subpixel) {
+        const float vx2 = v * 2.0f;
+        const float fxx = l + r - vx2;
+        const float fyy = get(1, 0, 1) + get(1, 2, 1) - vx2;
+        const float fxy = 0.25f * (get(1, 2, 2) + get(1, 0, 0) - get(1, 2, 0) - get(1, 0, 2));
+        const float fx = 0.5f * (r - l);
+        const float fy = 0.5f * (get(1, 2, 1) - get(1, 0, 1));
+        const float pc = get(0, 1, 1), nc = get(2, 1, 1);
+        const float fs = 0.5f * (nc - pc);
+        const float fss = (nc + pc - vx2);
+        const float fxs = 0.25f * (get(2, 1, 2) + get(0, 1, 0) - get(2, 1, 0) - get(0, 1, 2));
+        const float fys = 0.25f * (get(2, 2, 1) + get(0, 0, 1) - get(2, 0, 1) - get(0, 2, 1));
+        float4 A0 = fxx > 0 ? make_float4(fxx, fxy, fxs, -fx) : make_float4(-fxx, -fxy, -fxs, fx);
+        float4 A1 = fxy > 0 ? make_float4(fxy, fyy, fys, -fy) : make_float4(-fxy, -fyy, -fys, fy);
+        float4 A2 = fxs > 0 ? make_float4(fxs, fys, fss, -fs) : make_float4(-fxs, -fys, -fss, fs);
+        const float maxa = fmax_(fmax_(A0.x, A1.x), A2.x);
+        if ((double)maxa >= 1e-10) {   // double compare, as the reference's literal
+            if (maxa == A1.x) { float4 T = A1; A1 = A0; A0 = T; }
+            else if (maxa == A2.x) { float4 T = A2; A2 = A0; A0 = T; }
+            A0.y /= A0.x; A0.z /= A0.x; A0.w /= A0.x;
+            A1.y = fma_(-A1.x, A0.y, A1.y); A1.z = fma_(-A1.x, A0.z, A1.z); A1.w = fma_(-A1.x, A0.w, A1.w);
+            A2.y = fma_(-A2.x, A0.y, A2.y); A2.z = fma_(-A2.x, A0.z, A2.z); A2.w = fma_(-A2.x, A0.w, A2.w);
+            if (fabs_(A2.y) > fabs_(A1.y)) { float4 T = A2; A2 = A1; A1 = T; }
+            if ((double)fabs_(A1.y) >= 1e-10) {
+                A1.z /= A1.y; A1.w /= A1.y;
+                A2.z = fma_(-A2.y, A1.z, A2.z); A2.w = fma_(-A2.y, A1.w, A2.w);
+                if ((double)fabs_(A2.z) >= 1e-10) {
+                    ds = A2.w / A2.z;
+                    dy = fma_(-ds, A1.z, A1.w);
+                    dx = fma_(-dy, A0.y, fma_(-ds, A0.z, A0.w));
+                    const float dot = fma_(ds, fs, fma_(dx, fx, dy * fy));
+                    ok = fabs_(fma_(0.5f, dot, v)) > t && fabs_(ds) < 1.0f &&
+                         fabs_(dx) < 1.0f && fabs_(dy) < 1.0f;
+                }
+            }
+        }
+    }
+    if (ok) o.result = v > nmax ? 1.0f : -1.0f;
+    o.dx = dx; o.dy = dy; o.ds = ds;
+    return o;
+}
+
+// ------------------------------------------------------------------------------------------
+// Extremum detection for one octave: tile 64 x 16 pixels, all d DoG levels.  The d+2 DoG
+// planes (with a 1-pixel halo) are formed in LDS from the d+3 Gaussian planes: D_m = G_m -
+// G_{m-1} (ComputeDOG_Kernel, ProgramCU.cu:494).  Each wave covers 64 consecutive columns of a
+// row, so a ballot is directly the 64-bit mask of that row segment.
+constexpr int ET_X = 64, ET_Y = 16, ES = ET_X + 3;
+
+template <int ND>   // ND = number of DoG planes = d + 2
+__global__ __launch_bounds__(256) void k_extrema(const float* __restrict__ pyr,
+                                                 uint32_t* __restrict__ mask,
+                                                 uint32_t* __restrict__ row_count,
+                                                 const FeatureParams fp, int o) {
+    __shared__ float s_d[ND * (ET_Y + 2) * ES];
+    const OctaveDesc& od = fp.oct[o];
+    const int W = od.wa, H = od.h;
+    const int b = blockIdx.z, tid = threadIdx.x;
+    const int x0 = blockIdx.x * ET_X, y0 = blockIdx.y * ET_Y;
+    const long long npx = (long long)W * H;
+    const float* g0 = pyr + od.gauss_off + (long long)b * npx;
+    for (int i = tid; i < (ET_Y + 2) * (ET_X + 2); i += 256) {
+        int ty = i / (ET_X + 2), tx = i - ty * (ET_X + 2);
+        int gy = y0 - 1 + ty, gx = x0 - 1 + tx;
+        bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
+        long long p = (long long)gy * W + gx;
+        float prev = in ? g0[p] : 0.f;
+#pragma unroll
+        for (int m = 1; m <= ND; m++) {
+            float cur = in ? g0[p + m * od.level_stride] : 0.f;
+            s_d[(m - 1) * (ET_Y + 2) * ES + ty * ES + tx] = cur - prev;
+            prev = cur;
+        }
+    }
+    __syncthreads();
+    const int lane = tid & 63, wave = tid >> 6;
+    const int x = x0 + lane;
+    for (int rr = 0; rr < 4; rr++) {
+        const int ly = wave * 4 + rr;
+        const int y = y0 + ly;
+        if (y >= H) break;
+        const bool interior = x > 0 && x < W - 1 && y > 0 && y < H - 1;
+        for (int j = 0; j < ND - 2; j++) {
+            bool flag = false;
+            if (interior) {
+                const float* base = s_d + j * (ET_Y + 2) * ES + (ly + 1) * ES + (lane + 1);
+                auto get = [&](int m, int r, int c) {
+                    return base[m * (ET_Y + 2) * ES + (r - 1) * ES + (c - 1)];
+                };
+                KeyOut k = key_test(get, fp.t0, fp.t, fp.edge, fp.subpixel);
+                flag = k.result != 0.f;
+            }
+            const unsigned long long bal = __ballot(flag);
+            if (lane == 0) {
+                uint32_t* mrow = mask + od.mask_off + j * od.mask_level_stride +
+                                 ((long long)b * H + y) * od.nwords;
+                const int w0 = x0 >> 5;
+                mrow[w0] = (uint32_t)bal;
+                if (w0 + 1 < od.nwords) mrow[w0 + 1] = (uint32_t)(bal >> 32);
+                const int cnt = __popcll(bal);
+                if (cnt)
+                    atomicAdd(&row_count[(long long)b * fp.rows_per_image + fp.row_off[o] +
+                                         j * H + y],
+                              (uint32_t)cnt);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Exclusive scan (uint32), 1024 elements per block.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_scan_block(const uint32_t* __restrict__ in,
+                                                    uint32_t* __restrict__ out, size_t n,
+                                                    uint32_t* __restrict__ block_sums) {
+    __shared__ uint32_t s_w[4];
+    const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x * 4;
+    uint32_t v[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) v[i] = (base + i < n) ? in[base + i] : 0u;
+    uint32_t tsum = v[0] + v[1] + v[2] + v[3];
+    uint32_t incl = wave_incl_scan(tsum);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t wofs = 0, total = 0;
+    for (int w = 0; w < 4; w++) {
+        if (w < wave) wofs += s_w[w];
+        total += s_w[w];
+    }
+    uint32_t run = wofs + incl - tsum;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        if (base + i < n) out[base + i] = run;
+        run += v[i];
+    }
+    if (threadIdx.x == 0) {
+        if (block_sums) block_sums[blockIdx.x] = total;
+        else out[n] = total;   // single-block scan writes the total itself
+    }
+}
+
+__global__ __launch_bounds__(256) void k_scan_add(uint32_t* __restrict__ out, size_t n,
+                                                  const uint32_t* __restrict__ block_ofs) {
+    const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x * 4;
+    const uint32_t add = block_ofs[blockIdx.x];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        if (base + i < n) out[base + i] += add;
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = block_ofs[gridDim.x];
+}
+
+// ------------------------------------------------------------------------------------------
+// Gradient of a Gaussian level at an interior pixel, as ComputeDOG_Kernel stores it
+// (ProgramCU.cu:495-502): (0.5 |grad|, atan2(dy, dx)), atan2 skipped when the magnitude is 0.
+__device__ __forceinline__ float2 grad_at(const float* __restrict__ g, int W, int x, int y) {
+    const float* p = g + (long long)y * W + x;
+    const float dx = p[1] - p[-1];
+    const float dy = p[W] - p[-W];
+    const float grd = 0.5f * sqrt_(fma_(dx, dx, dy * dy));
+    const float rot = grd == 0.0f ? 0.0f : atan2_(dy, dx);
+    return make_float2(grd, rot);
+}
+
+// Locate keypoint f: the row whose scanned base <= f (binary search), then the k-th set bit.
+struct KeyLoc { int b, o, j, row, col; };
+
+__device__ __forceinline__ KeyLoc locate(uint32_t f, const uint32_t* __restrict__ row_base,
+                                         int total_rows, const uint32_t* __restrict__ mask,
+                                         const FeatureParams& fp) {
+    int lo = 0, hi = total_rows;   // find last index with row_base[idx] <= f
+    while (hi - lo > 1) {
+        int mid = (lo + hi) >> 1;
+        if (row_base[mid] <= f) lo = mid; else hi = mid;
+    }
+    KeyLoc L;
+    uint32_t k = f - row_base[lo];
+    L.b = lo / fp.rows_per_image;
+    int rem = lo - L.b * fp.rows_per_image;
+    int o = 0;
+    while (o + 1 < fp.n_octaves && fp.row_off[o + 1] <= rem) o++;
+    L.o = o;
+    rem -= fp.row_off[o];
+    const OctaveDesc& od = fp.oct[o];
+    L.j = rem / od.h;
+    L.row = rem - L.j * od.h;
+    const uint32_t* mrow = mask + od.mask_off + L.j * od.mask_level_stride +
+                           ((long long)L.b * od.h + L.row) * od.nwords;
+    int col = 0;
+    for (int w = 0; w < od.nwords; w++) {
+        uint32_t m = mrow[w];
+        uint32_t c = __popc(m);
+        if (k < c) {
+            for (uint32_t q = 0; q < k; q++) m &= m - 1;
+            col = w * 32 + (__ffs(m) - 1);
+            break;
+        }
+        k -= c;
+    }
+    L.col = col;
+    return L;
+}
+
+// Recompute (result, dx, dy, ds) of a located keypoint from the Gaussian planes.
+__device__ __forceinline__ KeyOut key_at(const float* __restrict__ pyr, const FeatureParams& fp,
+                                         const KeyLoc& L) {
+    const OctaveDesc& od = fp.oct[L.o];
+    const long long npx = (long long)od.wa * od.h;
+    const float* g = pyr + od.gauss_off + (long long)L.b * npx + (long long)L.row * od.wa + L.col;
+    // DoG plane (1 + j + m) = G[1+j+m] - G[j+m]
+    auto get = [&](int m, int r, int c) {
+        const long long p = (long long)(r - 1) * od.wa + (c - 1);
+        const float* gm = g + (long long)(L.j + m) * od.level_stride;
+        return gm[od.level_stride + p] - gm[p];
+    };
+    return key_test(get, fp.t0, fp.t, fp.edge, fp.subpixel);
+}
+
+// ------------------------------------------------------------------------------------------
+// ComputeOrientation_Kernel (ProgramCU.cu:813-977), one thread per keypoint.
+__global__ __launch_bounds__(64) void k_orientation(const float* __restrict__ pyr,
+                                                    const uint32_t* __restrict__ mask,
+                                                    const uint32_t* __restrict__ row_base,
+                                                    int total_rows,
+                                                    const uint32_t* __restrict__ n_cand_dev,
+                                                    const FeatureParams fp,
+                                                    float4* __restrict__ out4,
+                                                    int2* __restrict__ info,
+                                                    uint32_t* __restrict__ ocount) {
+    const uint32_t f = blockIdx.x * 64 + threadIdx.x;
+    if (f >= *n_cand_dev) return;
+    const KeyLoc L = locate(f, row_base, total_rows, mask, fp);
+    const KeyOut kv = key_at(pyr, fp, L);
+    const OctaveDesc& od = fp.oct[L.o];
+    const float ten_degree_per_radius = (float)5.7295779513082320876798154814105;
+    const float radius_per_ten_degrees = (float)(1.0 / 5.7295779513082320876798154814105);
+
+    float kx = L.col + 0.5f, ky = L.row + 0.5f, kz = fp.level_sigma[L.j];
+    if (fp.subpixel) {
+        kx += kv.dx;
+        ky += kv.dy;
+        kz *= pow_(fp.sigma_step, kv.ds);
+    }
+    if (fp.keep_sign) kz *= kv.result;
+    info[f] = make_int2(L.b, L.o * fp.d + L.j);
+    if (fp.num_orientation == 0) {
+        out4[f] = make_float4(kx, ky, kz, 0.0f);
+        ocount[f] = 1;
+        return;
+    }
+    // gradient of Gaussian level 1 + j (PyramidCU.cpp:1204)
+    const float* g = pyr + od.gauss_off + (long long)(1 + L.j) * od.level_stride +
+                     (long long)L.b * od.wa * od.h;
+    const int W = od.wa, H = od.h;
+    float vote[37];
+    const float gsigma = kz * fp.gaussian_factor;
+    const float win = fabs_(kz) * fp.sample_factor;
+    const float dist_threshold = (float)((double)(win * win) + 0.5);
+    const float factor = -0.5f / (gsigma * gsigma);
+    const float xmin = fmax_(1.5f, floor_(kx - win) + 0.5f);
+    const float ymin = fmax_(1.5f, floor_(ky - win) + 0.5f);
+    const float xmax = fmin_(W - 1.5f, floor_(kx + win) + 0.5f);
+    const float ymax = fmin_(H - 1.5f, floor_(ky + win) + 0.5f);
+#pragma unroll
+    for (int i = 0; i < 36; ++i) vote[i] = 0.0f;
+    for (float y = ymin; y <= ymax; y += 1.0f) {
+        for (float x = xmin; x <= xmax; x += 1.0f) {
+            const float dx = x - kx, dy = y - ky;
+            const float sq = fma_(dx, dx, dy * dy);
+            if (fp.circular && sq >= dist_threshold) continue;
+            const float2 gr = grad_at(g, W, (int)x, (int)y);
+            const float weight = gr.x * exp_(sq * factor);
+            int oidx = (int)floor_(gr.y * ten_degree_per_radius);
+            if (oidx < 0) oidx += 36;
+            vote[oidx] += weight;
+        }
+    }
+    const float one_third = (float)(1.0 / 3.0);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        vote[36] = vote[0];
+        float pre = vote[35];
+#pragma unroll
+        for (int j = 0; j < 36; ++j) {
+            const float temp = one_third * (pre + vote[j] + vote[j + 1]);
+            pre = vote[j];
+            vote[j] = temp;
+        }
+    }
+    vote[36] = vote[0];
+    if (fp.num_orientation == 1) {
+        int index_max = 0;
+        float max_vote = vote[0];
+#pragma unroll
+        for (int i = 1; i < 36; ++i) {
+            index_max = vote[i] > max_vote ? i : index_max;
+            max_vote = fmax_(max_vote, vote[i]);
+        }
+        const float pre = vote[index_max == 0 ? 35 : index_max - 1];
+        const float next = vote[index_max + 1];
+        const float off = 0.5f * ((next - pre) * (1.0f / (max_vote + max_vote - next - pre)));
+        out4[f] = make_float4(kx, ky, kz, radius_per_ten_degrees * (index_max + 0.5f + off));
+        ocount[f] = 1;
+        return;
+    }
+    float max_vote = vote[0];
+#pragma unroll
+    for (int i = 1; i < 36; ++i) max_vote = fmax_(max_vote, vote[i]);
+    const float vote_threshold = max_vote * 0.8f;
+    float pre = vote[35];
+    float rot0 = 0.f, rot1 = 0.f, vot0 = 0.f, vot1 = 0.f;
+    int ocnt = 0;
+#pragma unroll
+    for (int i = 0; i < 36; ++i) {
+        const float next = vote[i + 1];
+        const float vi = vote[i];
+        if (vi > vote_threshold && vi > pre && vi > next) {
+            const float di = 0.5f * ((next - pre) * (1.0f / (vi + vi - next - pre)));
+            const float rot = i + di + 0.5f;
+            if (vi > vot1) {
+                if (vi > vot0) { vot1 = vot0; rot1 = rot0; vot0 = vi; rot0 = rot; }
+                else { vot1 = vi; rot1 = rot; }
+                ocnt++;
+            }
+        }
+        pre = vi;
+    }
+    float fr1 = rot0 / 36.0f;
+    if (fr1 < 0) fr1 += 1.0f;
+    const uint32_t us1 = ocnt == 0 ? 65535u : (uint32_t)(unsigned short)floor_(fr1 * 65535.0f);
+    uint32_t us2 = 65535u;
+    if (ocnt > 1) {
+        float fr2 = rot1 / 36.0f;
+        if (fr2 < 0) fr2 += 1.0f;
+        us2 = (uint32_t)(unsigned short)floor_(fr2 * 65535.0f);
+    }
+    out4[f] = make_float4(kx, ky, kz, as_float((us2 << 16) | us1));
+    // ReshapeFeatureListCPU (PyramidCU.cpp:560-578): drop "no orientation", keep a distinct
+    // second orientation
+    ocount[f] = us1 == 65535u ? 0u : (1u + ((us2 != 65535u && us2 != us1) ? 1u : 0u));
+}
+
+// ------------------------------------------------------------------------------------------
+// Feature expansion + image coordinates (PyramidCU.cpp:521-606 / 701-751).
+__global__ __launch_bounds__(256) void k_expand(const float4* __restrict__ cand,
+                                                const int2* __restrict__ info,
+                                                const uint32_t* __restrict__ eoff,
+                                                const uint32_t* __restrict__ n_cand_dev,
+                                                const FeatureParams fp, float4* __restrict__ feat,
+                                                int2* __restrict__ feat_info,
+                                                float4* __restrict__ keys) {
+    const uint32_t f = blockIdx.x * 256 + threadIdx.x;
+    if (f >= *n_cand_dev) return;
+    const uint32_t e0 = eoff[f], n = eoff[f + 1] - e0;
+    if (n == 0) return;
+    const float4 c = cand[f];
+    const int2 in = info[f];
+    const int o = in.y / fp.d;
+    const float oss = (float)(1 << o);
+    const double twopi = 2.0 * 3.14159265358979323846;
+    float ang[2];
+    if (fp.num_orientation >= 2) {
+        const double factor = 2.0 * 3.14159265358979323846 / 65535.0;
+        const uint32_t pk = as_uint(c.w);
+        ang[0] = (float)(factor * (double)(pk & 0xffffu));
+        ang[1] = (float)(factor * (double)(pk >> 16));
+    } else {
+        ang[0] = ang[1] = c.w;
+    }
+    for (uint32_t q = 0; q < n; q++) {
+        const uint32_t e = e0 + q;
+        feat[e] = make_float4(c.x, c.y, c.z, ang[q]);
+        feat_info[e] = in;
+        keys[e] = make_float4(oss * (c.x - 0.5f) + fp.origin_offset,
+                              oss * (c.y - 0.5f) + fp.origin_offset, oss * c.z,
+                              (float)fmod(twopi - (double)ang[q], twopi));
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// ComputeDescriptor_Kernel<false> (ProgramCU.cu:1013-1101) + NormalizeDescriptor_Kernel
+// (:1173-1208).  16 lanes per feature (one 4x4 grid cell each, as the reference), 4 features
+// per wave; normalisation sums are formed in the reference's sequential order via shuffles.
+__device__ __forceinline__ float sq4(float a, float b, float c, float d) {
+    float t = a * a;
+    t = fma_(b, b, t);
+    t = fma_(c, c, t);
+    return fma_(d, d, t);
+}
+
+__global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ pyr,
+                                                    const float4* __restrict__ feat,
+                                                    const int2* __restrict__ feat_info,
+                                                    const uint32_t* __restrict__ n_feat_dev,
+                                                    const FeatureParams fp,
+                                                    float* __restrict__ desc) {
+    const uint32_t gt = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t e = gt >> 4;
+    const int bidx = gt & 15, ix = bidx & 3, iy = bidx >> 2;
+    const uint32_t n_feat = *n_feat_dev;
+    const bool active = e < n_feat;
+    float des[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) des[i] = 0.0f;
+    if (active) {
+        const float4 key = feat[e];
+        const int2 in = feat_info[e];
+        const int o = in.y / fp.d, j = in.y - o * fp.d;
+        const OctaveDesc& od = fp.oct[o];
+        const int W = od.wa, H = od.h;
+        const float* g = pyr + od.gauss_off + (long long)(1 + j) * od.level_stride +
+                         (long long)in.x * W * H;
+        const float rpi = (float)(4.0 / 3.14159265358979323846);
+        const float spt = fabs_(key.z * fp.window_factor);
+        float s, c;
+        sincos_(key.w, &s, &c);
+        const float anglef = (double)key.w > 3.14159265358979323846
+                                 ? (float)((double)key.w - (2.0 * 3.14159265358979323846))
+                                 : key.w;
+        const float cspt = c * spt, sspt = s * spt;
+        const float crspt = c / spt, srspt = s / spt;
+        const float ox = ix - 1.5f, oy = iy - 1.5f;
+        const float ptx = fma_(cspt, ox, -(sspt * oy)) + key.x;
+        const float pty = fma_(cspt, oy, sspt * ox) + key.y;
+        const float bsz = fabs_(cspt) + fabs_(sspt);
+        const float xmin = fmax_(1.5f, floor_(ptx - bsz) + 0.5f);
+        const float ymin = fmax_(1.5f, floor_(pty - bsz) + 0.5f);
+        const float xmax = fmin_(W - 1.5f, floor_(ptx + bsz) + 0.5f);
+        const float ymax = fmin_(H - 1.5f, floor_(pty + bsz) + 0.5f);
+        for (float y = ymin; y <= ymax; y += 1.0f) {
+            for (float x = xmin; x <= xmax; x += 1.0f) {
+                const float dx = x - ptx, dy = y - pty;
+                const float nx = fma_(crspt, dx, srspt * dy);
+                const float ny = fma_(crspt, dy, -(srspt * dx));
+                const float nxn = fabs_(nx), nyn = fabs_(ny);
+                if (nxn < 1.0f && nyn < 1.0f) {
+                    const float2 cc = grad_at(g, W, (int)x, (int)y);
+                    const float dnx = nx + ox, dny = ny + oy;
+                    const float ww = exp_(-0.125f * fma_(dnx, dnx, dny * dny));
+                    const float wx = (float)(1.0 - (double)nxn), wy = (float)(1.0 - (double)nyn);
+                    const float weight = ww * wx * wy * cc.x;
+                    float theta = (anglef - cc.y) * rpi;
+                    if (theta < 0) theta += 8.0f;
+                    const float fo = floor_(theta);
+                    const int fidx = (int)fo;
+                    const float weight1 = fo + 1.0f - theta;
+                    const float weight2 = theta - fo;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        if (k == fidx) {
+                            des[k] = fma_(weight1, weight, des[k]);
+                            des[k + 1] = fma_(weight2, weight, des[k + 1]);
+                        }
+                    }
+                }
+            }
+        }
+        des[0] += des[8];
+    }
+    if (fp.normalize) {
+        const int lane = threadIdx.x & 63, g0 = lane & ~15;
+        float a = sq4(des[0], des[1], des[2], des[3]);
+        float bq = sq4(des[4], des[5], des[6], des[7]);
+        float norm1 = 0.f;
+        for (int q = 0; q < 16; q++) {
+            norm1 += __shfl(a, g0 + q, 64);
+            norm1 += __shfl(bq, g0 + q, 64);
+        }
+        norm1 = rsqrt_(norm1);
+#pragma unroll
+        for (int i = 0; i < 8; i++) des[i] = fmin_(0.2f, des[i] * norm1);
+        a = sq4(des[0], des[1], des[2], des[3]);
+        bq = sq4(des[4], des[5], des[6], des[7]);
+        float norm2 = 0.f;
+        for (int q = 0; q < 16; q++) {
+            norm2 += __shfl(a, g0 + q, 64);
+            norm2 += __shfl(bq, g0 + q, 64);
+        }
+        norm2 = rsqrt_(norm2);
+#pragma unroll
+        for (int i = 0; i < 8; i++) des[i] *= norm2;
+    }
+    if (active) {
+        float4* dst = reinterpret_cast<float4*>(desc + (size_t)e * 128 + bidx * 8);
+        dst[0] = make_float4(des[0], des[1], des[2], des[3]);
+        dst[1] = make_float4(des[4], des[5], des[6], des[7]);
+    }
+}
+
+__global__ void k_image_offsets(const uint32_t* __restrict__ row_base,
+                                const uint32_t* __restrict__ eoff, int batch, int rows_per_image,
+                                int total_rows, int64_t* __restrict__ off) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > batch) return;
+    const int r = b == batch ? total_rows : b * rows_per_image;
+    off[b] = (int64_t)eoff[row_base[r]];
+}
+
+__global__ __launch_bounds__(64) void k_debug_candidates(
+    const float* __restrict__ pyr, const uint32_t* __restrict__ mask,
+    const uint32_t* __restrict__ row_base, int total_rows, const uint32_t* __restrict__ n_cand_dev,
+    const FeatureParams fp, int4* __restrict__ ints, float4* __restrict__ floats) {
+    const uint32_t f = blockIdx.x * 64 + threadIdx.x;
+    if (f >= *n_cand_dev) return;
+    const KeyLoc L = locate(f, row_base, total_rows, mask, fp);
+    const KeyOut kv = key_at(pyr, fp, L);
+    ints[f] = make_int4(L.col, L.row, L.o * fp.d + L.j, L.b);
+    floats[f] = make_float4(kv.dx, kv.dy, kv.ds, kv.result);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
+                        long long src_img_stride, float* dst, long long dst_img_stride, int w,
+                        int h, int fw, const Taps& taps, int batch, float* ds_dst, int ds_w,
+                        int ds_h, long long ds_img_stride, hipStream_t stream) {
+#define SGK_GAUSS(FW)                                                                        \
+    case FW:                                                                                  \
+        return gauss_dispatch<FW>(src, src_u8, src_stride, src_img_stride, dst, dst_img_stride, \
+                                  w, h, taps, batch, ds_dst, ds_w, ds_h, ds_img_stride, stream);
+    switch (fw) {
+        SGK_GAUSS(5) SGK_GAUSS(7) SGK_GAUSS(9) SGK_GAUSS(11) SGK_GAUSS(13) SGK_GAUSS(15)
+        SGK_GAUSS(17) SGK_GAUSS(19) SGK_GAUSS(21) SGK_GAUSS(23) SGK_GAUSS(25) SGK_GAUSS(27)
+        SGK_GAUSS(29) SGK_GAUSS(31) SGK_GAUSS(33)
+        default: return hipErrorInvalidValue;
+    }
+#undef SGK_GAUSS
+}
+
+hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
+                          const FeatureParams& fp, int octave, hipStream_t stream) {
+    const OctaveDesc& od = fp.oct[octave];
+    dim3 grid((od.wa + ET_X - 1) / ET_X, (od.h + ET_Y - 1) / ET_Y, fp.batch);
+    switch (fp.d + 2) {
+#define SGK_EXT(ND) \
+    case ND: hipLaunchKernelGGL((k_extrema<ND>), grid, dim3(256), 0, stream, pyr, mask, row_count, fp, octave); break;
+        SGK_EXT(3) SGK_EXT(4) SGK_EXT(5) SGK_EXT(6) SGK_EXT(7) SGK_EXT(8)
+        default: return hipErrorInvalidValue;
+#undef SGK_EXT
+    }
+    return hipGetLastError();
+}
+
+static size_t scan_blocks(size_t n) { return (n + 1023) / 1024; }
+
+size_t scan_tmp_words(size_t n) {
+    size_t words = 0;
+    while (n > 1024) {
+        size_t nb = scan_blocks(n);
+        words += nb + nb + 1;   // block sums + their scan
+        n = nb;
+    }
+    return words + 16;
+}
+
+hipError_t launch_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
+                       hipStream_t stream) {
+    if (n <= 1024) {
+        hipLaunchKernelGGL(k_scan_block, dim3(1), dim3(256), 0, stream, in, out, n,
+                           (uint32_t*)nullptr);
+        return hipGetLastError();
+    }
+    const size_t nb = scan_blocks(n);
+    uint32_t* sums = tmp;
+    uint32_t* sums_scan = tmp + nb;
+    hipLaunchKernelGGL(k_scan_block, dim3((unsigned)nb), dim3(256), 0, stream, in, out, n, sums);
+    hipError_t e = launch_scan(sums, sums_scan, nb, tmp + nb + nb + 1, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(256), 0, stream, out, n, sums_scan);
+    return hipGetLastError();
+}
+
+hipError_t launch_orientation(const float* pyr, const uint32_t* mask, const uint32_t* row_base,
+                              int total_rows, const uint32_t* n_cand_dev, int n_cand_cap,
+                              const FeatureParams& fp, float4* out4, int2* info,
+                              uint32_t* ocount, hipStream_t stream) {
+    if (n_cand_cap <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_orientation, dim3((n_cand_cap + 63) / 64), dim3(64), 0, stream, pyr,
+                       mask, row_base, total_rows, n_cand_dev, fp, out4, info, ocount);
+    return hipGetLastError();
+}
+
+hipError_t launch_expand(const float4* cand, const int2* info, const uint32_t* eoff,
+                         const uint32_t* n_cand_dev, int n_cand_cap, const FeatureParams& fp,
+                         float4* feat, int2* feat_info, float4* keys, hipStream_t stream) {
+    if (n_cand_cap <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_expand, dim3((n_cand_cap + 255) / 256), dim3(256), 0, stream, cand,
+                       info, eoff, n_cand_dev, fp, feat, feat_info, keys);
+    return hipGetLastError();
+}
+
+hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* feat_info,
+                             const uint32_t* n_feat_dev, int n_feat_cap, const FeatureParams& fp,
+                             float* desc, hipStream_t stream) {
+    if (n_feat_cap <= 0) return hipSuccess;
+    const long long threads = (long long)n_feat_cap * 16;
+    hipLaunchKernelGGL(k_descriptor, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                       stream, pyr, feat, feat_info, n_feat_dev, fp, desc);
+    return hipGetLastError();
+}
+
+hipError_t launch_image_offsets(const uint32_t* row_base, const uint32_t* eoff, int batch,
+                                int rows_per_image, int total_rows, int64_t* off,
+                                hipStream_t stream) {
+    hipLaunchKernelGGL(k_image_offsets, dim3((batch + 1 + 255) / 256), dim3(256), 0, stream,
+                       row_base, eoff, batch, rows_per_image, total_rows, off);
+    return hipGetLastError();
+}
+
+hipError_t launch_debug_candidates(const float* pyr, const uint32_t* mask,
+                                   const uint32_t* row_base, int total_rows,
+                                   const uint32_t* n_cand_dev, int n_cand_cap,
+                                   const FeatureParams& fp, int4* ints, float4* floats,
+                                   hipStream_t stream) {
+    if (n_cand_cap <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_debug_candidates, dim3((n_cand_cap + 63) / 64), dim3(64), 0, stream,
+                       pyr, mask, row_base, total_rows, n_cand_dev, fp, ints, floats);
+    return hipGetLastError();
+}
+
+}  // namespace sgk

@@ -1,0 +1,590 @@
+// siftgpu_api.cpp -- the reference's C++ API (include/SiftGPU.h) on top of the C ABI.
+//
+// Mirrors SiftGPU/SiftGPU.cpp (SiftGPU, SiftParam), SiftGPU/SiftMatch.cpp:549-687 (SiftMatchGPU
+// front-end) and SiftGPU/SiftMatchCU.cpp (descriptor quantisation, max_sift clamp) with the same
+// call semantics and return values.  Differences, by design:
+//   * options are per instance (the reference keeps them in process-global statics,
+//     GlobalUtil.cpp:50-141), so instances on different GPUs are independent;
+//   * no OpenGL: CreateContextGL()/VerifyContextGL() create the HIP context and return
+//     SIFTGPU_FULL_SUPPORTED (2) when a gfx950 device is usable, 0 otherwise;
+//   * image files: PGM/PPM (P2/P3/P5/P6) as the reference's SIFTGPU_NO_DEVIL loader
+//     (GLTexImage.cpp:1128-1189); DevIL formats are not available.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iomanip>
+#include <iostream>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/SiftGPU.h"
+#include "../../include/sgpu.h"
+#include "sift_params.h"
+
+namespace {
+
+constexpr unsigned kGL_LUMINANCE = 0x1909, kGL_LUMINANCE_ALPHA = 0x190A, kGL_RGB = 0x1907,
+                   kGL_RGBA = 0x1908, kGL_BGR = 0x80E0, kGL_BGRA = 0x80E1;
+constexpr unsigned kGL_UNSIGNED_BYTE = 0x1401, kGL_UNSIGNED_SHORT = 0x1403, kGL_FLOAT = 0x1406;
+
+// Host-side input image, stored in the slot of the reference's GLTexInput* member.
+struct HostImage {
+    int w = 0, h = 0;
+    bool is_float = false;
+    std::vector<uint8_t> u8;
+    std::vector<float> f32;
+};
+
+// Runtime state, stored in the slot of the reference's SiftPyramid* member.
+struct Runtime {
+    sgpu_options opt;
+    int device = 0;
+    sgpu_ctx* ctx = nullptr;
+    int binary = 0;             // -b
+    int verbose = 1;
+    int feature_num = 0;
+    std::vector<float> keys, desc;
+    Runtime() { sgpu_default_options(&opt); }
+};
+
+struct ImageListImpl : std::vector<std::string> {};
+
+Runtime* RT(SiftPyramid* p) { return reinterpret_cast<Runtime*>(p); }
+HostImage* IMG(GLTexInput* p) { return reinterpret_cast<HostImage*>(p); }
+ImageListImpl* LIST(ImageList* p) { return reinterpret_cast<ImageListImpl*>(p); }
+
+constexpr int kMaxPath = 4096;
+
+// GLTexInput::LoadImageFile, SIFTGPU_NO_DEVIL branch (GLTexImage.cpp:1128-1189).
+bool load_pnm(const char* path, HostImage* img) {
+    FILE* f = fopen(path, "rb");
+    if (!f) return false;
+    char buf[8] = {0};
+    int width, height, cn;
+    if (fscanf(f, "%7s %d %d %d", buf, &width, &height, &cn) < 4 || cn > 255 || width < 0 ||
+        height < 0) {
+        fclose(f);
+        std::cerr << "ERROR: fileformat not supported\n";
+        return false;
+    }
+    std::vector<uint8_t> data((size_t)width * height);
+    bool ok = true;
+    if (!strcmp(buf, "P5")) {
+        fgetc(f);
+        ok = fread(data.data(), 1, data.size(), f) == data.size();
+    } else if (!strcmp(buf, "P2")) {
+        for (size_t i = 0; i < data.size(); i++) {
+            int g = 0;
+            if (fscanf(f, "%d", &g) != 1) { ok = false; break; }
+            data[i] = (uint8_t)g;
+        }
+    } else if (!strcmp(buf, "P6")) {
+        fgetc(f);
+        for (size_t i = 0; i < data.size(); i++) {
+            uint8_t p[3];
+            if (fread(p, 1, 3, f) != 3) { ok = false; break; }
+            data[i] = (uint8_t)int(0.10454f * p[2] + 0.60581f * p[1] + 0.28965f * p[0]);
+        }
+    } else if (!strcmp(buf, "P3")) {
+        for (size_t i = 0; i < data.size(); i++) {
+            int r, g, b;
+            if (fscanf(f, "%d %d %d", &r, &g, &b) != 3) { ok = false; break; }
+            data[i] = (uint8_t)int(0.10454f * b + 0.60581f * g + 0.28965f * r);
+        }
+    } else {
+        std::cerr << "ERROR: fileformat not supported\n";
+        ok = false;
+    }
+    fclose(f);
+    if (!ok) return false;
+    img->w = width;
+    img->h = height;
+    img->is_float = false;
+    img->u8.swap(data);
+    return true;
+}
+
+// GLTexInput::SetImageData for the CUDA path (GLTexImage.cpp:918-1009) with down-sampling 1:
+// u8 luminance stays u8 (converted to float on the GPU, value / 255.0f); every other format is
+// converted to float luminance on the host with the reference's formulas (:808-916).
+template <class T>
+void to_float(const T* p, unsigned fmt, int w, int h, float factor, std::vector<float>* out) {
+    out->resize((size_t)w * h);
+    const int step = (fmt == kGL_LUMINANCE) ? 1 : (fmt == kGL_LUMINANCE_ALPHA) ? 2
+                     : (fmt == kGL_RGB || fmt == kGL_BGR) ? 3 : 4;
+    float* o = out->data();
+    for (int i = 0; i < w * h; i++, p += step) {
+        if (fmt == kGL_LUMINANCE || fmt == kGL_LUMINANCE_ALPHA) o[i] = p[0] / factor;
+        else if (fmt == kGL_RGB || fmt == kGL_RGBA)
+            o[i] = (19595 * p[0] + 38470 * p[1] + 7471 * p[2]) / (65535.0f * factor);
+        else o[i] = (7471 * p[0] + 38470 * p[1] + 19595 * p[2]) / (65535.0f * factor);
+    }
+}
+
+void to_float_f(const float* p, unsigned fmt, int w, int h, std::vector<float>* out) {
+    out->resize((size_t)w * h);
+    const int step = (fmt == kGL_LUMINANCE) ? 1 : (fmt == kGL_LUMINANCE_ALPHA) ? 2
+                     : (fmt == kGL_RGB || fmt == kGL_BGR) ? 3 : 4;
+    float* o = out->data();
+    for (int i = 0; i < w * h; i++, p += step) {
+        if (fmt == kGL_LUMINANCE || fmt == kGL_LUMINANCE_ALPHA) o[i] = p[0];
+        else if (fmt == kGL_RGB || fmt == kGL_RGBA) o[i] = 0.299f * p[0] + 0.587f * p[1] + 0.114f * p[2];
+        else o[i] = 0.114f * p[0] + 0.587f * p[1] + 0.299f * p[2];
+    }
+}
+
+bool set_image(HostImage* img, int w, int h, const void* data, unsigned fmt, unsigned type) {
+    const bool fmt_ok = fmt == kGL_LUMINANCE || fmt == kGL_LUMINANCE_ALPHA || fmt == kGL_RGB ||
+                        fmt == kGL_RGBA || fmt == kGL_BGR || fmt == kGL_BGRA;
+    const bool type_ok = type == kGL_UNSIGNED_BYTE || type == kGL_UNSIGNED_SHORT || type == kGL_FLOAT;
+    if (!fmt_ok || !type_ok) {
+        std::cerr << "Input format not supported under current settings.\n";
+        return false;
+    }
+    img->w = w;
+    img->h = h;
+    if (fmt == kGL_LUMINANCE && type == kGL_UNSIGNED_BYTE) {
+        img->is_float = false;
+        img->u8.assign((const uint8_t*)data, (const uint8_t*)data + (size_t)w * h);
+        return true;
+    }
+    img->is_float = true;
+    if (type == kGL_UNSIGNED_BYTE) to_float((const uint8_t*)data, fmt, w, h, 255.0f, &img->f32);
+    else if (type == kGL_UNSIGNED_SHORT) to_float((const uint16_t*)data, fmt, w, h, 65535.0f, &img->f32);
+    else to_float_f((const float*)data, fmt, w, h, &img->f32);
+    return true;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------- SiftParam
+SiftParam::SiftParam() {
+    _sigma = nullptr;
+    _level_min = -1;
+    _dog_level_num = 3;
+    _level_max = 0;
+    _sigma0 = 0;
+    _sigman = 0;
+    _edge_threshold = 0;
+    _dog_threshold = 0;
+    _sigma_skip0 = _sigma_skip1 = 0;
+    _sigma_num = _level_num = _level_ds = 0;
+}
+
+float SiftParam::GetLevelSigma(int lev) {
+    return _sigma0 * powf(2.0f, float(lev) / float(_dog_level_num));
+}
+
+float SiftParam::GetInitialSmoothSigma(int octave_min) {
+    float sa = _sigma0 * powf(2.0f, float(_level_min) / float(_dog_level_num));
+    float sb = _sigman / powf(2.0f, float(octave_min));
+    return sa > sb + 0.001 ? sqrtf(sa * sa - sb * sb) : 0.0f;
+}
+
+void SiftParam::ParseSiftParam() {
+    sgp::Options po;
+    po.dog_level_num = _dog_level_num;
+    po.dog_threshold = _dog_threshold;
+    po.edge_threshold = _edge_threshold;
+    sgp::Schedule s = sgp::make_schedule(po);
+    _dog_level_num = s.dog_level_num;
+    _level_max = s.level_max;
+    _sigma0 = s.sigma0;
+    _sigman = s.sigman;
+    _level_num = s.level_num;
+    _level_ds = s.level_ds;
+    _sigma_skip0 = s.sigma_skip0;
+    _sigma_skip1 = s.sigma_skip1;
+    _sigma_num = s.level_max - s.level_min;
+    delete[] _sigma;
+    _sigma = new float[_sigma_num];
+    for (int i = 0; i < _sigma_num; i++) _sigma[i] = s.sigma[i];
+    _dog_threshold = s.dog_threshold;
+    _edge_threshold = s.edge_threshold;
+}
+
+// ---------------------------------------------------------------------------------- SiftGPU
+void* SiftGPU::operator new(size_t size) {
+    void* p = malloc(size);
+    if (!p) throw std::bad_alloc();
+    return p;
+}
+
+SiftGPU::SiftGPU(int) {
+    _texImage = reinterpret_cast<GLTexInput*>(new HostImage());
+    _imgpath = new char[kMaxPath];
+    _outpath = new char[kMaxPath];
+    _imgpath[0] = _outpath[0] = 0;
+    _initialized = 0;
+    _image_loaded = 0;
+    _current = 0;
+    _list = reinterpret_cast<ImageList*>(new ImageListImpl());
+    _pyramid = reinterpret_cast<SiftPyramid*>(new Runtime());
+    for (float& t : _timing) t = 0;
+}
+
+SiftGPU::~SiftGPU() {
+    Runtime* rt = RT(_pyramid);
+    if (rt->ctx) sgpu_ctx_destroy(rt->ctx);
+    delete rt;
+    delete IMG(_texImage);
+    delete LIST(_list);
+    delete[] _imgpath;
+    delete[] _outpath;
+    delete[] _sigma;
+}
+
+void SiftGPU::PrintUsage() {
+    std::cout << "SiftGPU (MI355X) usage: -i <files> -o <file> -f <float> -w <float> -dw <float>\n"
+                 "  -fo 0 -no <int> -d <int> -t <float> -e <float> -m [int] -s [int] -sd -unn -b\n"
+                 "  -loweo -ofix -sign -cuda [device] -v <int>\n";
+}
+
+void SiftGPU::InitSiftGPU() {
+    if (_initialized) return;
+    Runtime* rt = RT(_pyramid);
+    _dog_level_num = rt->opt.dog_level_num;
+    _dog_threshold = rt->opt.dog_threshold;
+    _edge_threshold = rt->opt.edge_threshold;
+    ParseSiftParam();
+    if (!rt->ctx) {
+        int rc = sgpu_ctx_create(rt->device, &rt->opt, &rt->ctx);
+        if (rc != SGPU_OK) {
+            std::cerr << "SiftGPU: no usable MI355X device " << rt->device << " (code " << rc << ")\n";
+            rt->ctx = nullptr;
+            return;
+        }
+    }
+    _initialized = 1;
+}
+
+void SiftGPU::LoadImageList(const char* imlist) {
+    std::ifstream in(imlist);
+    std::string name;
+    while (in >> name) LIST(_list)->push_back(name);
+    if (!LIST(_list)->empty()) strncpy(_imgpath, LIST(_list)->at(0).c_str(), kMaxPath - 1);
+    _image_loaded = 0;
+}
+
+void SiftGPU::SetImageList(int nimage, const char** filelist) {
+    LIST(_list)->clear();
+    for (int i = 0; i < nimage; i++) LIST(_list)->push_back(filelist[i]);
+    _current = 0;
+}
+
+int SiftGPU::GetFeatureNum() { return RT(_pyramid)->feature_num; }
+
+void SiftGPU::GetFeatureVector(SiftKeypoint* keys, float* descriptors) {
+    Runtime* rt = RT(_pyramid);
+    const size_t n = rt->feature_num;
+    if (keys && n) memcpy(keys, rt->keys.data(), n * 4 * sizeof(float));
+    if (descriptors && n && rt->opt.descriptors)
+        memcpy(descriptors, rt->desc.data(), n * 128 * sizeof(float));
+}
+
+// SiftPyramid::SaveSIFT (SiftPyramid.cpp:313-387): Lowe's format, (y, x, s, o) per line.
+void SiftGPU::SaveSIFT(const char* szFileName) {
+    Runtime* rt = RT(_pyramid);
+    const int n = rt->feature_num;
+    if (n <= 0) return;
+    const float* pk = rt->keys.data();
+    const bool has_desc = rt->opt.descriptors != 0;
+    if (rt->binary) {
+        std::ofstream out(szFileName, std::ios::binary);
+        out.write((const char*)&n, sizeof(int));
+        const int dim = has_desc ? 128 : 0;
+        out.write((const char*)&dim, sizeof(int));
+        for (int i = 0; i < n; i++, pk += 4) {
+            out.write((const char*)(pk + 1), sizeof(float));
+            out.write((const char*)pk, sizeof(float));
+            out.write((const char*)(pk + 2), 2 * sizeof(float));
+            if (has_desc) out.write((const char*)(rt->desc.data() + (size_t)i * 128), 128 * sizeof(float));
+        }
+        return;
+    }
+    std::ofstream out(szFileName);
+    out.flags(std::ios::fixed);
+    if (has_desc) {
+        const float* pd = rt->desc.data();
+        out << n << " 128" << std::endl;
+        for (int i = 0; i < n; i++, pk += 4) {
+            out << std::setprecision(2) << pk[1] << " " << std::setprecision(2) << pk[0] << " "
+                << std::setprecision(3) << pk[2] << " " << std::setprecision(3) << pk[3] << std::endl;
+            for (int k = 0; k < 128; k++, pd++) {
+                if (rt->opt.normalized) out << ((unsigned int)floor(0.5 + 512.0f * (*pd))) << " ";
+                else out << std::setprecision(8) << pd[0] << " ";
+                if ((k + 1) % 20 == 0) out << std::endl;
+            }
+            out << std::endl;
+        }
+    } else {
+        out << n << " 0" << std::endl;
+        for (int i = 0; i < n; i++, pk += 4)
+            out << pk[1] << " " << pk[0] << " " << pk[2] << " " << pk[3] << std::endl;
+    }
+}
+
+void SiftGPU::SetKeypointList(int, const SiftKeypoint*, int) {
+    std::cerr << "SiftGPU (MI355X): SetKeypointList is not implemented yet\n";
+}
+
+int SiftGPU::CreateContextGL() { return VerifyContextGL(); }
+
+int SiftGPU::VerifyContextGL() {
+    InitSiftGPU();
+    return _initialized ? SIFTGPU_FULL_SUPPORTED : SIFTGPU_NOT_SUPPORTED;
+}
+
+int SiftGPU::IsFullSupported() { return _initialized ? 1 : 0; }
+
+void SiftGPU::SetVerbose(int verbose) { RT(_pyramid)->verbose = verbose; }
+
+// SiftGPU::ParseParam (SiftGPU.cpp:801-1246): algorithm options go through sgpu_parse_args;
+// file options (-i, -il, -o, -b) are handled here.
+void SiftGPU::ParseParam(int argc, char** argv) {
+    Runtime* rt = RT(_pyramid);
+    if (!_initialized) {
+        sgpu_parse_args(&rt->opt, argc, argv, &rt->device);
+    } else {
+        // after initialisation only the run-time options may change (SimpleSIFT.cpp:190-193)
+        sgpu_options o = rt->opt;
+        int dev = rt->device;
+        sgpu_parse_args(&o, argc, argv, &dev);
+        rt->opt.descriptor_window_factor = o.descriptor_window_factor;
+        rt->opt.fixed_orientation = o.fixed_orientation;
+        rt->opt.normalized = o.normalized;
+        if (rt->ctx) sgpu_ctx_set_options(rt->ctx, &rt->opt);
+    }
+    for (int i = 0; i < argc; i++) {
+        const char* a = argv[i];
+        if (!a || a[0] != '-') continue;
+        std::string k(a + 1);
+        for (char& c : k) c = (char)tolower(c);
+        if (k == "h" || k == "help") PrintUsage();
+        else if (k == "b") rt->binary = 1;
+        else if (k == "v" && i + 1 < argc) rt->verbose = atoi(argv[i + 1]);
+        else if (k == "i" && i + 1 < argc) {
+            strncpy(_imgpath, argv[++i], kMaxPath - 1);
+            LIST(_list)->push_back(argv[i]);
+            while (i + 1 < argc && argv[i + 1][0] != '-') LIST(_list)->push_back(argv[++i]);
+        } else if (k == "il" && i + 1 < argc) LoadImageList(argv[++i]);
+        else if (k == "o" && i + 1 < argc) strncpy(_outpath, argv[++i], kMaxPath - 1);
+    }
+    if (_outpath[0] && LIST(_list)->size() > 1) _outpath[0] = 0;
+}
+
+int SiftGPU::RunSIFT(const char* imgpath) {
+    if (imgpath && imgpath[0]) {
+        strncpy(_imgpath, imgpath, kMaxPath - 1);
+        _image_loaded = 0;
+        return RunSIFT();
+    }
+    return 0;
+}
+
+int SiftGPU::RunSIFT(int index) {
+    ImageListImpl* l = LIST(_list);
+    if (l->empty()) return 0;
+    index = index % (int)l->size();
+    if (strcmp(_imgpath, l->at(index).c_str())) {
+        strncpy(_imgpath, l->at(index).c_str(), kMaxPath - 1);
+        _image_loaded = 0;
+        _current = index;
+    }
+    return RunSIFT();
+}
+
+int SiftGPU::RunSIFT(int width, int height, const void* data, unsigned int gl_format,
+                     unsigned int gl_type) {
+    if (!_initialized) InitSiftGPU();
+    if (!_initialized) return 0;
+    if (width <= 0 || height <= 0 || !data) return 0;
+    _imgpath[0] = 0;
+    if (!set_image(IMG(_texImage), width, height, data, gl_format, gl_type)) return 0;
+    _image_loaded = 2;
+    return RunSIFT();
+}
+
+int SiftGPU::RunSIFT() {
+    if (_imgpath[0] == 0 && _image_loaded == 0) return 0;
+    if (!_initialized) InitSiftGPU();
+    if (!_initialized) return 0;
+    Runtime* rt = RT(_pyramid);
+    HostImage* img = IMG(_texImage);
+    if (_image_loaded == 0) {
+        if (!load_pnm(_imgpath, img)) {
+            std::cerr << "Unable to open image " << _imgpath << "\n";
+            return 0;
+        }
+        _image_loaded = 1;
+    }
+    int rc = img->is_float
+                 ? sgpu_extract_f32(rt->ctx, img->f32.data(), 1, img->w, img->h, img->w, SGPU_INPUT_HOST)
+                 : sgpu_extract(rt->ctx, img->u8.data(), 1, img->w, img->h, img->w, SGPU_INPUT_HOST);
+    if (rc != SGPU_OK) {
+        std::cerr << "SiftGPU: " << sgpu_last_error(rt->ctx) << "\n";
+        rt->feature_num = 0;
+        return 0;
+    }
+    rt->feature_num = sgpu_feature_count(rt->ctx, 0);
+    rt->keys.resize((size_t)rt->feature_num * 4);
+    rt->desc.resize(rt->opt.descriptors ? (size_t)rt->feature_num * 128 : 0);
+    rc = sgpu_copy_features(rt->ctx, 0, rt->keys.data(), rt->opt.descriptors ? rt->desc.data() : nullptr);
+    if (rc != SGPU_OK) return 0;
+    float t[9] = {0};
+    sgpu_last_timing(rt->ctx, t, 9);
+    for (int i = 0; i < 10; i++) _timing[i] = 0;
+    _timing[0] = t[0] * 1e-3f;                 // upload
+    for (int i = 0; i < 5; i++) _timing[2 + i] = t[1 + i] * 1e-3f;   // stages
+    _timing[7] = t[6] * 1e-3f;
+    if (rt->verbose) std::cout << "[SiftGPU MI355X]: " << rt->feature_num << " features, " << t[7] << " ms\n";
+    if (_outpath[0]) {
+        SaveSIFT(_outpath);
+        _outpath[0] = 0;
+    }
+    return 1;
+}
+
+int SiftGPU::RunSIFT(int num, const SiftKeypoint*, int) {
+    if (num <= 0) return 0;
+    std::cerr << "SiftGPU (MI355X): descriptors for user keypoints are not implemented yet\n";
+    return 0;
+}
+
+int SiftGPU::GetImageCount() { return (int)LIST(_list)->size(); }
+void SiftGPU::SetTightPyramid(int) {}
+int SiftGPU::AllocatePyramid(int, int) { return 1; }
+void SiftGPU::SetMaxDimension(int) {}
+
+// ---------------------------------------------------------------------------------- matcher
+namespace {
+struct MatchState {
+    sgpu_ctx* ctx = nullptr;
+    int device = 0;
+    int max_sift = 14096;
+    int num[2] = {0, 0};
+    int id[2] = {0, 0};
+    std::vector<uint8_t> des[2];
+};
+MatchState* MS(SiftMatchGPU* p) { return reinterpret_cast<MatchState*>(p); }
+}  // namespace
+
+void* SiftMatchGPU::operator new(size_t size) {
+    void* p = malloc(size);
+    if (!p) throw std::bad_alloc();
+    return p;
+}
+
+SiftMatchGPU::SiftMatchGPU(int max_sift) {
+    __max_sift = std::max(max_sift, 1024);   // SiftMatch.cpp:616
+    __language = 0;
+    __matcher = nullptr;
+}
+
+SiftMatchGPU::~SiftMatchGPU() {
+    MatchState* m = MS(__matcher);
+    if (m) {
+        if (m->ctx) sgpu_ctx_destroy(m->ctx);
+        delete m;
+    }
+}
+
+int SiftMatchGPU::_CreateContextGL() { return _VerifyContextGL(); }
+
+int SiftMatchGPU::_VerifyContextGL() {
+    if (__matcher) return MS(__matcher)->ctx ? 1 : 0;
+    MatchState* m = new MatchState();
+    m->device = __language > SIFTMATCH_CUDA ? __language - SIFTMATCH_CUDA : 0;
+    // SiftMatchCU::SiftMatchCU (SiftMatchCU.cpp:46): round up to a multiple of 32
+    m->max_sift = __max_sift <= 0 ? 14096 : ((__max_sift + 31) / 32 * 32);
+    if (sgpu_ctx_create(m->device, nullptr, &m->ctx) != SGPU_OK) {
+        std::cerr << "SiftMatchGPU: no usable MI355X device " << m->device << "\n";
+        m->ctx = nullptr;
+    }
+    __matcher = reinterpret_cast<SiftMatchGPU*>(m);
+    return m->ctx ? 1 : 0;
+}
+
+void SiftMatchGPU::SetLanguage(int language) {
+    if (__matcher) return;
+    __language = language;
+}
+
+void SiftMatchGPU::SetDeviceParam(int argc, char** argv) {
+    if (__matcher) return;
+    sgpu_options o;
+    sgpu_default_options(&o);
+    int dev = -1;
+    sgpu_parse_args(&o, argc, argv, &dev);
+    if (dev >= 0) __language = SIFTMATCH_CUDA + dev;
+}
+
+void SiftMatchGPU::SetMaxSift(int max_sift) {
+    max_sift = std::max(128, max_sift);
+    if (__matcher) MS(__matcher)->max_sift = ((max_sift + 31) / 32) * 32;
+    else __max_sift = max_sift;
+}
+
+// SiftMatchCU::SetDescriptors (SiftMatchCU.cpp:71-101)
+void SiftMatchGPU::SetDescriptors(int index, int num, const unsigned char* descriptors, int id) {
+    MatchState* m = MS(__matcher);
+    if (!m || !m->ctx) return;
+    index = std::min(std::max(index, 0), 1);
+    if (id != -1 && id == m->id[index]) return;
+    m->id[index] = id;
+    if (num > m->max_sift) num = m->max_sift;
+    m->num[index] = num;
+    m->des[index].assign(descriptors, descriptors + (size_t)num * 128);
+}
+
+void SiftMatchGPU::SetDescriptors(int index, int num, const float* descriptors, int id) {
+    MatchState* m = MS(__matcher);
+    if (!m || !m->ctx) return;
+    index = std::min(std::max(index, 0), 1);
+    if (num > m->max_sift) num = m->max_sift;
+    std::vector<uint8_t> q((size_t)num * 128);
+    sgpu_quantize_descriptors(descriptors, q.size(), q.data());
+    m->id[index] = -1;   // a float upload always replaces the set
+    SetDescriptors(index, num, q.data(), id);
+}
+
+int SiftMatchGPU::GetSiftMatch(int max_match, int match_buffer[][2], float distmax,
+                               float ratiomax, int mutual_best_match) {
+    MatchState* m = MS(__matcher);
+    if (!m || !m->ctx || m->num[0] <= 0 || m->num[1] <= 0) return 0;
+    int r = sgpu_match(m->ctx, m->des[0].data(), m->num[0], m->des[1].data(), m->num[1], distmax,
+                       ratiomax, mutual_best_match, max_match, &match_buffer[0][0], SGPU_INPUT_HOST);
+    return r < 0 ? 0 : r;
+}
+
+void SiftMatchGPU::SetFeautreLocation(int, const float*, int) {}
+
+// SiftMatch.cpp:663-677: without H and F this is GetSiftMatch.
+int SiftMatchGPU::GetGuidedSiftMatch(int max_match, int match_buffer[][2], float H[3][3],
+                                     float F[3][3], float distmax, float ratiomax, float, float,
+                                     int mutual_best_match) {
+    if (H == NULL && F == NULL)
+        return GetSiftMatch(max_match, match_buffer, distmax, ratiomax, mutual_best_match);
+    std::cerr << "SiftMatchGPU (MI355X): guided matching is not implemented yet\n";
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------- factories
+void* ComboSiftGPU::operator new(size_t size) {
+    void* p = malloc(size);
+    if (!p) throw std::bad_alloc();
+    return p;
+}
+
+SiftGPU* CreateNewSiftGPU(int np) { return new SiftGPU(np); }
+SiftMatchGPU* CreateNewSiftMatchGPU(int max_sift) { return new SiftMatchGPU(max_sift); }
+ComboSiftGPU* CreateComboSiftGPU() { return new ComboSiftGPU(); }
+ComboSiftGPU* CreateRemoteSiftGPU(int, char*) { return new ComboSiftGPU(); }
+int CreateLiteWindow(LiteWindow*) { return 0; }
+void RunServerLoop(int, int, char**) {
+    std::cerr << "RunServerLoop: no remote server on this platform\n";
+}

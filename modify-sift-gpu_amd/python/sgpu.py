@@ -1,0 +1,194 @@
+"""ctypes binding of the C ABI (include/sgpu.h) of lib/libsiftgpu.so.
+
+The binding fails loudly when the library or a usable GPU is missing: there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from sgpu_types import SgpuOptions, default_options
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG, "lib", "libsiftgpu.so")
+
+SGPU_OK, SGPU_EINVAL, SGPU_ENODEV, SGPU_ENOMEM, SGPU_ERANGE = 0, -1, -2, -3, -4
+SGPU_INPUT_HOST, SGPU_INPUT_DEVICE = 0, 1
+
+# every extern "C" symbol include/sgpu.h declares (tests check the library exports them all)
+C_API = [
+    "sgpu_default_options", "sgpu_parse_args", "sgpu_ctx_create", "sgpu_ctx_destroy",
+    "sgpu_ctx_set_options", "sgpu_last_error", "sgpu_device_count", "sgpu_extract",
+    "sgpu_extract_f32", "sgpu_feature_count", "sgpu_feature_total", "sgpu_copy_features",
+    "sgpu_device_features", "sgpu_match", "sgpu_quantize_descriptors", "sgpu_last_timing",
+    "sgpu_debug_geometry", "sgpu_debug_gaussian", "sgpu_debug_candidates",
+]
+
+_LIB = None
+
+
+def build():
+    subprocess.check_call(["make", "-C", PKG, "-j8"])
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: build it with `make -C {PKG}`")
+        L = ctypes.CDLL(LIB_PATH)
+        P, c = ctypes.POINTER, ctypes
+        vp = c.c_void_p
+        L.sgpu_default_options.argtypes = [P(SgpuOptions)]
+        L.sgpu_parse_args.argtypes = [P(SgpuOptions), c.c_int, P(c.c_char_p), P(c.c_int)]
+        L.sgpu_ctx_create.argtypes = [c.c_int, P(SgpuOptions), P(vp)]
+        L.sgpu_ctx_destroy.argtypes = [vp]
+        L.sgpu_ctx_set_options.argtypes = [vp, P(SgpuOptions)]
+        L.sgpu_last_error.argtypes = [vp]
+        L.sgpu_last_error.restype = c.c_char_p
+        L.sgpu_extract.argtypes = [vp, vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int]
+        L.sgpu_extract_f32.argtypes = [vp, vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int]
+        L.sgpu_feature_count.argtypes = [vp, c.c_int]
+        L.sgpu_feature_total.argtypes = [vp]
+        L.sgpu_feature_total.restype = c.c_int64
+        L.sgpu_copy_features.argtypes = [vp, c.c_int, vp, vp]
+        L.sgpu_device_features.argtypes = [vp, P(vp), P(vp), P(vp)]
+        L.sgpu_match.argtypes = [vp, vp, c.c_int, vp, c.c_int, c.c_float, c.c_float, c.c_int,
+                                 c.c_int, vp, c.c_int]
+        L.sgpu_quantize_descriptors.argtypes = [vp, c.c_size_t, vp]
+        L.sgpu_last_timing.argtypes = [vp, vp, c.c_int]
+        L.sgpu_debug_geometry.argtypes = [vp, P(c.c_int), vp, c.c_int]
+        L.sgpu_debug_gaussian.argtypes = [vp, c.c_int, c.c_int, c.c_int, vp]
+        L.sgpu_debug_candidates.argtypes = [vp, vp, vp, c.c_int, P(c.c_int)]
+        _LIB = L
+    return _LIB
+
+
+def device_count() -> int:
+    return lib().sgpu_device_count()
+
+
+def quantize(desc: np.ndarray) -> np.ndarray:
+    d = np.ascontiguousarray(desc, np.float32)
+    out = np.empty(d.shape, np.uint8)
+    lib().sgpu_quantize_descriptors(d.ctypes.data, d.size, out.ctypes.data)
+    return out
+
+
+class SiftContext:
+    """One HIP device context (sgpu_ctx)."""
+
+    def __init__(self, device: int = 0, opts: SgpuOptions | None = None):
+        self.opts = opts or default_options()
+        self._ctx = ctypes.c_void_p()
+        rc = lib().sgpu_ctx_create(device, ctypes.byref(self.opts), ctypes.byref(self._ctx))
+        if rc != SGPU_OK:
+            raise RuntimeError(f"sgpu_ctx_create(device={device}) failed with {rc}: "
+                               "no usable gfx950 device")
+        self.batch = 0
+
+    def close(self):
+        if self._ctx:
+            lib().sgpu_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != SGPU_OK:
+            raise RuntimeError(f"{what} failed ({rc}): {lib().sgpu_last_error(self._ctx).decode()}")
+
+    def set_options(self, opts: SgpuOptions):
+        self.opts = opts
+        self._check(lib().sgpu_ctx_set_options(self._ctx, ctypes.byref(opts)), "set_options")
+
+    def extract(self, images: np.ndarray | int, shape=None, device_ptr=False):
+        """images: u8 [n, h, w] (or [h, w]) host array, or an int device pointer with
+        shape=(n, h, w, stride)."""
+        if device_ptr:
+            n, h, w, stride = shape
+            rc = lib().sgpu_extract(self._ctx, ctypes.c_void_p(images), n, w, h, stride,
+                                    SGPU_INPUT_DEVICE)
+        else:
+            a = np.ascontiguousarray(images)
+            if a.ndim == 2:
+                a = a[None]
+            n, h, w = a.shape
+            if a.dtype == np.uint8:
+                rc = lib().sgpu_extract(self._ctx, a.ctypes.data, n, w, h, w, SGPU_INPUT_HOST)
+            elif a.dtype == np.float32:
+                rc = lib().sgpu_extract_f32(self._ctx, a.ctypes.data, n, w, h, w, SGPU_INPUT_HOST)
+            else:
+                raise TypeError(a.dtype)
+        self._check(rc, "sgpu_extract")
+        self.batch = n
+        return self
+
+    def count(self, image: int = 0) -> int:
+        return lib().sgpu_feature_count(self._ctx, image)
+
+    def total(self) -> int:
+        return lib().sgpu_feature_total(self._ctx)
+
+    def features(self, image: int = 0, descriptors: bool = True):
+        n = self.count(image)
+        keys = np.zeros((n, 4), np.float32)
+        desc = np.zeros((n, 128), np.float32) if descriptors else None
+        self._check(lib().sgpu_copy_features(self._ctx, image, keys.ctypes.data if n else None,
+                                             desc.ctypes.data if (n and descriptors) else None),
+                    "sgpu_copy_features")
+        return keys, desc
+
+    def timing(self):
+        t = np.zeros(9, np.float32)
+        lib().sgpu_last_timing(self._ctx, t.ctypes.data, 9)
+        return dict(zip(["upload", "pyramid", "detect", "orientation", "expand", "descriptor",
+                         "download", "total", "match"], t.tolist()))
+
+    def match(self, d1: np.ndarray, d2: np.ndarray, distmax=0.7, ratiomax=0.8, mbm=1,
+              max_match=None, device_ptrs=None):
+        if device_ptrs is not None:
+            p1, n1, p2, n2 = device_ptrs
+            flags = SGPU_INPUT_DEVICE
+        else:
+            d1 = np.ascontiguousarray(d1, np.uint8)
+            d2 = np.ascontiguousarray(d2, np.uint8)
+            p1, n1, p2, n2 = d1.ctypes.data, d1.shape[0], d2.ctypes.data, d2.shape[0]
+            flags = SGPU_INPUT_HOST
+        max_match = n1 if max_match is None else max_match
+        out = np.zeros((max(max_match, 1), 2), np.int32)
+        m = lib().sgpu_match(self._ctx, ctypes.c_void_p(p1), n1, ctypes.c_void_p(p2), n2,
+                             distmax, ratiomax, mbm, max_match, out.ctypes.data, flags)
+        if m < 0:
+            self._check(m, "sgpu_match")
+        return out[:m]
+
+    # ---- test hooks
+    def geometry(self):
+        n = ctypes.c_int(0)
+        dims = np.zeros(48, np.int32)
+        lib().sgpu_debug_geometry(self._ctx, ctypes.byref(n), dims.ctypes.data, 16)
+        return [tuple(dims[3 * i:3 * i + 3]) for i in range(n.value)]
+
+    def gaussian(self, image, octave, level):
+        w, h, wa = self.geometry()[octave]
+        out = np.zeros(wa * h, np.float32)
+        self._check(lib().sgpu_debug_gaussian(self._ctx, image, octave, level, out.ctypes.data),
+                    "sgpu_debug_gaussian")
+        return out
+
+    def candidates(self):
+        n = ctypes.c_int(0)
+        lib().sgpu_debug_candidates(self._ctx, None, None, 0, ctypes.byref(n))
+        ints = np.zeros((max(n.value, 1), 4), np.int32)
+        fl = np.zeros((max(n.value, 1), 4), np.float32)
+        self._check(lib().sgpu_debug_candidates(self._ctx, ints.ctypes.data, fl.ctypes.data,
+                                                n.value, ctypes.byref(n)), "sgpu_debug_candidates")
+        return ints[:n.value], fl[:n.value]

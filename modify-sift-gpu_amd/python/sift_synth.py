@@ -1,0 +1,80 @@
+"""Deterministic synthetic inputs for tests and bench.py ("Synthetic inputs").
+
+Images: background 128, anisotropic Gaussian blobs, rotated rectangles, Gaussian noise, rounded and
+clamped to u8.  Descriptor sets: SIFT-like (|N(0,1)| with 60 % zeros, normalize, clip 0.2,
+renormalize) with planted near-duplicates so the ratio test fires.  Everything is a pure function
+of the seed (numpy PCG64).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def synth_image(w: int, h: int, seed: int, n_blobs: int = 400, n_rects: int = 200,
+                noise: float = 4.0) -> np.ndarray:
+    rng = np.random.Generator(np.random.PCG64(seed))
+    img = np.full((h, w), 128.0, dtype=np.float64)
+    scale = min(w, h) / 1080.0
+    for _ in range(n_blobs):
+        cx, cy = rng.uniform(0, w), rng.uniform(0, h)
+        amp = rng.uniform(-96, 96)
+        sx, sy = rng.uniform(2, 40) * max(scale, 0.15), rng.uniform(2, 40) * max(scale, 0.15)
+        th = rng.uniform(0, np.pi)
+        r = 4.0 * max(sx, sy)
+        x0, x1 = int(max(0, cx - r)), int(min(w, cx + r + 1))
+        y0, y1 = int(max(0, cy - r)), int(min(h, cy + r + 1))
+        if x0 >= x1 or y0 >= y1:
+            continue
+        yy, xx = np.mgrid[y0:y1, x0:x1]
+        dx, dy = xx - cx, yy - cy
+        c, s = np.cos(th), np.sin(th)
+        u, v = c * dx + s * dy, -s * dx + c * dy
+        img[y0:y1, x0:x1] += amp * np.exp(-0.5 * ((u / sx) ** 2 + (v / sy) ** 2))
+    for _ in range(n_rects):
+        cx, cy = rng.uniform(0, w), rng.uniform(0, h)
+        step = rng.uniform(-64, 64)
+        hw, hh = rng.uniform(3, 60) * max(scale, 0.15), rng.uniform(3, 60) * max(scale, 0.15)
+        th = rng.uniform(0, np.pi)
+        r = np.hypot(hw, hh) + 1
+        x0, x1 = int(max(0, cx - r)), int(min(w, cx + r + 1))
+        y0, y1 = int(max(0, cy - r)), int(min(h, cy + r + 1))
+        if x0 >= x1 or y0 >= y1:
+            continue
+        yy, xx = np.mgrid[y0:y1, x0:x1]
+        dx, dy = xx - cx, yy - cy
+        c, s = np.cos(th), np.sin(th)
+        u, v = c * dx + s * dy, -s * dx + c * dy
+        img[y0:y1, x0:x1] += step * ((np.abs(u) <= hw) & (np.abs(v) <= hh))
+    img += rng.normal(0.0, noise, size=img.shape)
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+
+
+def synth_batch(n: int, w: int, h: int, seed0: int, unique: int | None = None) -> np.ndarray:
+    """n images [n, h, w]; with `unique` set, only that many distinct images are generated and
+    the batch cycles through them (generation cost only; every image is still processed)."""
+    k = n if unique is None else max(1, min(unique, n))
+    base = [synth_image(w, h, seed0 + i) for i in range(k)]
+    return np.stack([base[i % k] for i in range(n)])
+
+
+def synth_descriptors(n: int, seed: int, base: np.ndarray | None = None,
+                      n_dup: int = 0, dup_noise: float = 0.02) -> np.ndarray:
+    """n float SIFT-like descriptors [n, 128].  With `base`, the first n_dup rows are noisy
+    copies of base rows (planted near-duplicates)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    d = np.abs(rng.normal(size=(n, 128)))
+    d[rng.uniform(size=(n, 128)) < 0.6] = 0.0
+    if base is not None and n_dup > 0:
+        d[:n_dup] = base[:n_dup] + rng.normal(0.0, dup_noise, size=(n_dup, 128))
+        d[:n_dup] = np.abs(d[:n_dup])
+    d /= np.maximum(np.linalg.norm(d, axis=1, keepdims=True), 1e-12)
+    d = np.minimum(d, 0.2)
+    d /= np.maximum(np.linalg.norm(d, axis=1, keepdims=True), 1e-12)
+    return d.astype(np.float32)
+
+
+def quantize(d: np.ndarray) -> np.ndarray:
+    """(unsigned char)int(512*d + 0.5) of SiftMatchCU.cpp:96-99 (float product, double add,
+    truncation, modulo-256 narrowing)."""
+    v = (np.float32(512.0) * d.astype(np.float32)).astype(np.float64) + 0.5
+    return (np.trunc(v).astype(np.int64) & 0xFF).astype(np.uint8)

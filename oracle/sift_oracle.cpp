@@ -1,0 +1,721 @@
+// sift_oracle.cpp -- CPU restatement of the SiftGPU CUDA hot path.
+//
+// TEST INFRASTRUCTURE ONLY (see sift_oracle.h).  Written to follow the reference line by line,
+// in its own data layout (a float4 key image, the histogram pyramid, per-level lists), so that a
+// mistake in the HIP kernels' different structure shows up as a mismatch.
+//
+// Floating-point conventions (shared with the HIP kernels): nvcc contracts
+// a*b+c into FMA; we fix one contraction per expression and write it out with fma_():
+//   acc += a*b          -> fma(a, b, acc)          acc -= a*b  -> fma(-a, b, acc)
+//   a*a + b*b           -> fma(a, a, b*b)          a*b - c*d   -> fma(a, b, -(c*d))
+// Everything else is evaluated without contraction (-ffp-contract=off on both sides).
+// Transcendentals come from sift_math.h (deterministic, shared with the kernels).
+#include "sift_oracle.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "../modify-sift-gpu_amd/csrc/sift_math.h"
+
+using namespace sgm;
+
+namespace oracle {
+namespace {
+
+// --- ingest: GLTexInput::SetImageData + DownSamplePixelDataI2F<u8> (GLTexImage.cpp:918-1009,
+//     808-831): width truncated to a multiple of 4, value p / 255.0f.
+Image ingest(const uint8_t* img, int w, int h, int stride) {
+    Image o;
+    o.w = w & ~3;
+    o.h = h;
+    o.px.resize((size_t)o.w * h);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < o.w; x++) o.px[(size_t)y * o.w + x] = img[(size_t)y * stride + x] / 255.0f;
+    return o;
+}
+
+// --- FilterH<FW> + FilterV<FW> (ProgramCU.cu:115-222, driven by FilterImage :406-446):
+//     horizontal pass clamps within the row, vertical pass clamps to rows 0..H-1; each output
+//     sums taps i = 0..FW-1 in order (value += data[..]*k[i] -> fma).
+Image filter(const Image& src, const float* k, int fw) {
+    const int W = src.w, H = src.h, half = fw >> 1;
+    Image tmp, dst;
+    tmp.w = dst.w = W;
+    tmp.h = dst.h = H;
+    tmp.px.resize(src.px.size());
+    dst.px.resize(src.px.size());
+    for (int y = 0; y < H; y++) {
+        const float* row = &src.px[(size_t)y * W];
+        for (int x = 0; x < W; x++) {
+            float v = 0.0f;
+            for (int i = 0; i < fw; i++) {
+                int xx = std::min(std::max(x - half + i, 0), W - 1);
+                v = fma_(row[xx], k[i], v);
+            }
+            tmp.px[(size_t)y * W + x] = v;
+        }
+    }
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            float v = 0.0f;
+            for (int i = 0; i < fw; i++) {
+                int yy = std::min(std::max(y - half + i, 0), H - 1);
+                v = fma_(tmp.px[(size_t)yy * W + x], k[i], v);
+            }
+            dst.px[(size_t)y * W + x] = v;
+        }
+    return dst;
+}
+
+// --- DownsampleKernel<1> (ProgramCU.cu:287-298): dst(r,c) = src(2r, min(2c, Wsrc-1)).
+Image downsample(const Image& src, int wdst, int hdst) {
+    Image d;
+    d.w = wdst;
+    d.h = hdst;
+    d.px.resize((size_t)wdst * hdst);
+    for (int r = 0; r < hdst; r++)
+        for (int c = 0; c < wdst; c++)
+            d.px[(size_t)r * wdst + c] = src.at(std::min(c << 1, src.w - 1), r << 1);
+    return d;
+}
+
+// tex1Dfetch on linear memory: indices outside the bound allocation return 0 (CuTexImage
+// allocations are exactly wa*h floats for reused-size pyramids).
+inline float fetch(const Image& im, long idx) {
+    if (idx < 0 || idx >= (long)im.px.size()) return 0.0f;
+    return im.px[(size_t)idx];
+}
+
+// --- ComputeDOG_Kernel (ProgramCU.cu:485-517): dog = G[m] - G[m-1]; gradient of G[m] from
+//     flat-index neighbours (row wrap at the left/right edge, 0 beyond the buffer).
+void compute_dog(const Image& g, const Image& gp, Image* dog, std::vector<float>* grad) {
+    const int W = g.w, H = g.h;
+    dog->w = W;
+    dog->h = H;
+    dog->px.resize(g.px.size());
+    if (grad) grad->resize(g.px.size() * 2);
+    for (int r = 0; r < H; r++)
+        for (int c = 0; c < W; c++) {
+            long idx = (long)r * W + c;
+            float vp = gp.px[idx], v = g.px[idx];
+            dog->px[idx] = v - vp;
+            if (!grad) continue;
+            float vxn = fetch(g, idx + 1), vxp = fetch(g, idx - 1);
+            float vyp = fetch(g, idx - W), vyn = fetch(g, idx + W);
+            float dx = vxn - vxp, dy = vyn - vyp;
+            float grd = 0.5f * sqrt_(fma_(dx, dx, dy * dy));
+            float rot = (grd == 0.0f ? 0.0f : atan2_(dy, dx));
+            (*grad)[idx * 2] = grd;
+            (*grad)[idx * 2 + 1] = rot;
+        }
+}
+
+struct Key4 { float x, y, z, w; };
+
+// --- ComputeKEY_Kernel (ProgramCU.cu:553-671) with READ_CMP_DOG_DATA (:534-550).
+//     Interior pixels only (row, col in [1, dim-2]); the comparison order and the early exits
+//     are kept, because ties are resolved by that order.
+void compute_key(const Image& dp, const Image& dc, const Image& dn, float t0, float t,
+                 float edge, int subpixel, std::vector<Key4>* key) {
+    const int W = dc.w, H = dc.h;
+    key->assign((size_t)W * H, Key4{0, 0, 0, 0});
+    for (int row = 1; row < H - 1; row++)
+        for (int col = 1; col < W - 1; col++) {
+            const long index = (long)row * W + col;
+            const long idx[3] = {index - W, index, index + W};
+            float data[3][3], datap[3][3], datan[3][3];
+            float v, nmax, nmin, result = 0.0f, dx = 0, dy = 0, ds = 0;
+            bool offset_ok = true;
+            // READ_CMP_DOG_DATA as a lambda returning false on "goto key_finish"
+            auto read_cmp = [&](float* d3, const Image& im, long i) {
+                d3[0] = im.px[i - 1];
+                d3[1] = im.px[i];
+                d3[2] = im.px[i + 1];
+                if (v > nmax) {
+                    nmax = fmax_(nmax, d3[0]);
+                    nmax = fmax_(nmax, d3[1]);
+                    nmax = fmax_(nmax, d3[2]);
+                    if (v < nmax) return false;
+                } else {
+                    nmin = fmin_(nmin, d3[0]);
+                    nmin = fmin_(nmin, d3[1]);
+                    nmin = fmin_(nmin, d3[2]);
+                    if (v > nmin) return false;
+                }
+                return true;
+            };
+            data[1][1] = v = dc.px[idx[1]];
+            if (fabs_(v) <= t0) goto finish;
+            data[1][0] = dc.px[idx[1] - 1];
+            data[1][2] = dc.px[idx[1] + 1];
+            nmax = fmax_(data[1][0], data[1][2]);
+            nmin = fmin_(data[1][0], data[1][2]);
+            if (v <= nmax && v >= nmin) goto finish;
+            if (!read_cmp(data[0], dc, idx[0])) goto finish;
+            if (!read_cmp(data[2], dc, idx[2])) goto finish;
+            {
+                float vx2 = v * 2.0f;
+                float fxx = data[1][0] + data[1][2] - vx2;
+                float fyy = data[0][1] + data[2][1] - vx2;
+                float fxy = 0.25f * (data[2][2] + data[0][0] - data[2][0] - data[0][2]);
+                float temp1 = fma_(fxx, fyy, -(fxy * fxy));
+                float temp2 = (fxx + fyy) * (fxx + fyy);
+                if (temp1 <= 0 || temp2 > edge * temp1) goto finish;
+            }
+            if (!read_cmp(datap[0], dp, idx[0])) goto finish;
+            if (!read_cmp(datap[1], dp, idx[1])) goto finish;
+            if (!read_cmp(datap[2], dp, idx[2])) goto finish;
+            if (!read_cmp(datan[0], dn, idx[0])) goto finish;
+            if (!read_cmp(datan[1], dn, idx[1])) goto finish;
+            if (!read_cmp(datan[2], dn, idx[2])) goto finish;
+            if (subpixel) {
+                float vx2 = v * 2.0f;
+                float fxx = data[1][0] + data[1][2] - vx2;
+                float fyy = data[0][1] + data[2][1] - vx2;
+                float fxy = 0.25f * (data[2][2] + data[0][0] - data[2][0] - data[0][2]);
+                float fx = 0.5f * (data[1][2] - data[1][0]);
+                float fy = 0.5f * (data[2][1] - data[0][1]);
+                float fs = 0.5f * (datan[1][1] - datap[1][1]);
+                float fss = (datan[1][1] + datap[1][1] - vx2);
+                float fxs = 0.25f * (datan[1][2] + datap[1][0] - datan[1][0] - datap[1][2]);
+                float fys = 0.25f * (datan[2][1] + datap[0][1] - datan[0][1] - datap[2][1]);
+                // rows (a, b, c, rhs) with the sign flip of ProgramCU.cu:629-631
+                float A0[4], A1[4], A2[4];
+                auto setrow = [](float* A, float a, float b, float c, float r) {
+                    if (a > 0) { A[0] = a; A[1] = b; A[2] = c; A[3] = -r; }
+                    else { A[0] = -a; A[1] = -b; A[2] = -c; A[3] = r; }
+                };
+                setrow(A0, fxx, fxy, fxs, fx);
+                setrow(A1, fxy, fyy, fys, fy);
+                setrow(A2, fxs, fys, fss, fs);
+                float maxa = fmax_(fmax_(A0[0], A1[0]), A2[0]);
+                if (maxa >= 1e-10) {
+                    if (maxa == A1[0]) { for (int q = 0; q < 4; q++) std::swap(A0[q], A1[q]); }
+                    else if (maxa == A2[0]) { for (int q = 0; q < 4; q++) std::swap(A0[q], A2[q]); }
+                    A0[1] /= A0[0]; A0[2] /= A0[0]; A0[3] /= A0[0];
+                    A1[1] = fma_(-A1[0], A0[1], A1[1]);
+                    A1[2] = fma_(-A1[0], A0[2], A1[2]);
+                    A1[3] = fma_(-A1[0], A0[3], A1[3]);
+                    A2[1] = fma_(-A2[0], A0[1], A2[1]);
+                    A2[2] = fma_(-A2[0], A0[2], A2[2]);
+                    A2[3] = fma_(-A2[0], A0[3], A2[3]);
+                    if (fabs_(A2[1]) > fabs_(A1[1])) { for (int q = 0; q < 4; q++) std::swap(A1[q], A2[q]); }
+                    if (fabs_(A1[1]) >= 1e-10) {
+                        A1[2] /= A1[1]; A1[3] /= A1[1];
+                        A2[2] = fma_(-A2[1], A1[2], A2[2]);
+                        A2[3] = fma_(-A2[1], A1[3], A2[3]);
+                        if (fabs_(A2[2]) >= 1e-10) {
+                            ds = A2[3] / A2[2];
+                            dy = fma_(-ds, A1[2], A1[3]);
+                            dx = fma_(-dy, A0[1], fma_(-ds, A0[2], A0[3]));
+                            float dot = fma_(ds, fs, fma_(dx, fx, dy * fy));
+                            offset_ok = fabs_(fma_(0.5f, dot, data[1][1])) > t &&
+                                        fabs_(ds) < 1.0f && fabs_(dx) < 1.0f && fabs_(dy) < 1.0f;
+                        }
+                    }
+                }
+            }
+            if (offset_ok) result = v > nmax ? 1.0f : -1.0f;
+        finish:
+            (*key)[index] = Key4{result, dx, dy, ds};
+        }
+}
+
+// --- histogram pyramid list generation, literal: InitHist_Kernel (ProgramCU.cu:698-721),
+//     ReduceHist_Kernel (:739-757), FitHistogramPyramid (PyramidCU.cpp:1175-1193), the CPU seed
+//     list (PyramidCU.cpp:781-811) and ListGen_Kernel (ProgramCU.cu:775-798).
+std::vector<Candidate> histo_list(const std::vector<Key4>& key, int W, int H, int hp_levels) {
+    struct I4 { int v[4]; };
+    // level widths, finest (w = (W+2)>>2) first
+    std::vector<int> widths;
+    int w = (W + 2) >> 2;
+    for (int k = 0; k < hp_levels; k++) {
+        widths.push_back(w);
+        if (w == 1) break;
+        w = (w + 3) >> 2;
+    }
+    std::vector<std::vector<I4>> hist(widths.size());
+    hist[0].resize((size_t)widths[0] * H);
+    for (int row = 0; row < H; row++)
+        for (int col = 0; col < widths[0]; col++) {
+            I4 o{{0, 0, 0, 0}};
+            if (row > 0 && row < H - 1)
+                for (int i = 0; i < 4; i++) {
+                    int scol = (col << 2) + i;
+                    long sidx = (long)row * W + scol;
+                    // texture fetch beyond the key buffer returns 0 (scol < W always here)
+                    float kx = (scol < W) ? key[sidx].x : 0.0f;
+                    o.v[i] = (scol < W - 1 && scol > 0 && kx != 0) ? 1 : 0;
+                }
+            hist[0][(size_t)row * widths[0] + col] = o;
+        }
+    for (size_t l = 1; l < widths.size(); l++) {
+        int ws = widths[l - 1], wd = widths[l];
+        hist[l].resize((size_t)wd * H);
+        for (int row = 0; row < H; row++)
+            for (int col = 0; col < wd; col++) {
+                I4 o{{0, 0, 0, 0}};
+                int scol = col << 2;
+                for (int i = 0; i < 4 && scol < ws; ++i, ++scol) {
+                    const I4& t = hist[l - 1][(size_t)row * ws + scol];
+                    o.v[i] = t.v[0] + t.v[1] + t.v[2] + t.v[3];
+                }
+                hist[l][(size_t)row * wd + col] = o;
+            }
+    }
+    // top level must be one int4 per row (PyramidCU.cpp:781 reads height*4 ints)
+    const std::vector<I4>& top = hist.back();
+    struct P { int x, y, z; };
+    std::vector<P> list;
+    for (int ii = 0; ii < H * 4; ++ii) {
+        int cnt = top[ii / 4].v[ii % 4];
+        if (!(cnt >= 0)) cnt = 0;
+        for (int jj = 0; jj < cnt; ++jj) list.push_back(P{ii % 4, ii / 4, jj});
+    }
+    // descend: GenerateList against levels top-1 .. 0
+    for (int l = (int)widths.size() - 2; l >= 0; --l) {
+        int wl = widths[l];
+        for (P& p : list) {
+            const I4& t = hist[l][(size_t)p.y * wl + p.x];
+            int sum1 = t.v[0] + t.v[1], sum2 = sum1 + t.v[2];
+            p.x <<= 2;
+            if (p.z >= sum2) { p.x += 3; p.z -= sum2; }
+            else if (p.z >= sum1) { p.x += 2; p.z -= sum1; }
+            else if (p.z >= t.v[0]) { p.x += 1; p.z -= t.v[0]; }
+        }
+    }
+    std::vector<Candidate> out;
+    out.reserve(list.size());
+    for (const P& p : list) {
+        const Key4& k = key[(size_t)p.y * W + p.x];
+        out.push_back(Candidate{p.x, p.y, k.y, k.z, k.w});
+    }
+    return out;
+}
+
+inline uint32_t f2u(float f) { return as_uint(f); }
+inline float u2f(uint32_t u) { return as_float(u); }
+
+// --- ComputeOrientation_Kernel (ProgramCU.cu:813-977) for one list entry.  grad is the
+//     float2 gradient image of G[1+j] (texture point sampling at x = k + 0.5 -> texel k).
+void orientation(const Candidate& c, const std::vector<float>& grad, int W, int H, float sigma,
+                 float sigma_step, float gaussian_factor, float sample_factor,
+                 int num_orientation, int subpixel, int keepsign, int circular, float* out) {
+    const float ten_degree_per_radius = (float)5.7295779513082320876798154814105;
+    const float radius_per_ten_degrees = (float)(1.0 / 5.7295779513082320876798154814105);
+    Key4 key;
+    key.x = c.col + 0.5f;
+    key.y = c.row + 0.5f;
+    key.z = sigma;
+    key.w = 0;
+    if (subpixel) {
+        key.x += c.dx;
+        key.y += c.dy;
+        key.z *= pow_(sigma_step, c.ds);
+    }
+    (void)keepsign;  // -sign multiplies by the extremum sign; handled by the caller
+    if (num_orientation == 0) {
+        out[0] = key.x; out[1] = key.y; out[2] = key.z; out[3] = 0.0f;
+        return;
+    }
+    float vote[37];
+    float gsigma = key.z * gaussian_factor;
+    float win = fabs_(key.z) * sample_factor;
+    float dist_threshold = (float)(win * win + 0.5);
+    float factor = -0.5f / (gsigma * gsigma);
+    float xmin = fmax_(1.5f, floor_(key.x - win) + 0.5f);
+    float ymin = fmax_(1.5f, floor_(key.y - win) + 0.5f);
+    float xmax = fmin_(W - 1.5f, floor_(key.x + win) + 0.5f);
+    float ymax = fmin_(H - 1.5f, floor_(key.y + win) + 0.5f);
+    for (int i = 0; i < 36; ++i) vote[i] = 0.0f;
+    for (float y = ymin; y <= ymax; y += 1.0f)
+        for (float x = xmin; x <= xmax; x += 1.0f) {
+            float dx = x - key.x, dy = y - key.y;
+            float sq_dist = fma_(dx, dx, dy * dy);
+            if (circular && sq_dist >= dist_threshold) continue;   // ProgramCU-0.cu:834
+            size_t t = ((size_t)(int)y * W + (int)x) * 2;
+            float gm = grad[t], ga = grad[t + 1];
+            float weight = gm * exp_(sq_dist * factor);
+            float fidx = floor_(ga * ten_degree_per_radius);
+            int oidx = (int)fidx;
+            if (oidx < 0) oidx += 36;
+            vote[oidx] += weight;
+        }
+    const float one_third = (float)(1.0 / 3.0);
+    for (int i = 0; i < 6; ++i) {
+        vote[36] = vote[0];
+        float pre = vote[35];
+        for (int j = 0; j < 36; ++j) {
+            float temp = one_third * (pre + vote[j] + vote[j + 1]);
+            pre = vote[j];
+            vote[j] = temp;
+        }
+    }
+    vote[36] = vote[0];
+    // __fdividef(a, b) is stated as a * (1/b) (two roundings) on both sides
+    auto fdiv = [](float a, float b) { return a * (1.0f / b); };
+    if (num_orientation == 1) {
+        int index_max = 0;
+        float max_vote = vote[0];
+        for (int i = 1; i < 36; ++i) {
+            index_max = vote[i] > max_vote ? i : index_max;
+            max_vote = fmax_(max_vote, vote[i]);
+        }
+        float pre = vote[index_max == 0 ? 35 : index_max - 1];
+        float next = vote[index_max + 1];
+        float weight = max_vote;
+        float off = 0.5f * fdiv(next - pre, weight + weight - next - pre);
+        key.w = radius_per_ten_degrees * (index_max + 0.5f + off);
+        out[0] = key.x; out[1] = key.y; out[2] = key.z; out[3] = key.w;
+        return;
+    }
+    float max_vote = vote[0];
+    for (int i = 1; i < 36; ++i) max_vote = fmax_(max_vote, vote[i]);
+    float vote_threshold = max_vote * 0.8f;
+    float pre = vote[35];
+    float max_rot[2] = {0, 0}, max_vot[2] = {0, 0};
+    int ocount = 0;
+    for (int i = 0; i < 36; ++i) {
+        float next = vote[i + 1];
+        if (vote[i] > vote_threshold && vote[i] > pre && vote[i] > next) {
+            float di = 0.5f * fdiv(next - pre, vote[i] + vote[i] - next - pre);
+            float rot = i + di + 0.5f;
+            float weight = vote[i];
+            if (weight > max_vot[1]) {
+                if (weight > max_vot[0]) {
+                    max_vot[1] = max_vot[0];
+                    max_rot[1] = max_rot[0];
+                    max_vot[0] = weight;
+                    max_rot[0] = rot;
+                } else {
+                    max_vot[1] = weight;
+                    max_rot[1] = rot;
+                }
+                ocount++;
+            }
+        }
+        pre = vote[i];
+    }
+    float fr1 = max_rot[0] / 36.0f;
+    if (fr1 < 0) fr1 += 1.0f;
+    unsigned short us1 = ocount == 0 ? 65535 : (unsigned short)floor_(fr1 * 65535.0f);
+    unsigned short us2 = 65535;
+    if (ocount > 1) {
+        float fr2 = max_rot[1] / 36.0f;
+        if (fr2 < 0) fr2 += 1.0f;
+        us2 = (unsigned short)floor_(fr2 * 65535.0f);
+    }
+    uint32_t uspack = ((uint32_t)us2 << 16) | us1;
+    out[0] = key.x; out[1] = key.y; out[2] = key.z; out[3] = u2f(uspack);
+}
+
+// --- ComputeDescriptor_Kernel<false> (ProgramCU.cu:1013-1101) + NormalizeDescriptor_Kernel
+//     (:1173-1208) for one feature (fx, fy, s, o) in octave coordinates.
+void descriptor(const float* key, const std::vector<float>& grad, int W, int H,
+                float window_factor, int normalize, float* des128) {
+    const float rpi = (float)(4.0 / 3.14159265358979323846);
+    for (int bidx = 0; bidx < 16; bidx++) {
+        int ix = bidx & 3, iy = bidx >> 2;
+        float spt = fabs_(key[2] * window_factor);
+        float s, c;
+        sincos_(key[3], &s, &c);
+        float anglef = key[3] > 3.14159265358979323846
+                           ? (float)(key[3] - (2.0 * 3.14159265358979323846)) : key[3];
+        float cspt = c * spt, sspt = s * spt;
+        float crspt = c / spt, srspt = s / spt;
+        float ox = ix - 1.5f, oy = iy - 1.5f;
+        float ptx = fma_(cspt, ox, -(sspt * oy)) + key[0];
+        float pty = fma_(cspt, oy, sspt * ox) + key[1];
+        float bsz = fabs_(cspt) + fabs_(sspt);
+        float xmin = fmax_(1.5f, floor_(ptx - bsz) + 0.5f);
+        float ymin = fmax_(1.5f, floor_(pty - bsz) + 0.5f);
+        float xmax = fmin_(W - 1.5f, floor_(ptx + bsz) + 0.5f);
+        float ymax = fmin_(H - 1.5f, floor_(pty + bsz) + 0.5f);
+        float des[9];
+        for (int i = 0; i < 9; ++i) des[i] = 0.0f;
+        for (float y = ymin; y <= ymax; y += 1.0f)
+            for (float x = xmin; x <= xmax; x += 1.0f) {
+                float dx = x - ptx, dy = y - pty;
+                float nx = fma_(crspt, dx, srspt * dy);
+                float ny = fma_(crspt, dy, -(srspt * dx));
+                float nxn = fabs_(nx), nyn = fabs_(ny);
+                if (nxn < 1.0f && nyn < 1.0f) {
+                    size_t t = ((size_t)(int)y * W + (int)x) * 2;
+                    float gm = grad[t], ga = grad[t + 1];
+                    float dnx = nx + ox, dny = ny + oy;
+                    float ww = exp_(-0.125f * fma_(dnx, dnx, dny * dny));
+                    float wx = (float)(1.0 - nxn), wy = (float)(1.0 - nyn);
+                    float weight = ww * wx * wy * gm;
+                    float theta = (anglef - ga) * rpi;
+                    if (theta < 0) theta += 8.0f;
+                    float fo = floor_(theta);
+                    int fidx = (int)fo;
+                    float weight1 = fo + 1.0f - theta;
+                    float weight2 = theta - fo;
+                    if (fidx >= 0 && fidx < 8) {   // the unrolled k == fidx test drops fidx == 8
+                        des[fidx] = fma_(weight1, weight, des[fidx]);
+                        des[fidx + 1] = fma_(weight2, weight, des[fidx + 1]);
+                    }
+                }
+            }
+        des[0] += des[8];
+        for (int i = 0; i < 8; i++) des128[bidx * 8 + i] = des[i];
+    }
+    if (!normalize) return;
+    auto sq4 = [](const float* p) {
+        float t = p[0] * p[0];
+        t = fma_(p[1], p[1], t);
+        t = fma_(p[2], p[2], t);
+        t = fma_(p[3], p[3], t);
+        return t;
+    };
+    float norm1 = 0, norm2 = 0;
+    for (int i = 0; i < 32; ++i) norm1 += sq4(des128 + 4 * i);
+    norm1 = rsqrt_(norm1);
+    for (int i = 0; i < 128; ++i) des128[i] = fmin_(0.2f, des128[i] * norm1);
+    for (int i = 0; i < 32; ++i) norm2 += sq4(des128 + 4 * i);
+    norm2 = rsqrt_(norm2);
+    for (int i = 0; i < 128; ++i) des128[i] *= norm2;
+}
+
+}  // namespace
+
+Result extract(const uint8_t* img, int w, int h, int stride, const sgpu_options& opt,
+               bool keep) {
+    sgp::Options po;
+    po.filter_width_factor = opt.filter_width_factor;
+    po.dog_level_num = opt.dog_level_num;
+    po.dog_threshold = opt.dog_threshold;
+    po.edge_threshold = opt.edge_threshold;
+    po.octave_min = 0;
+    const sgp::Schedule S = sgp::make_schedule(po);
+    const int d = S.dog_level_num, nlev = S.level_num;
+    Result R;
+    R.octaves = sgp::make_octaves(w, h, opt.octave_num, 0);
+    const int noct = (int)R.octaves.size();
+
+    // ResizeFeatureStorage (PyramidCU.cpp:341-347): histopyramid depth from the base level
+    int whmax = std::max(R.octaves[0].wa, R.octaves[0].h);
+    int hp_levels = (int)std::ceil(std::log(double(whmax)) / std::log(4.0));
+
+    Image input = ingest(img, w, h, stride);
+    float taps[sgp::kMaxFilterWidth];
+    std::vector<Image> prev;  // previous octave's Gaussian levels
+    const float sigma_step = powf(2.0f, 1.0f / d);  // PyramidCU.cpp:1200
+    const float tdog1 = (opt.subpixel ? 0.8f : 1.0f) * S.dog_threshold;   // ProgramCU.cu:677
+    const float tedge = (S.edge_threshold + 1) * (S.edge_threshold + 1) / S.edge_threshold;
+    const int num_orientation = opt.fixed_orientation ? 0 : opt.max_orientation;
+    const double twopi = 2.0 * 3.14159265358979323846;
+    const float offset = opt.lowe_origin ? 0.0f : 0.5f;
+
+    for (int o = 0; o < noct; o++) {
+        const sgp::Octave& oc = R.octaves[o];
+        std::vector<Image> g(nlev);
+        // BuildPyramid (PyramidCU.cpp:979-1044)
+        if (o == 0) {
+            int fw = sgp::make_filter(S.initial_smooth, opt.filter_width_factor, taps);
+            g[0] = filter(input, taps, fw);
+        } else {
+            g[0] = downsample(prev[S.level_ds - S.level_min], oc.wa, oc.h);
+            if (S.sigma_skip1 > 0) {
+                int fw = sgp::make_filter(S.sigma_skip1, opt.filter_width_factor, taps);
+                g[0] = filter(g[0], taps, fw);
+            }
+        }
+        for (int k = 1; k < nlev; k++) {
+            int fw = sgp::make_filter(S.sigma[k - 1], opt.filter_width_factor, taps);
+            g[k] = filter(g[k - 1], taps, fw);
+        }
+        // DetectKeypointsEX (PyramidCU.cpp:1046-1114): dog 1..nlev-1, grad for 1..d
+        std::vector<Image> dog(nlev);
+        std::vector<std::vector<float>> grad(nlev);
+        for (int m = 1; m < nlev; m++)
+            compute_dog(g[m], g[m - 1], &dog[m], (m >= 1 && m < 1 + d) ? &grad[m] : nullptr);
+        for (int j = 0; j < d; j++) {
+            std::vector<Key4> key;
+            compute_key(dog[1 + j], dog[2 + j], dog[3 + j], tdog1, S.dog_threshold, tedge,
+                        opt.subpixel, &key);
+            LevelResult L;
+            L.octave = o;
+            L.level = j;
+            L.candidates = histo_list(key, oc.wa, oc.h, hp_levels);
+            // GetFeatureOrientations (PyramidCU.cpp:1195-1222): grad of G[1+j], GetLevelSigma(j)
+            float sigma = sgp::level_sigma(S, j + S.level_min + 1);
+            L.oriented.resize(L.candidates.size() * 4);
+            for (size_t f = 0; f < L.candidates.size(); f++) {
+                orientation(L.candidates[f], grad[1 + j], oc.wa, oc.h, sigma, sigma_step,
+                            opt.orientation_gaussian_factor,
+                            opt.orientation_gaussian_factor * opt.orientation_window_factor,
+                            num_orientation, opt.subpixel, opt.keep_extremum_sign,
+                            opt.circular_window, &L.oriented[f * 4]);
+                if (opt.keep_extremum_sign) {  // ProgramCU.cu:849: z *= sign of the extremum
+                    const Key4& kk = key[(size_t)L.candidates[f].row * oc.wa + L.candidates[f].col];
+                    L.oriented[f * 4 + 2] *= kk.x;
+                }
+            }
+            // feature expansion + image coordinates
+            const float oss = (float)(1 << o);
+            auto emit = [&](const float* src, float ang) {
+                R.feat_oct.insert(R.feat_oct.end(), {src[0], src[1], src[2], ang});
+                R.keys.push_back(oss * (src[0] - 0.5f) + offset);
+                R.keys.push_back(oss * (src[1] - 0.5f) + offset);
+                R.keys.push_back(oss * src[2]);
+                R.keys.push_back((float)std::fmod(twopi - ang, twopi));
+                R.feat_level.push_back(o * d + j);
+            };
+            for (size_t f = 0; f < L.candidates.size(); f++) {
+                const float* src = &L.oriented[f * 4];
+                if (num_orientation >= 2) {
+                    // ReshapeFeatureListCPU (PyramidCU.cpp:521-606)
+                    const double factor = 2.0 * 3.14159265358979323846 / 65535.0;
+                    uint32_t pk = f2u(src[3]);
+                    unsigned short o1 = pk & 0xffff, o2 = pk >> 16;
+                    if (o1 != 65535) {
+                        emit(src, float(factor * o1));
+                        if (o2 != 65535 && o2 != o1) emit(src, float(factor * o2));
+                    }
+                } else {
+                    // DownloadKeypoints (PyramidCU.cpp:701-751)
+                    emit(src, src[3]);
+                }
+            }
+            if (opt.descriptors) {
+                // GetFeatureDescriptors (PyramidCU.cpp:413-452): grad of G[1+j]
+                size_t nf = R.feat_level.size();
+                size_t first = R.desc.size() / 128;
+                R.desc.resize(nf * 128);
+                for (size_t f = first; f < nf; f++)
+                    descriptor(&R.feat_oct[f * 4], grad[1 + j], oc.wa, oc.h,
+                               opt.descriptor_window_factor, opt.normalized, &R.desc[f * 128]);
+            }
+            R.levels.push_back(std::move(L));
+        }
+        prev = std::move(g);
+        if (keep) R.gauss.push_back(prev);
+    }
+    return R;
+}
+
+float match_distance(int dot) {
+    // RowMatch_Kernel / ColMatch_Kernel (ProgramCU.cu:1838-1839, 1884-1885):
+    // float product, min with 1.0 in double, acos in double, stored as float.
+    return (float)std::acos(std::min((double)(dot * 0.000003814697265625f), 1.0));
+}
+
+std::vector<int> match(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float distmax,
+                       float ratiomax, int mbm, int max_match) {
+    struct Top2 { int max = 0, idx = -1, second = 0; };
+    std::vector<Top2> rows(n1), cols(n2);
+    // MultiplyDescriptor_Kernel (ProgramCU.cu:1466-1564): exact int dot products
+    for (int i = 0; i < n1; i++)
+        for (int j = 0; j < n2; j++) {
+            int dot = 0;
+            for (int k = 0; k < 128; k++) dot += (int)d1[i * 128 + k] * (int)d2[j * 128 + k];
+            // RowMatch (ProgramCU.cu:1803-1835) and the texCRT / ColMatch merge (:1540-1552,
+            // 1874-1882): running top-2 with strict '>', ties push the old max to second
+            Top2& r = rows[i];
+            if (dot > r.max) { r.second = r.max; r.max = dot; r.idx = j; }
+            else r.second = std::max(r.second, dot);
+            Top2& c = cols[j];
+            if (dot > c.max) { c.second = c.max; c.max = dot; c.idx = i; }
+            else c.second = std::max(c.second, dot);
+        }
+    auto accept = [&](const Top2& t) {
+        float dist = match_distance(std::min(t.max, 262144));
+        float distn = match_distance(std::min(t.second, 262144));
+        return (dist < distmax) && (dist < distn * ratiomax) ? t.idx : -1;
+    };
+    std::vector<int> out;
+    for (int i = 0; i < n1 && (int)out.size() / 2 < max_match; ++i) {
+        int j = accept(rows[i]);
+        if (j >= 0 && (!mbm || accept(cols[j]) == i)) {   // SiftMatchCU.cpp:166-176
+            out.push_back(i);
+            out.push_back(j);
+        }
+    }
+    return out;
+}
+
+}  // namespace oracle
+
+// ---------------------------------------------------------------------------------------------
+// C entry points for ctypes (tests / bench cpu_baseline).
+extern "C" {
+
+int oracle_extract(const uint8_t* img, int w, int h, int stride, const sgpu_options* opt,
+                   float* keys, float* desc, int cap, int* n_out) {
+    oracle::Result R = oracle::extract(img, w, h, stride, *opt, false);
+    int n = (int)R.feat_level.size();
+    *n_out = n;
+    if (n > cap) return -4;
+    if (keys) memcpy(keys, R.keys.data(), sizeof(float) * 4 * n);
+    if (desc && opt->descriptors) memcpy(desc, R.desc.data(), sizeof(float) * 128 * n);
+    return 0;
+}
+
+// Gaussian level (octave o, level k) of the oracle pyramid.
+int oracle_gaussian(const uint8_t* img, int w, int h, int stride, const sgpu_options* opt,
+                    int octave, int level, float* out, int cap) {
+    sgpu_options o2 = *opt;
+    o2.descriptors = 0;
+    oracle::Result R = oracle::extract(img, w, h, stride, o2, true);
+    if (octave >= (int)R.gauss.size()) return -1;
+    const oracle::Image& g = R.gauss[octave][level];
+    if ((int)g.px.size() > cap) return -4;
+    memcpy(out, g.px.data(), g.px.size() * sizeof(float));
+    return (int)g.px.size();
+}
+
+// Candidates in reference order: ints {col,row,level_id,0}, floats {dx,dy,ds,0}.
+int oracle_candidates(const uint8_t* img, int w, int h, int stride, const sgpu_options* opt,
+                      int* ints, float* floats, int cap, int* n_out) {
+    sgpu_options o2 = *opt;
+    o2.descriptors = 0;
+    oracle::Result R = oracle::extract(img, w, h, stride, o2, false);
+    int n = 0, d = opt->dog_level_num;
+    for (const auto& L : R.levels)
+        for (const auto& c : L.candidates) {
+            if (n < cap) {
+                int* p = ints + 4 * n;
+                p[0] = c.col; p[1] = c.row; p[2] = L.octave * d + L.level; p[3] = 0;
+                float* q = floats + 4 * n;
+                q[0] = c.dx; q[1] = c.dy; q[2] = c.ds; q[3] = 0;
+            }
+            n++;
+        }
+    *n_out = n;
+    return n > cap ? -4 : 0;
+}
+
+int oracle_match(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float distmax,
+                 float ratiomax, int mbm, int max_match, int* out_pairs) {
+    std::vector<int> m = oracle::match(d1, n1, d2, n2, distmax, ratiomax, mbm, max_match);
+    memcpy(out_pairs, m.data(), m.size() * sizeof(int));
+    return (int)m.size() / 2;
+}
+
+float oracle_match_distance(int dot) { return oracle::match_distance(dot); }
+
+void oracle_schedule(int dog_level_num, float* sigma0, float* sigma_skip0, float* sigmas,
+                     int* widths) {
+    sgp::Options po;
+    po.dog_level_num = dog_level_num;
+    sgp::Schedule S = sgp::make_schedule(po);
+    *sigma0 = S.sigma0;
+    *sigma_skip0 = S.sigma_skip0;
+    float taps[sgp::kMaxFilterWidth];
+    widths[0] = sgp::make_filter(S.initial_smooth, 4.0f, taps);
+    for (int i = 0; i < S.level_num - 1; i++) {
+        sigmas[i] = S.sigma[i];
+        widths[i + 1] = sgp::make_filter(S.sigma[i], 4.0f, taps);
+    }
+}
+
+// deterministic math probes (accuracy tests against libm)
+float oracle_exp(float x) { return sgm::exp_(x); }
+float oracle_atan2(float y, float x) { return sgm::atan2_(y, x); }
+float oracle_log(float x) { return sgm::log_(x); }
+void oracle_sincos(float x, float* s, float* c) { sgm::sincos_(x, s, c); }
+
+}  // extern "C"

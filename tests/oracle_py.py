@@ -1,0 +1,120 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so) -- test infrastructure only."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "modify-sift-gpu_amd", "python"))
+
+from sgpu_types import SgpuOptions, default_options  # noqa: E402
+
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(ROOT, "oracle", "liboracle.so")
+        if not os.path.exists(path):
+            subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle")])
+        L = ctypes.CDLL(path)
+        P = ctypes.POINTER
+        L.oracle_extract.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     P(SgpuOptions), ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_int, P(ctypes.c_int)]
+        L.oracle_gaussian.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      P(SgpuOptions), ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_void_p, ctypes.c_int]
+        L.oracle_candidates.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        P(SgpuOptions), ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_int, P(ctypes.c_int)]
+        L.oracle_match.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                   ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_void_p]
+        L.oracle_match_distance.argtypes = [ctypes.c_int]
+        L.oracle_match_distance.restype = ctypes.c_float
+        L.oracle_schedule.argtypes = [ctypes.c_int, P(ctypes.c_float), P(ctypes.c_float),
+                                      ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_exp.argtypes = [ctypes.c_float]
+        L.oracle_exp.restype = ctypes.c_float
+        L.oracle_log.argtypes = [ctypes.c_float]
+        L.oracle_log.restype = ctypes.c_float
+        L.oracle_atan2.argtypes = [ctypes.c_float, ctypes.c_float]
+        L.oracle_atan2.restype = ctypes.c_float
+        L.oracle_sincos.argtypes = [ctypes.c_float, P(ctypes.c_float), P(ctypes.c_float)]
+        L.oracle_bench_extract.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, P(SgpuOptions),
+                                           ctypes.c_int, P(ctypes.c_longlong)]
+        L.oracle_bench_extract.restype = ctypes.c_double
+        _LIB = L
+    return _LIB
+
+
+def _img(img):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    return img, img.ctypes.data
+
+
+def extract(img: np.ndarray, opts: SgpuOptions | None = None):
+    """Returns (keys [n,4], desc [n,128]) for a gray u8 image [h, w]."""
+    opts = opts or default_options()
+    img, p = _img(img)
+    h, w = img.shape
+    n = ctypes.c_int(0)
+    lib().oracle_extract(p, w, h, w, ctypes.byref(opts), None, None, 0, ctypes.byref(n))
+    keys = np.zeros((max(n.value, 1), 4), np.float32)
+    desc = np.zeros((max(n.value, 1), 128), np.float32)
+    rc = lib().oracle_extract(p, w, h, w, ctypes.byref(opts), keys.ctypes.data,
+                              desc.ctypes.data, n.value, ctypes.byref(n))
+    assert rc == 0, rc
+    return keys[:n.value], desc[:n.value]
+
+
+def gaussian(img, octave, level, opts=None):
+    opts = opts or default_options()
+    img, p = _img(img)
+    h, w = img.shape
+    cap = (w + 4) * h
+    out = np.zeros(cap, np.float32)
+    n = lib().oracle_gaussian(p, w, h, w, ctypes.byref(opts), octave, level, out.ctypes.data, cap)
+    assert n > 0, n
+    return out[:n]
+
+
+def candidates(img, opts=None):
+    opts = opts or default_options()
+    img, p = _img(img)
+    h, w = img.shape
+    n = ctypes.c_int(0)
+    lib().oracle_candidates(p, w, h, w, ctypes.byref(opts), None, None, 0, ctypes.byref(n))
+    ints = np.zeros((max(n.value, 1), 4), np.int32)
+    fl = np.zeros((max(n.value, 1), 4), np.float32)
+    lib().oracle_candidates(p, w, h, w, ctypes.byref(opts), ints.ctypes.data, fl.ctypes.data,
+                            n.value, ctypes.byref(n))
+    return ints[:n.value], fl[:n.value]
+
+
+def match(d1: np.ndarray, d2: np.ndarray, distmax=0.7, ratiomax=0.8, mbm=1, max_match=None):
+    d1 = np.ascontiguousarray(d1, np.uint8)
+    d2 = np.ascontiguousarray(d2, np.uint8)
+    n1, n2 = d1.shape[0], d2.shape[0]
+    max_match = n1 if max_match is None else max_match
+    out = np.zeros((max(max_match, 1), 2), np.int32)
+    m = lib().oracle_match(d1.ctypes.data, n1, d2.ctypes.data, n2, distmax, ratiomax, mbm,
+                           max_match, out.ctypes.data)
+    return out[:m]
+
+
+def bench_extract(images: np.ndarray, opts=None, threads=1):
+    opts = opts or default_options()
+    images = np.ascontiguousarray(images, np.uint8)
+    n, h, w = images.shape
+    feats = ctypes.c_longlong(0)
+    secs = lib().oracle_bench_extract(images.ctypes.data, n, w, h, w, ctypes.byref(opts),
+                                      threads, ctypes.byref(feats))
+    return secs, feats.value
