@@ -712,6 +712,30 @@ void oracle_schedule(int dog_level_num, float* sigma0, float* sigma_skip0, float
     }
 }
 
+// Octave geometry (w, h, wa per octave) for an input of w x h (PyramidCU.cpp:89-271).
+int oracle_geometry(int w, int h, int octave_num, int* dims, int max) {
+    std::vector<sgp::Octave> oc = sgp::make_octaves(w, h, octave_num, 0);
+    for (int o = 0; o < (int)oc.size() && o < max; o++) {
+        dims[3 * o] = oc[o].w; dims[3 * o + 1] = oc[o].h; dims[3 * o + 2] = oc[o].wa;
+    }
+    return (int)oc.size();
+}
+
+// Histogram-pyramid level widths for a key image of width W inside a pyramid whose base level
+// is base_w x base_h (FitHistogramPyramid PyramidCU.cpp:1175-1193 with the depth of
+// ResizeFeatureStorage PyramidCU.cpp:341-347).
+int oracle_hist_widths(int W, int base_w, int base_h, int* widths, int max) {
+    int whmax = std::max(base_w, base_h);
+    int levels = (int)std::ceil(std::log(double(whmax)) / std::log(4.0));
+    int w = (W + 2) >> 2, n = 0;
+    for (int k = 0; k < levels && n < max; k++) {
+        widths[n++] = w;
+        if (w == 1) break;
+        w = (w + 3) >> 2;
+    }
+    return n;
+}
+
 // deterministic math probes (accuracy tests against libm)
 float oracle_exp(float x) { return sgm::exp_(x); }
 float oracle_atan2(float y, float x) { return sgm::atan2_(y, x); }

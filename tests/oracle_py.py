@@ -40,6 +40,10 @@ def lib():
         L.oracle_match_distance.restype = ctypes.c_float
         L.oracle_schedule.argtypes = [ctypes.c_int, P(ctypes.c_float), P(ctypes.c_float),
                                       ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_geometry.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                      ctypes.c_int]
+        L.oracle_hist_widths.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_void_p, ctypes.c_int]
         L.oracle_exp.argtypes = [ctypes.c_float]
         L.oracle_exp.restype = ctypes.c_float
         L.oracle_log.argtypes = [ctypes.c_float]

@@ -1,0 +1,172 @@
+"""CPU tests of the oracle: the reference's own known-answer values, the deterministic math it
+shares with the kernels, independent restatements of the list order and the matcher, and the
+committed golden fixtures."""
+import ctypes
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from sgpu_types import default_options
+from sift_synth import synth_image, synth_descriptors, quantize
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _schedule(d=3):
+    s0, sk = ctypes.c_float(), ctypes.c_float()
+    sig = np.zeros(16, np.float32)
+    wd = np.zeros(16, np.int32)
+    O.lib().oracle_schedule(d, ctypes.byref(s0), ctypes.byref(sk), sig.ctypes.data,
+                            wd.ctypes.data)
+    return s0.value, sk.value, sig, wd
+
+
+def test_sigma_schedule_kat():
+    # SiftGPU.cpp:459-497 (comments state the default values)
+    s0, sk, sig, wd = _schedule(3)
+    assert np.float32(s0) == np.float32(2.0158737)
+    assert np.float32(sk) == np.float32(1.5198685)
+    np.testing.assert_array_equal(sig[:5], np.array([1.2262735, 1.5450078, 1.9465880, 2.4525471,
+                                                     3.0900161], np.float32))
+    # filter widths: initial 13, then {11, 13, 17, 21, 25} (SURVEY.md §4 KAT list)
+    assert list(wd[:6]) == [13, 11, 13, 17, 21, 25]
+    assert np.float32(0.02) / np.float32(3) == np.float32(0.0066666664)   # dog threshold, SiftGPU.cpp:495
+
+
+def test_octave_geometry_kat():
+    # PyramidCU.cpp:985: 800*600---400*300--200*150--100*75--52*37--28*18
+    dims = np.zeros(48, np.int32)
+    n = O.lib().oracle_geometry(800, 600, -1, dims.ctypes.data, 16)
+    got = [(dims[3 * i + 2], dims[3 * i + 1]) for i in range(n)]
+    assert got == [(800, 600), (400, 300), (200, 150), (100, 75), (52, 37), (28, 18)]
+    # 1080p with -no 4 (config C2): sum of wa*h = 2,754,000
+    n = O.lib().oracle_geometry(1920, 1080, 4, dims.ctypes.data, 16)
+    assert n == 4
+    assert sum(int(dims[3 * i + 2]) * int(dims[3 * i + 1]) for i in range(n)) == 2754000
+    # 4096^2 with -no 6 (config C4): 22,364,160 px
+    n = O.lib().oracle_geometry(4096, 4096, 6, dims.ctypes.data, 16)
+    assert sum(int(dims[3 * i + 2]) * int(dims[3 * i + 1]) for i in range(n)) == 22364160
+
+
+def test_histopyramid_widths_kat():
+    # PyramidCU.cpp:346-348 / 773: width 800 -> 200, 50, 13, 4, 1 (5 levels)
+    w = np.zeros(16, np.int32)
+    n = O.lib().oracle_hist_widths(800, 800, 600, w.ctypes.data, 16)
+    assert list(w[:n]) == [200, 50, 13, 4, 1]
+
+
+@pytest.mark.parametrize("name,fn,ref,lo,hi", [
+    ("exp", "oracle_exp", np.exp, -100.0, 80.0),
+    ("log", "oracle_log", np.log, 1e-30, 1e30),
+])
+def test_det_math_unary(name, fn, ref, lo, hi):
+    rng = np.random.default_rng(7)
+    xs = rng.uniform(lo, hi, 20000) if name == "exp" else np.exp(rng.uniform(math.log(lo), math.log(hi), 20000))
+    f = getattr(O.lib(), fn)
+    got = np.array([f(float(x)) for x in xs.astype(np.float32)], np.float64)
+    want = ref(xs.astype(np.float32).astype(np.float64))
+    ok = np.isfinite(want) & (np.abs(want) > 1e-37)
+    rel = np.abs(got[ok] - want[ok]) / np.abs(want[ok])
+    assert rel.max() < 4e-7, (name, rel.max())
+
+
+def test_det_math_atan2_sincos():
+    rng = np.random.default_rng(8)
+    ys = rng.normal(size=20000).astype(np.float32)
+    xs = rng.normal(size=20000).astype(np.float32)
+    got = np.array([O.lib().oracle_atan2(float(y), float(x)) for y, x in zip(ys, xs)])
+    want = np.arctan2(ys.astype(np.float64), xs.astype(np.float64))
+    assert np.max(np.abs(got - want)) < 5e-7
+    assert O.lib().oracle_atan2(0.0, -1.0) == np.float32(np.pi)
+    assert O.lib().oracle_atan2(0.0, 1.0) == 0.0
+    s, c = ctypes.c_float(), ctypes.c_float()
+    for x in rng.uniform(-7, 7, 5000).astype(np.float32):
+        O.lib().oracle_sincos(float(x), ctypes.byref(s), ctypes.byref(c))
+        assert abs(s.value - math.sin(float(x))) < 3e-7
+        assert abs(c.value - math.cos(float(x))) < 3e-7
+
+
+def test_candidate_list_is_raster_order():
+    # the histogram pyramid (ListGen_Kernel) must produce row-major order per level
+    img = synth_image(320, 240, 11)
+    ints, _ = O.candidates(img)
+    assert len(ints) > 20
+    for lv in np.unique(ints[:, 2]):
+        sel = ints[ints[:, 2] == lv]
+        key = sel[:, 1].astype(np.int64) * 100000 + sel[:, 0]
+        assert np.all(np.diff(key) > 0)
+    assert np.all(np.diff(ints[:, 2]) >= 0)   # level-major
+
+
+def test_extract_deterministic_and_sane():
+    img = synth_image(320, 240, 12)
+    k1, d1 = O.extract(img)
+    k2, d2 = O.extract(img)
+    assert k1.shape[0] > 30
+    np.testing.assert_array_equal(k1, k2)
+    np.testing.assert_array_equal(d1, d2)
+    assert np.all((k1[:, 0] >= 0) & (k1[:, 0] < 320) & (k1[:, 1] >= 0) & (k1[:, 1] < 240))
+    assert np.all((k1[:, 3] >= 0) & (k1[:, 3] < 2 * np.pi + 1e-6))
+    np.testing.assert_allclose(np.linalg.norm(d1, axis=1), 1.0, atol=1e-5)
+    assert np.all(d1 <= 0.2 / np.float32(0.2 * np.sqrt(1) ) + 1)   # finite
+
+
+def _numpy_match(q1, q2, distmax=0.7, ratiomax=0.8, mbm=1):
+    """Independent float64 restatement of RowMatch/ColMatch + GetBestMatch."""
+    dot = q1.astype(np.int64) @ q2.astype(np.int64).T
+
+    def top(dm):
+        arg = np.argmax(dm, axis=1)
+        mx = dm[np.arange(dm.shape[0]), arg]
+        srt = np.sort(dm, axis=1)
+        sec = srt[:, -2] if dm.shape[1] > 1 else np.zeros_like(mx)
+        mx, sec = np.maximum(mx, 0), np.maximum(sec, 0)
+        dist = lambda v: np.arccos(np.minimum((v.astype(np.float32) * np.float32(2 ** -18)).astype(np.float64), 1.0)).astype(np.float32)
+        d1, d2 = dist(mx), dist(sec)
+        ok = (d1 < np.float32(distmax)) & (d1 < d2 * np.float32(ratiomax))
+        return np.where(ok & (mx > 0), arg, -1)
+
+    r = top(dot)
+    c = top(dot.T)
+    out = [(i, j) for i, j in enumerate(r) if j >= 0 and (not mbm or c[j] == i)]
+    return np.array(out, np.int32).reshape(-1, 2)
+
+
+@pytest.mark.parametrize("mbm", [1, 0])
+def test_matcher_oracle_vs_numpy(mbm):
+    d1 = synth_descriptors(400, 5000)
+    d2 = synth_descriptors(350, 5001, base=d1, n_dup=150)
+    q1, q2 = quantize(d1), quantize(d2)
+    got = O.match(q1, q2, mbm=mbm)
+    want = _numpy_match(q1, q2, mbm=mbm)
+    assert len(want) > 50
+    np.testing.assert_array_equal(got, want)
+
+
+def test_matcher_ties_and_wrap():
+    # duplicated rows create exact ties (second == max -> rejected); 512*d wraps past 255
+    q1 = np.zeros((4, 128), np.uint8)
+    q1[:, :3] = [[200, 10, 0], [0, 200, 10], [10, 0, 200], [90, 90, 90]]
+    q2 = np.concatenate([q1, q1[:1]])          # row 0 appears twice -> tie for i = 0
+    got = O.match(q1, q2)
+    want = _numpy_match(q1, q2)
+    np.testing.assert_array_equal(got, want)
+    assert 0 not in got[:, 0]
+    assert quantize(np.array([[0.5]], np.float32))[0, 0] == 0      # int(256.5) -> 256 -> 0
+
+
+def test_golden_fixtures():
+    files = sorted(f for f in os.listdir(GOLDEN) if f.startswith("extract_") and f.endswith(".npz"))
+    assert files, "golden fixtures missing (tests/make_golden.py)"
+    for f in files:
+        z = np.load(os.path.join(GOLDEN, f))
+        img = z["image"]
+        opts = default_options(**{k: int(v) for k, v in zip(z["opt_names"], z["opt_values"])})
+        k, d = O.extract(img, opts)
+        np.testing.assert_array_equal(k, z["keys"], err_msg=f)
+        np.testing.assert_array_equal(d, z["desc"], err_msg=f)
+    z = np.load(os.path.join(GOLDEN, "match_small.npz"))
+    np.testing.assert_array_equal(O.match(z["q1"], z["q2"]), z["pairs"])
