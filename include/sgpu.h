@@ -71,6 +71,12 @@ int sgpu_device_count(void);
 /* Input flags. */
 #define SGPU_INPUT_HOST   0   /* `images` is a host pointer                                */
 #define SGPU_INPUT_DEVICE 1   /* `images` is a device pointer on the context's device      */
+#define SGPU_INPUT_STAGED 2   /* use the batch staged in HBM by sgpu_stage_input (images
+                                 may be NULL); the input stays resident across calls       */
+
+/* Copy a batch of u8 images (same layout as sgpu_extract) into the context's device input
+ * buffer, so that later extract calls with SGPU_INPUT_STAGED start from HBM-resident input. */
+int sgpu_stage_input(sgpu_ctx* ctx, const uint8_t* images, int n, int w, int h, int stride);
 
 /* Extract SIFT features from n gray u8 images of w x h pixels, row stride `stride` bytes,
  * image i at images + i*stride*h.  Replaces SiftGPU::RunSIFT(w, h, data, GL_LUMINANCE,

@@ -57,6 +57,7 @@ struct sgpu_ctx {
     sgk::FeatureParams fp{};
     int total_rows = 0;
     uint32_t n_cand = 0;
+    size_t staged_bytes = 0;
     std::vector<int64_t> img_off;
     DevBuf input, pyr, mask, row_count, row_base, scan_tmp, cand, info, ocount, eoff, feat,
         feat_info, keys, desc, img_off_dev, n_dev;
@@ -235,8 +236,11 @@ const char* sgpu_last_error(const sgpu_ctx* ctx) { return ctx ? ctx->err.c_str()
 static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, int w, int h,
                         int stride, int flags) {
     if (!ctx) return SGPU_EINVAL;
-    if (!images || n <= 0 || w < 8 || h < 8 || stride < w)
+    const bool staged = (flags & SGPU_INPUT_STAGED) != 0;
+    if ((!images && !staged) || n <= 0 || w < 8 || h < 8 || stride < w)
         return ctx->fail(SGPU_EINVAL, "bad image arguments");
+    if (staged && (is_f32 || ctx->staged_bytes < (size_t)n * h * stride))
+        return ctx->fail(SGPU_EINVAL, "staged input does not match the batch");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     const sgpu_options& O = ctx->opt;
@@ -302,8 +306,9 @@ static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
     ALLOCCHK(ctx, ctx->n_dev.ensure(16));
 
     HIPCHK(ctx, hipEventRecord(ctx->ev[0], st));
-    const void* src_in = images;
-    if (!(flags & SGPU_INPUT_DEVICE)) {
+    const void* src_in = staged ? ctx->input.p : images;
+    if (!(flags & (SGPU_INPUT_DEVICE | SGPU_INPUT_STAGED))) {
+        ctx->staged_bytes = 0;
         ALLOCCHK(ctx, ctx->input.ensure(in_bytes));
         HIPCHK(ctx, hipMemcpyAsync(ctx->input.p, images, in_bytes, hipMemcpyHostToDevice, st));
         src_in = ctx->input.p;
@@ -477,6 +482,16 @@ int sgpu_match(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d2, int 
         }
     }
     return nmatch;
+}
+
+int sgpu_stage_input(sgpu_ctx* ctx, const uint8_t* images, int n, int w, int h, int stride) {
+    if (!ctx || !images || n <= 0 || stride < w) return SGPU_EINVAL;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const size_t bytes = (size_t)n * h * stride;
+    ALLOCCHK(ctx, ctx->input.ensure(bytes));
+    HIPCHK(ctx, hipMemcpy(ctx->input.p, images, bytes, hipMemcpyHostToDevice));
+    ctx->staged_bytes = bytes;
+    return SGPU_OK;
 }
 
 int sgpu_extract(sgpu_ctx* ctx, const uint8_t* images, int n, int w, int h, int stride,

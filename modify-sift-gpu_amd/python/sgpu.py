@@ -16,13 +16,13 @@ PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG, "lib", "libsiftgpu.so")
 
 SGPU_OK, SGPU_EINVAL, SGPU_ENODEV, SGPU_ENOMEM, SGPU_ERANGE = 0, -1, -2, -3, -4
-SGPU_INPUT_HOST, SGPU_INPUT_DEVICE = 0, 1
+SGPU_INPUT_HOST, SGPU_INPUT_DEVICE, SGPU_INPUT_STAGED = 0, 1, 2
 
 # every extern "C" symbol include/sgpu.h declares (tests check the library exports them all)
 C_API = [
     "sgpu_default_options", "sgpu_parse_args", "sgpu_ctx_create", "sgpu_ctx_destroy",
     "sgpu_ctx_set_options", "sgpu_last_error", "sgpu_device_count", "sgpu_extract",
-    "sgpu_extract_f32", "sgpu_feature_count", "sgpu_feature_total", "sgpu_copy_features",
+    "sgpu_extract_f32", "sgpu_stage_input", "sgpu_feature_count", "sgpu_feature_total", "sgpu_copy_features",
     "sgpu_device_features", "sgpu_match", "sgpu_quantize_descriptors", "sgpu_last_timing",
     "sgpu_debug_geometry", "sgpu_debug_gaussian", "sgpu_debug_candidates",
 ]
@@ -50,6 +50,7 @@ def lib():
         L.sgpu_last_error.argtypes = [vp]
         L.sgpu_last_error.restype = c.c_char_p
         L.sgpu_extract.argtypes = [vp, vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int]
+        L.sgpu_stage_input.argtypes = [vp, vp, c.c_int, c.c_int, c.c_int, c.c_int]
         L.sgpu_extract_f32.argtypes = [vp, vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int]
         L.sgpu_feature_count.argtypes = [vp, c.c_int]
         L.sgpu_feature_total.argtypes = [vp]
@@ -108,6 +109,23 @@ class SiftContext:
     def set_options(self, opts: SgpuOptions):
         self.opts = opts
         self._check(lib().sgpu_ctx_set_options(self._ctx, ctypes.byref(opts)), "set_options")
+
+    def stage(self, images: np.ndarray):
+        """Upload a u8 batch [n, h, w] once; extract_staged() then starts from HBM."""
+        a = np.ascontiguousarray(images, np.uint8)
+        if a.ndim == 2:
+            a = a[None]
+        n, h, w = a.shape
+        self._check(lib().sgpu_stage_input(self._ctx, a.ctypes.data, n, w, h, w), "stage")
+        self._staged = (n, h, w)
+        return self
+
+    def extract_staged(self):
+        n, h, w = self._staged
+        self._check(lib().sgpu_extract(self._ctx, None, n, w, h, w, SGPU_INPUT_STAGED),
+                    "sgpu_extract(staged)")
+        self.batch = n
+        return self
 
     def extract(self, images: np.ndarray | int, shape=None, device_ptr=False):
         """images: u8 [n, h, w] (or [h, w]) host array, or an int device pointer with
