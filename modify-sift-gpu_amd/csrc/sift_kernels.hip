@@ -48,23 +48,37 @@ __global__ __launch_bounds__(256) void k_gauss(const float* __restrict__ src,
     __shared__ float s_h[IN_H * HS];
 
     const int tid = threadIdx.x;
-    const int b = blockIdx.z;
-    const int x0 = blockIdx.x * GT, y0 = blockIdx.y * GT;
+    // XCD-aware tile order (cdna_hip_programming.md T1): workgroups are dealt round-robin to the
+    // 8 XCDs, so remap the linear id so that each XCD walks a contiguous run of tiles and
+    // neighbouring tiles (which share halo rows) meet in the same L2.
+    const int tiles_x = (W + GT - 1) / GT, tiles_y = (H + GT - 1) / GT;
+    const int nwg = gridDim.x;
+    int wid;
+    {
+        const int id = blockIdx.x, xcd = id & 7, q = nwg >> 3, r = nwg & 7;
+        wid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+    }
+    const int bx = wid % tiles_x, rest = wid / tiles_x;
+    const int by = rest % tiles_y, b = rest / tiles_y;
+    const int x0 = bx * GT, y0 = by * GT;
 
-    // ---- load (clamped) input tile
-    if (U8) {
-        const uint8_t* s = src8 + (long long)b * src_img_stride;
-        for (int i = tid; i < IN_H * IN_W; i += 256) {
-            int ty = i / IN_W, tx = i - ty * IN_W;
-            int gy = clampi(y0 - HALF + ty, 0, H - 1), gx = clampi(x0 - HALF + tx, 0, W - 1);
-            s_in[ty * IN_S + tx] = (float)s[(long long)gy * src_stride + gx] / 255.0f;
-        }
-    } else {
-        const float* s = src + (long long)b * src_img_stride;
-        for (int i = tid; i < IN_H * IN_W; i += 256) {
-            int ty = i / IN_W, tx = i - ty * IN_W;
-            int gy = clampi(y0 - HALF + ty, 0, H - 1), gx = clampi(x0 - HALF + tx, 0, W - 1);
-            s_in[ty * IN_S + tx] = s[(long long)gy * src_stride + gx];
+    // ---- load (clamped) input tile: each wave streams whole tile rows (coalesced)
+    {
+        const int lane = tid & 63, wave = tid >> 6;
+        if (U8) {
+            const uint8_t* s = src8 + (long long)b * src_img_stride;
+            for (int ty = wave; ty < IN_H; ty += 4) {
+                const uint8_t* row = s + (long long)clampi(y0 - HALF + ty, 0, H - 1) * src_stride;
+                for (int tx = lane; tx < IN_W; tx += 64)
+                    s_in[ty * IN_S + tx] = (float)row[clampi(x0 - HALF + tx, 0, W - 1)] / 255.0f;
+            }
+        } else {
+            const float* s = src + (long long)b * src_img_stride;
+            for (int ty = wave; ty < IN_H; ty += 4) {
+                const float* row = s + (long long)clampi(y0 - HALF + ty, 0, H - 1) * src_stride;
+                for (int tx = lane; tx < IN_W; tx += 64)
+                    s_in[ty * IN_S + tx] = row[clampi(x0 - HALF + tx, 0, W - 1)];
+            }
         }
     }
     __syncthreads();
@@ -142,7 +156,7 @@ hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
                           long long src_img_stride, float* dst, long long dst_img_stride, int w,
                           int h, const Taps& taps, int batch, float* ds, int dsw, int dsh,
                           long long ds_img_stride, hipStream_t stream) {
-    dim3 grid((w + GT - 1) / GT, (h + GT - 1) / GT, batch);
+    dim3 grid(((w + GT - 1) / GT) * ((h + GT - 1) / GT) * batch);
     if (src8)
         hipLaunchKernelGGL((k_gauss<FW, true>), grid, dim3(256), 0, stream, src, src8,
                            src_stride, src_img_stride, dst, dst_img_stride, w, h, taps, ds, dsw,
@@ -252,25 +266,36 @@ __global__ __launch_bounds__(256) void k_extrema(const float* __restrict__ pyr,
     __shared__ float s_d[ND * (ET_Y + 2) * ES];
     const OctaveDesc& od = fp.oct[o];
     const int W = od.wa, H = od.h;
-    const int b = blockIdx.z, tid = threadIdx.x;
-    const int x0 = blockIdx.x * ET_X, y0 = blockIdx.y * ET_Y;
+    const int tid = threadIdx.x;
+    // XCD-aware tile order (as k_gauss): neighbouring tiles share halo rows in one L2
+    const int tiles_x = (W + ET_X - 1) / ET_X, tiles_y = (H + ET_Y - 1) / ET_Y;
+    int wid;
+    {
+        const int nwg = gridDim.x, id = blockIdx.x, xcd = id & 7, q = nwg >> 3, r = nwg & 7;
+        wid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+    }
+    const int bx = wid % tiles_x, rest = wid / tiles_x;
+    const int by = rest % tiles_y, b = rest / tiles_y;
+    const int x0 = bx * ET_X, y0 = by * ET_Y;
     const long long npx = (long long)W * H;
     const float* g0 = pyr + od.gauss_off + (long long)b * npx;
-    for (int i = tid; i < (ET_Y + 2) * (ET_X + 2); i += 256) {
-        int ty = i / (ET_X + 2), tx = i - ty * (ET_X + 2);
-        int gy = y0 - 1 + ty, gx = x0 - 1 + tx;
-        bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
-        long long p = (long long)gy * W + gx;
-        float prev = in ? g0[p] : 0.f;
+    const int lane = tid & 63, wave = tid >> 6;
+    // each wave streams whole halo rows; the ND+1 Gaussian planes are loaded together
+    for (int ty = wave; ty < ET_Y + 2; ty += 4) {
+        const int gy = y0 - 1 + ty;
+        for (int tx = lane; tx < ET_X + 2; tx += 64) {
+            const int gx = x0 - 1 + tx;
+            const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
+            const long long p = (long long)gy * W + gx;
+            float gv[ND + 1];
 #pragma unroll
-        for (int m = 1; m <= ND; m++) {
-            float cur = in ? g0[p + m * od.level_stride] : 0.f;
-            s_d[(m - 1) * (ET_Y + 2) * ES + ty * ES + tx] = cur - prev;
-            prev = cur;
+            for (int m = 0; m <= ND; m++) gv[m] = in ? g0[p + m * od.level_stride] : 0.f;
+#pragma unroll
+            for (int m = 1; m <= ND; m++)
+                s_d[(m - 1) * (ET_Y + 2) * ES + ty * ES + tx] = gv[m] - gv[m - 1];
         }
     }
     __syncthreads();
-    const int lane = tid & 63, wave = tid >> 6;
     const int x = x0 + lane;
     for (int rr = 0; rr < 4; rr++) {
         const int ly = wave * 4 + rr;
@@ -423,18 +448,44 @@ __device__ __forceinline__ KeyOut key_at(const float* __restrict__ pyr, const Fe
 }
 
 // ------------------------------------------------------------------------------------------
-// ComputeOrientation_Kernel (ProgramCU.cu:813-977), one thread per keypoint.
-__global__ __launch_bounds__(64) void k_orientation(const float* __restrict__ pyr,
-                                                    const uint32_t* __restrict__ mask,
-                                                    const uint32_t* __restrict__ row_base,
-                                                    int total_rows,
-                                                    const uint32_t* __restrict__ n_cand_dev,
-                                                    const FeatureParams fp,
-                                                    float4* __restrict__ out4,
-                                                    int2* __restrict__ info,
-                                                    uint32_t* __restrict__ ocount) {
-    const uint32_t f = blockIdx.x * 64 + threadIdx.x;
-    if (f >= *n_cand_dev) return;
+// Quad (4-lane) broadcast of lane S through DPP quad_perm [S,S,S,S]: no LDS traffic.
+template <int S>
+__device__ __forceinline__ int qbcast(int v) {
+    return __builtin_amdgcn_mov_dpp(v, S * 0x55, 0xF, 0xF, false);
+}
+template <int S>
+__device__ __forceinline__ float qbcastf(float v) {
+    return as_float((uint32_t)qbcast<S>((int)as_uint(v)));
+}
+
+// Row-major walk of a window of ncols columns, advanced 4 samples at a time (one per quad lane).
+struct Walk {
+    int r, c;
+    __device__ __forceinline__ void init(int i, int ncols) { r = i / ncols; c = i - r * ncols; }
+    __device__ __forceinline__ void step(int ncols) {
+        c += 4;
+        while (c >= ncols) { c -= ncols; r++; }
+    }
+};
+
+// ComputeOrientation_Kernel (ProgramCU.cu:813-977).  One quad (4 lanes) per keypoint: the
+// lanes evaluate consecutive window samples (gradient, Gaussian weight, bin) in parallel and
+// every lane then applies the quad's 4 votes in the reference's (y, x) order to the keypoint's
+// 36-bin histogram in LDS, so each bin sees exactly the reference's sequence of float adds.
+__global__ __launch_bounds__(256) void k_orientation(const float* __restrict__ pyr,
+                                                     const uint32_t* __restrict__ mask,
+                                                     const uint32_t* __restrict__ row_base,
+                                                     int total_rows,
+                                                     const uint32_t* __restrict__ n_cand_dev,
+                                                     const FeatureParams fp,
+                                                     float4* __restrict__ out4,
+                                                     int2* __restrict__ info,
+                                                     uint32_t* __restrict__ ocount) {
+    __shared__ float s_vote[64 * 37];
+    const int sub = threadIdx.x & 3, slot = threadIdx.x >> 2;
+    const uint32_t f = blockIdx.x * 64 + slot;
+    if (f >= *n_cand_dev) return;                  // uniform per quad
+    float* vote_l = s_vote + slot * 37;
     const KeyLoc L = locate(f, row_base, total_rows, mask, fp);
     const KeyOut kv = key_at(pyr, fp, L);
     const OctaveDesc& od = fp.oct[L.o];
@@ -448,17 +499,18 @@ __global__ __launch_bounds__(64) void k_orientation(const float* __restrict__ py
         kz *= pow_(fp.sigma_step, kv.ds);
     }
     if (fp.keep_sign) kz *= kv.result;
-    info[f] = make_int2(L.b, L.o * fp.d + L.j);
+    if (sub == 0) info[f] = make_int2(L.b, L.o * fp.d + L.j);
     if (fp.num_orientation == 0) {
-        out4[f] = make_float4(kx, ky, kz, 0.0f);
-        ocount[f] = 1;
+        if (sub == 0) {
+            out4[f] = make_float4(kx, ky, kz, 0.0f);
+            ocount[f] = 1;
+        }
         return;
     }
     // gradient of Gaussian level 1 + j (PyramidCU.cpp:1204)
     const float* g = pyr + od.gauss_off + (long long)(1 + L.j) * od.level_stride +
                      (long long)L.b * od.wa * od.h;
     const int W = od.wa, H = od.h;
-    float vote[37];
     const float gsigma = kz * fp.gaussian_factor;
     const float win = fabs_(kz) * fp.sample_factor;
     const float dist_threshold = (float)((double)(win * win) + 0.5);
@@ -467,20 +519,40 @@ __global__ __launch_bounds__(64) void k_orientation(const float* __restrict__ py
     const float ymin = fmax_(1.5f, floor_(ky - win) + 0.5f);
     const float xmax = fmin_(W - 1.5f, floor_(kx + win) + 0.5f);
     const float ymax = fmin_(H - 1.5f, floor_(ky + win) + 0.5f);
-#pragma unroll
-    for (int i = 0; i < 36; ++i) vote[i] = 0.0f;
-    for (float y = ymin; y <= ymax; y += 1.0f) {
-        for (float x = xmin; x <= xmax; x += 1.0f) {
+    for (int i = sub; i < 36; i += 4) vote_l[i] = 0.0f;
+    const int ncols = xmax >= xmin ? (int)(xmax - xmin) + 1 : 0;
+    const int nrows = ymax >= ymin ? (int)(ymax - ymin) + 1 : 0;
+    const int total = ncols * nrows;
+    Walk wk;
+    if (total > 0) wk.init(sub, ncols);
+    for (int base = 0; base < total; base += 4) {
+        // this lane's sample: index base + sub
+        int bin = -1;
+        float weight = 0.0f;
+        if (base + sub < total) {
+            const float x = xmin + (float)wk.c, y = ymin + (float)wk.r;
             const float dx = x - kx, dy = y - ky;
             const float sq = fma_(dx, dx, dy * dy);
-            if (fp.circular && sq >= dist_threshold) continue;
-            const float2 gr = grad_at(g, W, (int)x, (int)y);
-            const float weight = gr.x * exp_(sq * factor);
-            int oidx = (int)floor_(gr.y * ten_degree_per_radius);
-            if (oidx < 0) oidx += 36;
-            vote[oidx] += weight;
+            if (!(fp.circular && sq >= dist_threshold)) {
+                const float2 gr = grad_at(g, W, (int)x, (int)y);
+                weight = gr.x * exp_(sq * factor);
+                bin = (int)floor_(gr.y * ten_degree_per_radius);
+                if (bin < 0) bin += 36;
+            }
+            wk.step(ncols);
         }
+        // apply the 4 votes in sample order (all 4 lanes do the same LDS update)
+        const int b0 = qbcast<0>(bin), b1 = qbcast<1>(bin), b2 = qbcast<2>(bin), b3 = qbcast<3>(bin);
+        const float w0 = qbcastf<0>(weight), w1 = qbcastf<1>(weight), w2 = qbcastf<2>(weight),
+                    w3 = qbcastf<3>(weight);
+        if (b0 >= 0) vote_l[b0] += w0;
+        if (b1 >= 0) vote_l[b1] += w1;
+        if (b2 >= 0) vote_l[b2] += w2;
+        if (b3 >= 0) vote_l[b3] += w3;
     }
+    float vote[37];
+#pragma unroll
+    for (int i = 0; i < 36; ++i) vote[i] = vote_l[i];
     const float one_third = (float)(1.0 / 3.0);
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
@@ -494,6 +566,7 @@ __global__ __launch_bounds__(64) void k_orientation(const float* __restrict__ py
         }
     }
     vote[36] = vote[0];
+    if (sub != 0) return;
     if (fp.num_orientation == 1) {
         int index_max = 0;
         float max_vote = vote[0];
@@ -502,8 +575,10 @@ __global__ __launch_bounds__(64) void k_orientation(const float* __restrict__ py
             index_max = vote[i] > max_vote ? i : index_max;
             max_vote = fmax_(max_vote, vote[i]);
         }
-        const float pre = vote[index_max == 0 ? 35 : index_max - 1];
-        const float next = vote[index_max + 1];
+        float pre = vote[35], next = vote[1];
+#pragma unroll
+        for (int i = 1; i < 36; ++i)
+            if (i == index_max) { pre = vote[i - 1]; next = vote[i + 1]; }
         const float off = 0.5f * ((next - pre) * (1.0f / (max_vote + max_vote - next - pre)));
         out4[f] = make_float4(kx, ky, kz, radius_per_ten_degrees * (index_max + 0.5f + off));
         ocount[f] = 1;
@@ -600,77 +675,98 @@ __global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ py
                                                     const uint32_t* __restrict__ n_feat_dev,
                                                     const FeatureParams fp,
                                                     float* __restrict__ desc) {
-    const uint32_t gt = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t e = gt >> 4;
-    const int bidx = gt & 15, ix = bidx & 3, iy = bidx >> 2;
-    const uint32_t n_feat = *n_feat_dev;
-    const bool active = e < n_feat;
+    // one wave per feature: lanes 4c..4c+3 own grid cell c (the reference's 16 threads per
+    // feature, ProgramCU.cu:1017-1021); the quad evaluates consecutive window samples in
+    // parallel and every lane applies the 4 contributions in the reference's (y, x) order, so
+    // the 9 accumulators see the reference's exact sequence of fma's.
+    const int lane = threadIdx.x & 63, cell = lane >> 2, sub = lane & 3;
+    const uint32_t e = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (e >= *n_feat_dev) return;                  // uniform per wave
+    const int ix = cell & 3, iy = cell >> 2;
     float des[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) des[i] = 0.0f;
-    if (active) {
-        const float4 key = feat[e];
-        const int2 in = feat_info[e];
-        const int o = in.y / fp.d, j = in.y - o * fp.d;
-        const OctaveDesc& od = fp.oct[o];
-        const int W = od.wa, H = od.h;
-        const float* g = pyr + od.gauss_off + (long long)(1 + j) * od.level_stride +
-                         (long long)in.x * W * H;
-        const float rpi = (float)(4.0 / 3.14159265358979323846);
-        const float spt = fabs_(key.z * fp.window_factor);
-        float s, c;
-        sincos_(key.w, &s, &c);
-        const float anglef = (double)key.w > 3.14159265358979323846
-                                 ? (float)((double)key.w - (2.0 * 3.14159265358979323846))
-                                 : key.w;
-        const float cspt = c * spt, sspt = s * spt;
-        const float crspt = c / spt, srspt = s / spt;
-        const float ox = ix - 1.5f, oy = iy - 1.5f;
-        const float ptx = fma_(cspt, ox, -(sspt * oy)) + key.x;
-        const float pty = fma_(cspt, oy, sspt * ox) + key.y;
-        const float bsz = fabs_(cspt) + fabs_(sspt);
-        const float xmin = fmax_(1.5f, floor_(ptx - bsz) + 0.5f);
-        const float ymin = fmax_(1.5f, floor_(pty - bsz) + 0.5f);
-        const float xmax = fmin_(W - 1.5f, floor_(ptx + bsz) + 0.5f);
-        const float ymax = fmin_(H - 1.5f, floor_(pty + bsz) + 0.5f);
-        for (float y = ymin; y <= ymax; y += 1.0f) {
-            for (float x = xmin; x <= xmax; x += 1.0f) {
-                const float dx = x - ptx, dy = y - pty;
-                const float nx = fma_(crspt, dx, srspt * dy);
-                const float ny = fma_(crspt, dy, -(srspt * dx));
-                const float nxn = fabs_(nx), nyn = fabs_(ny);
-                if (nxn < 1.0f && nyn < 1.0f) {
-                    const float2 cc = grad_at(g, W, (int)x, (int)y);
-                    const float dnx = nx + ox, dny = ny + oy;
-                    const float ww = exp_(-0.125f * fma_(dnx, dnx, dny * dny));
-                    const float wx = (float)(1.0 - (double)nxn), wy = (float)(1.0 - (double)nyn);
-                    const float weight = ww * wx * wy * cc.x;
-                    float theta = (anglef - cc.y) * rpi;
-                    if (theta < 0) theta += 8.0f;
-                    const float fo = floor_(theta);
-                    const int fidx = (int)fo;
-                    const float weight1 = fo + 1.0f - theta;
-                    const float weight2 = theta - fo;
+    const float4 key = feat[e];
+    const int2 in = feat_info[e];
+    const int o = in.y / fp.d, j = in.y - o * fp.d;
+    const OctaveDesc& od = fp.oct[o];
+    const int W = od.wa, H = od.h;
+    const float* g = pyr + od.gauss_off + (long long)(1 + j) * od.level_stride +
+                     (long long)in.x * W * H;
+    const float rpi = (float)(4.0 / 3.14159265358979323846);
+    const float spt = fabs_(key.z * fp.window_factor);
+    float s, c;
+    sincos_(key.w, &s, &c);
+    const float anglef = (double)key.w > 3.14159265358979323846
+                             ? (float)((double)key.w - (2.0 * 3.14159265358979323846))
+                             : key.w;
+    const float cspt = c * spt, sspt = s * spt;
+    const float crspt = c / spt, srspt = s / spt;
+    const float ox = ix - 1.5f, oy = iy - 1.5f;
+    const float ptx = fma_(cspt, ox, -(sspt * oy)) + key.x;
+    const float pty = fma_(cspt, oy, sspt * ox) + key.y;
+    const float bsz = fabs_(cspt) + fabs_(sspt);
+    const float xmin = fmax_(1.5f, floor_(ptx - bsz) + 0.5f);
+    const float ymin = fmax_(1.5f, floor_(pty - bsz) + 0.5f);
+    const float xmax = fmin_(W - 1.5f, floor_(ptx + bsz) + 0.5f);
+    const float ymax = fmin_(H - 1.5f, floor_(pty + bsz) + 0.5f);
+    const int ncols = xmax >= xmin ? (int)(xmax - xmin) + 1 : 0;
+    const int nrows = ymax >= ymin ? (int)(ymax - ymin) + 1 : 0;
+    const int total = ncols * nrows;
+    Walk wk;
+    if (total > 0) wk.init(sub, ncols);
+    for (int base = 0; base < total; base += 4) {
+        int fidx = -1;
+        float weight = 0.f, weight1 = 0.f, weight2 = 0.f;
+        if (base + sub < total) {
+            const float x = xmin + (float)wk.c, y = ymin + (float)wk.r;
+            const float dx = x - ptx, dy = y - pty;
+            const float nx = fma_(crspt, dx, srspt * dy);
+            const float ny = fma_(crspt, dy, -(srspt * dx));
+            const float nxn = fabs_(nx), nyn = fabs_(ny);
+            if (nxn < 1.0f && nyn < 1.0f) {
+                const float2 cc = grad_at(g, W, (int)x, (int)y);
+                const float dnx = nx + ox, dny = ny + oy;
+                const float ww = exp_(-0.125f * fma_(dnx, dnx, dny * dny));
+                const float wx = (float)(1.0 - (double)nxn), wy = (float)(1.0 - (double)nyn);
+                weight = ww * wx * wy * cc.x;
+                float theta = (anglef - cc.y) * rpi;
+                if (theta < 0) theta += 8.0f;
+                const float fo = floor_(theta);
+                fidx = (int)fo;
+                weight1 = fo + 1.0f - theta;
+                weight2 = theta - fo;
+            }
+            wk.step(ncols);
+        }
+        const int f4[4] = {qbcast<0>(fidx), qbcast<1>(fidx), qbcast<2>(fidx), qbcast<3>(fidx)};
+        const float w4[4] = {qbcastf<0>(weight), qbcastf<1>(weight), qbcastf<2>(weight),
+                             qbcastf<3>(weight)};
+        const float a4[4] = {qbcastf<0>(weight1), qbcastf<1>(weight1), qbcastf<2>(weight1),
+                             qbcastf<3>(weight1)};
+        const float b4[4] = {qbcastf<0>(weight2), qbcastf<1>(weight2), qbcastf<2>(weight2),
+                             qbcastf<3>(weight2)};
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        if (k == fidx) {
-                            des[k] = fma_(weight1, weight, des[k]);
-                            des[k + 1] = fma_(weight2, weight, des[k + 1]);
-                        }
-                    }
+        for (int q = 0; q < 4; q++) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (k == f4[q]) {   // fidx outside 0..7 (incl. 8 at theta == 8) adds nothing
+                    des[k] = fma_(a4[q], w4[q], des[k]);
+                    des[k + 1] = fma_(b4[q], w4[q], des[k + 1]);
                 }
             }
         }
-        des[0] += des[8];
     }
+    des[0] += des[8];
     if (fp.normalize) {
-        const int lane = threadIdx.x & 63, g0 = lane & ~15;
+        // NormalizeDescriptor_Kernel: sums over the 32 float4s in order (cells 0..15)
+        const int g0 = lane & ~63;
         float a = sq4(des[0], des[1], des[2], des[3]);
         float bq = sq4(des[4], des[5], des[6], des[7]);
         float norm1 = 0.f;
         for (int q = 0; q < 16; q++) {
-            norm1 += __shfl(a, g0 + q, 64);
-            norm1 += __shfl(bq, g0 + q, 64);
+            norm1 += __shfl(a, g0 + 4 * q, 64);
+            norm1 += __shfl(bq, g0 + 4 * q, 64);
         }
         norm1 = rsqrt_(norm1);
 #pragma unroll
@@ -679,17 +775,17 @@ __global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ py
         bq = sq4(des[4], des[5], des[6], des[7]);
         float norm2 = 0.f;
         for (int q = 0; q < 16; q++) {
-            norm2 += __shfl(a, g0 + q, 64);
-            norm2 += __shfl(bq, g0 + q, 64);
+            norm2 += __shfl(a, g0 + 4 * q, 64);
+            norm2 += __shfl(bq, g0 + 4 * q, 64);
         }
         norm2 = rsqrt_(norm2);
 #pragma unroll
         for (int i = 0; i < 8; i++) des[i] *= norm2;
     }
-    if (active) {
-        float4* dst = reinterpret_cast<float4*>(desc + (size_t)e * 128 + bidx * 8);
-        dst[0] = make_float4(des[0], des[1], des[2], des[3]);
-        dst[1] = make_float4(des[4], des[5], des[6], des[7]);
+    if (sub < 2) {
+        float4* dst = reinterpret_cast<float4*>(desc + (size_t)e * 128 + cell * 8 + sub * 4);
+        *dst = sub == 0 ? make_float4(des[0], des[1], des[2], des[3])
+                        : make_float4(des[4], des[5], des[6], des[7]);
     }
 }
 
@@ -737,7 +833,7 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
 hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
                           const FeatureParams& fp, int octave, hipStream_t stream) {
     const OctaveDesc& od = fp.oct[octave];
-    dim3 grid((od.wa + ET_X - 1) / ET_X, (od.h + ET_Y - 1) / ET_Y, fp.batch);
+    dim3 grid(((od.wa + ET_X - 1) / ET_X) * ((od.h + ET_Y - 1) / ET_Y) * fp.batch);
     switch (fp.d + 2) {
 #define SGK_EXT(ND) \
     case ND: hipLaunchKernelGGL((k_extrema<ND>), grid, dim3(256), 0, stream, pyr, mask, row_count, fp, octave); break;
@@ -782,7 +878,7 @@ hipError_t launch_orientation(const float* pyr, const uint32_t* mask, const uint
                               const FeatureParams& fp, float4* out4, int2* info,
                               uint32_t* ocount, hipStream_t stream) {
     if (n_cand_cap <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_orientation, dim3((n_cand_cap + 63) / 64), dim3(64), 0, stream, pyr,
+    hipLaunchKernelGGL(k_orientation, dim3((n_cand_cap + 63) / 64), dim3(256), 0, stream, pyr,
                        mask, row_base, total_rows, n_cand_dev, fp, out4, info, ocount);
     return hipGetLastError();
 }
@@ -800,8 +896,7 @@ hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* f
                              const uint32_t* n_feat_dev, int n_feat_cap, const FeatureParams& fp,
                              float* desc, hipStream_t stream) {
     if (n_feat_cap <= 0) return hipSuccess;
-    const long long threads = (long long)n_feat_cap * 16;
-    hipLaunchKernelGGL(k_descriptor, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(k_descriptor, dim3((unsigned)((n_feat_cap + 3) / 4)), dim3(256), 0,
                        stream, pyr, feat, feat_info, n_feat_dev, fp, desc);
     return hipGetLastError();
 }
