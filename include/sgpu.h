@@ -124,6 +124,8 @@ void sgpu_quantize_descriptors(const float* d, size_t count, uint8_t* out);
 int sgpu_last_timing(const sgpu_ctx* ctx, float* times, int n);
 
 /* ---- test hooks (parity tests read intermediate stages; not part of the drop-in surface) ---- */
+/* Select a kernel variant for in-process A/B timing (0 = shipped configuration). */
+int sgpu_debug_set_variant(int variant);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);
 /* Gaussian level (image, octave, level 0..level_num-1) as wa*h floats. */

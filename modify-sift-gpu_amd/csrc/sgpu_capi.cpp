@@ -550,6 +550,10 @@ int sgpu_last_timing(const sgpu_ctx* ctx, float* times, int n) {
     return SGPU_OK;
 }
 
+int sgpu_debug_set_variant(int variant) {
+    return sgk::set_variant(variant) == hipSuccess ? SGPU_OK : SGPU_ENODEV;
+}
+
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims, int max) {
     if (!ctx || !n_octaves) return SGPU_EINVAL;
     *n_octaves = (int)ctx->oct.size();

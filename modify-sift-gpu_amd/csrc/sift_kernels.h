@@ -13,6 +13,9 @@ constexpr int kMaxOctaves = 16;
 
 struct Taps { float k[33]; };
 
+// In-process A/B switch for kernel variants (test hook; 0 = shipped configuration).
+hipError_t set_variant(int v);
+
 // Per-octave geometry and buffer offsets used by the feature kernels.
 struct OctaveDesc {
     int w, h, wa;          // wa = padded width = row stride of every level image

@@ -24,6 +24,9 @@ namespace {
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// Kernel variant switch for in-process A/B measurements (SGPU_VARIANT env, default 0).
+__constant__ int g_variant;
+
 // ------------------------------------------------------------------------------------------
 // Gaussian level: FilterH<FW> then FilterV<FW> (ProgramCU.cu:115-222) fused in one tile.
 // Output tile 64 x 64, 256 threads.  The input tile (64+FW-1)^2 is loaded with the clamped
@@ -53,8 +56,8 @@ __global__ __launch_bounds__(256) void k_gauss(const float* __restrict__ src,
     // neighbouring tiles (which share halo rows) meet in the same L2.
     const int tiles_x = (W + GT - 1) / GT, tiles_y = (H + GT - 1) / GT;
     const int nwg = gridDim.x;
-    int wid;
-    {
+    int wid = blockIdx.x;
+    if (g_variant & 1) {
         const int id = blockIdx.x, xcd = id & 7, q = nwg >> 3, r = nwg & 7;
         wid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
     }
@@ -63,7 +66,23 @@ __global__ __launch_bounds__(256) void k_gauss(const float* __restrict__ src,
     const int x0 = bx * GT, y0 = by * GT;
 
     // ---- load (clamped) input tile: each wave streams whole tile rows (coalesced)
-    {
+    if (g_variant & 2) {
+        if (U8) {
+            const uint8_t* s = src8 + (long long)b * src_img_stride;
+            for (int i = tid; i < IN_H * IN_W; i += 256) {
+                int ty = i / IN_W, tx = i - ty * IN_W;
+                int gy = clampi(y0 - HALF + ty, 0, H - 1), gx = clampi(x0 - HALF + tx, 0, W - 1);
+                s_in[ty * IN_S + tx] = (float)s[(long long)gy * src_stride + gx] / 255.0f;
+            }
+        } else {
+            const float* s = src + (long long)b * src_img_stride;
+            for (int i = tid; i < IN_H * IN_W; i += 256) {
+                int ty = i / IN_W, tx = i - ty * IN_W;
+                int gy = clampi(y0 - HALF + ty, 0, H - 1), gx = clampi(x0 - HALF + tx, 0, W - 1);
+                s_in[ty * IN_S + tx] = s[(long long)gy * src_stride + gx];
+            }
+        }
+    } else {
         const int lane = tid & 63, wave = tid >> 6;
         if (U8) {
             const uint8_t* s = src8 + (long long)b * src_img_stride;
@@ -269,8 +288,8 @@ __global__ __launch_bounds__(256) void k_extrema(const float* __restrict__ pyr,
     const int tid = threadIdx.x;
     // XCD-aware tile order (as k_gauss): neighbouring tiles share halo rows in one L2
     const int tiles_x = (W + ET_X - 1) / ET_X, tiles_y = (H + ET_Y - 1) / ET_Y;
-    int wid;
-    {
+    int wid = blockIdx.x;
+    if (g_variant & 4) {
         const int nwg = gridDim.x, id = blockIdx.x, xcd = id & 7, q = nwg >> 3, r = nwg & 7;
         wid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
     }
@@ -813,11 +832,13 @@ __global__ __launch_bounds__(64) void k_debug_candidates(
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
+hipError_t set_variant(int v) { return hipMemcpyToSymbol(HIP_SYMBOL(g_variant), &v, sizeof(int)); }
+
 hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         long long src_img_stride, float* dst, long long dst_img_stride, int w,
                         int h, int fw, const Taps& taps, int batch, float* ds_dst, int ds_w,
                         int ds_h, long long ds_img_stride, hipStream_t stream) {
-#define SGK_GAUSS(FW)                                                                        \
+#define SGK_GAUSS(FW)                                                                       \
     case FW:                                                                                  \
         return gauss_dispatch<FW>(src, src_u8, src_stride, src_img_stride, dst, dst_img_stride, \
                                   w, h, taps, batch, ds_dst, ds_w, ds_h, ds_img_stride, stream);

@@ -25,6 +25,7 @@ C_API = [
     "sgpu_extract_f32", "sgpu_stage_input", "sgpu_feature_count", "sgpu_feature_total", "sgpu_copy_features",
     "sgpu_device_features", "sgpu_match", "sgpu_quantize_descriptors", "sgpu_last_timing",
     "sgpu_debug_geometry", "sgpu_debug_gaussian", "sgpu_debug_candidates",
+    "sgpu_debug_set_variant",
 ]
 
 _LIB = None
@@ -61,6 +62,7 @@ def lib():
                                  c.c_int, vp, c.c_int]
         L.sgpu_quantize_descriptors.argtypes = [vp, c.c_size_t, vp]
         L.sgpu_last_timing.argtypes = [vp, vp, c.c_int]
+        L.sgpu_debug_set_variant.argtypes = [c.c_int]
         L.sgpu_debug_geometry.argtypes = [vp, P(c.c_int), vp, c.c_int]
         L.sgpu_debug_gaussian.argtypes = [vp, c.c_int, c.c_int, c.c_int, vp]
         L.sgpu_debug_candidates.argtypes = [vp, vp, vp, c.c_int, P(c.c_int)]

@@ -1,0 +1,44 @@
+"""Multi-GPU batch extraction: one process per GPU, images sharded, one collective.
+
+Reference analogue: TestWin/MultiThreadSIFT.cpp:141-155 (one SiftGPU instance per device thread)
+and the per-port server processes of ServerSiftGPU (ServerSiftGPU.cpp:156-194).  Here each rank
+(torch.distributed, backend "nccl" = RCCL over xGMI on MI355X, "gloo" on CPU for tests) owns a
+contiguous shard of the batch and runs the whole hot path locally; the only exchange is one
+all-gather of the per-image feature counts, from which every rank knows the global output layout
+(image i's features start at offsets[i]).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def shard(n_total: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous shard [start, end) of n_total images for `rank` (sizes differ by <= 1)."""
+    base, extra = divmod(n_total, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def gather_counts(local_counts: np.ndarray, n_total: int, dist, device=None) -> np.ndarray:
+    """All-gather per-image feature counts of every rank's shard into the global [n_total]
+    array (one collective; shards are padded to the largest shard size)."""
+    import torch
+    world = dist.get_world_size()
+    width = max(shard(n_total, r, world)[1] - shard(n_total, r, world)[0] for r in range(world))
+    buf = torch.zeros(width, dtype=torch.int32, device=device)
+    buf[: len(local_counts)] = torch.from_numpy(np.ascontiguousarray(local_counts, np.int32))
+    out = torch.zeros(width * world, dtype=torch.int32, device=device)
+    dist.all_gather_into_tensor(out, buf)
+    out = out.cpu().numpy().reshape(world, width)
+    parts = []
+    for r in range(world):
+        s, e = shard(n_total, r, world)
+        parts.append(out[r, : e - s])
+    return np.concatenate(parts)
+
+
+def global_offsets(counts: np.ndarray) -> np.ndarray:
+    """offsets[i] = first global feature index of image i; offsets[n] = total."""
+    off = np.zeros(len(counts) + 1, np.int64)
+    np.cumsum(counts, out=off[1:])
+    return off
