@@ -26,6 +26,7 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 
 // Kernel variant switch for in-process A/B measurements (SGPU_VARIANT env, default 0).
 __constant__ int g_variant;
+int g_host_variant = 0;   // host copy: selects launch configurations
 
 // ------------------------------------------------------------------------------------------
 // Gaussian level: FilterH<FW> then FilterV<FW> (ProgramCU.cu:115-222) fused in one tile.
@@ -65,8 +66,8 @@ __global__ __launch_bounds__(256) void k_gauss(const float* __restrict__ src,
     const int by = rest % tiles_y, b = rest / tiles_y;
     const int x0 = bx * GT, y0 = by * GT;
 
-    // ---- load (clamped) input tile: each wave streams whole tile rows (coalesced)
-    if (g_variant & 2) {
+    // ---- load (clamped) input tile (bit 2 of the variant: row-streaming loader)
+    if (!(g_variant & 2)) {
         if (U8) {
             const uint8_t* s = src8 + (long long)b * src_img_stride;
             for (int i = tid; i < IN_H * IN_W; i += 256) {
@@ -170,11 +171,169 @@ __global__ __launch_bounds__(256) void k_gauss(const float* __restrict__ src,
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Gaussian level, strip-streaming form (the shipped one).  A workgroup owns a 64-column strip
+// of `rows_per_strip` output rows and walks it top to bottom in chunks of SR = 16 rows:
+//   * the input rows of chunk c+1 are loaded into registers while chunk c is filtered
+//     (register-staged prefetch, written to LDS after the next barrier), so HBM loads overlap
+//     the filter arithmetic instead of alternating with it;
+//   * the horizontal pass writes 16 filtered rows into a ring of (D+1)*16 rows in LDS,
+//     D = ceil((FW-1)/16); the vertical pass emits output chunk c-D from the ring;
+//   * every input row is read once per strip (vertical halo (FW-1)/rows_per_strip), the
+//     horizontal halo (FW-1)/64 goes through L2; ~12-25 KB of LDS, 4-6 workgroups per CU.
+// Arithmetic and clamping are exactly those of k_gauss (taps summed i = 0..FW-1 with fma).
+constexpr int SR = 16;
+
+template <int FW, bool U8>
+__global__ __launch_bounds__(256) void k_gauss_strip(
+    const float* __restrict__ src, const uint8_t* __restrict__ src8, int src_stride,
+    long long src_img_stride, float* __restrict__ dst, long long dst_img_stride, int W, int H,
+    Taps taps, float* __restrict__ ds, int dsw, int dsh, long long ds_img_stride,
+    int rows_per_strip) {
+    constexpr int HALF = FW >> 1;
+    constexpr int NV4 = (FW + 3 + 3) / 4;
+    constexpr int IN_S = 60 + 4 * NV4;               // >= 64 + FW - 1, multiple of 4
+    constexpr int D = (FW - 1 + SR - 1) / SR;        // output lag in chunks
+    constexpr int RS = (D + 1) * SR;                 // ring rows
+    constexpr int HS = GT + 1;
+    constexpr int NLD = (SR * IN_S + 255) / 256;     // staged elements per thread per chunk
+    __shared__ __attribute__((aligned(16))) float s_in[2][SR * IN_S];
+    __shared__ float s_h[RS * HS];
+
+    const int tid = threadIdx.x;
+    const int strips_x = (W + GT - 1) / GT;
+    const int strips_y = (H + rows_per_strip - 1) / rows_per_strip;
+    const int id = blockIdx.x;
+    const int sx = id % strips_x, rest = id / strips_x;
+    const int sy = rest % strips_y, b = rest / strips_y;
+    const int x0 = sx * GT;
+    const int yb = sy * rows_per_strip;
+    const int ye = min(H, yb + rows_per_strip);
+    const int nin = (ye - yb) + FW - 1;              // input rows of this strip
+    const int nchunk_in = (nin + SR - 1) / SR;
+    const int nchunk_out = (ye - yb + SR - 1) / SR;
+
+    const float* sf = U8 ? nullptr : src + (long long)b * src_img_stride;
+    const uint8_t* s8 = U8 ? src8 + (long long)b * src_img_stride : nullptr;
+    float stage[NLD];
+    auto load_chunk = [&](int c) {
+#pragma unroll
+        for (int m = 0; m < NLD; m++) {
+            const int e = tid + 256 * m;
+            const int r = e / IN_S, col = e - r * IN_S;
+            const int gy = clampi(yb - HALF + c * SR + r, 0, H - 1);
+            const int gx = clampi(x0 - HALF + col, 0, W - 1);
+            if (e < SR * IN_S) {
+                if (U8) stage[m] = (float)s8[(long long)gy * src_stride + gx] / 255.0f;
+                else stage[m] = sf[(long long)gy * src_stride + gx];
+            }
+        }
+    };
+    auto store_chunk = [&](int buf) {
+#pragma unroll
+        for (int m = 0; m < NLD; m++) {
+            const int e = tid + 256 * m;
+            if (e < SR * IN_S) s_in[buf][e] = stage[m];
+        }
+    };
+
+    float k[FW];
+#pragma unroll
+    for (int i = 0; i < FW; i++) k[i] = taps.k[i];
+
+    load_chunk(0);
+    store_chunk(0);
+    __syncthreads();
+    float* d = dst + (long long)b * dst_img_stride;
+    float* dd = ds ? ds + (long long)b * ds_img_stride : nullptr;
+    const int c0 = (tid & 15) * 4, hr = tid >> 4;     // H pass: row hr, outputs c0..c0+3
+    const int vc = tid & 63, vr = (tid >> 6) * 4;      // V pass: column vc, rows vr..vr+3
+    const int x = x0 + vc;
+    for (int c = 0; c < nchunk_out + D; c++) {
+        const bool has_in = c < nchunk_in, has_next = c + 1 < nchunk_in;
+        if (has_next) load_chunk(c + 1);
+        if (has_in) {   // H pass of input chunk c -> ring rows c*SR .. c*SR+15
+            const float4* row = reinterpret_cast<const float4*>(&s_in[c & 1][hr * IN_S + c0]);
+            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+            for (int q = 0; q < NV4; q++) {
+                const float4 v4 = row[q];
+                const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int m = q * 4 + e;
+                    const float v = vv[e];
+                    if (m < FW) a0 = fma_(v, k[m], a0);
+                    if (m >= 1 && m - 1 < FW) a1 = fma_(v, k[m - 1], a1);
+                    if (m >= 2 && m - 2 < FW) a2 = fma_(v, k[m - 2], a2);
+                    if (m >= 3 && m - 3 < FW) a3 = fma_(v, k[m - 3], a3);
+                }
+            }
+            float* o = &s_h[((c * SR + hr) % RS) * HS + c0];
+            o[0] = a0; o[1] = a1; o[2] = a2; o[3] = a3;
+        }
+        __syncthreads();
+        const int kout = c - D;
+        if (kout >= 0) {   // V pass of output chunk kout: needs ring rows kout*SR .. +SR+FW-2
+            const int t0 = kout * SR + vr;
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int m = 0; m < FW + 3; m++) {
+                const float v = s_h[((t0 + m) % RS) * HS + vc];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int i = m - j;
+                    if (i >= 0 && i < FW) acc[j] = fma_(v, k[i], acc[j]);
+                }
+            }
+            if (x < W) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int y = yb + t0 + j;
+                    if (y < ye) {
+                        d[(long long)y * W + x] = acc[j];
+                        // DownsampleKernel<1> (ProgramCU.cu:287-298) into the next octave's
+                        // level 0: dst(r, c) = src(2r, min(2c, W-1)).
+                        if (dd && !(y & 1) && (y >> 1) < dsh) {
+                            float* drow = dd + (long long)(y >> 1) * dsw;
+                            if (!(x & 1) && (x >> 1) < dsw) drow[x >> 1] = acc[j];
+                            if (x == W - 1)
+                                for (int cc = W >> 1; cc < dsw; cc++) drow[cc] = acc[j];
+                        }
+                    }
+                }
+            }
+        }
+        if (has_next) store_chunk((c + 1) & 1);
+        __syncthreads();
+    }
+}
+
 template <int FW>
 hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
                           long long src_img_stride, float* dst, long long dst_img_stride, int w,
                           int h, const Taps& taps, int batch, float* ds, int dsw, int dsh,
                           long long ds_img_stride, hipStream_t stream) {
+    if (!(g_host_variant & 8)) {
+        // strips: enough workgroups for ~8 per CU, strip height a multiple of SR
+        const int strips_x = (w + GT - 1) / GT;
+        const long long per_col = (long long)strips_x * batch;
+        int nsy = (int)std::min<long long>((2048 + per_col - 1) / per_col, (h + SR - 1) / SR);
+        nsy = std::max(nsy, 1);
+        int rows = (h + nsy - 1) / nsy;
+        rows = (rows + SR - 1) / SR * SR;
+        nsy = (h + rows - 1) / rows;
+        dim3 grid((unsigned)(strips_x * nsy * batch));
+        if (src8)
+            hipLaunchKernelGGL((k_gauss_strip<FW, true>), grid, dim3(256), 0, stream, src, src8,
+                               src_stride, src_img_stride, dst, dst_img_stride, w, h, taps, ds,
+                               dsw, dsh, ds_img_stride, rows);
+        else
+            hipLaunchKernelGGL((k_gauss_strip<FW, false>), grid, dim3(256), 0, stream, src, src8,
+                               src_stride, src_img_stride, dst, dst_img_stride, w, h, taps, ds,
+                               dsw, dsh, ds_img_stride, rows);
+        return hipGetLastError();
+    }
     dim3 grid(((w + GT - 1) / GT) * ((h + GT - 1) / GT) * batch);
     if (src8)
         hipLaunchKernelGGL((k_gauss<FW, true>), grid, dim3(256), 0, stream, src, src8,
@@ -832,7 +991,10 @@ __global__ __launch_bounds__(64) void k_debug_candidates(
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
-hipError_t set_variant(int v) { return hipMemcpyToSymbol(HIP_SYMBOL(g_variant), &v, sizeof(int)); }
+hipError_t set_variant(int v) {
+    g_host_variant = v;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_variant), &v, sizeof(int));
+}
 
 hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         long long src_img_stride, float* dst, long long dst_img_stride, int w,
