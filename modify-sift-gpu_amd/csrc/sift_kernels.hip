@@ -861,9 +861,10 @@ __global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ py
     const uint32_t e = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (e >= *n_feat_dev) return;                  // uniform per wave
     const int ix = cell & 3, iy = cell >> 2;
-    float des[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) des[i] = 0.0f;
+    // each quad lane owns two of the cell's 8 orientation bins (lane 0 also bin 8): every bin's
+    // fma chain is the reference's, and a sample costs 4 compares instead of an 8-way select
+    const int kb = 2 * sub;
+    float acc0 = 0.0f, acc1 = 0.0f, acc8 = 0.0f;
     const float4 key = feat[e];
     const int2 in = feat_info[e];
     const int o = in.y / fp.d, j = in.y - o * fp.d;
@@ -926,16 +927,22 @@ __global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ py
                              qbcastf<3>(weight2)};
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                if (k == f4[q]) {   // fidx outside 0..7 (incl. 8 at theta == 8) adds nothing
-                    des[k] = fma_(a4[q], w4[q], des[k]);
-                    des[k + 1] = fma_(b4[q], w4[q], des[k + 1]);
-                }
-            }
+            // sample q adds w1*w to bin f and w2*w to bin f+1, for f in 0..7 only (the
+            // reference's unrolled k == fidx test drops fidx == 8 at theta == 8)
+            const int f = f4[q];
+            if (f == kb) acc0 = fma_(a4[q], w4[q], acc0);
+            else if (f >= 0 && f + 1 == kb) acc0 = fma_(b4[q], w4[q], acc0);
+            if (f == kb + 1) acc1 = fma_(a4[q], w4[q], acc1);
+            else if (f == kb) acc1 = fma_(b4[q], w4[q], acc1);
+            if (f == 7) acc8 = fma_(b4[q], w4[q], acc8);
         }
     }
-    des[0] += des[8];
+    if (sub == 0) acc0 += acc8;   // des[0] += des[8]
+    float des[8];
+    des[0] = qbcastf<0>(acc0); des[1] = qbcastf<0>(acc1);
+    des[2] = qbcastf<1>(acc0); des[3] = qbcastf<1>(acc1);
+    des[4] = qbcastf<2>(acc0); des[5] = qbcastf<2>(acc1);
+    des[6] = qbcastf<3>(acc0); des[7] = qbcastf<3>(acc1);
     if (fp.normalize) {
         // NormalizeDescriptor_Kernel: sums over the 32 float4s in order (cells 0..15)
         const int g0 = lane & ~63;
