@@ -507,6 +507,100 @@ __global__ __launch_bounds__(256) void k_extrema(const float* __restrict__ pyr,
     }
 }
 
+// Extremum detection, strip-pipelined form (the shipped one): a workgroup walks a 64-column
+// strip tile by tile (64 x 16 pixels + 1-pixel halo); the ND+1 Gaussian planes of tile t+1 are
+// loaded into registers while tile t is evaluated from LDS, so HBM loads overlap the tests.
+// Same DoG arithmetic (D_m = G_m - G_{m-1}), same key_test, same mask / count outputs.
+template <int ND>
+__global__ __launch_bounds__(256) void k_extrema_strip(const float* __restrict__ pyr,
+                                                       uint32_t* __restrict__ mask,
+                                                       uint32_t* __restrict__ row_count,
+                                                       const FeatureParams fp, int o,
+                                                       int rows_per_strip) {
+    constexpr int NP = (ET_Y + 2) * (ET_X + 2);   // halo tile positions
+    constexpr int NM = (NP + 255) / 256;          // positions per thread
+    constexpr int PLANE = (ET_Y + 2) * ES;
+    __shared__ float s_d[ND * PLANE];
+    const OctaveDesc& od = fp.oct[o];
+    const int W = od.wa, H = od.h;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int strips_x = (W + ET_X - 1) / ET_X;
+    const int strips_y = (H + rows_per_strip - 1) / rows_per_strip;
+    const int sx = blockIdx.x % strips_x, rest = blockIdx.x / strips_x;
+    const int sy = rest % strips_y, b = rest / strips_y;
+    const int x0 = sx * ET_X, yb = sy * rows_per_strip, ye = min(H, yb + rows_per_strip);
+    const int ntiles = (ye - yb + ET_Y - 1) / ET_Y;
+    const long long npx = (long long)W * H;
+    const float* g0 = pyr + od.gauss_off + (long long)b * npx;
+    float stage[NM][ND + 1];
+    auto load_tile = [&](int t) {
+        const int y0 = yb + t * ET_Y;
+#pragma unroll
+        for (int m = 0; m < NM; m++) {
+            const int p = tid + 256 * m;
+            const int ty = p / (ET_X + 2), tx = p - ty * (ET_X + 2);
+            const int gy = y0 - 1 + ty, gx = x0 - 1 + tx;
+            const bool in = p < NP && gy >= 0 && gy < H && gx >= 0 && gx < W;
+            const long long q = in ? (long long)gy * W + gx : 0;
+#pragma unroll
+            for (int mm = 0; mm <= ND; mm++) stage[m][mm] = in ? g0[q + mm * od.level_stride] : 0.f;
+        }
+    };
+    auto store_tile = [&]() {
+#pragma unroll
+        for (int m = 0; m < NM; m++) {
+            const int p = tid + 256 * m;
+            if (p < NP) {
+                const int ty = p / (ET_X + 2), tx = p - ty * (ET_X + 2);
+#pragma unroll
+                for (int mm = 1; mm <= ND; mm++)
+                    s_d[(mm - 1) * PLANE + ty * ES + tx] = stage[m][mm] - stage[m][mm - 1];
+            }
+        }
+    };
+    load_tile(0);
+    store_tile();
+    __syncthreads();
+    const int x = x0 + lane;
+    for (int t = 0; t < ntiles; t++) {
+        const bool has_next = t + 1 < ntiles;
+        if (has_next) load_tile(t + 1);
+        const int y0 = yb + t * ET_Y;
+        for (int rr = 0; rr < 4; rr++) {
+            const int ly = wave * 4 + rr;
+            const int y = y0 + ly;
+            if (y >= ye) break;
+            const bool interior = x > 0 && x < W - 1 && y > 0 && y < H - 1;
+            for (int j = 0; j < ND - 2; j++) {
+                bool flag = false;
+                if (interior) {
+                    const float* base = s_d + j * PLANE + (ly + 1) * ES + (lane + 1);
+                    auto get = [&](int m, int r, int c) {
+                        return base[m * PLANE + (r - 1) * ES + (c - 1)];
+                    };
+                    flag = key_test(get, fp.t0, fp.t, fp.edge, fp.subpixel).result != 0.f;
+                }
+                const unsigned long long bal = __ballot(flag);
+                if (lane == 0) {
+                    uint32_t* mrow = mask + od.mask_off + j * od.mask_level_stride +
+                                     ((long long)b * H + y) * od.nwords;
+                    const int w0 = x0 >> 5;
+                    mrow[w0] = (uint32_t)bal;
+                    if (w0 + 1 < od.nwords) mrow[w0 + 1] = (uint32_t)(bal >> 32);
+                    const int cnt = __popcll(bal);
+                    if (cnt)
+                        atomicAdd(&row_count[(long long)b * fp.rows_per_image + fp.row_off[o] +
+                                             j * H + y],
+                                  (uint32_t)cnt);
+                }
+            }
+        }
+        __syncthreads();
+        if (has_next) store_tile();
+        __syncthreads();
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Exclusive scan (uint32), 1024 elements per block.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
@@ -1023,6 +1117,24 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
 hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
                           const FeatureParams& fp, int octave, hipStream_t stream) {
     const OctaveDesc& od = fp.oct[octave];
+    if (!(g_host_variant & 16)) {
+        const int strips_x = (od.wa + ET_X - 1) / ET_X;
+        const long long per_col = (long long)strips_x * fp.batch;
+        int nsy = (int)std::min<long long>((2048 + per_col - 1) / per_col, (od.h + ET_Y - 1) / ET_Y);
+        nsy = std::max(nsy, 1);
+        int rows = (od.h + nsy - 1) / nsy;
+        rows = (rows + ET_Y - 1) / ET_Y * ET_Y;
+        nsy = (od.h + rows - 1) / rows;
+        dim3 sgrid((unsigned)(strips_x * nsy * fp.batch));
+        switch (fp.d + 2) {
+#define SGK_EXTS(ND) \
+    case ND: hipLaunchKernelGGL((k_extrema_strip<ND>), sgrid, dim3(256), 0, stream, pyr, mask, row_count, fp, octave, rows); break;
+            SGK_EXTS(3) SGK_EXTS(4) SGK_EXTS(5) SGK_EXTS(6) SGK_EXTS(7) SGK_EXTS(8)
+            default: return hipErrorInvalidValue;
+#undef SGK_EXTS
+        }
+        return hipGetLastError();
+    }
     dim3 grid(((od.wa + ET_X - 1) / ET_X) * ((od.h + ET_Y - 1) / ET_Y) * fp.batch);
     switch (fp.d + 2) {
 #define SGK_EXT(ND) \
