@@ -194,7 +194,7 @@ __global__ __launch_bounds__(256) void k_gauss_strip(
     constexpr int NV4 = (FW + 3 + 3) / 4;
     constexpr int IN_S = 60 + 4 * NV4;               // >= 64 + FW - 1, multiple of 4
     constexpr int D = (FW - 1 + SR - 1) / SR;        // output lag in chunks
-    constexpr int RS = (D + 1) * SR;                 // ring rows
+    constexpr int RS = (D + 1) * SR <= 32 ? 32 : 64;  // ring rows (power of two >= (D+1)*SR)
     constexpr int HS = GT + 1;
     constexpr int NLD = (SR * IN_S + 255) / 256;     // staged elements per thread per chunk
     __shared__ __attribute__((aligned(16))) float s_in[2][SR * IN_S];
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void k_gauss_strip(
                     if (m >= 3 && m - 3 < FW) a3 = fma_(v, k[m - 3], a3);
                 }
             }
-            float* o = &s_h[((c * SR + hr) % RS) * HS + c0];
+            float* o = &s_h[((c * SR + hr) & (RS - 1)) * HS + c0];
             o[0] = a0; o[1] = a1; o[2] = a2; o[3] = a3;
         }
         __syncthreads();
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(256) void k_gauss_strip(
             float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int m = 0; m < FW + 3; m++) {
-                const float v = s_h[((t0 + m) % RS) * HS + vc];
+                const float v = s_h[((t0 + m) & (RS - 1)) * HS + vc];
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const int i = m - j;
@@ -531,19 +531,22 @@ __global__ __launch_bounds__(256) void k_extrema_strip(const float* __restrict__
     const int x0 = sx * ET_X, yb = sy * rows_per_strip, ye = min(H, yb + rows_per_strip);
     const int ntiles = (ye - yb + ET_Y - 1) / ET_Y;
     const long long npx = (long long)W * H;
+    const long long lstride = od.level_stride;
     const float* g0 = pyr + od.gauss_off + (long long)b * npx;
     float stage[NM][ND + 1];
+    // Loads are unconditional (coordinates clamped into the image): halo positions outside the
+    // image are only ever neighbours of non-interior pixels, whose tests are skipped, so their
+    // values do not matter -- and a branch-free load stream keeps ~30 loads in flight per lane.
     auto load_tile = [&](int t) {
         const int y0 = yb + t * ET_Y;
 #pragma unroll
         for (int m = 0; m < NM; m++) {
-            const int p = tid + 256 * m;
+            const int p = min(tid + 256 * m, NP - 1);
             const int ty = p / (ET_X + 2), tx = p - ty * (ET_X + 2);
-            const int gy = y0 - 1 + ty, gx = x0 - 1 + tx;
-            const bool in = p < NP && gy >= 0 && gy < H && gx >= 0 && gx < W;
-            const long long q = in ? (long long)gy * W + gx : 0;
+            const int gy = clampi(y0 - 1 + ty, 0, H - 1), gx = clampi(x0 - 1 + tx, 0, W - 1);
+            const float* q = g0 + (long long)gy * W + gx;
 #pragma unroll
-            for (int mm = 0; mm <= ND; mm++) stage[m][mm] = in ? g0[q + mm * od.level_stride] : 0.f;
+            for (int mm = 0; mm <= ND; mm++) stage[m][mm] = q[mm * lstride];
         }
     };
     auto store_tile = [&]() {
