@@ -351,6 +351,8 @@ static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
 
     // ---- extrema + row scan
     HIPCHK(ctx, hipMemsetAsync(ctx->row_count.p, 0, (size_t)ctx->total_rows * 4, st));
+    // the strip extremum kernel only sets the bits of accepted pixels
+    HIPCHK(ctx, hipMemsetAsync(ctx->mask.p, 0, (size_t)moff * sizeof(uint32_t), st));
     for (int o = 0; o < noct; o++)
         HIPCHK(ctx, sgk::launch_extrema(pyr, ctx->mask.as<uint32_t>(), ctx->row_count.as<uint32_t>(),
                                         fp, o, st));

@@ -521,6 +521,7 @@ __global__ __launch_bounds__(256) void k_extrema_strip(const float* __restrict__
     constexpr int NM = (NP + 255) / 256;          // positions per thread
     constexpr int PLANE = (ET_Y + 2) * ES;
     __shared__ float s_d[ND * PLANE];
+    __shared__ uint16_t s_list[4 * 4 * (ND - 2) * 64];   // per-wave candidate lists
     const OctaveDesc& od = fp.oct[o];
     const int W = od.wa, H = od.h;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -565,36 +566,74 @@ __global__ __launch_bounds__(256) void k_extrema_strip(const float* __restrict__
     store_tile();
     __syncthreads();
     const int x = x0 + lane;
+    constexpr int NJ = ND - 2;
+    uint16_t* list = s_list + wave * (4 * NJ * 64);
     for (int t = 0; t < ntiles; t++) {
         const bool has_next = t + 1 < ntiles;
         if (has_next) load_tile(t + 1);
         const int y0 = yb + t * ET_Y;
+        // (1) Branch-free pre-filter.  key_test accepts only pixels with |v| > t0 that are >= or
+        // <= all 26 neighbours (its tie rules are stricter), so "v is the max or the min of its
+        // 3x3x3 block" is a superset of its accept set.  Per plane: 3-wide row max/min of the
+        // six LDS rows this wave's four rows touch, then 3-high column max/min.
+        float vmx[ND][4], vmn[ND][4], cv[ND][4];
+#pragma unroll
+        for (int m = 0; m < ND; m++) {
+            float hmx[6], hmn[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                const float* p = s_d + m * PLANE + (wave * 4 + k) * ES + lane;
+                const float a = p[0], c = p[1], e = p[2];
+                hmx[k] = fmax_(fmax_(a, c), e);
+                hmn[k] = fmin_(fmin_(a, c), e);
+                if (k >= 1 && k <= 4) cv[m][k - 1] = c;
+            }
+#pragma unroll
+            for (int rr = 0; rr < 4; rr++) {
+                vmx[m][rr] = fmax_(fmax_(hmx[rr], hmx[rr + 1]), hmx[rr + 2]);
+                vmn[m][rr] = fmin_(fmin_(hmn[rr], hmn[rr + 1]), hmn[rr + 2]);
+            }
+        }
+        // (2) compact the candidates of this wave's 4 rows x NJ levels into its LDS list
+        int ncand = 0;
+#pragma unroll
         for (int rr = 0; rr < 4; rr++) {
-            const int ly = wave * 4 + rr;
-            const int y = y0 + ly;
-            if (y >= ye) break;
-            const bool interior = x > 0 && x < W - 1 && y > 0 && y < H - 1;
-            for (int j = 0; j < ND - 2; j++) {
-                bool flag = false;
-                if (interior) {
-                    const float* base = s_d + j * PLANE + (ly + 1) * ES + (lane + 1);
-                    auto get = [&](int m, int r, int c) {
-                        return base[m * PLANE + (r - 1) * ES + (c - 1)];
-                    };
-                    flag = key_test(get, fp.t0, fp.t, fp.edge, fp.subpixel).result != 0.f;
+            const int y = y0 + wave * 4 + rr;
+            const bool interior = x > 0 && x < W - 1 && y > 0 && y < H - 1 && y < ye;
+#pragma unroll
+            for (int j = 0; j < NJ; j++) {
+                const float v = cv[j + 1][rr];
+                const float mx = fmax_(fmax_(vmx[j][rr], vmx[j + 1][rr]), vmx[j + 2][rr]);
+                const float mn = fmin_(fmin_(vmn[j][rr], vmn[j + 1][rr]), vmn[j + 2][rr]);
+                const bool cand = interior && fabs_(v) > fp.t0 && (v >= mx || v <= mn);
+                const unsigned long long bal = __ballot(cand);
+                if (cand) {
+                    const int pos = ncand + __builtin_amdgcn_mbcnt_hi(
+                                                (uint32_t)(bal >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                    list[pos] = (uint16_t)((rr << 9) | (j << 6) | lane);
                 }
-                const unsigned long long bal = __ballot(flag);
-                if (lane == 0) {
+                ncand += __popcll(bal);
+            }
+        }
+        // (3) the exact reference test on the compacted candidates, 64 at a time; accepted
+        // ones set their mask bit (mask zeroed beforehand) and count in their row.
+        for (int c0 = 0; c0 < ncand; c0 += 64) {
+            if (c0 + lane < ncand) {
+                const int code = list[c0 + lane];
+                const int rr = code >> 9, j = (code >> 6) & 7, cl = code & 63;
+                const int ly = wave * 4 + rr;
+                const float* base = s_d + j * PLANE + (ly + 1) * ES + (cl + 1);
+                auto get = [&](int m, int r, int c) {
+                    return base[m * PLANE + (r - 1) * ES + (c - 1)];
+                };
+                if (key_test(get, fp.t0, fp.t, fp.edge, fp.subpixel).result != 0.f) {
+                    const int y = y0 + ly, xx = x0 + cl;
                     uint32_t* mrow = mask + od.mask_off + j * od.mask_level_stride +
                                      ((long long)b * H + y) * od.nwords;
-                    const int w0 = x0 >> 5;
-                    mrow[w0] = (uint32_t)bal;
-                    if (w0 + 1 < od.nwords) mrow[w0 + 1] = (uint32_t)(bal >> 32);
-                    const int cnt = __popcll(bal);
-                    if (cnt)
-                        atomicAdd(&row_count[(long long)b * fp.rows_per_image + fp.row_off[o] +
-                                             j * H + y],
-                                  (uint32_t)cnt);
+                    atomicOr(&mrow[xx >> 5], 1u << (xx & 31));
+                    atomicAdd(&row_count[(long long)b * fp.rows_per_image + fp.row_off[o] +
+                                         j * H + y], 1u);
                 }
             }
         }
@@ -1003,7 +1042,7 @@ __global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ py
             if (nxn < 1.0f && nyn < 1.0f) {
                 const float2 cc = grad_at(g, W, (int)x, (int)y);
                 const float dnx = nx + ox, dny = ny + oy;
-                const float ww = exp_(-0.125f * fma_(dnx, dnx, dny * dny));
+                const float ww = exp_mid_(-0.125f * fma_(dnx, dnx, dny * dny));   // in [-1.6, 0]
                 const float wx = (float)(1.0 - (double)nxn), wy = (float)(1.0 - (double)nyn);
                 weight = ww * wx * wy * cc.x;
                 float theta = (anglef - cc.y) * rpi;
@@ -1026,12 +1065,15 @@ __global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ py
         for (int q = 0; q < 4; q++) {
             // sample q adds w1*w to bin f and w2*w to bin f+1, for f in 0..7 only (the
             // reference's unrolled k == fidx test drops fidx == 8 at theta == 8)
+            // Branch-free: a non-matching bin adds fma(0, w, acc) = acc exactly (accumulators
+            // and weights are >= +0, and an invalid sample has w = 0).
             const int f = f4[q];
-            if (f == kb) acc0 = fma_(a4[q], w4[q], acc0);
-            else if (f >= 0 && f + 1 == kb) acc0 = fma_(b4[q], w4[q], acc0);
-            if (f == kb + 1) acc1 = fma_(a4[q], w4[q], acc1);
-            else if (f == kb) acc1 = fma_(b4[q], w4[q], acc1);
-            if (f == 7) acc8 = fma_(b4[q], w4[q], acc8);
+            const float s0 = f == kb ? a4[q] : (f + 1 == kb ? b4[q] : 0.0f);
+            const float s1 = f == kb + 1 ? a4[q] : (f == kb ? b4[q] : 0.0f);
+            const float s8 = f == 7 ? b4[q] : 0.0f;
+            acc0 = fma_(s0, w4[q], acc0);
+            acc1 = fma_(s1, w4[q], acc1);
+            acc8 = fma_(s8, w4[q], acc8);
         }
     }
     if (sub == 0) acc0 += acc8;   // des[0] += des[8]

@@ -37,11 +37,9 @@ SG_HD float exp2i_(int k) {
     return as_float(1u << (k + 149));  // subnormal power of two
 }
 
-// e^x.  Cody-Waite reduction x = k ln2 + r, |r| <= ln2/2, degree-7 Taylor in Horner form.
-SG_HD float exp_(float x) {
-    if (!(x == x)) return x;  // NaN
-    if (x > 88.7228394f) return as_float(0x7f800000u);
-    if (x < -103.972084f) return 0.0f;
+// e^x core: Cody-Waite reduction x = k ln2 + r, |r| <= ln2/2, degree-7 Taylor in Horner form.
+// Returns the polynomial; *ki = k.
+SG_HD float exp_poly_(float x, int* ki) {
     const float kLog2e = 1.44269502f;
     const float kLn2Hi = 0.693145752f;      // 12 significant bits: k * kLn2Hi exact
     const float kLn2Lo = 1.42860677e-06f;
@@ -56,11 +54,29 @@ SG_HD float exp_(float x) {
     p = fma_(p, r, 0.5f);
     p = fma_(p, r, 1.0f);
     p = fma_(p, r, 1.0f);
-    int ki = (int)k;
+    *ki = (int)k;
+    return p;
+}
+
+// e^x.
+SG_HD float exp_(float x) {
+    if (!(x == x)) return x;  // NaN
+    if (x > 88.7228394f) return as_float(0x7f800000u);
+    if (x < -103.972084f) return 0.0f;
+    int ki;
+    const float p = exp_poly_(x, &ki);
     // scale in two exact steps so that subnormal results round once.
     if (ki < -125) return (p * exp2i_(ki + 64)) * exp2i_(-64);
     if (ki > 127) return (p * exp2i_(ki - 1)) * 2.0f;
     return p * exp2i_(ki);
+}
+
+// e^x for x in [-80, 80] (the Gaussian window weights): the same bits as exp_ there, without
+// its range branches.
+SG_HD float exp_mid_(float x) {
+    int ki;
+    const float p = exp_poly_(x, &ki);
+    return p * as_float((uint32_t)(ki + 127) << 23);
 }
 
 // natural log for x > 0 (finite).  x = m 2^e with m in [sqrt(1/2), sqrt(2)), atanh series.
@@ -93,34 +109,33 @@ SG_HD float log_(float x) {
 // a^b for a > 0 (the only use is pow(sigma_step, ds), ProgramCU.cu:847).
 SG_HD float pow_(float a, float b) { return exp_(b * log_(a)); }
 
-// atan2(y, x) in (-pi, pi].  Reduce to t in [0, 1], then to |t'| <= tan(pi/8), odd Taylor series.
+// atan2(y, x) in (-pi, pi].  With a = min(|x|,|y|), b = max(|x|,|y|): t = a / b, or
+// t = (a - b) / (a + b) (angle - pi/4) when a > tan(pi/8) b, so |t| <= tan(pi/8); odd Taylor
+// series to t^19.  One division and no data-dependent branches (selects only).
 SG_HD float atan2_(float y, float x) {
     const float kPi = 3.14159265f, kPi2 = 1.57079633f, kPi4 = 0.785398163f;
-    float ax = fabs_(x), ay = fabs_(y);
-    if (!(ax == ax) || !(ay == ay)) return x + y;
-    float mx = ax > ay ? ax : ay, mn = ax > ay ? ay : ax;
-    float r;
-    if (mx == 0.0f) {
-        r = (as_uint(x) >> 31) ? kPi : 0.0f;
-    } else {
-        float t = mn / mx;
-        float base = 0.0f;
-        if (t > 0.414213562f) { t = (t - 1.0f) / (t + 1.0f); base = kPi4; }
-        float z = t * t;
-        float p = -0.0526315789f;            // -1/19
-        p = fma_(p, z, 0.0588235294f);       //  1/17
-        p = fma_(p, z, -0.0666666667f);      // -1/15
-        p = fma_(p, z, 0.0769230769f);       //  1/13
-        p = fma_(p, z, -0.0909090909f);      // -1/11
-        p = fma_(p, z, 0.111111111f);        //  1/9
-        p = fma_(p, z, -0.142857143f);       // -1/7
-        p = fma_(p, z, 0.2f);                //  1/5
-        p = fma_(p, z, -0.333333333f);       // -1/3
-        r = fma_(p * z, t, t) + base;
-        if (ay > ax) r = kPi2 - r;
-        if (as_uint(x) >> 31) r = kPi - r;
-    }
-    return (as_uint(y) >> 31) ? -r : r;
+    const float ax = fabs_(x), ay = fabs_(y);
+    const bool swap = ay > ax;
+    const float mx = swap ? ay : ax, mn = swap ? ax : ay;
+    const bool red = mn > 0.414213562f * mx;
+    const float t = (red ? mn - mx : mn) / (red ? mn + mx : mx);
+    const float z = t * t;
+    float p = -0.0526315789f;            // -1/19
+    p = fma_(p, z, 0.0588235294f);       //  1/17
+    p = fma_(p, z, -0.0666666667f);      // -1/15
+    p = fma_(p, z, 0.0769230769f);       //  1/13
+    p = fma_(p, z, -0.0909090909f);      // -1/11
+    p = fma_(p, z, 0.111111111f);        //  1/9
+    p = fma_(p, z, -0.142857143f);       // -1/7
+    p = fma_(p, z, 0.2f);                //  1/5
+    p = fma_(p, z, -0.333333333f);       // -1/3
+    float r = fma_(p * z, t, t) + (red ? kPi4 : 0.0f);
+    r = swap ? kPi2 - r : r;
+    const bool xneg = (as_uint(x) >> 31) != 0;
+    r = xneg ? kPi - r : r;
+    r = mx == 0.0f ? (xneg ? kPi : 0.0f) : r;
+    r = (as_uint(y) >> 31) ? -r : r;
+    return (ax == ax && ay == ay) ? r : x + y;
 }
 
 // sin and cos of x (|x| < 1e5), Cody-Waite with a 3-part pi/2.
