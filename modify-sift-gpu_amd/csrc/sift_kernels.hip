@@ -1027,14 +1027,50 @@ __global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ py
     const float ymax = fmin_(H - 1.5f, floor_(pty + bsz) + 0.5f);
     const int ncols = xmax >= xmin ? (int)(xmax - xmin) + 1 : 0;
     const int nrows = ymax >= ymin ? (int)(ymax - ymin) + 1 : 0;
-    const int total = ncols * nrows;
-    Walk wk;
-    if (total > 0) wk.init(sub, ncols);
-    for (int base = 0; base < total; base += 4) {
+    // The reference visits every sample of the cell's axis-aligned box and keeps those with
+    // |nx| < 1 and |ny| < 1 (the rotated square).  Only the samples it keeps contribute, so the
+    // quad walks, row by row, a column span that covers the square with one sample of margin
+    // (bounds in float; the exact test below still decides each sample) -- same samples, same
+    // (y, x) order, ~40% fewer iterations for rotated features.
+    const bool use_c = fabs_(crspt) > 1e-4f / spt, use_s = fabs_(srspt) > 1e-4f / spt;
+    const float icr = use_c ? 1.0f / crspt : 0.0f, isr = use_s ? 1.0f / srspt : 0.0f;
+    const float kInf = as_float(0x7f800000u);
+    auto row_span = [&](int r, int& lo, int& len) {
+        const float dy = (ymin + (float)r) - pty;
+        float a = -kInf, bnd = kInf;
+        if (use_c) {
+            const float p = (-1.0f - srspt * dy) * icr, q = (1.0f - srspt * dy) * icr;
+            a = fmax_(a, fmin_(p, q));
+            bnd = fmin_(bnd, fmax_(p, q));
+        }
+        if (use_s) {
+            const float p = (crspt * dy - 1.0f) * isr, q = (crspt * dy + 1.0f) * isr;
+            a = fmax_(a, fmin_(p, q));
+            bnd = fmin_(bnd, fmax_(p, q));
+        }
+        const float cl = fmax_(0.0f, ceilf(ptx + a - xmin) - 1.0f);
+        const float ch = fmin_((float)(ncols - 1), floor_(ptx + bnd - xmin) + 1.0f);
+        lo = (int)cl;
+        len = ch >= cl ? (int)ch - lo + 1 : 0;
+    };
+    // lane sub starts at sample sub of the span sequence, then advances 4 samples per step
+    int wr = 0, wc = sub, wlo = 0, wlen = 0;
+    if (nrows > 0 && ncols > 0) row_span(0, wlo, wlen);
+    else wr = nrows;
+    auto normalize = [&]() {
+        while (wr < nrows && wc >= wlen) {
+            wc -= wlen;
+            if (++wr < nrows) row_span(wr, wlo, wlen);
+        }
+    };
+    normalize();
+    for (;;) {
+        // the quad's lane 0 holds its earliest sample: the quad stops together
+        if (qbcast<0>(wr < nrows ? 1 : 0) == 0) break;
         int fidx = -1;
         float weight = 0.f, weight1 = 0.f, weight2 = 0.f;
-        if (base + sub < total) {
-            const float x = xmin + (float)wk.c, y = ymin + (float)wk.r;
+        if (wr < nrows) {
+            const float x = xmin + (float)(wlo + wc), y = ymin + (float)wr;
             const float dx = x - ptx, dy = y - pty;
             const float nx = fma_(crspt, dx, srspt * dy);
             const float ny = fma_(crspt, dy, -(srspt * dx));
@@ -1052,7 +1088,8 @@ __global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ py
                 weight1 = fo + 1.0f - theta;
                 weight2 = theta - fo;
             }
-            wk.step(ncols);
+            wc += 4;
+            normalize();
         }
         const int f4[4] = {qbcast<0>(fidx), qbcast<1>(fidx), qbcast<2>(fidx), qbcast<3>(fidx)};
         const float w4[4] = {qbcastf<0>(weight), qbcastf<1>(weight), qbcastf<2>(weight),
