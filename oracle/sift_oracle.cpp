@@ -688,6 +688,22 @@ int oracle_candidates(const uint8_t* img, int w, int h, int stride, const sgpu_o
     return n > cap ? -4 : 0;
 }
 
+// Features in octave coordinates (x, y, s, o: the descriptor's input) with their level id
+// (octave*d + j), in output order.  For the independent float64 cross-check (tests/ref_numpy.py).
+int oracle_features_oct(const uint8_t* img, int w, int h, int stride, const sgpu_options* opt,
+                        float* feat, int* level, int cap, int* n_out) {
+    sgpu_options o2 = *opt;
+    o2.descriptors = 0;
+    oracle::Result R = oracle::extract(img, w, h, stride, o2, false);
+    const int n = (int)R.feat_level.size();
+    for (int i = 0; i < n && i < cap; i++) {
+        memcpy(feat + 4 * i, &R.feat_oct[4 * (size_t)i], 4 * sizeof(float));
+        level[i] = R.feat_level[i];
+    }
+    *n_out = n;
+    return n > cap ? -4 : 0;
+}
+
 int oracle_match(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float distmax,
                  float ratiomax, int mbm, int max_match, int* out_pairs) {
     std::vector<int> m = oracle::match(d1, n1, d2, n2, distmax, ratiomax, mbm, max_match);

@@ -4,7 +4,8 @@
 // GetSiftMatch), written against include/SiftGPU.h.  Used by the GPU tests: the reference file
 // itself does not exist on the GPU box.
 //   usage: simple_sift_replica <libsiftgpu.so> <img1.pgm> <img2.pgm> <out1.sift> <out2.sift>
-// Prints "num1 num2 num_match" on success.
+// Prints "RESULT num1 num2 num_match" and one "PAIR i j" line per match on success (the
+// library's own -v 1 progress text goes to the same stdout).
 #include <dlfcn.h>
 
 #include <cstdio>
@@ -48,8 +49,8 @@ int main(int argc, char** argv) {
     matcher->SetDescriptors(1, num2, &descriptors2[0]);
     int(*match_buf)[2] = new int[num1][2];
     int num_match = matcher->GetSiftMatch(num1, match_buf);
-    printf("%d %d %d\n", num1, num2, num_match);
-    for (int i = 0; i < num_match; ++i) printf("%d %d\n", match_buf[i][0], match_buf[i][1]);
+    printf("RESULT %d %d %d\n", num1, num2, num_match);
+    for (int i = 0; i < num_match; ++i) printf("PAIR %d %d\n", match_buf[i][0], match_buf[i][1]);
     delete[] match_buf;
     delete sift;
     delete matcher;

@@ -33,6 +33,9 @@ def lib():
         L.oracle_candidates.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         P(SgpuOptions), ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_int, P(ctypes.c_int)]
+        L.oracle_features_oct.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, P(SgpuOptions), ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_int, P(ctypes.c_int)]
         L.oracle_match.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                    ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_void_p]
@@ -101,6 +104,20 @@ def candidates(img, opts=None):
     lib().oracle_candidates(p, w, h, w, ctypes.byref(opts), ints.ctypes.data, fl.ctypes.data,
                             n.value, ctypes.byref(n))
     return ints[:n.value], fl[:n.value]
+
+
+def features_oct(img, opts=None):
+    """Features in octave coordinates [n, 4] (x, y, s, o) and their level ids (octave*d + j)."""
+    opts = opts or default_options()
+    img, p = _img(img)
+    h, w = img.shape
+    n = ctypes.c_int(0)
+    lib().oracle_features_oct(p, w, h, w, ctypes.byref(opts), None, None, 0, ctypes.byref(n))
+    feat = np.zeros((max(n.value, 1), 4), np.float32)
+    lvl = np.zeros(max(n.value, 1), np.int32)
+    lib().oracle_features_oct(p, w, h, w, ctypes.byref(opts), feat.ctypes.data, lvl.ctypes.data,
+                              n.value, ctypes.byref(n))
+    return feat[:n.value], lvl[:n.value]
 
 
 def match(d1: np.ndarray, d2: np.ndarray, distmax=0.7, ratiomax=0.8, mbm=1, max_match=None):
