@@ -119,11 +119,13 @@ def main():
         dist.all_reduce(f)
         feats = int(f.item())
 
+    n_gauss = 1 + args.octaves * 5                      # level 0 of octave 0 + 5 levels/octave
     total_images = B * world * args.steps
     sumN = geometry_sum(W, H, args.octaves)
     pyr_bytes = 48.0 * sumN * B * args.steps          # 48 B per pyramid px
     achieved = pyr_bytes / (pyr_ms * 1e-3) / 1e9 if pyr_ms > 0 else 0.0
 
+    traffic, prof_note = profiled_traffic(B, W, H, args.octaves)
     result = {
         "metric": "SIFT images/sec at 1080p (features/sec alongside), 1/2/4/8 MI355X",
         "value": total_images / elapsed,
@@ -147,14 +149,18 @@ def main():
         "features_per_image": local_feats / (B * args.steps),
         "stage_ms_per_step": {k: v / args.steps for k, v in stage_acc.items() if k != "match"},
         "roofline": {
-            "kernel": "k_gauss (fused separable Gaussian level, all 21 launches of a step)",
+            "kernel": f"k_gauss_strip (separable Gaussian level; all {n_gauss} launches of a step, "
+                      "HIP events around them on the library's stream)",
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
-            "algorithmic_bytes_per_step": 48.0 * sumN * B,
+            "traffic": traffic,
+            "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE + WRITE_SIZE)",
+            "traffic_source": prof_note,
+            "algorithmic_bytes_per_launch": 48.0 * sumN * B / n_gauss,
+            "avg_launch_ms": pyr_ms / args.steps / n_gauss,
         },
     }
 
@@ -167,6 +173,25 @@ def main():
     if dist is not None:
         dist.destroy_process_group()
     ctx.close()
+
+
+def profiled_traffic(B, W, H, octaves):
+    """HBM bytes per Gaussian launch from the committed rocprofv3 summary of this workload
+    (tests/profile_kernels.sh + tests/pmc_summary.py), or None when no summary matches."""
+    import glob
+    if (B, W, H, octaves) != (128, 1920, 1080, 4):
+        return None, "no profile for this workload"
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")))
+    for path in reversed(files):
+        try:
+            s = json.load(open(path))
+            fam = "k_gauss_strip"
+            n = s["launches_per_extract"][fam]
+            b = s["fetch_bytes_per_extract"][fam] + s["write_bytes_per_extract"][fam]
+            return b / n, os.path.relpath(path, ROOT)
+        except (KeyError, ValueError, OSError):
+            continue
+    return None, "no profile summary committed"
 
 
 def bench_match(ctx, n):
@@ -189,14 +214,15 @@ def bench_match(ctx, n):
 
 def cpu_baseline(imgs, opts):
     """The CPU oracle (oracle/, a C++ restatement of the reference) on a bounded sample of the
-    same workload, one image per thread."""
+    same workload: one staged image per OpenMP thread (about 1 s of wall time, 15-20 s of CPU
+    work on 16 threads)."""
     import oracle_py
-    n = 4
-    threads = min(4, os.cpu_count() or 1)
+    threads = max(1, min(16, os.cpu_count() or 1, len(imgs)))
+    n = threads
     secs, feats = oracle_py.bench_extract(imgs[:n], opts, threads=threads)
     return {"value": n / secs, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} of the staged 1920x1080 images, -no 4, oracle/liboracle.so "
-                      f"(g++ -O2), {threads} OpenMP threads, one image per thread",
+            "sample": f"{n} of the staged 1920x1080 images (-fo 0 -no 4 -d 3), one per OpenMP "
+                      f"thread, oracle/liboracle.so (g++ -O3, strict IEEE)",
             "features_per_image": feats / n}
 
 

@@ -120,7 +120,8 @@ void sgpu_quantize_descriptors(const float* d, size_t count, uint8_t* out);
 
 /* Timing of the last call: stage times in milliseconds measured with HIP events
  * (SiftGPU::_timing, SiftPyramid.cpp:48-56).  times[0..7] =
- * {upload, pyramid, detect, orientation, expand, descriptor, download, total}. */
+ * {upload, pyramid, detect, orientation, expand, descriptor, download, total} of the last
+ * extract; times[8] = the last sgpu_match call. */
 int sgpu_last_timing(const sgpu_ctx* ctx, float* times, int n);
 
 /* ---- test hooks (parity tests read intermediate stages; not part of the drop-in surface) ---- */
