@@ -28,8 +28,8 @@ def _one(pattern):
 
 
 def family(name):
-    base = name.split("(")[0].replace("void ", "").replace("sgk::(anonymous namespace)::", "")
-    return base.split("<")[0]
+    base = name.replace("void ", "").replace("sgk::(anonymous namespace)::", "")
+    return base.split("(")[0].split("<")[0]
 
 
 def main():
