@@ -24,7 +24,10 @@ namespace {
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-// Kernel variant switch for in-process A/B measurements (SGPU_VARIANT env, default 0).
+// Kernel variant switch for in-process A/B measurements (sgpu_debug_set_variant; 0 = shipped).
+// Bits: 1 XCD remap in the tile Gaussian, 2 row-streaming loader in the tile Gaussian, 4 XCD
+// remap in the tile extremum kernel, 8 tile Gaussian instead of strips, 16 tile extremum kernel
+// instead of strips, 32 scalar-FMA strip Gaussian instead of the packed one.
 __constant__ int g_variant;
 int g_host_variant = 0;   // host copy: selects launch configurations
 
@@ -309,6 +312,157 @@ __global__ __launch_bounds__(256) void k_gauss_strip(
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Gaussian level, strip-streaming with packed FP32 (the shipped form).  Same strip walk,
+// register-staged prefetch and LDS ring as k_gauss_strip, but every FMA is a v_pk_fma_f32 on
+// two independent outputs, which halves the VALU issue of the filter (gfx950 runs packed FP32 at
+// twice the scalar rate):
+//   * the input chunk is stored in LDS as row PAIRS, s_in[pair][col] = (row 2p, row 2p+1), so
+//     the H pass of a thread (rows 2p, 2p+1; columns c, c+1) reads two float2 per ds_read_b128
+//     and issues pk_fma((in[2p][c+k], in[2p+1][c+k]), k[k], acc_c) -- 2*FW packed FMAs for 4
+//     outputs;
+//   * the V pass of a thread (columns c, c+1; rows r, r+1) reads float2 ring rows and issues
+//     pk_fma((h[r+k][c], h[r+k][c+1]), k[k], acc_r) -- again 2*FW for 4 outputs, and its stores
+//     are float2.
+// Each packed lane is an IEEE fma: the sums are bit-identical to k_gauss / the oracle.
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2v pk_fma(f2v a, float b, f2v c) {
+    return __builtin_elementwise_fma(a, f2v{b, b}, c);
+}
+
+// p / 255.0f for an integer p in [0, 255] (GLTexImage.cpp:818: the reference's u8 -> float),
+// correctly rounded without a division: q = p * (1/255) then one fma residual correction.  Exact
+// for all 256 inputs (tests/test_oracle.py::test_u8_scale_is_exact_division).
+__device__ __forceinline__ float u8_to_unit(uint32_t p) {
+    const float x = (float)p, c = 1.0f / 255.0f;
+    const float q = x * c;
+    return fma_(fma_(-q, 255.0f, x), c, q);
+}
+
+template <int FW, bool U8>
+__global__ __launch_bounds__(256) void k_gauss_pk(
+    const float* __restrict__ src, const uint8_t* __restrict__ src8, int src_stride,
+    long long src_img_stride, float* __restrict__ dst, long long dst_img_stride, int W, int H,
+    Taps taps, float* __restrict__ ds, int dsw, int dsh, long long ds_img_stride,
+    int rows_per_strip) {
+    constexpr int HALF = FW >> 1;
+    constexpr int IN_W = GT + FW - 1;                 // input columns of a strip
+    constexpr int NRD = (FW + 1) / 2;                 // ds_read_b128 per H-pass thread
+    constexpr int IN_S = (GT + FW + 1 + 3) & ~3;      // float2 per row pair (>= 64 + FW + 1)
+    constexpr int D = (FW - 1 + SR - 1) / SR;         // output lag in chunks
+    constexpr int RS = (D + 1) * SR <= 32 ? 32 : 64;  // ring rows (power of two)
+    constexpr int HS = GT + 4;                        // ring row stride (floats)
+    constexpr int NLD = ((SR / 2) * IN_W + 255) / 256;   // staged row-pair elements per thread
+    __shared__ __attribute__((aligned(16))) f2v s_in[2][(SR / 2) * IN_S];
+    __shared__ __attribute__((aligned(16))) float s_h[RS * HS];
+
+    const int tid = threadIdx.x;
+    const int strips_x = (W + GT - 1) / GT;
+    const int strips_y = (H + rows_per_strip - 1) / rows_per_strip;
+    const int id = blockIdx.x;
+    const int sx = id % strips_x, rest = id / strips_x;
+    const int sy = rest % strips_y, b = rest / strips_y;
+    const int x0 = sx * GT;
+    const int yb = sy * rows_per_strip;
+    const int ye = min(H, yb + rows_per_strip);
+    const int nin = (ye - yb) + FW - 1;
+    const int nchunk_in = (nin + SR - 1) / SR;
+    const int nchunk_out = (ye - yb + SR - 1) / SR;
+
+    const float* sf = U8 ? nullptr : src + (long long)b * src_img_stride;
+    const uint8_t* s8 = U8 ? src8 + (long long)b * src_img_stride : nullptr;
+    f2v stage[NLD];
+    auto load_chunk = [&](int c) {
+#pragma unroll
+        for (int m = 0; m < NLD; m++) {
+            const int e = min(tid + 256 * m, (SR / 2) * IN_W - 1);
+            const int p = e / IN_W, col = e - p * IN_W;
+            const int gy0 = clampi(yb - HALF + c * SR + 2 * p, 0, H - 1);
+            const int gy1 = clampi(yb - HALF + c * SR + 2 * p + 1, 0, H - 1);
+            const int gx = clampi(x0 - HALF + col, 0, W - 1);
+            if (U8) {
+                stage[m] = f2v{u8_to_unit(s8[(long long)gy0 * src_stride + gx]),
+                               u8_to_unit(s8[(long long)gy1 * src_stride + gx])};
+            } else {
+                stage[m] = f2v{sf[(long long)gy0 * src_stride + gx],
+                               sf[(long long)gy1 * src_stride + gx]};
+            }
+        }
+    };
+    auto store_chunk = [&](int buf) {
+#pragma unroll
+        for (int m = 0; m < NLD; m++) {
+            const int e = tid + 256 * m;
+            if (e < (SR / 2) * IN_W) {
+                const int p = e / IN_W, col = e - p * IN_W;
+                s_in[buf][p * IN_S + col] = stage[m];
+            }
+        }
+    };
+
+    load_chunk(0);
+    store_chunk(0);
+    __syncthreads();
+    float* d = dst + (long long)b * dst_img_stride;
+    float* dd = ds ? ds + (long long)b * ds_img_stride : nullptr;
+    const int pr = tid >> 5, pc = (tid & 31) * 2;     // rows 2pr, 2pr+1; columns pc, pc+1
+    const int x = x0 + pc;
+    for (int c = 0; c < nchunk_out + D; c++) {
+        const bool has_in = c < nchunk_in, has_next = c + 1 < nchunk_in;
+        if (has_next) load_chunk(c + 1);
+        if (has_in) {   // H pass of input chunk c -> ring rows c*SR .. c*SR+15
+            const float4* row = reinterpret_cast<const float4*>(&s_in[c & 1][pr * IN_S + pc]);
+            f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};   // column pc / pc+1, (row 2pr, row 2pr+1)
+#pragma unroll
+            for (int q = 0; q < NRD; q++) {
+                const float4 v = row[q];             // pair columns pc+2q, pc+2q+1
+                const f2v e0 = {v.x, v.y}, e1 = {v.z, v.w};
+                const int m0 = 2 * q, m1 = 2 * q + 1;
+                if (m0 < FW) a0 = pk_fma(e0, taps.k[m0], a0);
+                if (m0 >= 1 && m0 - 1 < FW) a1 = pk_fma(e0, taps.k[m0 - 1], a1);
+                if (m1 < FW) a0 = pk_fma(e1, taps.k[m1], a0);
+                if (m1 - 1 < FW) a1 = pk_fma(e1, taps.k[m1 - 1], a1);
+            }
+            const int r0 = (c * SR + 2 * pr) & (RS - 1);
+            *reinterpret_cast<f2v*>(&s_h[r0 * HS + pc]) = f2v{a0.x, a1.x};
+            *reinterpret_cast<f2v*>(&s_h[(r0 + 1) * HS + pc]) = f2v{a0.y, a1.y};
+        }
+        __syncthreads();
+        const int kout = c - D;
+        if (kout >= 0) {   // V pass of output chunk kout
+            const int t0 = kout * SR + 2 * pr;
+            f2v acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};   // row t0 / t0+1, (col pc, col pc+1)
+#pragma unroll
+            for (int m = 0; m <= FW; m++) {
+                const f2v v = *reinterpret_cast<const f2v*>(&s_h[((t0 + m) & (RS - 1)) * HS + pc]);
+                if (m < FW) acc0 = pk_fma(v, taps.k[m], acc0);
+                if (m >= 1) acc1 = pk_fma(v, taps.k[m - 1], acc1);
+            }
+            if (x < W) {
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    const int y = yb + t0 + j;
+                    const f2v a = j ? acc1 : acc0;
+                    if (y < ye) {
+                        *reinterpret_cast<f2v*>(&d[(long long)y * W + x]) = a;
+                        // DownsampleKernel<1> (ProgramCU.cu:287-298) into the next octave's
+                        // level 0: dst(r, c) = src(2r, min(2c, W-1)); x is even, W is even.
+                        if (dd && !(y & 1) && (y >> 1) < dsh) {
+                            float* drow = dd + (long long)(y >> 1) * dsw;
+                            if ((x >> 1) < dsw) drow[x >> 1] = a.x;
+                            if (x + 1 == W - 1)
+                                for (int cc = W >> 1; cc < dsw; cc++) drow[cc] = a.y;
+                        }
+                    }
+                }
+            }
+        }
+        if (has_next) store_chunk((c + 1) & 1);
+        __syncthreads();
+    }
+}
+
 template <int FW>
 hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
                           long long src_img_stride, float* dst, long long dst_img_stride, int w,
@@ -324,6 +478,17 @@ hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
         rows = (rows + SR - 1) / SR * SR;
         nsy = (h + rows - 1) / rows;
         dim3 grid((unsigned)(strips_x * nsy * batch));
+        if (!(g_host_variant & 32)) {
+            if (src8)
+                hipLaunchKernelGGL((k_gauss_pk<FW, true>), grid, dim3(256), 0, stream, src, src8,
+                                   src_stride, src_img_stride, dst, dst_img_stride, w, h, taps,
+                                   ds, dsw, dsh, ds_img_stride, rows);
+            else
+                hipLaunchKernelGGL((k_gauss_pk<FW, false>), grid, dim3(256), 0, stream, src,
+                                   src8, src_stride, src_img_stride, dst, dst_img_stride, w, h,
+                                   taps, ds, dsw, dsh, ds_img_stride, rows);
+            return hipGetLastError();
+        }
         if (src8)
             hipLaunchKernelGGL((k_gauss_strip<FW, true>), grid, dim3(256), 0, stream, src, src8,
                                src_stride, src_img_stride, dst, dst_img_stride, w, h, taps, ds,

@@ -170,3 +170,29 @@ def test_golden_fixtures():
         np.testing.assert_array_equal(d, z["desc"], err_msg=f)
     z = np.load(os.path.join(GOLDEN, "match_small.npz"))
     np.testing.assert_array_equal(O.match(z["q1"], z["q2"]), z["pairs"])
+
+
+def _round_f32(fr):
+    """Round an exact rational to the nearest float32 (ties to even)."""
+    from fractions import Fraction
+    c = np.float32(float(fr))
+    best = None
+    for cand in (np.nextafter(c, np.float32(-np.inf)), c, np.nextafter(c, np.float32(np.inf))):
+        err = abs(Fraction(float(cand)) - fr)
+        key = (err, int(cand.view(np.uint32)) & 1)
+        if best is None or key < best[0]:
+            best = (key, cand)
+    return best[1]
+
+
+def test_u8_scale_is_exact_division():
+    """The Gaussian kernel's u8 ingest computes p/255.0f as q = p*(1/255), q + fma(fma(-q, 255,
+    p), 1/255, q) (sift_kernels.hip u8_to_unit); exhaustively equal to the IEEE quotient."""
+    from fractions import Fraction
+    c = np.float32(1.0) / np.float32(255.0)
+    for p in range(256):
+        x = np.float32(p)
+        q = np.float32(x * c)
+        r = _round_f32(-Fraction(float(q)) * 255 + Fraction(float(x)))
+        q2 = _round_f32(Fraction(float(r)) * Fraction(float(c)) + Fraction(float(q)))
+        assert q2 == np.float32(x / np.float32(255.0)), p
