@@ -27,7 +27,8 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 // Kernel variant switch for in-process A/B measurements (sgpu_debug_set_variant; 0 = shipped).
 // Bits: 1 XCD remap in the tile Gaussian, 2 row-streaming loader in the tile Gaussian, 4 XCD
 // remap in the tile extremum kernel, 8 tile Gaussian instead of strips, 16 tile extremum kernel
-// instead of strips, 32 scalar-FMA strip Gaussian instead of the packed one.
+// instead of strips, 32 scalar-FMA strip Gaussian instead of the packed one, 64 16-row packed
+// strip Gaussian (k_gauss_pk) instead of the 32-row one (k_gauss_pk2).
 __constant__ int g_variant;
 int g_host_variant = 0;   // host copy: selects launch configurations
 
@@ -372,8 +373,9 @@ __global__ __launch_bounds__(256) void k_gauss_pk(
 
     const float* sf = U8 ? nullptr : src + (long long)b * src_img_stride;
     const uint8_t* s8 = U8 ? src8 + (long long)b * src_img_stride : nullptr;
-    f2v stage[NLD];
-    auto load_chunk = [&](int c) {
+    // two register stages: chunk c+1 waits in one while chunk c+2 is in flight in the other
+    f2v stA[NLD], stB[NLD];
+    auto load_chunk = [&](f2v (&stage)[NLD], int c) {
 #pragma unroll
         for (int m = 0; m < NLD; m++) {
             const int e = min(tid + 256 * m, (SR / 2) * IN_W - 1);
@@ -390,7 +392,7 @@ __global__ __launch_bounds__(256) void k_gauss_pk(
             }
         }
     };
-    auto store_chunk = [&](int buf) {
+    auto store_chunk = [&](const f2v (&stage)[NLD], int buf) {
 #pragma unroll
         for (int m = 0; m < NLD; m++) {
             const int e = tid + 256 * m;
@@ -401,16 +403,18 @@ __global__ __launch_bounds__(256) void k_gauss_pk(
         }
     };
 
-    load_chunk(0);
-    store_chunk(0);
+    load_chunk(stA, 0);
+    store_chunk(stA, 0);
+    if (1 < nchunk_in) load_chunk(stA, 1);
     __syncthreads();
     float* d = dst + (long long)b * dst_img_stride;
     float* dd = ds ? ds + (long long)b * ds_img_stride : nullptr;
     const int pr = tid >> 5, pc = (tid & 31) * 2;     // rows 2pr, 2pr+1; columns pc, pc+1
     const int x = x0 + pc;
-    for (int c = 0; c < nchunk_out + D; c++) {
+    // iteration c: chunk c is in LDS, chunk c+1 in `cur` registers; load chunk c+2 into `nxt`
+    auto step = [&](int c, f2v (&cur)[NLD], f2v (&nxt)[NLD]) {
         const bool has_in = c < nchunk_in, has_next = c + 1 < nchunk_in;
-        if (has_next) load_chunk(c + 1);
+        if (c + 2 < nchunk_in) load_chunk(nxt, c + 2);
         if (has_in) {   // H pass of input chunk c -> ring rows c*SR .. c*SR+15
             const float4* row = reinterpret_cast<const float4*>(&s_in[c & 1][pr * IN_S + pc]);
             f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};   // column pc / pc+1, (row 2pr, row 2pr+1)
@@ -458,8 +462,153 @@ __global__ __launch_bounds__(256) void k_gauss_pk(
                 }
             }
         }
-        if (has_next) store_chunk((c + 1) & 1);
+        if (has_next) store_chunk(cur, (c + 1) & 1);
         __syncthreads();
+    };
+    const int nsteps = nchunk_out + D;
+    for (int c = 0; c < nsteps; c += 2) {
+        step(c, stA, stB);
+        if (c + 1 < nsteps) step(c + 1, stB, stA);
+    }
+}
+
+// k_gauss_pk with 32-row chunks and 8 outputs per thread per pass (the shipped form).  A
+// thread's H pass covers 2 rows x 4 columns and its V pass 4 rows x 2 columns, so every value
+// read from LDS feeds 4 (instead of 2) packed FMAs: LDS traffic per output is halved and stays
+// below the FMA issue time even at FW = 25.  One s_in buffer suffices: the next chunk is
+// written after the V pass, when the H pass has finished reading.
+constexpr int SR2 = 32;
+
+template <int FW, bool U8>
+__global__ __launch_bounds__(256) void k_gauss_pk2(
+    const float* __restrict__ src, const uint8_t* __restrict__ src8, int src_stride,
+    long long src_img_stride, float* __restrict__ dst, long long dst_img_stride, int W, int H,
+    Taps taps, float* __restrict__ ds, int dsw, int dsh, long long ds_img_stride,
+    int rows_per_strip) {
+    constexpr int HALF = FW >> 1;
+    constexpr int IN_W = GT + FW - 1;                 // input columns of a strip
+    constexpr int NRD = (FW + 3) / 2;                 // ds_read_b128 per H-pass thread
+    constexpr int IN_S = (GT + FW + 3 + 3) & ~3;      // float2 per row pair (>= 64 + FW + 3)
+    constexpr int RS = 64;                            // ring rows: (1 + 1) * 32 for FW <= 33
+    constexpr int HS = GT + 4;                        // ring row stride (floats)
+    constexpr int NLD = ((SR2 / 2) * IN_W + 255) / 256;
+    static_assert(FW - 1 <= SR2, "ring holds one chunk of lag");
+    __shared__ __attribute__((aligned(16))) f2v s_in[(SR2 / 2) * IN_S];
+    __shared__ __attribute__((aligned(16))) float s_h[RS * HS];
+
+    const int tid = threadIdx.x;
+    const int strips_x = (W + GT - 1) / GT;
+    const int strips_y = (H + rows_per_strip - 1) / rows_per_strip;
+    const int id = blockIdx.x;
+    const int sx = id % strips_x, rest = id / strips_x;
+    const int sy = rest % strips_y, b = rest / strips_y;
+    const int x0 = sx * GT;
+    const int yb = sy * rows_per_strip;
+    const int ye = min(H, yb + rows_per_strip);
+    const int nin = (ye - yb) + FW - 1;
+    const int nchunk_in = (nin + SR2 - 1) / SR2;
+    const int nchunk_out = (ye - yb + SR2 - 1) / SR2;
+
+    const float* sf = U8 ? nullptr : src + (long long)b * src_img_stride;
+    const uint8_t* s8 = U8 ? src8 + (long long)b * src_img_stride : nullptr;
+    f2v stA[NLD], stB[NLD];
+    auto load_chunk = [&](f2v (&stage)[NLD], int c) {
+#pragma unroll
+        for (int m = 0; m < NLD; m++) {
+            const int e = min(tid + 256 * m, (SR2 / 2) * IN_W - 1);
+            const int p = e / IN_W, col = e - p * IN_W;
+            const int gy0 = clampi(yb - HALF + c * SR2 + 2 * p, 0, H - 1);
+            const int gy1 = clampi(yb - HALF + c * SR2 + 2 * p + 1, 0, H - 1);
+            const int gx = clampi(x0 - HALF + col, 0, W - 1);
+            if (U8) {
+                stage[m] = f2v{u8_to_unit(s8[(long long)gy0 * src_stride + gx]),
+                               u8_to_unit(s8[(long long)gy1 * src_stride + gx])};
+            } else {
+                stage[m] = f2v{sf[(long long)gy0 * src_stride + gx],
+                               sf[(long long)gy1 * src_stride + gx]};
+            }
+        }
+    };
+    auto store_chunk = [&](const f2v (&stage)[NLD]) {
+#pragma unroll
+        for (int m = 0; m < NLD; m++) {
+            const int e = tid + 256 * m;
+            if (e < (SR2 / 2) * IN_W) {
+                const int p = e / IN_W, col = e - p * IN_W;
+                s_in[p * IN_S + col] = stage[m];
+            }
+        }
+    };
+
+    load_chunk(stA, 0);
+    store_chunk(stA);
+    if (1 < nchunk_in) load_chunk(stA, 1);
+    __syncthreads();
+    float* d = dst + (long long)b * dst_img_stride;
+    float* dd = ds ? ds + (long long)b * ds_img_stride : nullptr;
+    const int hp = tid >> 4, hc = (tid & 15) * 4;     // H pass: rows 2hp, 2hp+1; columns hc..hc+3
+    const int vq = tid >> 5, vc = (tid & 31) * 2;     // V pass: rows 4vq..4vq+3; columns vc, vc+1
+    const int x = x0 + vc;
+    // iteration c: chunk c is in LDS, chunk c+1 in `cur` registers; load chunk c+2 into `nxt`
+    auto step = [&](int c, f2v (&cur)[NLD], f2v (&nxt)[NLD]) {
+        const bool has_in = c < nchunk_in, has_next = c + 1 < nchunk_in;
+        if (c + 2 < nchunk_in) load_chunk(nxt, c + 2);
+        if (has_in) {   // H pass of input chunk c -> ring rows c*SR2 .. c*SR2+31
+            const float4* row = reinterpret_cast<const float4*>(&s_in[hp * IN_S + hc]);
+            f2v a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};   // columns hc+i
+#pragma unroll
+            for (int q = 0; q < NRD; q++) {
+                const float4 v = row[q];             // pair columns hc+2q, hc+2q+1
+                const f2v e[2] = {{v.x, v.y}, {v.z, v.w}};
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const int m = 2 * q + u;
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        if (m - i >= 0 && m - i < FW) a[i] = pk_fma(e[u], taps.k[m - i], a[i]);
+                }
+            }
+            const int r0 = (c * SR2 + 2 * hp) & (RS - 1);
+            *reinterpret_cast<float4*>(&s_h[r0 * HS + hc]) = make_float4(a[0].x, a[1].x, a[2].x, a[3].x);
+            *reinterpret_cast<float4*>(&s_h[(r0 + 1) * HS + hc]) = make_float4(a[0].y, a[1].y, a[2].y, a[3].y);
+        }
+        __syncthreads();
+        const int kout = c - 1;
+        if (kout >= 0) {   // V pass of output chunk kout (lag 1 chunk: FW - 1 <= SR2)
+            const int t0 = kout * SR2 + 4 * vq;
+            f2v acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};   // rows t0+j
+#pragma unroll
+            for (int m = 0; m < FW + 3; m++) {
+                const f2v v = *reinterpret_cast<const f2v*>(&s_h[((t0 + m) & (RS - 1)) * HS + vc]);
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (m - j >= 0 && m - j < FW) acc[j] = pk_fma(v, taps.k[m - j], acc[j]);
+            }
+            if (x < W) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int y = yb + t0 + j;
+                    if (y < ye) {
+                        *reinterpret_cast<f2v*>(&d[(long long)y * W + x]) = acc[j];
+                        // DownsampleKernel<1> (ProgramCU.cu:287-298) into the next octave's
+                        // level 0: dst(r, c) = src(2r, min(2c, W-1)); x is even, W is even.
+                        if (dd && !(y & 1) && (y >> 1) < dsh) {
+                            float* drow = dd + (long long)(y >> 1) * dsw;
+                            if ((x >> 1) < dsw) drow[x >> 1] = acc[j].x;
+                            if (x + 1 == W - 1)
+                                for (int cc = W >> 1; cc < dsw; cc++) drow[cc] = acc[j].y;
+                        }
+                    }
+                }
+            }
+        }
+        if (has_next) store_chunk(cur);
+        __syncthreads();
+    };
+    const int nsteps = nchunk_out + 1;
+    for (int c = 0; c < nsteps; c += 2) {
+        step(c, stA, stB);
+        if (c + 1 < nsteps) step(c + 1, stB, stA);
     }
 }
 
@@ -478,6 +627,24 @@ hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
         rows = (rows + SR - 1) / SR * SR;
         nsy = (h + rows - 1) / rows;
         dim3 grid((unsigned)(strips_x * nsy * batch));
+        if (!(g_host_variant & (32 | 64))) {
+            // 32-row chunks: strip height a multiple of SR2
+            int nsy2 = (int)std::min<long long>((2048 + per_col - 1) / per_col, (h + SR2 - 1) / SR2);
+            nsy2 = std::max(nsy2, 1);
+            int rows2 = (h + nsy2 - 1) / nsy2;
+            rows2 = (rows2 + SR2 - 1) / SR2 * SR2;
+            nsy2 = (h + rows2 - 1) / rows2;
+            dim3 grid2((unsigned)(strips_x * nsy2 * batch));
+            if (src8)
+                hipLaunchKernelGGL((k_gauss_pk2<FW, true>), grid2, dim3(256), 0, stream, src,
+                                   src8, src_stride, src_img_stride, dst, dst_img_stride, w, h,
+                                   taps, ds, dsw, dsh, ds_img_stride, rows2);
+            else
+                hipLaunchKernelGGL((k_gauss_pk2<FW, false>), grid2, dim3(256), 0, stream, src,
+                                   src8, src_stride, src_img_stride, dst, dst_img_stride, w, h,
+                                   taps, ds, dsw, dsh, ds_img_stride, rows2);
+            return hipGetLastError();
+        }
         if (!(g_host_variant & 32)) {
             if (src8)
                 hipLaunchKernelGGL((k_gauss_pk<FW, true>), grid, dim3(256), 0, stream, src, src8,
