@@ -14,6 +14,8 @@
 //     (image, octave, level, row, column) order -- no histogram pyramid, no host round trips.
 // Floating-point conventions are those of oracle/sift_oracle.cpp (fma contractions written
 // out, transcendentals from sift_math.h); the build uses -ffp-contract=off.
+#include <type_traits>
+
 #include "sift_kernels.h"
 #include "sift_math.h"
 
@@ -28,7 +30,8 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 // Bits: 1 XCD remap in the tile Gaussian, 2 row-streaming loader in the tile Gaussian, 4 XCD
 // remap in the tile extremum kernel, 8 tile Gaussian instead of strips, 16 tile extremum kernel
 // instead of strips, 32 scalar-FMA strip Gaussian instead of the packed one, 64 16-row packed
-// strip Gaussian (k_gauss_pk) instead of the 32-row one (k_gauss_pk2).
+// strip Gaussian (k_gauss_pk) instead of the 32-row one (k_gauss_pk2), 128 timing probe (filters
+// replaced by copies, results wrong), 256 element-wise instead of quad loads in k_gauss_pk2.
 __constant__ int g_variant;
 int g_host_variant = 0;   // host copy: selects launch configurations
 
@@ -479,21 +482,30 @@ __global__ __launch_bounds__(256) void k_gauss_pk(
 // written after the V pass, when the H pass has finished reading.
 constexpr int SR2 = 32;
 
-template <int FW, bool U8>
+// VEC: the input rows are fetched as 16-byte (f32) / 4-byte (u8) aligned quads instead of one
+// element per lane: the strip's load window starts at a0 = x0 - HALF - OFF, OFF = (-HALF) & 3,
+// so every quad is aligned, and quads left of column 0 / right of W-1 replicate the edge value
+// (W is a multiple of 4, so a quad is entirely inside or entirely outside).  LDS column j holds
+// input column a0 + j in both forms.
+template <int FW, bool U8, bool VEC>
 __global__ __launch_bounds__(256) void k_gauss_pk2(
     const float* __restrict__ src, const uint8_t* __restrict__ src8, int src_stride,
     long long src_img_stride, float* __restrict__ dst, long long dst_img_stride, int W, int H,
     Taps taps, float* __restrict__ ds, int dsw, int dsh, long long ds_img_stride,
     int rows_per_strip) {
     constexpr int HALF = FW >> 1;
-    constexpr int IN_W = GT + FW - 1;                 // input columns of a strip
+    constexpr int OFF = VEC ? ((-HALF) & 3) : 0;      // LDS column of the strip's first input
+    constexpr int IN_W = GT + FW - 1 + OFF;           // input columns held per row
+    constexpr int NQ = (IN_W + 3) / 4;                // aligned quads per row (VEC)
     constexpr int NRD = (FW + 3) / 2;                 // ds_read_b128 per H-pass thread
-    constexpr int IN_S = (GT + FW + 3 + 3) & ~3;      // float2 per row pair (>= 64 + FW + 3)
+    constexpr int IN_S = (GT + FW + 3 + OFF + 3) & ~3;   // float2 per row pair
+    static_assert(!VEC || 4 * NQ <= IN_S, "quad stores stay inside the row pair");
     constexpr int RS = 64;                            // ring rows: (1 + 1) * 32 for FW <= 33
     constexpr int HS = GT + 4;                        // ring row stride (floats)
-    constexpr int NLD = ((SR2 / 2) * IN_W + 255) / 256;
+    constexpr int NLD = VEC ? ((SR2 / 2) * NQ + 255) / 256 : ((SR2 / 2) * IN_W + 255) / 256;
+    constexpr int IN_SV = IN_S;                       // LDS row-pair stride
     static_assert(FW - 1 <= SR2, "ring holds one chunk of lag");
-    __shared__ __attribute__((aligned(16))) f2v s_in[(SR2 / 2) * IN_S];
+    __shared__ __attribute__((aligned(16))) f2v s_in[(SR2 / 2) * IN_SV];
     __shared__ __attribute__((aligned(16))) float s_h[RS * HS];
 
     const int tid = threadIdx.x;
@@ -511,31 +523,73 @@ __global__ __launch_bounds__(256) void k_gauss_pk2(
 
     const float* sf = U8 ? nullptr : src + (long long)b * src_img_stride;
     const uint8_t* s8 = U8 ? src8 + (long long)b * src_img_stride : nullptr;
-    f2v stA[NLD], stB[NLD];
-    auto load_chunk = [&](f2v (&stage)[NLD], int c) {
+    const int a0 = x0 - HALF - OFF;
+    // stage element: VEC -> 4 pairs (rows 2p, 2p+1 of one aligned quad); else one pair
+    typedef typename std::conditional<VEC, f2v[4], f2v[1]>::type Elem;
+    Elem stA[NLD], stB[NLD];
+    auto load_chunk = [&](Elem (&stage)[NLD], int c) {
 #pragma unroll
         for (int m = 0; m < NLD; m++) {
-            const int e = min(tid + 256 * m, (SR2 / 2) * IN_W - 1);
-            const int p = e / IN_W, col = e - p * IN_W;
-            const int gy0 = clampi(yb - HALF + c * SR2 + 2 * p, 0, H - 1);
-            const int gy1 = clampi(yb - HALF + c * SR2 + 2 * p + 1, 0, H - 1);
-            const int gx = clampi(x0 - HALF + col, 0, W - 1);
-            if (U8) {
-                stage[m] = f2v{u8_to_unit(s8[(long long)gy0 * src_stride + gx]),
-                               u8_to_unit(s8[(long long)gy1 * src_stride + gx])};
+            if (VEC) {
+                const int e = min(tid + 256 * m, (SR2 / 2) * NQ - 1);
+                const int p = e / NQ, j = e - p * NQ;
+                const int gy0 = clampi(yb - HALF + c * SR2 + 2 * p, 0, H - 1);
+                const int gy1 = clampi(yb - HALF + c * SR2 + 2 * p + 1, 0, H - 1);
+                const int gq = a0 + 4 * j;                          // aligned first column
+                const int lq = clampi(gq, 0, W - 4);
+                float r0[4], r1[4];
+                if (U8) {
+                    const uint32_t w0 = *reinterpret_cast<const uint32_t*>(s8 + (long long)gy0 * src_stride + lq);
+                    const uint32_t w1 = *reinterpret_cast<const uint32_t*>(s8 + (long long)gy1 * src_stride + lq);
+#pragma unroll
+                    for (int t = 0; t < 4; t++) {
+                        r0[t] = u8_to_unit((w0 >> (8 * t)) & 255u);
+                        r1[t] = u8_to_unit((w1 >> (8 * t)) & 255u);
+                    }
+                } else {
+                    const float4 v0 = *reinterpret_cast<const float4*>(sf + (long long)gy0 * src_stride + lq);
+                    const float4 v1 = *reinterpret_cast<const float4*>(sf + (long long)gy1 * src_stride + lq);
+                    r0[0] = v0.x; r0[1] = v0.y; r0[2] = v0.z; r0[3] = v0.w;
+                    r1[0] = v1.x; r1[1] = v1.y; r1[2] = v1.z; r1[3] = v1.w;
+                }
+                // clamp-to-edge: a quad left of column 0 repeats column 0, right of W-1 repeats W-1
+                const bool left = gq < 0, right = gq > W - 4;
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const float u0 = left ? r0[0] : (right ? r0[3] : r0[t]);
+                    const float u1 = left ? r1[0] : (right ? r1[3] : r1[t]);
+                    stage[m][t] = f2v{u0, u1};
+                }
             } else {
-                stage[m] = f2v{sf[(long long)gy0 * src_stride + gx],
-                               sf[(long long)gy1 * src_stride + gx]};
+                const int e = min(tid + 256 * m, (SR2 / 2) * IN_W - 1);
+                const int p = e / IN_W, col = e - p * IN_W;
+                const int gy0 = clampi(yb - HALF + c * SR2 + 2 * p, 0, H - 1);
+                const int gy1 = clampi(yb - HALF + c * SR2 + 2 * p + 1, 0, H - 1);
+                const int gx = clampi(a0 + col, 0, W - 1);
+                if (U8) {
+                    stage[m][0] = f2v{u8_to_unit(s8[(long long)gy0 * src_stride + gx]),
+                                      u8_to_unit(s8[(long long)gy1 * src_stride + gx])};
+                } else {
+                    stage[m][0] = f2v{sf[(long long)gy0 * src_stride + gx],
+                                      sf[(long long)gy1 * src_stride + gx]};
+                }
             }
         }
     };
-    auto store_chunk = [&](const f2v (&stage)[NLD]) {
+    auto store_chunk = [&](const Elem (&stage)[NLD]) {
 #pragma unroll
         for (int m = 0; m < NLD; m++) {
             const int e = tid + 256 * m;
-            if (e < (SR2 / 2) * IN_W) {
+            if (VEC) {
+                if (e < (SR2 / 2) * NQ) {
+                    const int p = e / NQ, j = e - p * NQ;
+                    float4* q = reinterpret_cast<float4*>(&s_in[p * IN_SV + 4 * j]);
+                    q[0] = make_float4(stage[m][0].x, stage[m][0].y, stage[m][1].x, stage[m][1].y);
+                    q[1] = make_float4(stage[m][2].x, stage[m][2].y, stage[m][3].x, stage[m][3].y);
+                }
+            } else if (e < (SR2 / 2) * IN_W) {
                 const int p = e / IN_W, col = e - p * IN_W;
-                s_in[p * IN_S + col] = stage[m];
+                s_in[p * IN_SV + col] = stage[m][0];
             }
         }
     };
@@ -550,16 +604,26 @@ __global__ __launch_bounds__(256) void k_gauss_pk2(
     const int vq = tid >> 5, vc = (tid & 31) * 2;     // V pass: rows 4vq..4vq+3; columns vc, vc+1
     const int x = x0 + vc;
     // iteration c: chunk c is in LDS, chunk c+1 in `cur` registers; load chunk c+2 into `nxt`
-    auto step = [&](int c, f2v (&cur)[NLD], f2v (&nxt)[NLD]) {
+    auto step = [&](int c, Elem (&cur)[NLD], Elem (&nxt)[NLD]) {
         const bool has_in = c < nchunk_in, has_next = c + 1 < nchunk_in;
         if (c + 2 < nchunk_in) load_chunk(nxt, c + 2);
         if (has_in) {   // H pass of input chunk c -> ring rows c*SR2 .. c*SR2+31
-            const float4* row = reinterpret_cast<const float4*>(&s_in[hp * IN_S + hc]);
+            const f2v* rowp = &s_in[hp * IN_SV + hc + OFF];
             f2v a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};   // columns hc+i
+            if (g_variant & 128) {   // timing probe only: same memory traffic, no filter
+                a[0] = rowp[HALF]; a[1] = rowp[HALF + 1]; a[2] = rowp[HALF + 2]; a[3] = rowp[HALF + 3];
+            } else {
 #pragma unroll
             for (int q = 0; q < NRD; q++) {
-                const float4 v = row[q];             // pair columns hc+2q, hc+2q+1
-                const f2v e[2] = {{v.x, v.y}, {v.z, v.w}};
+                f2v e[2];                            // pair columns hc+2q, hc+2q+1
+                if (OFF % 2 == 0) {
+                    const float4 v = reinterpret_cast<const float4*>(rowp)[q];
+                    e[0] = f2v{v.x, v.y};
+                    e[1] = f2v{v.z, v.w};
+                } else {
+                    e[0] = rowp[2 * q];
+                    e[1] = rowp[2 * q + 1];
+                }
 #pragma unroll
                 for (int u = 0; u < 2; u++) {
                     const int m = 2 * q + u;
@@ -567,6 +631,7 @@ __global__ __launch_bounds__(256) void k_gauss_pk2(
                     for (int i = 0; i < 4; i++)
                         if (m - i >= 0 && m - i < FW) a[i] = pk_fma(e[u], taps.k[m - i], a[i]);
                 }
+            }
             }
             const int r0 = (c * SR2 + 2 * hp) & (RS - 1);
             *reinterpret_cast<float4*>(&s_h[r0 * HS + hc]) = make_float4(a[0].x, a[1].x, a[2].x, a[3].x);
@@ -577,12 +642,18 @@ __global__ __launch_bounds__(256) void k_gauss_pk2(
         if (kout >= 0) {   // V pass of output chunk kout (lag 1 chunk: FW - 1 <= SR2)
             const int t0 = kout * SR2 + 4 * vq;
             f2v acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};   // rows t0+j
+            if (g_variant & 128) {   // timing probe only
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    acc[j] = *reinterpret_cast<const f2v*>(&s_h[((t0 + j + HALF) & (RS - 1)) * HS + vc]);
+            } else {
 #pragma unroll
             for (int m = 0; m < FW + 3; m++) {
                 const f2v v = *reinterpret_cast<const f2v*>(&s_h[((t0 + m) & (RS - 1)) * HS + vc]);
 #pragma unroll
                 for (int j = 0; j < 4; j++)
                     if (m - j >= 0 && m - j < FW) acc[j] = pk_fma(v, taps.k[m - j], acc[j]);
+            }
             }
             if (x < W) {
 #pragma unroll
@@ -635,14 +706,21 @@ hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
             rows2 = (rows2 + SR2 - 1) / SR2 * SR2;
             nsy2 = (h + rows2 - 1) / rows2;
             dim3 grid2((unsigned)(strips_x * nsy2 * batch));
-            if (src8)
-                hipLaunchKernelGGL((k_gauss_pk2<FW, true>), grid2, dim3(256), 0, stream, src,
-                                   src8, src_stride, src_img_stride, dst, dst_img_stride, w, h,
-                                   taps, ds, dsw, dsh, ds_img_stride, rows2);
-            else
-                hipLaunchKernelGGL((k_gauss_pk2<FW, false>), grid2, dim3(256), 0, stream, src,
-                                   src8, src_stride, src_img_stride, dst, dst_img_stride, w, h,
-                                   taps, ds, dsw, dsh, ds_img_stride, rows2);
+            // aligned quads need 4-element row strides and image strides, a 16-B aligned base
+            // and a width that is a multiple of 4 (always true for pyramid levels)
+            const bool vec = !(g_host_variant & 256) && (src_stride % 4) == 0 &&
+                             (src_img_stride % 4) == 0 && (w % 4) == 0 && w >= 4 &&
+                             ((uintptr_t)(src8 ? (const void*)src8 : (const void*)src) % 16) == 0;
+#define SGK_PK2(U8, VEC)                                                                   \
+    hipLaunchKernelGGL((k_gauss_pk2<FW, U8, VEC>), grid2, dim3(256), 0, stream, src, src8,   \
+                       src_stride, src_img_stride, dst, dst_img_stride, w, h, taps, ds, dsw,  \
+                       dsh, ds_img_stride, rows2)
+            if (src8) {
+                if (vec) SGK_PK2(true, true); else SGK_PK2(true, false);
+            } else {
+                if (vec) SGK_PK2(false, true); else SGK_PK2(false, false);
+            }
+#undef SGK_PK2
             return hipGetLastError();
         }
         if (!(g_host_variant & 32)) {

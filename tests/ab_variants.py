@@ -18,6 +18,7 @@ def main():
     ap.add_argument("variants", type=int, nargs="+")
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--no-check", action="store_true", help="timing probes that change results")
     args = ap.parse_args()
     imgs = synth_batch(args.batch, 1920, 1080, 3000, unique=16)
     ctx = sgpu.SiftContext(0, default_options(octave_num=4))
@@ -33,7 +34,7 @@ def main():
                 res[v].append(t)
             tot = ctx.total()
             ref_total = tot if ref_total is None else ref_total
-            assert tot == ref_total, (v, tot, ref_total)
+            assert args.no_check or tot == ref_total, (v, tot, ref_total)
     sgpu.lib().sgpu_debug_set_variant(0)
     for v in args.variants:
         keys = res[v][0].keys()
