@@ -1489,7 +1489,9 @@ __global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ py
                 const float2 cc = grad_at(g, W, (int)x, (int)y);
                 const float dnx = nx + ox, dny = ny + oy;
                 const float ww = exp_mid_(-0.125f * fma_(dnx, dnx, dny * dny));   // in [-1.6, 0]
-                const float wx = (float)(1.0 - (double)nxn), wy = (float)(1.0 - (double)nyn);
+                // (float)(1.0 - (double)n) of the reference: 1 - n is exact in double, so the
+                // single float subtraction rounds to the same value
+                const float wx = 1.0f - nxn, wy = 1.0f - nyn;
                 weight = ww * wx * wy * cc.x;
                 float theta = (anglef - cc.y) * rpi;
                 if (theta < 0) theta += 8.0f;
