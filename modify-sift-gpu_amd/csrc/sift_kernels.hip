@@ -1439,9 +1439,9 @@ __global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ py
     const int nrows = ymax >= ymin ? (int)(ymax - ymin) + 1 : 0;
     // The reference visits every sample of the cell's axis-aligned box and keeps those with
     // |nx| < 1 and |ny| < 1 (the rotated square).  Only the samples it keeps contribute, so the
-    // quad walks, row by row, a column span that covers the square with one sample of margin
-    // (bounds in float; the exact test below still decides each sample) -- same samples, same
-    // (y, x) order, ~40% fewer iterations for rotated features.
+    // quad walks, row by row, a column span that covers the square with a 0.01-pixel margin
+    // (the float bounds and the float test differ by ~1e-5 pixel; the exact test below still
+    // decides each sample) -- same samples, same (y, x) order, ~45% fewer iterations.
     const bool use_c = fabs_(crspt) > 1e-4f / spt, use_s = fabs_(srspt) > 1e-4f / spt;
     const float icr = use_c ? 1.0f / crspt : 0.0f, isr = use_s ? 1.0f / srspt : 0.0f;
     const float kInf = as_float(0x7f800000u);
@@ -1458,8 +1458,8 @@ __global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ py
             a = fmax_(a, fmin_(p, q));
             bnd = fmin_(bnd, fmax_(p, q));
         }
-        const float cl = fmax_(0.0f, ceilf(ptx + a - xmin) - 1.0f);
-        const float ch = fmin_((float)(ncols - 1), floor_(ptx + bnd - xmin) + 1.0f);
+        const float cl = fmax_(0.0f, ceilf(ptx + a - xmin - 0.01f));
+        const float ch = fmin_((float)(ncols - 1), floor_(ptx + bnd - xmin + 0.01f));
         lo = (int)cl;
         len = ch >= cl ? (int)ch - lo + 1 : 0;
     };
