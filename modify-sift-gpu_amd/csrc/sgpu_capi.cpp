@@ -1,10 +1,15 @@
 // sgpu_capi.cpp -- the C ABI (include/sgpu.h) over the gfx950 kernels.
 //
 // Host orchestration of one batch (replaces SiftPyramid::RunSIFT, SiftPyramid.cpp:58-216, and
-// the PyramidCU stage methods).  Per batch the host syncs twice: once to size the keypoint
-// arrays after the row scan, once at the end to read the per-image offsets.  Everything else
-// is queued on one HIP stream; no per-level host round trips (the reference does four per
-// DoG level, PyramidCU.cpp:783-813).
+// the PyramidCU stage methods).  A batch can be split into parts of consecutive images, each
+// with its own HIP streams and buffers; part p+1 starts its pyramid when part p has finished
+// detection, so that the HBM-bound pyramid/extremum kernels of one part can run beside the
+// VALU-bound orientation/descriptor kernels of the previous one (one part by default, see
+// extract_impl).  Inside a part everything is queued
+// without host round trips (keypoint counts stay on the device; launch grids come from buffer
+// capacities); the host waits once per batch, reads the per-image offsets and, if a part's
+// candidates overflowed its capacity, grows the buffers and re-runs that part.  (The reference
+// does four host round trips per DoG level, PyramidCU.cpp:783-813.)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -43,24 +48,57 @@ struct DevBuf {
 
 enum { T_UPLOAD, T_PYRAMID, T_DETECT, T_ORIENT, T_EXPAND, T_DESC, T_DOWNLOAD, T_TOTAL, T_MATCH, T_N };
 
+// One part of a batch: consecutive images [img0, img0 + n) with their own stream and buffers.
+struct Part {
+    hipStream_t stream = nullptr;      // high priority: pyramid + detection
+    hipStream_t stream_lo = nullptr;   // low priority: orientation, descriptors, readback
+    size_t cand_hint = 0, feat_hint = 0;   // counts of the previous call (launch-grid sizing)
+    hipEvent_t ev[8] = {};   // start, pyramid, detect, orientation, expand, descriptor, end, (spare)
+    int img0 = 0, n = 0;
+    sgk::FeatureParams fp{};
+    int total_rows = 0;
+    long long mask_words = 0;
+    size_t cand_cap = 0;     // candidate capacity of cand/info/ocount (features: 2x)
+    uint32_t n_cand = 0;
+    std::vector<int64_t> img_off;          // local per-image offsets [n + 1]
+    int64_t* h_read = nullptr;             // pinned readback: [0] = n_cand, [1..n+1] = offsets
+    size_t h_read_n = 0;
+    DevBuf pyr, mask, row_count, row_base, scan_tmp, cand, info, ocount, eoff, feat, feat_info,
+        keys, desc, img_off_dev;
+    float timing[T_N] = {};
+
+    void release() {
+        DevBuf* bufs[] = {&pyr, &mask, &row_count, &row_base, &scan_tmp, &cand, &info, &ocount,
+                          &eoff, &feat, &feat_info, &keys, &desc, &img_off_dev};
+        for (DevBuf* b : bufs) b->release();
+        if (h_read) (void)hipHostFree(h_read);
+        h_read = nullptr;
+        for (hipEvent_t& e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+        if (stream_lo) (void)hipStreamDestroy(stream_lo);
+        stream = stream_lo = nullptr;
+    }
+};
+
+constexpr int kMaxParts = 4;
+
 }  // namespace
 
 struct sgpu_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;   // matcher, uploads, gathers
     sgpu_options opt{};
     sgp::Schedule sched{};
     std::string err;
     // last extract
-    int batch = 0, w = 0, h = 0;
+    int batch = 0, w = 0, h = 0, nparts = 0;
     std::vector<sgp::Octave> oct;
-    sgk::FeatureParams fp{};
-    int total_rows = 0;
-    uint32_t n_cand = 0;
     size_t staged_bytes = 0;
-    std::vector<int64_t> img_off;
-    DevBuf input, pyr, mask, row_count, row_base, scan_tmp, cand, info, ocount, eoff, feat,
-        feat_info, keys, desc, img_off_dev, n_dev;
+    std::vector<int64_t> img_off;          // global per-image offsets [batch + 1]
+    Part part[kMaxParts];
+    DevBuf input, all_keys, all_desc;      // all_*: lazily gathered multi-part outputs
+    bool gathered = false;
     hipEvent_t ev[T_N + 1] = {};
     float timing[T_N] = {};
     // matcher
@@ -75,6 +113,12 @@ struct sgpu_ctx {
             err += hipGetErrorString(e);
         }
         return code;
+    }
+    // part holding image i of the last batch
+    int part_of(int i) const {
+        for (int p = 0; p < nparts; p++)
+            if (i < part[p].img0 + part[p].n) return p;
+        return nparts - 1;
     }
 };
 
@@ -205,6 +249,18 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
         return SGPU_ENODEV;
     }
     for (int i = 0; i <= T_N; i++) (void)hipEventCreate(&ctx->ev[i]);
+    // the HBM-bound pyramid/detection stream of a part gets the dispatch priority over the
+    // VALU-bound orientation/descriptor stream of the previous part
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    for (Part& pt : ctx->part) {
+        if (hipStreamCreateWithPriority(&pt.stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+            hipStreamCreateWithPriority(&pt.stream_lo, hipStreamNonBlocking, prio_lo) != hipSuccess) {
+            sgpu_ctx_destroy(ctx);
+            return SGPU_ENODEV;
+        }
+        for (hipEvent_t& e : pt.ev) (void)hipEventCreate(&e);
+    }
     int rc = sgpu_ctx_set_options(ctx, opt);
     if (rc != SGPU_OK) {
         sgpu_ctx_destroy(ctx);
@@ -218,11 +274,13 @@ int sgpu_ctx_destroy(sgpu_ctx* ctx) {
     if (!ctx) return SGPU_EINVAL;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    DevBuf* bufs[] = {&ctx->input, &ctx->pyr, &ctx->mask, &ctx->row_count, &ctx->row_base,
-                      &ctx->scan_tmp, &ctx->cand, &ctx->info, &ctx->ocount, &ctx->eoff,
-                      &ctx->feat, &ctx->feat_info, &ctx->keys, &ctx->desc, &ctx->img_off_dev,
-                      &ctx->n_dev, &ctx->m_d1, &ctx->m_d2, &ctx->m_part, &ctx->m_terms,
-                      &ctx->m_match, &ctx->m_dist};
+    for (Part& pt : ctx->part) {
+        if (pt.stream) (void)hipStreamSynchronize(pt.stream);
+        if (pt.stream_lo) (void)hipStreamSynchronize(pt.stream_lo);
+        pt.release();
+    }
+    DevBuf* bufs[] = {&ctx->input, &ctx->all_keys, &ctx->all_desc, &ctx->m_d1, &ctx->m_d2,
+                      &ctx->m_part, &ctx->m_terms, &ctx->m_match, &ctx->m_dist};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i <= T_N; i++)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
@@ -233,31 +291,19 @@ int sgpu_ctx_destroy(sgpu_ctx* ctx) {
 
 const char* sgpu_last_error(const sgpu_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
-static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, int w, int h,
-                        int stride, int flags) {
-    if (!ctx) return SGPU_EINVAL;
-    const bool staged = (flags & SGPU_INPUT_STAGED) != 0;
-    if ((!images && !staged) || n <= 0 || w < 8 || h < 8 || stride < w)
-        return ctx->fail(SGPU_EINVAL, "bad image arguments");
-    if (staged && (is_f32 || ctx->staged_bytes < (size_t)n * h * stride))
-        return ctx->fail(SGPU_EINVAL, "staged input does not match the batch");
-    HIPCHK(ctx, hipSetDevice(ctx->device));
-    hipStream_t st = ctx->stream;
+// Queue the whole pipeline of one part on its stream.  `wait` (may be null) is an event the
+// part's pyramid must wait for.  No host synchronisation.
+static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32, int stride,
+                        hipEvent_t wait) {
+    hipStream_t st = pt.stream;
     const sgpu_options& O = ctx->opt;
     const sgp::Schedule& S = ctx->sched;
     const int d = S.dog_level_num, nlev = S.level_num;
-
-    ctx->oct = sgp::make_octaves(w, h, O.octave_num, 0);
     const int noct = (int)ctx->oct.size();
-    if (noct > sgk::kMaxOctaves) return ctx->fail(SGPU_EINVAL, "too many octaves");
-    for (const auto& oc : ctx->oct)
-        if (oc.w < 4 || oc.h < 4) return ctx->fail(SGPU_EINVAL, "image too small for the octave count");
-    ctx->batch = n;
-    ctx->w = w;
-    ctx->h = h;
+    const int n = pt.n, h = ctx->h;
 
     // ---- layout: pyramid [octave][level][image][h][wa]; mask [octave][dog level][image][h][words]
-    sgk::FeatureParams& fp = ctx->fp;
+    sgk::FeatureParams& fp = pt.fp;
     fp = sgk::FeatureParams{};
     fp.batch = n;
     fp.n_octaves = noct;
@@ -281,7 +327,8 @@ static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
         rows += d * oc.h;
     }
     fp.rows_per_image = rows;
-    ctx->total_rows = rows * n;
+    pt.total_rows = rows * n;
+    pt.mask_words = moff;
     for (int j = 0; j < d; j++) fp.level_sigma[j] = sgp::level_sigma(S, j + S.level_min + 1);
     fp.sigma_step = powf(2.0f, 1.0f / d);
     fp.t0 = (O.subpixel ? 0.8f : 1.0f) * S.dog_threshold;
@@ -297,28 +344,39 @@ static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
     fp.normalize = O.normalized;
     fp.origin_offset = O.lowe_origin ? 0.0f : 0.5f;
 
-    const size_t in_bytes = (size_t)n * h * stride * (is_f32 ? sizeof(float) : 1);
-    ALLOCCHK(ctx, ctx->pyr.ensure((size_t)goff * sizeof(float)));
-    ALLOCCHK(ctx, ctx->mask.ensure((size_t)moff * sizeof(uint32_t)));
-    ALLOCCHK(ctx, ctx->row_count.ensure((size_t)ctx->total_rows * sizeof(uint32_t)));
-    ALLOCCHK(ctx, ctx->row_base.ensure(((size_t)ctx->total_rows + 1) * sizeof(uint32_t)));
-    ALLOCCHK(ctx, ctx->img_off_dev.ensure((size_t)(n + 1) * sizeof(int64_t)));
-    ALLOCCHK(ctx, ctx->n_dev.ensure(16));
-
-    HIPCHK(ctx, hipEventRecord(ctx->ev[0], st));
-    const void* src_in = staged ? ctx->input.p : images;
-    if (!(flags & (SGPU_INPUT_DEVICE | SGPU_INPUT_STAGED))) {
-        ctx->staged_bytes = 0;
-        ALLOCCHK(ctx, ctx->input.ensure(in_bytes));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->input.p, images, in_bytes, hipMemcpyHostToDevice, st));
-        src_in = ctx->input.p;
+    // candidate capacity: grow-only, first guess one per 256 octave pixels
+    const size_t sum_px = (size_t)goff / (size_t)std::max(1, nlev) / (size_t)n;
+    pt.cand_cap = std::max(pt.cand_cap, std::max<size_t>(1024, sum_px / 256 * n));
+    const size_t nc = pt.cand_cap, ne_cap = 2 * nc;
+    ALLOCCHK(ctx, pt.pyr.ensure((size_t)goff * sizeof(float)));
+    ALLOCCHK(ctx, pt.mask.ensure((size_t)moff * sizeof(uint32_t)));
+    ALLOCCHK(ctx, pt.row_count.ensure((size_t)pt.total_rows * sizeof(uint32_t)));
+    ALLOCCHK(ctx, pt.row_base.ensure(((size_t)pt.total_rows + 1) * sizeof(uint32_t)));
+    ALLOCCHK(ctx, pt.img_off_dev.ensure((size_t)(n + 1) * sizeof(int64_t)));
+    ALLOCCHK(ctx, pt.cand.ensure(nc * sizeof(float4)));
+    ALLOCCHK(ctx, pt.info.ensure(nc * sizeof(int2)));
+    ALLOCCHK(ctx, pt.ocount.ensure(nc * sizeof(uint32_t)));
+    ALLOCCHK(ctx, pt.eoff.ensure((nc + 1) * sizeof(uint32_t)));
+    ALLOCCHK(ctx, pt.feat.ensure(ne_cap * sizeof(float4)));
+    ALLOCCHK(ctx, pt.feat_info.ensure(ne_cap * sizeof(int2)));
+    ALLOCCHK(ctx, pt.keys.ensure(ne_cap * sizeof(float4)));
+    if (O.descriptors) ALLOCCHK(ctx, pt.desc.ensure(ne_cap * 128 * sizeof(float)));
+    ALLOCCHK(ctx, pt.scan_tmp.ensure((sgk::scan_tmp_words(std::max<size_t>(nc, pt.total_rows)) + 16) * 4));
+    if (pt.h_read_n < (size_t)n + 2) {
+        if (pt.h_read) (void)hipHostFree(pt.h_read);
+        pt.h_read = nullptr;
+        ALLOCCHK(ctx, hipHostMalloc((void**)&pt.h_read, ((size_t)n + 2) * sizeof(int64_t)));
+        pt.h_read_n = (size_t)n + 2;
     }
-    const uint8_t* src8 = is_f32 ? nullptr : (const uint8_t*)src_in;
-    const float* srcf = is_f32 ? (const float*)src_in : nullptr;
-    HIPCHK(ctx, hipEventRecord(ctx->ev[1], st));
+
+    if (wait) HIPCHK(ctx, hipStreamWaitEvent(st, wait, 0));
+    HIPCHK(ctx, hipEventRecord(pt.ev[0], st));
+    const size_t img_elems = (size_t)stride * h;
+    const uint8_t* src8 = is_f32 ? nullptr : (const uint8_t*)src_in + (size_t)pt.img0 * img_elems;
+    const float* srcf = is_f32 ? (const float*)src_in + (size_t)pt.img0 * img_elems : nullptr;
 
     // ---- Gaussian pyramid (BuildPyramid, PyramidCU.cpp:979-1044)
-    float* pyr = ctx->pyr.as<float>();
+    float* pyr = pt.pyr.as<float>();
     sgk::Taps taps;
     for (int o = 0; o < noct; o++) {
         const sgk::OctaveDesc& od = fp.oct[o];
@@ -326,7 +384,7 @@ static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
         float* lvl0 = pyr + od.gauss_off;
         if (o == 0) {
             int fw = sgp::make_filter(S.initial_smooth, O.filter_width_factor, taps.k);
-            HIPCHK(ctx, sgk::launch_gauss(srcf, src8, stride, (long long)stride * h, lvl0, npx,
+            HIPCHK(ctx, sgk::launch_gauss(srcf, src8, stride, (long long)img_elems, lvl0, npx,
                                           od.wa, od.h, fw, taps, n, nullptr, 0, 0, 0, st));
         }
         for (int k = 1; k < nlev; k++) {
@@ -347,67 +405,161 @@ static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
                                           n, ds, dsw, dsh, ds_stride, st));
         }
     }
-    HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
+    HIPCHK(ctx, hipEventRecord(pt.ev[1], st));
 
-    // ---- extrema + row scan
-    HIPCHK(ctx, hipMemsetAsync(ctx->row_count.p, 0, (size_t)ctx->total_rows * 4, st));
-    // the strip extremum kernel only sets the bits of accepted pixels
-    HIPCHK(ctx, hipMemsetAsync(ctx->mask.p, 0, (size_t)moff * sizeof(uint32_t), st));
+    // ---- extrema + row scan (the strip extremum kernel only sets the bits it accepts)
+    HIPCHK(ctx, hipMemsetAsync(pt.row_count.p, 0, (size_t)pt.total_rows * 4, st));
+    HIPCHK(ctx, hipMemsetAsync(pt.mask.p, 0, (size_t)moff * sizeof(uint32_t), st));
     for (int o = 0; o < noct; o++)
-        HIPCHK(ctx, sgk::launch_extrema(pyr, ctx->mask.as<uint32_t>(), ctx->row_count.as<uint32_t>(),
+        HIPCHK(ctx, sgk::launch_extrema(pyr, pt.mask.as<uint32_t>(), pt.row_count.as<uint32_t>(),
                                         fp, o, st));
-    ALLOCCHK(ctx, ctx->scan_tmp.ensure((sgk::scan_tmp_words(ctx->total_rows) + 16) * 4));
-    HIPCHK(ctx, sgk::launch_scan(ctx->row_count.as<uint32_t>(), ctx->row_base.as<uint32_t>(),
-                                 ctx->total_rows, ctx->scan_tmp.as<uint32_t>(), st));
-    uint32_t ncand = 0;
-    HIPCHK(ctx, hipMemcpyAsync(&ncand, ctx->row_base.as<uint32_t>() + ctx->total_rows, 4,
-                               hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipEventRecord(ctx->ev[3], st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
-    ctx->n_cand = ncand;
+    HIPCHK(ctx, sgk::launch_scan(pt.row_count.as<uint32_t>(), pt.row_base.as<uint32_t>(),
+                                 pt.total_rows, pt.scan_tmp.as<uint32_t>(), st));
+    HIPCHK(ctx, hipEventRecord(pt.ev[2], st));
 
-    // ---- orientation (+ keypoint refinement), expansion, descriptors
-    const size_t nc = std::max<uint32_t>(ncand, 1);
-    ALLOCCHK(ctx, ctx->cand.ensure(nc * sizeof(float4)));
-    ALLOCCHK(ctx, ctx->info.ensure(nc * sizeof(int2)));
-    ALLOCCHK(ctx, ctx->ocount.ensure(nc * sizeof(uint32_t)));
-    ALLOCCHK(ctx, ctx->eoff.ensure((nc + 1) * sizeof(uint32_t)));
-    const size_t ne_cap = 2 * nc;
-    ALLOCCHK(ctx, ctx->feat.ensure(ne_cap * sizeof(float4)));
-    ALLOCCHK(ctx, ctx->feat_info.ensure(ne_cap * sizeof(int2)));
-    ALLOCCHK(ctx, ctx->keys.ensure(ne_cap * sizeof(float4)));
-    if (O.descriptors) ALLOCCHK(ctx, ctx->desc.ensure(ne_cap * 128 * sizeof(float)));
-    ALLOCCHK(ctx, ctx->scan_tmp.ensure((sgk::scan_tmp_words(nc) + 16) * 4));
-    const uint32_t* n_cand_dev = ctx->row_base.as<uint32_t>() + ctx->total_rows;
-    HIPCHK(ctx, sgk::launch_orientation(pyr, ctx->mask.as<uint32_t>(), ctx->row_base.as<uint32_t>(),
-                                        ctx->total_rows, n_cand_dev, (int)ncand, fp,
-                                        ctx->cand.as<float4>(), ctx->info.as<int2>(),
-                                        ctx->ocount.as<uint32_t>(), st));
-    HIPCHK(ctx, hipEventRecord(ctx->ev[4], st));
-    HIPCHK(ctx, sgk::launch_scan(ctx->ocount.as<uint32_t>(), ctx->eoff.as<uint32_t>(), ncand,
-                                 ctx->scan_tmp.as<uint32_t>(), st));
-    const uint32_t* n_feat_dev = ctx->eoff.as<uint32_t>() + ncand;
-    HIPCHK(ctx, sgk::launch_expand(ctx->cand.as<float4>(), ctx->info.as<int2>(),
-                                   ctx->eoff.as<uint32_t>(), n_cand_dev, (int)ncand, fp,
-                                   ctx->feat.as<float4>(), ctx->feat_info.as<int2>(),
-                                   ctx->keys.as<float4>(), st));
-    HIPCHK(ctx, hipEventRecord(ctx->ev[5], st));
+    // ---- orientation (+ keypoint refinement), expansion, descriptors on the low-priority
+    // stream: counts stay on the device, grids come from the previous call's counts (the
+    // kernels grid-stride over whatever the device count is)
+    st = pt.stream_lo;
+    HIPCHK(ctx, hipStreamWaitEvent(st, pt.ev[2], 0));
+    const uint32_t* n_cand_dev = pt.row_base.as<uint32_t>() + pt.total_rows;
+    HIPCHK(ctx, hipMemsetAsync(pt.ocount.p, 0, nc * sizeof(uint32_t), st));
+    const int cand_grid = (int)std::min(nc, pt.cand_hint ? pt.cand_hint : nc);
+    const int feat_grid = (int)std::min(ne_cap, pt.feat_hint ? pt.feat_hint : ne_cap);
+    HIPCHK(ctx, sgk::launch_orientation(pyr, pt.mask.as<uint32_t>(), pt.row_base.as<uint32_t>(),
+                                        pt.total_rows, n_cand_dev, (int)nc, cand_grid, fp,
+                                        pt.cand.as<float4>(), pt.info.as<int2>(),
+                                        pt.ocount.as<uint32_t>(), st));
+    HIPCHK(ctx, hipEventRecord(pt.ev[3], st));
+    HIPCHK(ctx, sgk::launch_scan(pt.ocount.as<uint32_t>(), pt.eoff.as<uint32_t>(), nc,
+                                 pt.scan_tmp.as<uint32_t>(), st));
+    const uint32_t* n_feat_dev = pt.eoff.as<uint32_t>() + nc;
+    HIPCHK(ctx, sgk::launch_expand(pt.cand.as<float4>(), pt.info.as<int2>(),
+                                   pt.eoff.as<uint32_t>(), n_cand_dev, (int)nc, fp,
+                                   pt.feat.as<float4>(), pt.feat_info.as<int2>(),
+                                   pt.keys.as<float4>(), st));
+    HIPCHK(ctx, hipEventRecord(pt.ev[4], st));
     if (O.descriptors)
-        HIPCHK(ctx, sgk::launch_descriptor(pyr, ctx->feat.as<float4>(), ctx->feat_info.as<int2>(),
-                                           n_feat_dev, (int)(2 * ncand), fp, ctx->desc.as<float>(),
-                                           st));
-    HIPCHK(ctx, hipEventRecord(ctx->ev[6], st));
-    HIPCHK(ctx, sgk::launch_image_offsets(ctx->row_base.as<uint32_t>(), ctx->eoff.as<uint32_t>(), n,
-                                          fp.rows_per_image, ctx->total_rows,
-                                          ctx->img_off_dev.as<int64_t>(), st));
-    ctx->img_off.assign(n + 1, 0);
-    HIPCHK(ctx, hipMemcpyAsync(ctx->img_off.data(), ctx->img_off_dev.p, (n + 1) * sizeof(int64_t),
+        HIPCHK(ctx, sgk::launch_descriptor(pyr, pt.feat.as<float4>(), pt.feat_info.as<int2>(),
+                                           n_feat_dev, feat_grid, fp, pt.desc.as<float>(), st));
+    HIPCHK(ctx, hipEventRecord(pt.ev[5], st));
+    HIPCHK(ctx, sgk::launch_image_offsets(pt.row_base.as<uint32_t>(), pt.eoff.as<uint32_t>(), n,
+                                          fp.rows_per_image, pt.total_rows, (int)nc,
+                                          pt.img_off_dev.as<int64_t>(), st));
+    return SGPU_OK;
+}
+
+// Queue the (pinned) readback of a part's counts and offsets.
+static int enqueue_readback(sgpu_ctx* ctx, Part& pt) {
+    hipStream_t st = pt.stream_lo;
+    pt.h_read[0] = 0;
+    HIPCHK(ctx, hipMemcpyAsync(pt.h_read, pt.row_base.as<uint32_t>() + pt.total_rows, 4,
                                hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipEventRecord(ctx->ev[7], st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
-    const int map[T_TOTAL + 1][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {6, 7}, {0, 7}};
-    for (int i = 0; i <= T_TOTAL; i++)
-        (void)hipEventElapsedTime(&ctx->timing[i], ctx->ev[map[i][0]], ctx->ev[map[i][1]]);
+    HIPCHK(ctx, hipMemcpyAsync(pt.h_read + 1, pt.img_off_dev.p, (size_t)(pt.n + 1) * sizeof(int64_t),
+                               hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipEventRecord(pt.ev[6], st));
+    return SGPU_OK;
+}
+
+static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, int w, int h,
+                        int stride, int flags) {
+    if (!ctx) return SGPU_EINVAL;
+    const bool staged = (flags & SGPU_INPUT_STAGED) != 0;
+    if ((!images && !staged) || n <= 0 || w < 8 || h < 8 || stride < w)
+        return ctx->fail(SGPU_EINVAL, "bad image arguments");
+    if (staged && (is_f32 || ctx->staged_bytes < (size_t)n * h * stride))
+        return ctx->fail(SGPU_EINVAL, "staged input does not match the batch");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const sgpu_options& O = ctx->opt;
+    ctx->oct = sgp::make_octaves(w, h, O.octave_num, 0);
+    const int noct = (int)ctx->oct.size();
+    if (noct > sgk::kMaxOctaves) return ctx->fail(SGPU_EINVAL, "too many octaves");
+    for (const auto& oc : ctx->oct)
+        if (oc.w < 4 || oc.h < 4) return ctx->fail(SGPU_EINVAL, "image too small for the octave count");
+    ctx->batch = n;
+    ctx->w = w;
+    ctx->h = h;
+    ctx->gathered = false;
+
+    // parts: one by default.  Measured on MI355X (profiles/): a second
+    // part's pyramid starves beside the previous part's descriptor kernel (the dispatcher keeps
+    // filling the CUs with descriptor workgroups despite the stream priorities), so splitting
+    // does not pay yet.  Test hook: variant 4096 -> 2 parts, 8192 -> 4 parts.
+    const int vv = sgk::get_variant();
+    int np = 1;
+    if ((vv & 4096) && n >= 2) np = 2;
+    if ((vv & 8192) && n >= 4) np = 4;
+    ctx->nparts = np;
+    for (int p = 0, i0 = 0; p < np; p++) {
+        const int cnt = n / np + (p < n % np ? 1 : 0);
+        ctx->part[p].img0 = i0;
+        ctx->part[p].n = cnt;
+        i0 += cnt;
+    }
+
+    // input: host batches are uploaded first on the context stream
+    const size_t in_bytes = (size_t)n * h * stride * (is_f32 ? sizeof(float) : 1);
+    HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+    const void* src_in = staged ? ctx->input.p : images;
+    if (!(flags & (SGPU_INPUT_DEVICE | SGPU_INPUT_STAGED))) {
+        ctx->staged_bytes = 0;
+        ALLOCCHK(ctx, ctx->input.ensure(in_bytes));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->input.p, images, in_bytes, hipMemcpyHostToDevice, ctx->stream));
+        src_in = ctx->input.p;
+    }
+    HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
+
+    // part p's pyramid starts when part p-1 has finished detection
+    for (int p = 0; p < np; p++) {
+        hipEvent_t wait = p == 0 ? ctx->ev[1] : ctx->part[p - 1].ev[2];
+        int rc = enqueue_part(ctx, ctx->part[p], src_in, is_f32, stride, wait);
+        if (rc != SGPU_OK) return rc;
+    }
+    for (int p = 0; p < np; p++) {
+        int rc = enqueue_readback(ctx, ctx->part[p]);
+        if (rc != SGPU_OK) return rc;
+    }
+    for (int p = 0; p < np; p++) {
+        HIPCHK(ctx, hipStreamSynchronize(ctx->part[p].stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->part[p].stream_lo));
+    }
+
+    // capacity check: a part whose candidates overflowed is re-run with larger buffers
+    for (int p = 0; p < np; p++) {
+        Part& pt = ctx->part[p];
+        uint32_t nc = (uint32_t)pt.h_read[0];
+        if (nc > pt.cand_cap) {
+            pt.cand_cap = (size_t)nc + nc / 4 + 1024;
+            int rc = enqueue_part(ctx, pt, src_in, is_f32, stride, nullptr);
+            if (rc == SGPU_OK) rc = enqueue_readback(ctx, pt);
+            if (rc != SGPU_OK) return rc;
+            HIPCHK(ctx, hipStreamSynchronize(pt.stream_lo));
+            nc = (uint32_t)pt.h_read[0];
+            if (nc > pt.cand_cap) return ctx->fail(SGPU_ERANGE, "keypoint capacity overflow");
+        }
+        pt.n_cand = nc;
+        pt.img_off.assign(pt.h_read + 1, pt.h_read + 2 + pt.n);
+        pt.cand_hint = (size_t)nc + nc / 16 + 64;
+        pt.feat_hint = (size_t)pt.img_off[pt.n] + pt.img_off[pt.n] / 16 + 64;
+    }
+    ctx->img_off.assign(n + 1, 0);
+    int64_t base = 0;
+    for (int p = 0; p < np; p++) {
+        const Part& pt = ctx->part[p];
+        for (int i = 0; i <= pt.n; i++) ctx->img_off[pt.img0 + i] = base + pt.img_off[i];
+        base += pt.img_off[pt.n];
+    }
+
+    // timings: stages of part 0 (its pyramid and detection run alone), total over all parts
+    Part& p0 = ctx->part[0];
+    (void)hipEventElapsedTime(&ctx->timing[T_UPLOAD], ctx->ev[0], ctx->ev[1]);
+    (void)hipEventElapsedTime(&ctx->timing[T_PYRAMID], p0.ev[0], p0.ev[1]);
+    (void)hipEventElapsedTime(&ctx->timing[T_DETECT], p0.ev[1], p0.ev[2]);
+    (void)hipEventElapsedTime(&ctx->timing[T_ORIENT], p0.ev[2], p0.ev[3]);
+    (void)hipEventElapsedTime(&ctx->timing[T_EXPAND], p0.ev[3], p0.ev[4]);
+    (void)hipEventElapsedTime(&ctx->timing[T_DESC], p0.ev[4], p0.ev[5]);
+    (void)hipEventElapsedTime(&ctx->timing[T_DOWNLOAD], p0.ev[5], p0.ev[6]);
+    (void)hipEventElapsedTime(&ctx->timing[T_TOTAL], ctx->ev[0], ctx->part[np - 1].ev[6]);
     return SGPU_OK;
 }
 
@@ -519,14 +671,16 @@ int64_t sgpu_feature_total(const sgpu_ctx* ctx) {
 int sgpu_copy_features(sgpu_ctx* ctx, int image, float* keys, float* descriptors) {
     if (!ctx || image < 0 || image >= ctx->batch || ctx->img_off.empty()) return SGPU_EINVAL;
     HIPCHK(ctx, hipSetDevice(ctx->device));
-    const int64_t a = ctx->img_off[image], nf = ctx->img_off[image + 1] - a;
+    const Part& pt = ctx->part[ctx->part_of(image)];
+    const int li = image - pt.img0;
+    const int64_t a = pt.img_off[li], nf = pt.img_off[li + 1] - a;
     if (nf <= 0) return SGPU_OK;
     if (keys)
-        HIPCHK(ctx, hipMemcpyAsync(keys, ctx->keys.as<float4>() + a, nf * sizeof(float4),
+        HIPCHK(ctx, hipMemcpyAsync(keys, pt.keys.as<float4>() + a, nf * sizeof(float4),
                                    hipMemcpyDeviceToHost, ctx->stream));
     if (descriptors) {
         if (!ctx->opt.descriptors) return ctx->fail(SGPU_EINVAL, "descriptors disabled (-sd)");
-        HIPCHK(ctx, hipMemcpyAsync(descriptors, ctx->desc.as<float>() + a * 128,
+        HIPCHK(ctx, hipMemcpyAsync(descriptors, pt.desc.as<float>() + a * 128,
                                    nf * 128 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
     }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -536,8 +690,38 @@ int sgpu_copy_features(sgpu_ctx* ctx, int image, float* keys, float* descriptors
 int sgpu_device_features(sgpu_ctx* ctx, const float** keys, const float** descriptors,
                          const int64_t** image_offsets) {
     if (!ctx) return SGPU_EINVAL;
-    if (keys) *keys = ctx->keys.as<float>();
-    if (descriptors) *descriptors = ctx->opt.descriptors ? ctx->desc.as<float>() : nullptr;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const float* k = nullptr;
+    const float* dsc = nullptr;
+    if (ctx->nparts == 1) {
+        k = ctx->part[0].keys.as<float>();
+        dsc = ctx->part[0].desc.as<float>();
+    } else if (ctx->nparts > 1) {
+        // one contiguous copy of the batch's features, gathered on first request
+        const int64_t total = ctx->img_off.empty() ? 0 : ctx->img_off[ctx->batch];
+        if (!ctx->gathered) {
+            ALLOCCHK(ctx, ctx->all_keys.ensure((size_t)std::max<int64_t>(total, 1) * sizeof(float4)));
+            if (ctx->opt.descriptors)
+                ALLOCCHK(ctx, ctx->all_desc.ensure((size_t)std::max<int64_t>(total, 1) * 128 * sizeof(float)));
+            for (int p = 0; p < ctx->nparts; p++) {
+                const Part& pt = ctx->part[p];
+                const int64_t base = ctx->img_off[pt.img0], nf = pt.img_off[pt.n];
+                if (nf <= 0) continue;
+                HIPCHK(ctx, hipMemcpyAsync(ctx->all_keys.as<float4>() + base, pt.keys.p,
+                                           nf * sizeof(float4), hipMemcpyDeviceToDevice, ctx->stream));
+                if (ctx->opt.descriptors)
+                    HIPCHK(ctx, hipMemcpyAsync(ctx->all_desc.as<float>() + base * 128, pt.desc.p,
+                                               nf * 128 * sizeof(float), hipMemcpyDeviceToDevice,
+                                               ctx->stream));
+            }
+            HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+            ctx->gathered = true;
+        }
+        k = ctx->all_keys.as<float>();
+        dsc = ctx->all_desc.as<float>();
+    }
+    if (keys) *keys = k;
+    if (descriptors) *descriptors = ctx->opt.descriptors ? dsc : nullptr;
     if (image_offsets) *image_offsets = ctx->img_off.data();
     return SGPU_OK;
 }
@@ -572,30 +756,47 @@ int sgpu_debug_gaussian(sgpu_ctx* ctx, int image, int octave, int level, float* 
         octave >= (int)ctx->oct.size() || level < 0 || level >= ctx->sched.level_num)
         return SGPU_EINVAL;
     HIPCHK(ctx, hipSetDevice(ctx->device));
-    const sgk::OctaveDesc& od = ctx->fp.oct[octave];
+    const Part& pt = ctx->part[ctx->part_of(image)];
+    const sgk::OctaveDesc& od = pt.fp.oct[octave];
     const long long npx = (long long)od.wa * od.h;
-    const float* src = ctx->pyr.as<float>() + od.gauss_off + level * od.level_stride + image * npx;
+    const float* src = pt.pyr.as<float>() + od.gauss_off + level * od.level_stride +
+                       (image - pt.img0) * npx;
     HIPCHK(ctx, hipMemcpy(out, src, npx * sizeof(float), hipMemcpyDeviceToHost));
     return SGPU_OK;
 }
 
 int sgpu_debug_candidates(sgpu_ctx* ctx, int* ints, float* floats, int cap, int* n) {
     if (!ctx || !n) return SGPU_EINVAL;
-    *n = (int)ctx->n_cand;
-    if (!ints || !floats || cap < (int)ctx->n_cand) return ctx->n_cand ? SGPU_ERANGE : SGPU_OK;
-    if (ctx->n_cand == 0) return SGPU_OK;
+    uint32_t total = 0;
+    for (int p = 0; p < ctx->nparts; p++) total += ctx->part[p].n_cand;
+    *n = (int)total;
+    if (!ints || !floats || cap < (int)total) return total ? SGPU_ERANGE : SGPU_OK;
+    if (total == 0) return SGPU_OK;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     DevBuf a, b;
-    ALLOCCHK(ctx, a.ensure(ctx->n_cand * sizeof(int4)));
-    ALLOCCHK(ctx, b.ensure(ctx->n_cand * sizeof(float4)));
-    HIPCHK(ctx, sgk::launch_debug_candidates(ctx->pyr.as<float>(), ctx->mask.as<uint32_t>(),
-                                             ctx->row_base.as<uint32_t>(), ctx->total_rows,
-                                             ctx->row_base.as<uint32_t>() + ctx->total_rows,
-                                             (int)ctx->n_cand, ctx->fp, a.as<int4>(), b.as<float4>(),
-                                             ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(ints, a.p, ctx->n_cand * sizeof(int4), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(floats, b.p, ctx->n_cand * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
+    ALLOCCHK(ctx, a.ensure(total * sizeof(int4)));
+    ALLOCCHK(ctx, b.ensure(total * sizeof(float4)));
+    uint32_t at = 0;
+    for (int p = 0; p < ctx->nparts; p++) {
+        const Part& pt = ctx->part[p];
+        if (!pt.n_cand) continue;
+        HIPCHK(ctx, sgk::launch_debug_candidates(pt.pyr.as<float>(), pt.mask.as<uint32_t>(),
+                                                 pt.row_base.as<uint32_t>(), pt.total_rows,
+                                                 pt.row_base.as<uint32_t>() + pt.total_rows,
+                                                 (int)pt.n_cand, pt.fp, a.as<int4>() + at,
+                                                 b.as<float4>() + at, ctx->stream));
+        at += pt.n_cand;
+    }
+    HIPCHK(ctx, hipMemcpyAsync(ints, a.p, total * sizeof(int4), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(floats, b.p, total * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    // the kernel reports part-local image indices
+    at = 0;
+    for (int p = 0; p < ctx->nparts; p++) {
+        const Part& pt = ctx->part[p];
+        for (uint32_t i = 0; i < pt.n_cand; i++) ints[4 * (at + i) + 3] += pt.img0;
+        at += pt.n_cand;
+    }
     a.release();
     b.release();
     return SGPU_OK;

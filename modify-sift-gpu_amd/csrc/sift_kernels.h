@@ -15,6 +15,7 @@ struct Taps { float k[33]; };
 
 // In-process A/B switch for kernel variants (test hook; 0 = shipped configuration).
 hipError_t set_variant(int v);
+int get_variant();
 
 // Per-octave geometry and buffer offsets used by the feature kernels.
 struct OctaveDesc {
@@ -61,12 +62,13 @@ size_t scan_tmp_words(size_t n);
 hipError_t launch_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
                        hipStream_t stream);
 
-// Keypoint materialisation + orientation: one thread per detected keypoint.
+// Keypoint materialisation + orientation: a quad per detected keypoint, grid-stride over
+// min(*n_cand_dev, n_cand_cap) keypoints (the grid is sized from the capacity).
 // out4: (x, y, s, packed orientations) in octave coordinates; info: (image, level id);
 // ocount: number of oriented features the keypoint expands to.
 hipError_t launch_orientation(const float* pyr, const uint32_t* mask, const uint32_t* row_base,
                               int total_rows, const uint32_t* n_cand_dev, int n_cand_cap,
-                              const FeatureParams& fp, float4* out4, int2* info,
+                              int grid_hint, const FeatureParams& fp, float4* out4, int2* info,
                               uint32_t* ocount, hipStream_t stream);
 
 // Expansion into oriented features (+ image-coordinate keypoints).
@@ -74,14 +76,16 @@ hipError_t launch_expand(const float4* cand, const int2* info, const uint32_t* e
                          const uint32_t* n_cand_dev, int n_cand_cap, const FeatureParams& fp,
                          float4* feat, int2* feat_info, float4* keys, hipStream_t stream);
 
-// Descriptors (+ normalisation) of the expanded features.
+// Descriptors (+ normalisation) of the expanded features; n_feat_cap sizes the grid (one wave
+// per feature), the kernel grid-strides over *n_feat_dev.
 hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* feat_info,
                              const uint32_t* n_feat_dev, int n_feat_cap, const FeatureParams& fp,
                              float* desc, hipStream_t stream);
 
-// Per-image feature offsets: off[b] = eoff[row_base[b * rows_per_image]] for b in [0, batch].
+// Per-image feature offsets: off[b] = eoff[min(row_base[b * rows_per_image], cap)] for b in
+// [0, batch] (cap = candidate capacity; the clamp only matters when the candidates overflowed).
 hipError_t launch_image_offsets(const uint32_t* row_base, const uint32_t* eoff, int batch,
-                                int rows_per_image, int total_rows, int64_t* off,
+                                int rows_per_image, int total_rows, int n_cand_cap, int64_t* off,
                                 hipStream_t stream);
 
 // Debug: candidates of the orientation stage back as (col, row, level id, image) + (dx,dy,ds).

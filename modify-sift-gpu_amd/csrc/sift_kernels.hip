@@ -31,7 +31,8 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 // remap in the tile extremum kernel, 8 tile Gaussian instead of strips, 16 tile extremum kernel
 // instead of strips, 32 scalar-FMA strip Gaussian instead of the packed one, 64 16-row packed
 // strip Gaussian (k_gauss_pk) instead of the 32-row one (k_gauss_pk2), 128 timing probe (filters
-// replaced by copies, results wrong), 256 element-wise instead of quad loads in k_gauss_pk2.
+// replaced by copies, results wrong), 256 element-wise instead of quad loads in k_gauss_pk2,
+// 4096 / 8192 two / four batch parts (sgpu_capi.cpp).
 __constant__ int g_variant;
 int g_host_variant = 0;   // host copy: selects launch configurations
 
@@ -1196,20 +1197,14 @@ struct Walk {
 // lanes evaluate consecutive window samples (gradient, Gaussian weight, bin) in parallel and
 // every lane then applies the quad's 4 votes in the reference's (y, x) order to the keypoint's
 // 36-bin histogram in LDS, so each bin sees exactly the reference's sequence of float adds.
-__global__ __launch_bounds__(256) void k_orientation(const float* __restrict__ pyr,
-                                                     const uint32_t* __restrict__ mask,
-                                                     const uint32_t* __restrict__ row_base,
-                                                     int total_rows,
-                                                     const uint32_t* __restrict__ n_cand_dev,
-                                                     const FeatureParams fp,
-                                                     float4* __restrict__ out4,
-                                                     int2* __restrict__ info,
-                                                     uint32_t* __restrict__ ocount) {
-    __shared__ float s_vote[64 * 37];
-    const int sub = threadIdx.x & 3, slot = threadIdx.x >> 2;
-    const uint32_t f = blockIdx.x * 64 + slot;
-    if (f >= *n_cand_dev) return;                  // uniform per quad
-    float* vote_l = s_vote + slot * 37;
+__device__ __forceinline__ void orientation_one(uint32_t f, int sub, float* vote_l,
+                                                const float* __restrict__ pyr,
+                                                const uint32_t* __restrict__ mask,
+                                                const uint32_t* __restrict__ row_base,
+                                                int total_rows, const FeatureParams& fp,
+                                                float4* __restrict__ out4,
+                                                int2* __restrict__ info,
+                                                uint32_t* __restrict__ ocount) {
     const KeyLoc L = locate(f, row_base, total_rows, mask, fp);
     const KeyOut kv = key_at(pyr, fp, L);
     const OctaveDesc& od = fp.oct[L.o];
@@ -1345,6 +1340,25 @@ __global__ __launch_bounds__(256) void k_orientation(const float* __restrict__ p
     ocount[f] = us1 == 65535u ? 0u : (1u + ((us2 != 65535u && us2 != us1) ? 1u : 0u));
 }
 
+// Grid-stride over the candidates (the grid is sized from the buffer capacity, the count is
+// read on the device, so no host round trip sits between detection and orientation).
+__global__ __launch_bounds__(256) void k_orientation(const float* __restrict__ pyr,
+                                                     const uint32_t* __restrict__ mask,
+                                                     const uint32_t* __restrict__ row_base,
+                                                     int total_rows,
+                                                     const uint32_t* __restrict__ n_cand_dev,
+                                                     uint32_t cap, const FeatureParams fp,
+                                                     float4* __restrict__ out4,
+                                                     int2* __restrict__ info,
+                                                     uint32_t* __restrict__ ocount) {
+    __shared__ float s_vote[64 * 37];
+    const int sub = threadIdx.x & 3, slot = threadIdx.x >> 2;
+    const uint32_t n = min(*n_cand_dev, cap);
+    float* vote_l = s_vote + slot * 37;
+    for (uint32_t f = blockIdx.x * 64 + slot; f < n; f += gridDim.x * 64)   // uniform per quad
+        orientation_one(f, sub, vote_l, pyr, mask, row_base, total_rows, fp, out4, info, ocount);
+}
+
 // ------------------------------------------------------------------------------------------
 // Feature expansion + image coordinates (PyramidCU.cpp:521-606 / 701-751).
 __global__ __launch_bounds__(256) void k_expand(const float4* __restrict__ cand,
@@ -1353,11 +1367,11 @@ __global__ __launch_bounds__(256) void k_expand(const float4* __restrict__ cand,
                                                 const uint32_t* __restrict__ n_cand_dev,
                                                 const FeatureParams fp, float4* __restrict__ feat,
                                                 int2* __restrict__ feat_info,
-                                                float4* __restrict__ keys) {
-    const uint32_t f = blockIdx.x * 256 + threadIdx.x;
-    if (f >= *n_cand_dev) return;
+                                                float4* __restrict__ keys, uint32_t cap) {
+    const uint32_t ncand = min(*n_cand_dev, cap);
+    for (uint32_t f = blockIdx.x * 256 + threadIdx.x; f < ncand; f += gridDim.x * 256) {
     const uint32_t e0 = eoff[f], n = eoff[f + 1] - e0;
-    if (n == 0) return;
+    if (n == 0) continue;
     const float4 c = cand[f];
     const int2 in = info[f];
     const int o = in.y / fp.d;
@@ -1380,6 +1394,7 @@ __global__ __launch_bounds__(256) void k_expand(const float4* __restrict__ cand,
                               oss * (c.y - 0.5f) + fp.origin_offset, oss * c.z,
                               (float)fmod(twopi - (double)ang[q], twopi));
     }
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1393,19 +1408,17 @@ __device__ __forceinline__ float sq4(float a, float b, float c, float d) {
     return fma_(d, d, t);
 }
 
-__global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ pyr,
-                                                    const float4* __restrict__ feat,
-                                                    const int2* __restrict__ feat_info,
-                                                    const uint32_t* __restrict__ n_feat_dev,
-                                                    const FeatureParams fp,
-                                                    float* __restrict__ desc) {
+__device__ __forceinline__ void descriptor_one(uint32_t e, int lane,
+                                               const float* __restrict__ pyr,
+                                               const float4* __restrict__ feat,
+                                               const int2* __restrict__ feat_info,
+                                               const FeatureParams& fp,
+                                               float* __restrict__ desc) {
     // one wave per feature: lanes 4c..4c+3 own grid cell c (the reference's 16 threads per
     // feature, ProgramCU.cu:1017-1021); the quad evaluates consecutive window samples in
     // parallel and every lane applies the 4 contributions in the reference's (y, x) order, so
     // the 9 accumulators see the reference's exact sequence of fma's.
-    const int lane = threadIdx.x & 63, cell = lane >> 2, sub = lane & 3;
-    const uint32_t e = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (e >= *n_feat_dev) return;                  // uniform per wave
+    const int cell = lane >> 2, sub = lane & 3;
     const int ix = cell & 3, iy = cell >> 2;
     // each quad lane owns two of the cell's 8 orientation bins (lane 0 also bin 8): every bin's
     // fma chain is the reference's, and a sample costs 4 compares instead of an 8-way select
@@ -1562,13 +1575,26 @@ __global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ py
     }
 }
 
+// One wave per feature, grid-stride over the features (count read on the device).
+__global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ pyr,
+                                                    const float4* __restrict__ feat,
+                                                    const int2* __restrict__ feat_info,
+                                                    const uint32_t* __restrict__ n_feat_dev,
+                                                    const FeatureParams fp,
+                                                    float* __restrict__ desc) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t n = *n_feat_dev;
+    for (uint32_t e = blockIdx.x * 4 + (threadIdx.x >> 6); e < n; e += gridDim.x * 4)
+        descriptor_one(e, lane, pyr, feat, feat_info, fp, desc);   // uniform per wave
+}
+
 __global__ void k_image_offsets(const uint32_t* __restrict__ row_base,
                                 const uint32_t* __restrict__ eoff, int batch, int rows_per_image,
-                                int total_rows, int64_t* __restrict__ off) {
+                                int total_rows, uint32_t cap, int64_t* __restrict__ off) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b > batch) return;
     const int r = b == batch ? total_rows : b * rows_per_image;
-    off[b] = (int64_t)eoff[row_base[r]];
+    off[b] = (int64_t)eoff[min(row_base[r], cap)];   // cap: only when the candidates overflowed
 }
 
 __global__ __launch_bounds__(64) void k_debug_candidates(
@@ -1586,6 +1612,8 @@ __global__ __launch_bounds__(64) void k_debug_candidates(
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
+int get_variant() { return g_host_variant; }
+
 hipError_t set_variant(int v) {
     g_host_variant = v;
     return hipMemcpyToSymbol(HIP_SYMBOL(g_variant), &v, sizeof(int));
@@ -1671,11 +1699,12 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tm
 
 hipError_t launch_orientation(const float* pyr, const uint32_t* mask, const uint32_t* row_base,
                               int total_rows, const uint32_t* n_cand_dev, int n_cand_cap,
-                              const FeatureParams& fp, float4* out4, int2* info,
+                              int grid_hint, const FeatureParams& fp, float4* out4, int2* info,
                               uint32_t* ocount, hipStream_t stream) {
     if (n_cand_cap <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_orientation, dim3((n_cand_cap + 63) / 64), dim3(256), 0, stream, pyr,
-                       mask, row_base, total_rows, n_cand_dev, fp, out4, info, ocount);
+    const unsigned grid = (unsigned)std::max(1LL, std::min(((long long)grid_hint + 63) / 64, 4096LL));
+    hipLaunchKernelGGL(k_orientation, dim3(grid), dim3(256), 0, stream, pyr, mask, row_base,
+                       total_rows, n_cand_dev, (uint32_t)n_cand_cap, fp, out4, info, ocount);
     return hipGetLastError();
 }
 
@@ -1683,8 +1712,9 @@ hipError_t launch_expand(const float4* cand, const int2* info, const uint32_t* e
                          const uint32_t* n_cand_dev, int n_cand_cap, const FeatureParams& fp,
                          float4* feat, int2* feat_info, float4* keys, hipStream_t stream) {
     if (n_cand_cap <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_expand, dim3((n_cand_cap + 255) / 256), dim3(256), 0, stream, cand,
-                       info, eoff, n_cand_dev, fp, feat, feat_info, keys);
+    const unsigned grid = (unsigned)std::min(((long long)n_cand_cap + 255) / 256, 1024LL);
+    hipLaunchKernelGGL(k_expand, dim3(grid), dim3(256), 0, stream, cand, info, eoff, n_cand_dev,
+                       fp, feat, feat_info, keys, (uint32_t)n_cand_cap);
     return hipGetLastError();
 }
 
@@ -1692,16 +1722,18 @@ hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* f
                              const uint32_t* n_feat_dev, int n_feat_cap, const FeatureParams& fp,
                              float* desc, hipStream_t stream) {
     if (n_feat_cap <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_descriptor, dim3((unsigned)((n_feat_cap + 3) / 4)), dim3(256), 0,
-                       stream, pyr, feat, feat_info, n_feat_dev, fp, desc);
+    const unsigned grid = (unsigned)std::min(((long long)n_feat_cap + 3) / 4, 65536LL);
+    hipLaunchKernelGGL(k_descriptor, dim3(grid), dim3(256), 0, stream, pyr, feat, feat_info,
+                       n_feat_dev, fp, desc);
     return hipGetLastError();
 }
 
 hipError_t launch_image_offsets(const uint32_t* row_base, const uint32_t* eoff, int batch,
-                                int rows_per_image, int total_rows, int64_t* off,
+                                int rows_per_image, int total_rows, int n_cand_cap, int64_t* off,
                                 hipStream_t stream) {
     hipLaunchKernelGGL(k_image_offsets, dim3((batch + 1 + 255) / 256), dim3(256), 0, stream,
-                       row_base, eoff, batch, rows_per_image, total_rows, off);
+                       row_base, eoff, batch, rows_per_image, total_rows, (uint32_t)n_cand_cap,
+                       off);
     return hipGetLastError();
 }
 

@@ -336,3 +336,25 @@ def test_simplesift_replica(tmp_path):
     k1 = _read_sift_ascii(s1)
     assert k1.shape == (num1, 4)
     assert np.allclose(k1[:, 0], rk1[:, 1], atol=1e-2) and np.allclose(k1[:, 1], rk1[:, 0], atol=1e-2)
+
+
+@pytest.mark.parametrize("variant", [4096, 8192])
+def test_batch_parts_match_single_part(gpu_ctx, variant):
+    """The batch split into 2 / 4 parts on separate streams (sgpu_capi.cpp extract_impl) gives
+    the single-part results image by image, including the gathered device arrays."""
+    imgs = np.stack([synth_image(320, 240, 900 + i) for i in range(7)])
+    gpu_ctx.set_options(default_options())
+    gpu_ctx.extract(imgs)
+    ref = [gpu_ctx.features(i) for i in range(7)]
+    ref_c = gpu_ctx.candidates()
+    try:
+        sgpu.lib().sgpu_debug_set_variant(variant)
+        gpu_ctx.extract(imgs)
+        got = [gpu_ctx.features(i) for i in range(7)]
+        got_c = gpu_ctx.candidates()
+    finally:
+        sgpu.lib().sgpu_debug_set_variant(0)
+    for (k, d), (rk, rd) in zip(got, ref):
+        assert np.array_equal(_bits(k), _bits(rk)) and np.array_equal(_bits(d), _bits(rd))
+    assert np.array_equal(got_c[0], ref_c[0])
+    assert gpu_ctx.total() == sum(len(k) for k, _ in ref)
