@@ -410,9 +410,8 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     // ---- extrema + row scan (the strip extremum kernel only sets the bits it accepts)
     HIPCHK(ctx, hipMemsetAsync(pt.row_count.p, 0, (size_t)pt.total_rows * 4, st));
     HIPCHK(ctx, hipMemsetAsync(pt.mask.p, 0, (size_t)moff * sizeof(uint32_t), st));
-    for (int o = 0; o < noct; o++)
-        HIPCHK(ctx, sgk::launch_extrema(pyr, pt.mask.as<uint32_t>(), pt.row_count.as<uint32_t>(),
-                                        fp, o, st));
+    HIPCHK(ctx, sgk::launch_extrema(pyr, pt.mask.as<uint32_t>(), pt.row_count.as<uint32_t>(),
+                                    fp, st));
     HIPCHK(ctx, sgk::launch_scan(pt.row_count.as<uint32_t>(), pt.row_base.as<uint32_t>(),
                                  pt.total_rows, pt.scan_tmp.as<uint32_t>(), st));
     HIPCHK(ctx, hipEventRecord(pt.ev[2], st));

@@ -51,10 +51,11 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         float* ds_dst, int ds_w, int ds_h, long long ds_img_stride,
                         hipStream_t stream);
 
-// Extremum detection for one octave, all d levels and all images: writes the keypoint bitmask
-// and adds per-row keypoint counts into row_count (rows ordered image, octave, level, row).
+// Extremum detection for all octaves, all d levels and all images (one launch): sets the
+// keypoint bits in the zeroed mask and adds per-row keypoint counts into the zeroed row_count
+// (rows ordered image, octave, level, row).
 hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
-                          const FeatureParams& fp, int octave, hipStream_t stream);
+                          const FeatureParams& fp, hipStream_t stream);
 
 // Exclusive scan of n uint32 values into out[0..n]; out[n] = total.  tmp needs
 // scan_tmp_words(n) words.

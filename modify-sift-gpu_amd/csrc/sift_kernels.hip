@@ -922,12 +922,24 @@ __global__ __launch_bounds__(256) void k_extrema(const float* __restrict__ pyr,
 // strip tile by tile (64 x 16 pixels + 1-pixel halo); the ND+1 Gaussian planes of tile t+1 are
 // loaded into registers while tile t is evaluated from LDS, so HBM loads overlap the tests.
 // Same DoG arithmetic (D_m = G_m - G_{m-1}), same key_test, same mask / count outputs.
-template <int ND>
+// All octaves in one launch: workgroups [block0[o], block0[o+1]) cover octave o, largest
+// first, so the small octaves fill the tail of the big one instead of paying their own launch
+// ramp-up and tail.
+struct ExtremaGrid {
+    int block0[kMaxOctaves + 1];
+    int rows_per_strip[kMaxOctaves];
+};
+
+template <int ND>   // ND = number of DoG planes = d + 2
 __global__ __launch_bounds__(256) void k_extrema_strip(const float* __restrict__ pyr,
                                                        uint32_t* __restrict__ mask,
                                                        uint32_t* __restrict__ row_count,
-                                                       const FeatureParams fp, int o,
-                                                       int rows_per_strip) {
+                                                       const FeatureParams fp,
+                                                       const ExtremaGrid eg) {
+    int o = 0;
+    while (o + 1 < fp.n_octaves && (int)blockIdx.x >= eg.block0[o + 1]) o++;
+    const int rows_per_strip = eg.rows_per_strip[o];
+    const int bid = blockIdx.x - eg.block0[o];
     constexpr int NP = (ET_Y + 2) * (ET_X + 2);   // halo tile positions
     constexpr int NM = (NP + 255) / 256;          // positions per thread
     constexpr int PLANE = (ET_Y + 2) * ES;
@@ -938,7 +950,7 @@ __global__ __launch_bounds__(256) void k_extrema_strip(const float* __restrict__
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int strips_x = (W + ET_X - 1) / ET_X;
     const int strips_y = (H + rows_per_strip - 1) / rows_per_strip;
-    const int sx = blockIdx.x % strips_x, rest = blockIdx.x / strips_x;
+    const int sx = bid % strips_x, rest = bid / strips_x;
     const int sy = rest % strips_y, b = rest / strips_y;
     const int x0 = sx * ET_X, yb = sy * rows_per_strip, ye = min(H, yb + rows_per_strip);
     const int ntiles = (ye - yb + ET_Y - 1) / ET_Y;
@@ -1637,35 +1649,47 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
 }
 
 hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
-                          const FeatureParams& fp, int octave, hipStream_t stream) {
-    const OctaveDesc& od = fp.oct[octave];
+                          const FeatureParams& fp, hipStream_t stream) {
     if (!(g_host_variant & 16)) {
-        const int strips_x = (od.wa + ET_X - 1) / ET_X;
-        const long long per_col = (long long)strips_x * fp.batch;
-        int nsy = (int)std::min<long long>((2048 + per_col - 1) / per_col, (od.h + ET_Y - 1) / ET_Y);
-        nsy = std::max(nsy, 1);
-        int rows = (od.h + nsy - 1) / nsy;
-        rows = (rows + ET_Y - 1) / ET_Y * ET_Y;
-        nsy = (od.h + rows - 1) / rows;
-        dim3 sgrid((unsigned)(strips_x * nsy * fp.batch));
+        ExtremaGrid eg{};
+        int nb = 0;
+        for (int o = 0; o < fp.n_octaves; o++) {
+            const OctaveDesc& od = fp.oct[o];
+            const int strips_x = (od.wa + ET_X - 1) / ET_X;
+            const long long per_col = (long long)strips_x * fp.batch;
+            int nsy = (int)std::min<long long>((2048 + per_col - 1) / per_col, (od.h + ET_Y - 1) / ET_Y);
+            nsy = std::max(nsy, 1);
+            int rows = (od.h + nsy - 1) / nsy;
+            rows = (rows + ET_Y - 1) / ET_Y * ET_Y;
+            nsy = (od.h + rows - 1) / rows;
+            eg.block0[o] = nb;
+            eg.rows_per_strip[o] = rows;
+            nb += strips_x * nsy * fp.batch;
+        }
+        eg.block0[fp.n_octaves] = nb;
         switch (fp.d + 2) {
 #define SGK_EXTS(ND) \
-    case ND: hipLaunchKernelGGL((k_extrema_strip<ND>), sgrid, dim3(256), 0, stream, pyr, mask, row_count, fp, octave, rows); break;
+    case ND: hipLaunchKernelGGL((k_extrema_strip<ND>), dim3(nb), dim3(256), 0, stream, pyr, mask, row_count, fp, eg); break;
             SGK_EXTS(3) SGK_EXTS(4) SGK_EXTS(5) SGK_EXTS(6) SGK_EXTS(7) SGK_EXTS(8)
             default: return hipErrorInvalidValue;
 #undef SGK_EXTS
         }
         return hipGetLastError();
     }
-    dim3 grid(((od.wa + ET_X - 1) / ET_X) * ((od.h + ET_Y - 1) / ET_Y) * fp.batch);
-    switch (fp.d + 2) {
+    for (int octave = 0; octave < fp.n_octaves; octave++) {
+        const OctaveDesc& od = fp.oct[octave];
+        dim3 grid(((od.wa + ET_X - 1) / ET_X) * ((od.h + ET_Y - 1) / ET_Y) * fp.batch);
+        switch (fp.d + 2) {
 #define SGK_EXT(ND) \
     case ND: hipLaunchKernelGGL((k_extrema<ND>), grid, dim3(256), 0, stream, pyr, mask, row_count, fp, octave); break;
-        SGK_EXT(3) SGK_EXT(4) SGK_EXT(5) SGK_EXT(6) SGK_EXT(7) SGK_EXT(8)
-        default: return hipErrorInvalidValue;
+            SGK_EXT(3) SGK_EXT(4) SGK_EXT(5) SGK_EXT(6) SGK_EXT(7) SGK_EXT(8)
+            default: return hipErrorInvalidValue;
 #undef SGK_EXT
+        }
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
     }
-    return hipGetLastError();
+    return hipSuccess;
 }
 
 static size_t scan_blocks(size_t n) { return (n + 1023) / 1024; }
