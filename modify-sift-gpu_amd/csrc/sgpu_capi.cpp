@@ -52,8 +52,10 @@ enum { T_UPLOAD, T_PYRAMID, T_DETECT, T_ORIENT, T_EXPAND, T_DESC, T_DOWNLOAD, T_
 struct Part {
     hipStream_t stream = nullptr;      // high priority: pyramid + detection
     hipStream_t stream_lo = nullptr;   // low priority: orientation, descriptors, readback
+    hipStream_t stream_aux = nullptr;  // high priority: pyramid octaves >= 1 beside octave 0
     size_t cand_hint = 0, feat_hint = 0;   // counts of the previous call (launch-grid sizing)
-    hipEvent_t ev[8] = {};   // start, pyramid, detect, orientation, expand, descriptor, end, (spare)
+    hipEvent_t ev[10] = {};  // start, pyramid, detect, orientation, expand, descriptor, end,
+                             // octave-1 base ready, octaves >= 1 done, (spare)
     int img0 = 0, n = 0;
     sgk::FeatureParams fp{};
     int total_rows = 0;
@@ -77,7 +79,8 @@ struct Part {
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
         if (stream_lo) (void)hipStreamDestroy(stream_lo);
-        stream = stream_lo = nullptr;
+        if (stream_aux) (void)hipStreamDestroy(stream_aux);
+        stream = stream_lo = stream_aux = nullptr;
     }
 };
 
@@ -255,6 +258,7 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     for (Part& pt : ctx->part) {
         if (hipStreamCreateWithPriority(&pt.stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+            hipStreamCreateWithPriority(&pt.stream_aux, hipStreamNonBlocking, prio_hi) != hipSuccess ||
             hipStreamCreateWithPriority(&pt.stream_lo, hipStreamNonBlocking, prio_lo) != hipSuccess) {
             sgpu_ctx_destroy(ctx);
             return SGPU_ENODEV;
@@ -277,6 +281,7 @@ int sgpu_ctx_destroy(sgpu_ctx* ctx) {
     for (Part& pt : ctx->part) {
         if (pt.stream) (void)hipStreamSynchronize(pt.stream);
         if (pt.stream_lo) (void)hipStreamSynchronize(pt.stream_lo);
+        if (pt.stream_aux) (void)hipStreamSynchronize(pt.stream_aux);
         pt.release();
     }
     DevBuf* bufs[] = {&ctx->input, &ctx->all_keys, &ctx->all_desc, &ctx->m_d1, &ctx->m_d2,
@@ -295,7 +300,7 @@ const char* sgpu_last_error(const sgpu_ctx* ctx) { return ctx ? ctx->err.c_str()
 // part's pyramid must wait for.  No host synchronisation.
 static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32, int stride,
                         hipEvent_t wait) {
-    hipStream_t st = pt.stream;
+    hipStream_t st = pt.stream;   // reassigned per stage below
     const sgpu_options& O = ctx->opt;
     const sgp::Schedule& S = ctx->sched;
     const int d = S.dog_level_num, nlev = S.level_num;
@@ -375,10 +380,16 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     const uint8_t* src8 = is_f32 ? nullptr : (const uint8_t*)src_in + (size_t)pt.img0 * img_elems;
     const float* srcf = is_f32 ? (const float*)src_in + (size_t)pt.img0 * img_elems : nullptr;
 
-    // ---- Gaussian pyramid (BuildPyramid, PyramidCU.cpp:979-1044)
+    // ---- Gaussian pyramid (BuildPyramid, PyramidCU.cpp:979-1044).  Octave 0 runs on the
+    // part's stream; octaves >= 1 run on the aux stream as soon as their base level (the
+    // decimated level d of octave 0) exists, so the small octaves overlap octave 0's last two
+    // levels instead of trailing them with launch-latency-bound kernels.
     float* pyr = pt.pyr.as<float>();
     sgk::Taps taps;
+    const bool two = noct > 1 && !(sgk::get_variant() & 16384);
     for (int o = 0; o < noct; o++) {
+        if (o == 1 && two) HIPCHK(ctx, hipStreamWaitEvent(pt.stream_aux, pt.ev[7], 0));
+        st = (o >= 1 && two) ? pt.stream_aux : pt.stream;
         const sgk::OctaveDesc& od = fp.oct[o];
         const long long npx = (long long)od.wa * od.h;
         float* lvl0 = pyr + od.gauss_off;
@@ -403,7 +414,13 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
             HIPCHK(ctx, sgk::launch_gauss(lvl0 + (k - 1) * od.level_stride, nullptr, od.wa, npx,
                                           lvl0 + k * od.level_stride, npx, od.wa, od.h, fw, taps,
                                           n, ds, dsw, dsh, ds_stride, st));
+            if (o == 0 && ds) HIPCHK(ctx, hipEventRecord(pt.ev[7], st));
         }
+    }
+    st = pt.stream;
+    if (two) {
+        HIPCHK(ctx, hipEventRecord(pt.ev[8], pt.stream_aux));
+        HIPCHK(ctx, hipStreamWaitEvent(st, pt.ev[8], 0));
     }
     HIPCHK(ctx, hipEventRecord(pt.ev[1], st));
 
