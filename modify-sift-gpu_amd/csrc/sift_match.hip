@@ -25,6 +25,16 @@ constexpr int kPanel = 128;      // A rows per workgroup (4 waves x 32)
 constexpr int kTile = 128;       // B columns per LDS tile
 constexpr int kLdsRow = 128 + 16;// bytes per staged B row (padding against bank conflicts)
 constexpr int kNeg = -(1 << 29); // "minus infinity" for running maxima (no overflow with offsets)
+constexpr int kNegCol = -(1 << 26);  // column term of a missing column: its dot stays far below
+                                     // every real one (|dot| < 2^23) and (dot << 3) fits in int32
+
+// v_med3_i32: the median of three.  With s <= m, med3(s, m, v) is the new second maximum after
+// seeing v (v > m -> m; s < v <= m -> v; v <= s -> s).
+__device__ __forceinline__ int med3i(int a, int b, int c) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 
 __global__ __launch_bounds__(256) void k_rowsum(const uint8_t* __restrict__ d, int n,
                                                 int* __restrict__ s, int scale, int bias) {
@@ -112,7 +122,7 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
 #pragma unroll
         for (int cb = 0; cb < 8; cb++) {
             const int col = tb + cb * 16 + l16;
-            const int ct = col < c_end ? col_term[col] : kNeg;
+            const int ct = col < c_end ? col_term[col] : kNegCol;
             acc[0][cb] = v4i{ct, ct, ct, ct};
             acc[1][cb] = acc[0][cb];
         }
@@ -128,21 +138,27 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
             }
         }
         // epilogue: fold the 2x8 tiles into the running top-2 (C layout: col = l16,
-        // row = quad*4 + i within the 16-row block)
+        // row = quad*4 + i within the 16-row block).  Values are folded as keys
+        // (dot << 3) | (7 - cb): one v_lshl_or, one v_max and one v_med3 per value; the key's
+        // low bits name the column block and the tile is recorded once per tile when the
+        // maximum moved.  Equal dots order by lower column first (the reference's strict '>'
+        // scan); the second key of an equal pair carries the same dot, so ties still reject.
 #pragma unroll
-        for (int cb = 0; cb < 8; cb++) {
-            const int col = tb + cb * 16 + l16;
+        for (int rb = 0; rb < 2; rb++)
 #pragma unroll
-            for (int rb = 0; rb < 2; rb++)
+            for (int i = 0; i < 4; i++) {
+                const int m0 = M[rb][i];
+                int m = m0, sv = S[rb][i];
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const int v = acc[rb][cb][i];
-                    const int m = M[rb][i];
-                    S[rb][i] = max(S[rb][i], min(m, v));   // med3(S, M, v) with S <= M
-                    I[rb][i] = v > m ? col : I[rb][i];
-                    M[rb][i] = max(m, v);
+                for (int cb = 0; cb < 8; cb++) {
+                    const int key = (acc[rb][cb][i] << 3) | (7 - cb);
+                    sv = med3i(sv, m, key);
+                    m = max(m, key);
                 }
-        }
+                I[rb][i] = m != m0 ? tb : I[rb][i];
+                M[rb][i] = m;
+                S[rb][i] = sv;
+            }
         __syncthreads();
         if (has_next) {
             buf ^= 1;
@@ -150,6 +166,16 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         }
         __syncthreads();
     }
+    // keys -> (dot, column): column = tile + 16 * (7 - low bits) + l16
+#pragma unroll
+    for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int k = M[rb][i];
+            I[rb][i] = I[rb][i] < 0 ? -1 : I[rb][i] + 16 * (7 - (k & 7)) + l16;
+            M[rb][i] = k >> 3;
+            S[rb][i] = S[rb][i] >> 3;
+        }
     // merge the 16 lanes that share a row (same quad): xor 1, 2, 4, 8
 #pragma unroll
     for (int off = 1; off < 16; off <<= 1) {
