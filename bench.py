@@ -149,7 +149,7 @@ def main():
         "features_per_image": local_feats / (B * args.steps),
         "stage_ms_per_step": {k: v / args.steps for k, v in stage_acc.items() if k != "match"},
         "roofline": {
-            "kernel": f"k_gauss_strip (separable Gaussian level; all {n_gauss} launches of a step, "
+            "kernel": f"k_gauss_pk2 (separable Gaussian level; all {n_gauss} launches of a step, "
                       "HIP events around them on the library's stream)",
             "bound": "hbm",
             "achieved": achieved,
@@ -185,9 +185,9 @@ def profiled_traffic(B, W, H, octaves):
     for path in reversed(files):
         try:
             s = json.load(open(path))
-            fam = "k_gauss_strip"
-            n = s["launches_per_extract"][fam]
-            b = s["fetch_bytes_per_extract"][fam] + s["write_bytes_per_extract"][fam]
+            fams = [f for f in s["launches_per_extract"] if f.startswith("k_gauss")]
+            n = sum(s["launches_per_extract"][f] for f in fams)
+            b = sum(s["fetch_bytes_per_extract"][f] + s["write_bytes_per_extract"][f] for f in fams)
             return b / n, os.path.relpath(path, ROOT)
         except (KeyError, ValueError, OSError):
             continue

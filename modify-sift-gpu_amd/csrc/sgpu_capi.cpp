@@ -380,13 +380,14 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     const uint8_t* src8 = is_f32 ? nullptr : (const uint8_t*)src_in + (size_t)pt.img0 * img_elems;
     const float* srcf = is_f32 ? (const float*)src_in + (size_t)pt.img0 * img_elems : nullptr;
 
-    // ---- Gaussian pyramid (BuildPyramid, PyramidCU.cpp:979-1044).  Octave 0 runs on the
-    // part's stream; octaves >= 1 run on the aux stream as soon as their base level (the
-    // decimated level d of octave 0) exists, so the small octaves overlap octave 0's last two
-    // levels instead of trailing them with launch-latency-bound kernels.
+    // ---- Gaussian pyramid (BuildPyramid, PyramidCU.cpp:979-1044).  Optionally (test hook,
+    // variant 16384) octaves >= 1 run on the aux stream as soon as their base level (the
+    // decimated level d of octave 0) exists, overlapping octave 0's last two levels.  That
+    // saves ~2% of the pyramid time but makes per-kernel durations overlap, so the shipped
+    // configuration keeps one stream and kernel times that add up to the stage time.
     float* pyr = pt.pyr.as<float>();
     sgk::Taps taps;
-    const bool two = noct > 1 && !(sgk::get_variant() & 16384);
+    const bool two = noct > 1 && (sgk::get_variant() & 16384);
     for (int o = 0; o < noct; o++) {
         if (o == 1 && two) HIPCHK(ctx, hipStreamWaitEvent(pt.stream_aux, pt.ev[7], 0));
         st = (o >= 1 && two) ? pt.stream_aux : pt.stream;

@@ -32,7 +32,8 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 // instead of strips, 32 scalar-FMA strip Gaussian instead of the packed one, 64 16-row packed
 // strip Gaussian (k_gauss_pk) instead of the 32-row one (k_gauss_pk2), 128 timing probe (filters
 // replaced by copies, results wrong), 256 element-wise instead of quad loads in k_gauss_pk2,
-// 4096 / 8192 two / four batch parts, 16384 all pyramid octaves on one stream (sgpu_capi.cpp).
+// 4096 / 8192 two / four batch parts, 16384 pyramid octaves >= 1 on a second stream
+// (sgpu_capi.cpp).
 __constant__ int g_variant;
 int g_host_variant = 0;   // host copy: selects launch configurations
 

@@ -37,15 +37,18 @@ def main():
     trace = _one(os.path.join(src, "trace", "**", "*kernel_trace.csv"))
     stats = _one(os.path.join(src, "trace", "**", "*kernel_stats.csv"))
     rows = list(csv.DictReader(open(trace)))
-    n_steps = sum(1 for r in rows if "k_gauss_strip<" in r["Kernel_Name"] and ", true>" in r["Kernel_Name"])
+    # one k_image_offsets launch per extract (per batch part: the bench runs one part)
+    n_steps = sum(1 for r in rows if "k_image_offsets" in r["Kernel_Name"])
     per_family = defaultdict(lambda: [0.0, 0])
     for r in rows:
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6   # ms
         f = family(r["Kernel_Name"])
         per_family[f][0] += d
         per_family[f][1] += 1
+    gauss = [f for f in per_family if f.startswith("k_gauss")]
     out = {
         "tag": tag,
+        "gauss_family": gauss,
         "extract_calls": n_steps,
         "ms_per_extract": {f: v[0] / n_steps for f, v in per_family.items() if v[1] >= n_steps},
         "launches_per_extract": {f: v[1] / n_steps for f, v in per_family.items() if v[1] >= n_steps},
@@ -61,7 +64,7 @@ def main():
             if r["Counter_Name"] != counter:
                 continue
             acc[family(r["Kernel_Name"])] += float(r["Counter_Value"]) * 1024.0   # kB -> B
-            if "k_gauss_strip<" in r["Kernel_Name"] and ", true>" in r["Kernel_Name"]:
+            if "k_image_offsets" in r["Kernel_Name"]:
                 calls += 1
         out[f"{kind}_bytes_per_extract"] = {f: v / max(calls, 1) for f, v in acc.items()}
     prof = os.path.join(ROOT, "profiles")
