@@ -941,8 +941,6 @@ __global__ __launch_bounds__(256) void k_extrema_strip(const float* __restrict__
     while (o + 1 < fp.n_octaves && (int)blockIdx.x >= eg.block0[o + 1]) o++;
     const int rows_per_strip = eg.rows_per_strip[o];
     const int bid = blockIdx.x - eg.block0[o];
-    constexpr int NP = (ET_Y + 2) * (ET_X + 2);   // halo tile positions
-    constexpr int NM = (NP + 255) / 256;          // positions per thread
     constexpr int PLANE = (ET_Y + 2) * ES;
     __shared__ float s_d[ND * PLANE];
     __shared__ uint16_t s_list[4 * 4 * (ND - 2) * 64];   // per-wave candidate lists
@@ -958,32 +956,47 @@ __global__ __launch_bounds__(256) void k_extrema_strip(const float* __restrict__
     const long long npx = (long long)W * H;
     const long long lstride = od.level_stride;
     const float* g0 = pyr + od.gauss_off + (long long)b * npx;
-    float stage[NM][ND + 1];
-    // Loads are unconditional (coordinates clamped into the image): halo positions outside the
-    // image are only ever neighbours of non-interior pixels, whose tests are skipped, so their
-    // values do not matter -- and a branch-free load stream keeps ~30 loads in flight per lane.
+    // Row-aligned loads: each wave instruction reads one aligned 64-float row segment of a plane
+    // (2 cache lines) -- wave w takes tile rows w, w+4, ... -- and 36 lanes fetch the two halo
+    // columns of the 18 rows.  Every thread keeps the same (row, column) slot for all d+3
+    // planes, so it forms the DoG differences itself.  Loads are unconditional (coordinates
+    // clamped into the image): halo positions outside the image are only ever neighbours of
+    // non-interior pixels, whose tests are skipped.
+    constexpr int NR = (ET_Y + 2 + 3) / 4;          // row slots per wave (5 for 18 rows)
+    float stage[NR][ND + 1], stage_h[ND + 1];
+    const bool has_h = tid < 2 * (ET_Y + 2);
+    const int h_ty = tid >> 1, h_tx = (tid & 1) ? ET_X + 1 : 0;
     auto load_tile = [&](int t) {
         const int y0 = yb + t * ET_Y;
+        const int gx = min(x0 + lane, W - 1);
 #pragma unroll
-        for (int m = 0; m < NM; m++) {
-            const int p = min(tid + 256 * m, NP - 1);
-            const int ty = p / (ET_X + 2), tx = p - ty * (ET_X + 2);
-            const int gy = clampi(y0 - 1 + ty, 0, H - 1), gx = clampi(x0 - 1 + tx, 0, W - 1);
+        for (int r = 0; r < NR; r++) {
+            const int ty = min(wave + 4 * r, ET_Y + 1);
+            const int gy = clampi(y0 - 1 + ty, 0, H - 1);
             const float* q = g0 + (long long)gy * W + gx;
 #pragma unroll
-            for (int mm = 0; mm <= ND; mm++) stage[m][mm] = q[mm * lstride];
+            for (int mm = 0; mm <= ND; mm++) stage[r][mm] = q[mm * lstride];
         }
+        const int hy = clampi(y0 - 1 + min(h_ty, ET_Y + 1), 0, H - 1);
+        const int hx = clampi(x0 - 1 + h_tx, 0, W - 1);
+        const float* q = g0 + (long long)hy * W + hx;
+#pragma unroll
+        for (int mm = 0; mm <= ND; mm++) stage_h[mm] = q[mm * lstride];
     };
     auto store_tile = [&]() {
 #pragma unroll
-        for (int m = 0; m < NM; m++) {
-            const int p = tid + 256 * m;
-            if (p < NP) {
-                const int ty = p / (ET_X + 2), tx = p - ty * (ET_X + 2);
+        for (int r = 0; r < NR; r++) {
+            const int ty = wave + 4 * r;
+            if (ty < ET_Y + 2) {
 #pragma unroll
                 for (int mm = 1; mm <= ND; mm++)
-                    s_d[(mm - 1) * PLANE + ty * ES + tx] = stage[m][mm] - stage[m][mm - 1];
+                    s_d[(mm - 1) * PLANE + ty * ES + lane + 1] = stage[r][mm] - stage[r][mm - 1];
             }
+        }
+        if (has_h) {
+#pragma unroll
+            for (int mm = 1; mm <= ND; mm++)
+                s_d[(mm - 1) * PLANE + h_ty * ES + h_tx] = stage_h[mm] - stage_h[mm - 1];
         }
     };
     load_tile(0);
