@@ -33,7 +33,7 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 // strip Gaussian (k_gauss_pk) instead of the 32-row one (k_gauss_pk2), 128 timing probe (filters
 // replaced by copies, results wrong), 256 element-wise instead of quad loads in k_gauss_pk2,
 // 4096 / 8192 two / four batch parts, 16384 pyramid octaves >= 1 on a second stream
-// (sgpu_capi.cpp).
+// (sgpu_capi.cpp), 65536 workgroup-tile strip extremum kernel instead of the wave-streaming one.
 __constant__ int g_variant;
 int g_host_variant = 0;   // host copy: selects launch configurations
 
@@ -1081,6 +1081,148 @@ __global__ __launch_bounds__(256) void k_extrema_strip(const float* __restrict__
 }
 
 // ------------------------------------------------------------------------------------------
+// Extremum detection, wave-streaming form (the shipped one).  Each WAVE owns a 64-column strip
+// segment of one image/octave and walks it row by row on its own -- no workgroup barriers, so
+// every wave keeps its loads in flight independently (a workgroup-synchronised tile walk
+// reached ~3.9 TB/s, the same read pattern without barriers ~5.9 TB/s, tests/microbench).
+//   * row y+1 of the d+3 Gaussian planes (64 columns + the two halo columns) is loaded into
+//     registers one step ahead, turned into the d+2 DoG rows (D_m = G_m - G_{m-1}) and written
+//     to a wave-private 4-row LDS ring;
+//   * the 3-wide row max/min of each DoG row is computed once and kept in registers for the
+//     three output rows it borders; a branch-free 3x3x3 max/min pre-filter selects candidates,
+//     which are compacted per wave (ballot + mbcnt) and given the exact ComputeKEY test
+//     (key_test) from the ring;
+//   * accepted pixels set their bit in the zeroed mask (atomicOr) and count in their row.
+struct ExtremaWaveGrid {
+    int wave0[kMaxOctaves + 1];        // first global wave of octave o
+    int seg_rows[kMaxOctaves];         // rows per strip segment
+    int nseg[kMaxOctaves];             // segments per strip column
+};
+
+template <int ND>   // ND = number of DoG planes = d + 2
+__global__ __launch_bounds__(256) void k_extrema_wave(const float* __restrict__ pyr,
+                                                      uint32_t* __restrict__ mask,
+                                                      uint32_t* __restrict__ row_count,
+                                                      const FeatureParams fp,
+                                                      const ExtremaWaveGrid eg) {
+    constexpr int RW = 68;                          // ring row: columns x0-1 .. x0+64 (+pad)
+    constexpr int NJ = ND - 2;
+    __shared__ float s_ring[4][ND][4][RW];          // [wave][plane][row & 3][column + 1]
+    __shared__ uint16_t s_list[4][NJ * 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int gw = blockIdx.x * 4 + wave;
+    if (gw >= eg.wave0[fp.n_octaves]) return;       // uniform per wave
+    int o = 0;
+    while (o + 1 < fp.n_octaves && gw >= eg.wave0[o + 1]) o++;
+    const OctaveDesc& od = fp.oct[o];
+    const int W = od.wa, H = od.h;
+    const int strips_x = (W + 63) / 64;
+    const int id = gw - eg.wave0[o];
+    const int sx = id % strips_x, rest = id / strips_x;
+    const int sg = rest % eg.nseg[o], b = rest / eg.nseg[o];
+    const int x0 = sx * 64;
+    const int ys = sg * eg.seg_rows[o], ye = min(H, ys + eg.seg_rows[o]);
+    const long long lstride = od.level_stride;
+    const float* g0 = pyr + od.gauss_off + (long long)b * W * H;
+    float(*ring)[4][RW] = s_ring[wave];
+    uint16_t* list = s_list[wave];
+
+    // this lane's columns: main x0 + lane; lanes 0 / 1 also fetch the halo columns x0-1 / x0+64
+    const int gx = min(x0 + lane, W - 1);
+    const bool halo = lane < 2;
+    const int hx = clampi(lane == 0 ? x0 - 1 : x0 + 64, 0, W - 1);
+    const int htx = lane == 0 ? 0 : 65;
+    float gm[ND + 1], gh[ND + 1];
+    auto fetch = [&](int y) {   // G row y (clamped) into registers
+        const float* q = g0 + (long long)clampi(y, 0, H - 1) * W;
+#pragma unroll
+        for (int m = 0; m <= ND; m++) gm[m] = q[gx + m * lstride];
+        if (halo) {
+#pragma unroll
+            for (int m = 0; m <= ND; m++) gh[m] = q[hx + m * lstride];
+        }
+    };
+    auto put = [&](int y) {     // DoG row y into the ring
+        float* r = &ring[0][y & 3][0];
+#pragma unroll
+        for (int m = 0; m < ND; m++) r[m * 4 * RW + lane + 1] = gm[m + 1] - gm[m];
+        if (halo) {
+#pragma unroll
+            for (int m = 0; m < ND; m++) r[m * 4 * RW + htx] = gh[m + 1] - gh[m];
+        }
+    };
+    // rolling 3-wide row max/min of DoG rows y-1 and y (per plane), refreshed per step
+    float hx0[ND], hn0[ND], hx1[ND], hn1[ND];
+    auto rowmm = [&](int y, float* mx, float* mn, float* cv) {
+#pragma unroll
+        for (int m = 0; m < ND; m++) {
+            const float* p = &ring[m][y & 3][lane];
+            const float a = p[0], c = p[1], e = p[2];
+            mx[m] = fmax_(fmax_(a, c), e);
+            mn[m] = fmin_(fmin_(a, c), e);
+            if (cv) cv[m] = c;
+        }
+    };
+    fetch(ys - 1);
+    put(ys - 1);
+    fetch(ys);
+    put(ys);
+    if (ys + 1 < ye + 1) fetch(ys + 1);
+    float cvx[ND];
+    rowmm(ys - 1, hx0, hn0, nullptr);
+    rowmm(ys, hx1, hn1, cvx);
+    const int x = x0 + lane;
+    for (int y = ys; y < ye; y++) {
+        put(y + 1);                                  // row y+1 arrived (fetched one step ago)
+        if (y + 2 < ye + 1) fetch(y + 2);            // next row in flight during this step
+        float hx2[ND], hn2[ND], cnx[ND];
+        rowmm(y + 1, hx2, hn2, cnx);
+        const bool interior = x > 0 && x < W - 1 && y > 0 && y < H - 1;
+        int ncand = 0;
+#pragma unroll
+        for (int j = 0; j < NJ; j++) {
+            const float v = cvx[j + 1];
+            float mx = hx0[j], mn = hn0[j];
+#pragma unroll
+            for (int m = j; m < j + 3; m++) {
+                mx = fmax_(mx, fmax_(fmax_(hx0[m], hx1[m]), hx2[m]));
+                mn = fmin_(mn, fmin_(fmin_(hn0[m], hn1[m]), hn2[m]));
+            }
+            const bool cand = interior && fabs_(v) > fp.t0 && (v >= mx || v <= mn);
+            const unsigned long long bal = __ballot(cand);
+            if (cand) {
+                const int pos = ncand + __builtin_amdgcn_mbcnt_hi(
+                                            (uint32_t)(bal >> 32),
+                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                list[pos] = (uint16_t)((j << 6) | lane);
+            }
+            ncand += __popcll(bal);
+        }
+        for (int c0 = 0; c0 < ncand; c0 += 64) {
+            if (c0 + lane < ncand) {
+                const int code = list[c0 + lane];
+                const int j = code >> 6, cl = code & 63;
+                auto get = [&](int m, int r, int c) { return ring[j + m][(y + r - 1) & 3][cl + c]; };
+                if (key_test(get, fp.t0, fp.t, fp.edge, fp.subpixel).result != 0.f) {
+                    const int xx = x0 + cl;
+                    uint32_t* mrow = mask + od.mask_off + j * od.mask_level_stride +
+                                     ((long long)b * H + y) * od.nwords;
+                    atomicOr(&mrow[xx >> 5], 1u << (xx & 31));
+                    atomicAdd(&row_count[(long long)b * fp.rows_per_image + fp.row_off[o] +
+                                         j * H + y], 1u);
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < ND; m++) {
+            hx0[m] = hx1[m]; hn0[m] = hn1[m];
+            hx1[m] = hx2[m]; hn1[m] = hn2[m];
+            cvx[m] = cnx[m];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Exclusive scan (uint32), 1024 elements per block.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     const int lane = threadIdx.x & 63;
@@ -1664,6 +1806,33 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
 
 hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
                           const FeatureParams& fp, hipStream_t stream) {
+    if (!(g_host_variant & (16 | 65536))) {
+        // one wave per (image, 64-column strip, row segment); ~32k waves in all
+        ExtremaWaveGrid eg{};
+        int nw = 0;
+        for (int o = 0; o < fp.n_octaves; o++) {
+            const OctaveDesc& od = fp.oct[o];
+            const int strips_x = (od.wa + 63) / 64;
+            const long long per_col = (long long)strips_x * fp.batch;
+            int nseg = (int)std::min<long long>(std::max<long long>(1, (32768 + per_col - 1) / per_col),
+                                                std::max(1, od.h / 16));
+            const int rows = (od.h + nseg - 1) / nseg;
+            nseg = (od.h + rows - 1) / rows;
+            eg.wave0[o] = nw;
+            eg.seg_rows[o] = rows;
+            eg.nseg[o] = nseg;
+            nw += strips_x * nseg * fp.batch;
+        }
+        eg.wave0[fp.n_octaves] = nw;
+        const unsigned nb = (unsigned)((nw + 3) / 4);
+        switch (fp.d + 2) {
+#define SGK_EXTW(ND)     case ND: hipLaunchKernelGGL((k_extrema_wave<ND>), dim3(nb), dim3(256), 0, stream, pyr, mask, row_count, fp, eg); break;
+            SGK_EXTW(3) SGK_EXTW(4) SGK_EXTW(5) SGK_EXTW(6) SGK_EXTW(7) SGK_EXTW(8)
+            default: return hipErrorInvalidValue;
+#undef SGK_EXTW
+        }
+        return hipGetLastError();
+    }
     if (!(g_host_variant & 16)) {
         ExtremaGrid eg{};
         int nb = 0;
