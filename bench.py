@@ -6,8 +6,9 @@ A step = one pass of the hot path (Gaussian pyramid -> DoG extrema -> orientatio
 descriptors, HIP kernels behind the C ABI of include/sgpu.h) over one batch of synthetic
 1920x1080 u8 images per GPU, already resident in HBM (staged once before timing).  Workload:
 the per-GPU shard of BASELINE config C3 (128 images per GPU) with the parameters of config C2
-(-fo 0 -no 4 -d 3).  Multi-GPU: one process per GPU, images sharded (weak scaling), RCCL only
-for the per-image feature-count all-gather.  Prints ONE JSON line on rank 0.
+(-fo 0 -no 4 -d 3).  Multi-GPU: one process per GPU, images sharded (weak scaling), RCCL (inside
+libsiftgpu, over xGMI) only for the per-image feature-count all-gather; torch.distributed
+(gloo, host) is the rendezvous.  Prints ONE JSON line on rank 0.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
 """
@@ -53,6 +54,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-match", action="store_true")
     ap.add_argument("--match-n", type=int, default=50000)
+    ap.add_argument("--dist-backend", default="rccl", choices=["rccl", "gloo"],
+                    help="rccl: the count all-gather runs on RCCL over xGMI inside libsiftgpu "
+                         "(the real run); gloo: host all-gather (rehearsal: ranks may then "
+                         "share one GPU)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -60,41 +65,54 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"note: WORLD_SIZE={world} differs from --gpus {args.gpus}", file=sys.stderr)
-    sgpu.lib()
+    sgpu.lib()   # libsiftgpu (and /opt/rocm's HIP runtime) before torch: torch never touches
+                 # the GPU here -- torch.distributed (gloo, host) is only the rendezvous
     dist = None
-    torch = None
+    device = local
     if world > 1:
-        import torch  # noqa: F811
         import torch.distributed as dist  # noqa: F811
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        # gloo announces its peers on stdout; keep stdout for the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
+        if args.dist_backend == "gloo":
+            device = local % max(1, sgpu.device_count())
 
     B, W, H = args.batch, args.width, args.height
     opts = default_options(octave_num=args.octaves)
-    ctx = sgpu.SiftContext(local, opts)
+    ctx = sgpu.SiftContext(device, opts)
+    rccl = world > 1 and args.dist_backend == "rccl"
+    if rccl:
+        # RCCL communicator of the per-rank contexts; the id travels over the host rendezvous
+        uid = [sgpu.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx.comm_init(world, rank, uid[0])
     # shard of the global batch: images [rank*B, (rank+1)*B), seeds 3000 + global index
     imgs = synth_batch(B, W, H, seed0=3000 + rank * B, unique=args.unique)
     ctx.stage(imgs)
 
-    counts_dev = None
-    gathered = None
-    if dist is not None:
-        counts_dev = torch.zeros(B, dtype=torch.int32, device=f"cuda:{local}")
-        gathered = torch.zeros(B * world, dtype=torch.int32, device=f"cuda:{local}")
-
     def step():
-        ctx.extract_staged()
+        ctx.extract_staged()   # returns after the GPU work of the step has completed
         counts = np.fromiter((ctx.count(i) for i in range(B)), np.int32, B)
-        if dist is not None:
-            counts_dev.copy_(torch.from_numpy(counts))
-            dist.all_gather_into_tensor(gathered, counts_dev)   # RCCL: global feature counts
+        if rccl:
+            ctx.allgather_i32(counts, world)   # RCCL over xGMI: global per-image feature counts
+        elif dist is not None:
+            import torch
+            out = [torch.zeros(B, dtype=torch.int32) for _ in range(world)]
+            dist.all_gather(out, torch.from_numpy(counts))
         return counts
 
     for _ in range(args.warmup):
         step()
     if dist is not None:
         dist.barrier()
-        torch.cuda.synchronize()
     pyr_ms = 0.0
     stage_acc = {}
     feats = 0
@@ -107,15 +125,18 @@ def main():
         for k, v in t.items():
             stage_acc[k] = stage_acc.get(k, 0.0) + v
     if dist is not None:
-        torch.cuda.synchronize()
         dist.barrier()
     elapsed = time.perf_counter() - t0
     local_feats = feats
-    if dist is not None:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+    if rccl:
+        elapsed = float(ctx.allreduce_f64(elapsed, op_max=True)[0])
+        feats = int(ctx.allreduce_f64(float(feats), op_max=False)[0])
+    elif dist is not None:
+        import torch
+        e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-        f = torch.tensor([feats], dtype=torch.int64, device=f"cuda:{local}")
+        f = torch.tensor([feats], dtype=torch.int64)
         dist.all_reduce(f)
         feats = int(f.item())
 

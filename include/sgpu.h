@@ -124,6 +124,21 @@ void sgpu_quantize_descriptors(const float* d, size_t count, uint8_t* out);
  * extract; times[8] = the last sgpu_match call. */
 int sgpu_last_timing(const sgpu_ctx* ctx, float* times, int n);
 
+/* ---- multi-GPU batch driver (no reference counterpart: the reference
+ * runs one SiftGPU per device thread, TestWin/MultiThreadSIFT.cpp:141-155).  One process per
+ * GPU, each with its own context; images are sharded and the only exchange is an RCCL
+ * all-gather (over xGMI) of the per-image feature counts.  Rendezvous: rank 0 creates the id,
+ * the launcher distributes it (bench.py uses torch.distributed on the host). */
+#define SGPU_COMM_ID_BYTES 128
+/* Create a communicator id (ncclGetUniqueId) into id[bytes], bytes >= SGPU_COMM_ID_BYTES. */
+int sgpu_comm_unique_id(uint8_t* id, int bytes);
+/* Join the communicator of nranks contexts (ncclCommInitRank, collective over the ranks). */
+int sgpu_comm_init(sgpu_ctx* ctx, int nranks, int rank, const uint8_t* id, int bytes);
+/* recv[r*n + i] = send of rank r, element i (host arrays; device staging + ncclAllGather). */
+int sgpu_comm_allgather_i32(sgpu_ctx* ctx, const int32_t* send, int n, int32_t* recv);
+/* In-place all-reduce of n doubles (op_max != 0: max, else sum). */
+int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
+
 /* ---- test hooks (parity tests read intermediate stages; not part of the drop-in surface) ---- */
 /* Select a kernel variant for in-process A/B timing (0 = shipped configuration). */
 int sgpu_debug_set_variant(int variant);

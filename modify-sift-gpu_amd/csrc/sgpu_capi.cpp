@@ -11,6 +11,7 @@
 // candidates overflowed its capacity, grows the buffers and re-runs that part.  (The reference
 // does four host round trips per DoG level, PyramidCU.cpp:783-813.)
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -108,6 +109,10 @@ struct sgpu_ctx {
     DevBuf m_d1, m_d2, m_part, m_terms, m_match, m_dist;
     std::vector<int> h_match;
     bool dist_ready = false;
+    // multi-GPU: RCCL communicator of this context's device (sgpu_comm_*)
+    ncclComm_t comm = nullptr;
+    int comm_ranks = 0, comm_rank = 0;
+    DevBuf c_buf;
 
     int fail(int code, const char* what, hipError_t e = hipSuccess) {
         err = what;
@@ -284,8 +289,10 @@ int sgpu_ctx_destroy(sgpu_ctx* ctx) {
         if (pt.stream_aux) (void)hipStreamSynchronize(pt.stream_aux);
         pt.release();
     }
+    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
     DevBuf* bufs[] = {&ctx->input, &ctx->all_keys, &ctx->all_desc, &ctx->m_d1, &ctx->m_d2,
-                      &ctx->m_part, &ctx->m_terms, &ctx->m_match, &ctx->m_dist};
+                      &ctx->m_part, &ctx->m_terms, &ctx->m_match, &ctx->m_dist, &ctx->c_buf};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i <= T_N; i++)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
@@ -653,6 +660,61 @@ int sgpu_match(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d2, int 
         }
     }
     return nmatch;
+}
+
+// ---- multi-GPU: one process per GPU, RCCL over xGMI ----
+int sgpu_comm_unique_id(uint8_t* id, int bytes) {
+    if (!id || bytes < (int)sizeof(ncclUniqueId)) return SGPU_EINVAL;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return SGPU_ENODEV;
+    memcpy(id, &u, sizeof(u));
+    return SGPU_OK;
+}
+
+int sgpu_comm_init(sgpu_ctx* ctx, int nranks, int rank, const uint8_t* id, int bytes) {
+    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks || bytes < (int)sizeof(ncclUniqueId))
+        return SGPU_EINVAL;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    const ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, u, rank);
+    if (r != ncclSuccess) {
+        ctx->comm = nullptr;
+        return ctx->fail(SGPU_ENODEV, ncclGetErrorString(r));
+    }
+    ctx->comm_ranks = nranks;
+    ctx->comm_rank = rank;
+    return SGPU_OK;
+}
+
+int sgpu_comm_allgather_i32(sgpu_ctx* ctx, const int32_t* send, int n, int32_t* recv) {
+    if (!ctx || !ctx->comm || n < 0 || (n && (!send || !recv))) return SGPU_EINVAL;
+    if (n == 0) return SGPU_OK;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const size_t total = (size_t)n * ctx->comm_ranks;
+    ALLOCCHK(ctx, ctx->c_buf.ensure((total + n) * sizeof(int32_t)));
+    int32_t* dsend = ctx->c_buf.as<int32_t>() + total;
+    HIPCHK(ctx, hipMemcpyAsync(dsend, send, n * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+    const ncclResult_t r = ncclAllGather(dsend, ctx->c_buf.p, (size_t)n, ncclInt32, ctx->comm, ctx->stream);
+    if (r != ncclSuccess) return ctx->fail(SGPU_ENODEV, ncclGetErrorString(r));
+    HIPCHK(ctx, hipMemcpyAsync(recv, ctx->c_buf.p, total * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return SGPU_OK;
+}
+
+int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max) {
+    if (!ctx || !ctx->comm || !v || n <= 0) return SGPU_EINVAL;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    ALLOCCHK(ctx, ctx->c_buf.ensure((size_t)n * sizeof(double)));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->c_buf.p, v, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    const ncclResult_t r = ncclAllReduce(ctx->c_buf.p, ctx->c_buf.p, (size_t)n, ncclFloat64,
+                                         op_max ? ncclMax : ncclSum, ctx->comm, ctx->stream);
+    if (r != ncclSuccess) return ctx->fail(SGPU_ENODEV, ncclGetErrorString(r));
+    HIPCHK(ctx, hipMemcpyAsync(v, ctx->c_buf.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return SGPU_OK;
 }
 
 int sgpu_stage_input(sgpu_ctx* ctx, const uint8_t* images, int n, int w, int h, int stride) {

@@ -25,7 +25,8 @@ C_API = [
     "sgpu_extract_f32", "sgpu_stage_input", "sgpu_feature_count", "sgpu_feature_total", "sgpu_copy_features",
     "sgpu_device_features", "sgpu_match", "sgpu_quantize_descriptors", "sgpu_last_timing",
     "sgpu_debug_geometry", "sgpu_debug_gaussian", "sgpu_debug_candidates",
-    "sgpu_debug_set_variant",
+    "sgpu_debug_set_variant", "sgpu_comm_unique_id", "sgpu_comm_init", "sgpu_comm_allgather_i32",
+    "sgpu_comm_allreduce_f64",
 ]
 
 _LIB = None
@@ -66,8 +67,21 @@ def lib():
         L.sgpu_debug_geometry.argtypes = [vp, P(c.c_int), vp, c.c_int]
         L.sgpu_debug_gaussian.argtypes = [vp, c.c_int, c.c_int, c.c_int, vp]
         L.sgpu_debug_candidates.argtypes = [vp, vp, vp, c.c_int, P(c.c_int)]
+        L.sgpu_comm_unique_id.argtypes = [vp, c.c_int]
+        L.sgpu_comm_init.argtypes = [vp, c.c_int, c.c_int, vp, c.c_int]
+        L.sgpu_comm_allgather_i32.argtypes = [vp, vp, c.c_int, vp]
+        L.sgpu_comm_allreduce_f64.argtypes = [vp, vp, c.c_int, c.c_int]
         _LIB = L
     return _LIB
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL communicator id (rank 0 creates it, the launcher distributes it)."""
+    buf = (ctypes.c_uint8 * 128)()
+    rc = lib().sgpu_comm_unique_id(buf, 128)
+    if rc != SGPU_OK:
+        raise RuntimeError(f"sgpu_comm_unique_id failed ({rc})")
+    return bytes(buf)
 
 
 def device_count() -> int:
@@ -189,6 +203,24 @@ class SiftContext:
         if m < 0:
             self._check(m, "sgpu_match")
         return out[:m]
+
+    # ---- multi-GPU (RCCL inside libsiftgpu)
+    def comm_init(self, nranks: int, rank: int, uid: bytes):
+        buf = (ctypes.c_uint8 * len(uid)).from_buffer_copy(uid)
+        self._check(lib().sgpu_comm_init(self._ctx, nranks, rank, buf, len(uid)), "sgpu_comm_init")
+
+    def allgather_i32(self, send: np.ndarray, nranks: int) -> np.ndarray:
+        a = np.ascontiguousarray(send, np.int32)
+        out = np.zeros(a.size * nranks, np.int32)
+        self._check(lib().sgpu_comm_allgather_i32(self._ctx, a.ctypes.data, a.size, out.ctypes.data),
+                    "sgpu_comm_allgather_i32")
+        return out
+
+    def allreduce_f64(self, v, op_max: bool) -> np.ndarray:
+        a = np.ascontiguousarray(np.atleast_1d(v), np.float64).copy()
+        self._check(lib().sgpu_comm_allreduce_f64(self._ctx, a.ctypes.data, a.size, 1 if op_max else 0),
+                    "sgpu_comm_allreduce_f64")
+        return a
 
     # ---- test hooks
     def geometry(self):

@@ -2,10 +2,11 @@
 
 Reference analogue: TestWin/MultiThreadSIFT.cpp:141-155 (one SiftGPU instance per device thread)
 and the per-port server processes of ServerSiftGPU (ServerSiftGPU.cpp:156-194).  Here each rank
-(torch.distributed, backend "nccl" = RCCL over xGMI on MI355X, "gloo" on CPU for tests) owns a
-contiguous shard of the batch and runs the whole hot path locally; the only exchange is one
+owns a contiguous shard of the batch and runs the whole hot path locally; the only exchange is one
 all-gather of the per-image feature counts, from which every rank knows the global output layout
-(image i's features start at offsets[i]).
+(image i's features start at offsets[i]).  On MI355X the all-gather is RCCL over xGMI inside
+libsiftgpu (sgpu_comm_allgather_i32, used by bench.py); gather_counts below is the same exchange
+through torch.distributed, used with gloo on CPU by the tests.
 """
 from __future__ import annotations
 

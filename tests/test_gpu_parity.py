@@ -358,3 +358,15 @@ def test_batch_parts_match_single_part(gpu_ctx, variant):
         assert np.array_equal(_bits(k), _bits(rk)) and np.array_equal(_bits(d), _bits(rd))
     assert np.array_equal(got_c[0], ref_c[0])
     assert gpu_ctx.total() == sum(len(k) for k, _ in ref)
+
+
+def test_rccl_single_rank_collectives(gpu_ctx):
+    """The RCCL communicator inside libsiftgpu (sgpu_comm_*), exercised with one rank on the
+    one-GPU box: the all-gather returns the send buffer, the all-reduces the values."""
+    uid = sgpu.comm_unique_id()
+    assert len(uid) == 128
+    gpu_ctx.comm_init(1, 0, uid)
+    counts = np.arange(37, dtype=np.int32) * 3
+    assert np.array_equal(gpu_ctx.allgather_i32(counts, 1), counts)
+    assert gpu_ctx.allreduce_f64([1.5, -2.0], op_max=True).tolist() == [1.5, -2.0]
+    assert gpu_ctx.allreduce_f64(4.25, op_max=False).tolist() == [4.25]
