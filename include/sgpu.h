@@ -105,6 +105,17 @@ int sgpu_copy_features(sgpu_ctx* ctx, int image, float* keys, float* descriptors
 int sgpu_device_features(sgpu_ctx* ctx, const float** keys, const float** descriptors,
                          const int64_t** image_offsets);
 
+/* Descriptors of caller-supplied keypoints on image `image` of the last extract (its pyramid is
+ * reused): SiftGPU::RunSIFT(num, keys, keys_have_orientation) (SiftGPU.cpp:287-291,
+ * SiftPyramid::SetKeypointList SiftPyramid.cpp:293-310, GenerateFeatureListTex
+ * PyramidCU.cpp:454-504).  keys: num x (x, y, scale, orientation) in image coordinates.  With
+ * has_orientation == 0 the strongest orientation is computed (ComputeOrientation_Kernel with
+ * existing_keypoint) and the keys are rewritten as DownloadKeypoints does.  Results (input order)
+ * replace the context's features: image `image` reports num features (sgpu_copy_features),
+ * every other image none. */
+int sgpu_extract_keypoints(sgpu_ctx* ctx, int image, const float* keys, int num,
+                           int has_orientation);
+
 /* Matcher.  d1 [n1][128], d2 [n2][128] u8 descriptors (the reference quantizes float
  * descriptors as (unsigned char)int(512*d+0.5), SiftMatchCU.cpp:87-101: see
  * sgpu_quantize_descriptors).  Replaces SiftMatchGPU::SetDescriptors + GetSiftMatch

@@ -587,6 +587,93 @@ static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
     return SGPU_OK;
 }
 
+// SiftGPU::RunSIFT(num, keys, keys_have_orientation) on image `image` of the last extract
+// (SiftPyramid::SetKeypointList with run_on_current, SiftPyramid.cpp:293-310): the keys are
+// assigned to levels as GenerateFeatureListTex does (PyramidCU.cpp:454-504, host side: a few
+// float ops per key), then the device computes the strongest orientation when the keys have
+// none and the descriptors, both written back in input order.  The results replace the
+// context's features: image `image` has `num` features, every other image none.
+int sgpu_extract_keypoints(sgpu_ctx* ctx, int image, const float* keys, int num,
+                           int has_orientation) {
+    if (!ctx || !keys || num <= 0) return SGPU_EINVAL;
+    if (ctx->batch <= 0 || image < 0 || image >= ctx->batch)
+        return ctx->fail(SGPU_EINVAL, "no extracted image to describe keypoints on");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const int p = ctx->part_of(image);
+    Part& pt = ctx->part[p];
+    const int b = image - pt.img0;
+    const sgpu_options& O = ctx->opt;
+    const sgp::Schedule& S = ctx->sched;
+    const int d = S.dog_level_num, noct = (int)ctx->oct.size();
+    const double twopi = 2.0 * 3.14159265358979323846;
+    const float sigma_half_step = powf(2.0f, 0.5f / d);
+    const float offset = O.lowe_origin ? 0.0f : 0.5f;
+    std::vector<float4> lf;
+    std::vector<int2> li;
+    std::vector<int> lidx;
+    float octave_sigma = 1.0f;
+    for (int i = 0; i < noct; i++, octave_sigma *= 2.0f)
+        for (int j = 0; j < d; j++) {
+            const float level_sigma = sgp::level_sigma(S, j + S.level_min + 1) * octave_sigma;
+            const float sigma_min = level_sigma / sigma_half_step;
+            const float sigma_max = level_sigma * sigma_half_step;
+            for (int k = 0; k < num; k++) {
+                const float* key = keys + 4 * (size_t)k;
+                const float sigmak = key[2];
+                if ((sigmak >= sigma_min && sigmak < sigma_max) ||
+                    (sigmak < sigma_min && i == 0 && j == 0) ||
+                    (sigmak > sigma_max && i == noct - 1 && j == d - 1)) {
+                    lf.push_back(make_float4((key[0] - offset) / octave_sigma + 0.5f,
+                                             (key[1] - offset) / octave_sigma + 0.5f,
+                                             key[2] / octave_sigma,
+                                             (float)std::fmod(twopi - key[3], twopi)));
+                    li.push_back(make_int2(b, i * d + j));
+                    lidx.push_back(k);
+                }
+            }
+        }
+    // the reference re-orders list entries i < num (_featureNum) only
+    const int m = std::min<int>(num, (int)lf.size());
+    hipStream_t st = ctx->stream;
+    const size_t cap = std::max<size_t>(lf.size(), (size_t)num);
+    ALLOCCHK(ctx, pt.feat.ensure(cap * sizeof(float4)));
+    ALLOCCHK(ctx, pt.feat_info.ensure(cap * sizeof(int2)));
+    ALLOCCHK(ctx, pt.keys.ensure((size_t)num * sizeof(float4)));
+    ALLOCCHK(ctx, pt.ocount.ensure((cap + 1) * sizeof(int)));   // list -> input index, count
+    if (O.descriptors) ALLOCCHK(ctx, pt.desc.ensure((size_t)num * 128 * sizeof(float)));
+    int* d_index = pt.ocount.as<int>();
+    uint32_t* d_m = pt.ocount.as<uint32_t>() + cap;
+    if (m > 0) {
+        HIPCHK(ctx, hipMemcpyAsync(pt.feat.p, lf.data(), m * sizeof(float4), hipMemcpyHostToDevice, st));
+        HIPCHK(ctx, hipMemcpyAsync(pt.feat_info.p, li.data(), m * sizeof(int2), hipMemcpyHostToDevice, st));
+        HIPCHK(ctx, hipMemcpyAsync(d_index, lidx.data(), m * sizeof(int), hipMemcpyHostToDevice, st));
+    }
+    const uint32_t mm = (uint32_t)m;
+    HIPCHK(ctx, hipMemcpyAsync(d_m, &mm, sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    // keys come back unchanged when they carry orientations (no DownloadKeypoints)
+    HIPCHK(ctx, hipMemcpyAsync(pt.keys.p, keys, (size_t)num * sizeof(float4), hipMemcpyHostToDevice, st));
+    if (!has_orientation)
+        HIPCHK(ctx, sgk::launch_orient_keys(pt.pyr.as<float>(), pt.feat.as<float4>(),
+                                            pt.feat_info.as<int2>(), d_index, m, pt.fp,
+                                            pt.keys.as<float4>(), st));
+    if (O.descriptors) {
+        HIPCHK(ctx, hipMemsetAsync(pt.desc.p, 0, (size_t)num * 128 * sizeof(float), st));
+        HIPCHK(ctx, sgk::launch_descriptor(pt.pyr.as<float>(), pt.feat.as<float4>(),
+                                           pt.feat_info.as<int2>(), d_m, std::max(m, 1), pt.fp,
+                                           pt.desc.as<float>(), st, d_index));
+    }
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    // the described image now owns the context's feature list
+    for (int q = 0; q < ctx->nparts; q++) {
+        Part& pq = ctx->part[q];
+        for (int i = 0; i <= pq.n; i++)
+            pq.img_off[i] = (q == p && pq.img0 + i > image) ? num : 0;
+    }
+    for (int i = 0; i <= ctx->batch; i++) ctx->img_off[i] = i > image ? num : 0;
+    ctx->gathered = false;
+    return SGPU_OK;
+}
+
 // SiftMatchGPU::SetDescriptors + GetSiftMatch (SiftMatchCU.cpp:71-179) in one call.
 int sgpu_match(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d2, int n2,
                float distmax, float ratiomax, int mbm, int max_match, int* out_pairs,

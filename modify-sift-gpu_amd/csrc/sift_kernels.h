@@ -78,10 +78,17 @@ hipError_t launch_expand(const float4* cand, const int2* info, const uint32_t* e
                          float4* feat, int2* feat_info, float4* keys, hipStream_t stream);
 
 // Descriptors (+ normalisation) of the expanded features; n_feat_cap sizes the grid (one wave
-// per feature), the kernel grid-strides over *n_feat_dev.
+// per feature), the kernel grid-strides over *n_feat_dev.  out_index (optional): feature e's
+// descriptor goes to row out_index[e].
 hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* feat_info,
                              const uint32_t* n_feat_dev, int n_feat_cap, const FeatureParams& fp,
-                             float* desc, hipStream_t stream);
+                             float* desc, hipStream_t stream, const int* out_index = nullptr);
+
+// Caller-supplied keypoints: strongest orientation into feat[e].w (num_orientation != 0, else
+// 0) and the image-coordinate key at keys_out[index[e]].
+hipError_t launch_orient_keys(const float* pyr, float4* feat, const int2* feat_info,
+                              const int* index, int n, const FeatureParams& fp, float4* keys_out,
+                              hipStream_t stream);
 
 // Per-image feature offsets: off[b] = eoff[min(row_base[b * rows_per_image], cap)] for b in
 // [0, batch] (cap = candidate capacity; the clamp only matters when the candidates overflowed).

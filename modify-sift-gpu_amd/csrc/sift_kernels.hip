@@ -1365,39 +1365,15 @@ struct Walk {
 // lanes evaluate consecutive window samples (gradient, Gaussian weight, bin) in parallel and
 // every lane then applies the quad's 4 votes in the reference's (y, x) order to the keypoint's
 // 36-bin histogram in LDS, so each bin sees exactly the reference's sequence of float adds.
-__device__ __forceinline__ void orientation_one(uint32_t f, int sub, float* vote_l,
-                                                const float* __restrict__ pyr,
-                                                const uint32_t* __restrict__ mask,
-                                                const uint32_t* __restrict__ row_base,
-                                                int total_rows, const FeatureParams& fp,
-                                                float4* __restrict__ out4,
-                                                int2* __restrict__ info,
-                                                uint32_t* __restrict__ ocount) {
-    const KeyLoc L = locate(f, row_base, total_rows, mask, fp);
-    const KeyOut kv = key_at(pyr, fp, L);
-    const OctaveDesc& od = fp.oct[L.o];
+// Orientation histogram of ComputeOrientation_Kernel (ProgramCU.cu:857-903) for a keypoint
+// (kx, ky, kz) of Gaussian level g (W x H): the quad's 4 lanes evaluate consecutive window
+// samples and every lane applies the 4 votes in the reference's (y, x) order to the 36-bin LDS
+// histogram; returns the 6-times smoothed histogram in vote[0..36] (vote[36] = vote[0]).
+__device__ __forceinline__ void orientation_hist(const float* __restrict__ g, int W, int H,
+                                                 float kx, float ky, float kz,
+                                                 const FeatureParams& fp, int sub, float* vote_l,
+                                                 float (&vote)[37]) {
     const float ten_degree_per_radius = (float)5.7295779513082320876798154814105;
-    const float radius_per_ten_degrees = (float)(1.0 / 5.7295779513082320876798154814105);
-
-    float kx = L.col + 0.5f, ky = L.row + 0.5f, kz = fp.level_sigma[L.j];
-    if (fp.subpixel) {
-        kx += kv.dx;
-        ky += kv.dy;
-        kz *= pow_(fp.sigma_step, kv.ds);
-    }
-    if (fp.keep_sign) kz *= kv.result;
-    if (sub == 0) info[f] = make_int2(L.b, L.o * fp.d + L.j);
-    if (fp.num_orientation == 0) {
-        if (sub == 0) {
-            out4[f] = make_float4(kx, ky, kz, 0.0f);
-            ocount[f] = 1;
-        }
-        return;
-    }
-    // gradient of Gaussian level 1 + j (PyramidCU.cpp:1204)
-    const float* g = pyr + od.gauss_off + (long long)(1 + L.j) * od.level_stride +
-                     (long long)L.b * od.wa * od.h;
-    const int W = od.wa, H = od.h;
     const float gsigma = kz * fp.gaussian_factor;
     const float win = fabs_(kz) * fp.sample_factor;
     const float dist_threshold = (float)((double)(win * win) + 0.5);
@@ -1437,7 +1413,6 @@ __device__ __forceinline__ void orientation_one(uint32_t f, int sub, float* vote
         if (b2 >= 0) vote_l[b2] += w2;
         if (b3 >= 0) vote_l[b3] += w3;
     }
-    float vote[37];
 #pragma unroll
     for (int i = 0; i < 36; ++i) vote[i] = vote_l[i];
     const float one_third = (float)(1.0 / 3.0);
@@ -1453,21 +1428,62 @@ __device__ __forceinline__ void orientation_one(uint32_t f, int sub, float* vote
         }
     }
     vote[36] = vote[0];
+}
+
+// The strongest orientation (ProgramCU.cu:904-919: num_orientation == 1 or a caller-supplied
+// keypoint list), in radians of the reference's internal convention.
+__device__ __forceinline__ float strongest_orientation(const float (&vote)[37]) {
+    const float radius_per_ten_degrees = (float)(1.0 / 5.7295779513082320876798154814105);
+    int index_max = 0;
+    float max_vote = vote[0];
+#pragma unroll
+    for (int i = 1; i < 36; ++i) {
+        index_max = vote[i] > max_vote ? i : index_max;
+        max_vote = fmax_(max_vote, vote[i]);
+    }
+    float pre = vote[35], next = vote[1];
+#pragma unroll
+    for (int i = 1; i < 36; ++i)
+        if (i == index_max) { pre = vote[i - 1]; next = vote[i + 1]; }
+    const float off = 0.5f * ((next - pre) * (1.0f / (max_vote + max_vote - next - pre)));
+    return radius_per_ten_degrees * (index_max + 0.5f + off);
+}
+
+__device__ __forceinline__ void orientation_one(uint32_t f, int sub, float* vote_l,
+                                                const float* __restrict__ pyr,
+                                                const uint32_t* __restrict__ mask,
+                                                const uint32_t* __restrict__ row_base,
+                                                int total_rows, const FeatureParams& fp,
+                                                float4* __restrict__ out4,
+                                                int2* __restrict__ info,
+                                                uint32_t* __restrict__ ocount) {
+    const KeyLoc L = locate(f, row_base, total_rows, mask, fp);
+    const KeyOut kv = key_at(pyr, fp, L);
+    const OctaveDesc& od = fp.oct[L.o];
+
+    float kx = L.col + 0.5f, ky = L.row + 0.5f, kz = fp.level_sigma[L.j];
+    if (fp.subpixel) {
+        kx += kv.dx;
+        ky += kv.dy;
+        kz *= pow_(fp.sigma_step, kv.ds);
+    }
+    if (fp.keep_sign) kz *= kv.result;
+    if (sub == 0) info[f] = make_int2(L.b, L.o * fp.d + L.j);
+    if (fp.num_orientation == 0) {
+        if (sub == 0) {
+            out4[f] = make_float4(kx, ky, kz, 0.0f);
+            ocount[f] = 1;
+        }
+        return;
+    }
+    // gradient of Gaussian level 1 + j (PyramidCU.cpp:1204)
+    const float* g = pyr + od.gauss_off + (long long)(1 + L.j) * od.level_stride +
+                     (long long)L.b * od.wa * od.h;
+    float vote[37];
+    orientation_hist(g, od.wa, od.h, kx, ky, kz, fp, sub, vote_l, vote);
     if (sub != 0) return;
     if (fp.num_orientation == 1) {
-        int index_max = 0;
-        float max_vote = vote[0];
-#pragma unroll
-        for (int i = 1; i < 36; ++i) {
-            index_max = vote[i] > max_vote ? i : index_max;
-            max_vote = fmax_(max_vote, vote[i]);
-        }
-        float pre = vote[35], next = vote[1];
-#pragma unroll
-        for (int i = 1; i < 36; ++i)
-            if (i == index_max) { pre = vote[i - 1]; next = vote[i + 1]; }
-        const float off = 0.5f * ((next - pre) * (1.0f / (max_vote + max_vote - next - pre)));
-        out4[f] = make_float4(kx, ky, kz, radius_per_ten_degrees * (index_max + 0.5f + off));
+        out4[f] = make_float4(kx, ky, kz, strongest_orientation(vote));
         ocount[f] = 1;
         return;
     }
@@ -1581,7 +1597,7 @@ __device__ __forceinline__ void descriptor_one(uint32_t e, int lane,
                                                const float4* __restrict__ feat,
                                                const int2* __restrict__ feat_info,
                                                const FeatureParams& fp,
-                                               float* __restrict__ desc) {
+                                               float* __restrict__ desc, uint32_t out) {
     // one wave per feature: lanes 4c..4c+3 own grid cell c (the reference's 16 threads per
     // feature, ProgramCU.cu:1017-1021); the quad evaluates consecutive window samples in
     // parallel and every lane applies the 4 contributions in the reference's (y, x) order, so
@@ -1737,7 +1753,7 @@ __device__ __forceinline__ void descriptor_one(uint32_t e, int lane,
         for (int i = 0; i < 8; i++) des[i] *= norm2;
     }
     if (sub < 2) {
-        float4* dst = reinterpret_cast<float4*>(desc + (size_t)e * 128 + cell * 8 + sub * 4);
+        float4* dst = reinterpret_cast<float4*>(desc + (size_t)out * 128 + cell * 8 + sub * 4);
         *dst = sub == 0 ? make_float4(des[0], des[1], des[2], des[3])
                         : make_float4(des[4], des[5], des[6], des[7]);
     }
@@ -1749,11 +1765,52 @@ __global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ py
                                                     const int2* __restrict__ feat_info,
                                                     const uint32_t* __restrict__ n_feat_dev,
                                                     const FeatureParams fp,
-                                                    float* __restrict__ desc) {
+                                                    float* __restrict__ desc,
+                                                    const int* __restrict__ out_index) {
     const int lane = threadIdx.x & 63;
     const uint32_t n = *n_feat_dev;
-    for (uint32_t e = blockIdx.x * 4 + (threadIdx.x >> 6); e < n; e += gridDim.x * 4)
-        descriptor_one(e, lane, pyr, feat, feat_info, fp, desc);   // uniform per wave
+    for (uint32_t e = blockIdx.x * 4 + (threadIdx.x >> 6); e < n; e += gridDim.x * 4)   // uniform per wave
+        descriptor_one(e, lane, pyr, feat, feat_info, fp, desc,
+                       out_index ? (uint32_t)out_index[e] : e);
+}
+
+// Caller-supplied keypoints (SiftGPU::RunSIFT(num, keys, keys_have_orientation),
+// SiftPyramid.cpp:83-89, 129-147, 167-177): feat holds the keypoint list in octave coordinates,
+// grouped by level as GenerateFeatureListTex (PyramidCU.cpp:454-504) builds it.  The strongest
+// orientation (ComputeOrientation_Kernel with existing_keypoint, ProgramCU.cu:830-833, 904)
+// replaces feat.w, and the keys are rewritten in image coordinates at keys_out[index[e]]
+// (DownloadKeypoints, PyramidCU.cpp:701-751).
+__global__ __launch_bounds__(256) void k_orient_keys(const float* __restrict__ pyr,
+                                                     float4* __restrict__ feat,
+                                                     const int2* __restrict__ feat_info,
+                                                     const int* __restrict__ index, int n,
+                                                     const FeatureParams fp,
+                                                     float4* __restrict__ keys_out) {
+    __shared__ float s_vote[64 * 37];
+    const int sub = threadIdx.x & 3, slot = threadIdx.x >> 2;
+    float* vote_l = s_vote + slot * 37;
+    const double twopi = 2.0 * 3.14159265358979323846;
+    for (int e = blockIdx.x * 64 + slot; e < n; e += gridDim.x * 64) {   // uniform per quad
+        const float4 k = feat[e];
+        const int2 in = feat_info[e];
+        const int o = in.y / fp.d, j = in.y - o * fp.d;
+        const OctaveDesc& od = fp.oct[o];
+        float angle = 0.0f;
+        if (fp.num_orientation != 0) {
+            const float* g = pyr + od.gauss_off + (long long)(1 + j) * od.level_stride +
+                             (long long)in.x * od.wa * od.h;
+            float vote[37];
+            orientation_hist(g, od.wa, od.h, k.x, k.y, k.z, fp, sub, vote_l, vote);
+            angle = strongest_orientation(vote);
+        }
+        if (sub == 0) {
+            feat[e].w = angle;
+            const float os = (float)(1 << o);
+            keys_out[index[e]] = make_float4(os * (k.x - 0.5f) + fp.origin_offset,
+                                             os * (k.y - 0.5f) + fp.origin_offset, os * k.z,
+                                             (float)fmod(twopi - (double)angle, twopi));
+        }
+    }
 }
 
 __global__ void k_image_offsets(const uint32_t* __restrict__ row_base,
@@ -1925,13 +1982,23 @@ hipError_t launch_expand(const float4* cand, const int2* info, const uint32_t* e
     return hipGetLastError();
 }
 
+hipError_t launch_orient_keys(const float* pyr, float4* feat, const int2* feat_info,
+                              const int* index, int n, const FeatureParams& fp, float4* keys_out,
+                              hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)std::min((n + 63) / 64, 4096);
+    hipLaunchKernelGGL(k_orient_keys, dim3(grid), dim3(256), 0, stream, pyr, feat, feat_info,
+                       index, n, fp, keys_out);
+    return hipGetLastError();
+}
+
 hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* feat_info,
                              const uint32_t* n_feat_dev, int n_feat_cap, const FeatureParams& fp,
-                             float* desc, hipStream_t stream) {
+                             float* desc, hipStream_t stream, const int* out_index) {
     if (n_feat_cap <= 0) return hipSuccess;
     const unsigned grid = (unsigned)std::min(((long long)n_feat_cap + 3) / 4, 65536LL);
     hipLaunchKernelGGL(k_descriptor, dim3(grid), dim3(256), 0, stream, pyr, feat, feat_info,
-                       n_feat_dev, fp, desc);
+                       n_feat_dev, fp, desc, out_index);
     return hipGetLastError();
 }
 

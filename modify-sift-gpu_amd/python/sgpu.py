@@ -26,7 +26,7 @@ C_API = [
     "sgpu_device_features", "sgpu_match", "sgpu_quantize_descriptors", "sgpu_last_timing",
     "sgpu_debug_geometry", "sgpu_debug_gaussian", "sgpu_debug_candidates",
     "sgpu_debug_set_variant", "sgpu_comm_unique_id", "sgpu_comm_init", "sgpu_comm_allgather_i32",
-    "sgpu_comm_allreduce_f64",
+    "sgpu_comm_allreduce_f64", "sgpu_extract_keypoints",
 ]
 
 _LIB = None
@@ -67,6 +67,7 @@ def lib():
         L.sgpu_debug_geometry.argtypes = [vp, P(c.c_int), vp, c.c_int]
         L.sgpu_debug_gaussian.argtypes = [vp, c.c_int, c.c_int, c.c_int, vp]
         L.sgpu_debug_candidates.argtypes = [vp, vp, vp, c.c_int, P(c.c_int)]
+        L.sgpu_extract_keypoints.argtypes = [vp, c.c_int, vp, c.c_int, c.c_int]
         L.sgpu_comm_unique_id.argtypes = [vp, c.c_int]
         L.sgpu_comm_init.argtypes = [vp, c.c_int, c.c_int, vp, c.c_int]
         L.sgpu_comm_allgather_i32.argtypes = [vp, vp, c.c_int, vp]
@@ -163,6 +164,15 @@ class SiftContext:
                 raise TypeError(a.dtype)
         self._check(rc, "sgpu_extract")
         self.batch = n
+        return self
+
+    def extract_keypoints(self, keys: np.ndarray, has_orientation: bool = True, image: int = 0):
+        """Descriptors of caller-supplied keys [n, 4] (x, y, scale, orientation) on image
+        `image` of the last extract (SiftGPU::RunSIFT(num, keys, keys_have_orientation))."""
+        k = np.ascontiguousarray(keys, np.float32).reshape(-1, 4)
+        self._check(lib().sgpu_extract_keypoints(self._ctx, image, k.ctypes.data, len(k),
+                                                 1 if has_orientation else 0),
+                    "sgpu_extract_keypoints")
         return self
 
     def count(self, image: int = 0) -> int:

@@ -299,11 +299,13 @@ inline float u2f(uint32_t u) { return as_float(u); }
 
 // --- ComputeOrientation_Kernel (ProgramCU.cu:813-977) for one list entry.  grad is the
 //     float2 gradient image of G[1+j] (texture point sampling at x = k + 0.5 -> texel k).
+void orientation_key(Key4 key, const std::vector<float>& grad, int W, int H,
+                     float gaussian_factor, float sample_factor, int num_orientation,
+                     int existing, int circular, float* out);
+
 void orientation(const Candidate& c, const std::vector<float>& grad, int W, int H, float sigma,
                  float sigma_step, float gaussian_factor, float sample_factor,
                  int num_orientation, int subpixel, int keepsign, int circular, float* out) {
-    const float ten_degree_per_radius = (float)5.7295779513082320876798154814105;
-    const float radius_per_ten_degrees = (float)(1.0 / 5.7295779513082320876798154814105);
     Key4 key;
     key.x = c.col + 0.5f;
     key.y = c.row + 0.5f;
@@ -315,6 +317,18 @@ void orientation(const Candidate& c, const std::vector<float>& grad, int W, int 
         key.z *= pow_(sigma_step, c.ds);
     }
     (void)keepsign;  // -sign multiplies by the extremum sign; handled by the caller
+    orientation_key(key, grad, W, H, gaussian_factor, sample_factor, num_orientation, 0,
+                    circular, out);
+}
+
+// The kernel body after the key is formed.  existing != 0: a caller-supplied keypoint list
+// (texDataF4 input, ProgramCU.cu:830-833), which keeps only the strongest orientation
+// (ProgramCU.cu:904: num_orientation == 1 || existing_keypoint).
+void orientation_key(Key4 key, const std::vector<float>& grad, int W, int H,
+                     float gaussian_factor, float sample_factor, int num_orientation,
+                     int existing, int circular, float* out) {
+    const float ten_degree_per_radius = (float)5.7295779513082320876798154814105;
+    const float radius_per_ten_degrees = (float)(1.0 / 5.7295779513082320876798154814105);
     if (num_orientation == 0) {
         out[0] = key.x; out[1] = key.y; out[2] = key.z; out[3] = 0.0f;
         return;
@@ -355,7 +369,7 @@ void orientation(const Candidate& c, const std::vector<float>& grad, int W, int 
     vote[36] = vote[0];
     // __fdividef(a, b) is stated as a * (1/b) (two roundings) on both sides
     auto fdiv = [](float a, float b) { return a * (1.0f / b); };
-    if (num_orientation == 1) {
+    if (num_orientation == 1 || existing) {
         int index_max = 0;
         float max_vote = vote[0];
         for (int i = 1; i < 36; ++i) {
@@ -597,6 +611,101 @@ Result extract(const uint8_t* img, int w, int h, int stride, const sgpu_options&
     return R;
 }
 
+// --- Caller-supplied keypoints: SiftPyramid::SetKeypointList / SiftGPU::RunSIFT(num, keys,
+//     keys_have_orientation) (SiftPyramid.cpp:293-310, SiftGPU.cpp:287-291).  The pyramid of the
+//     image is built as usual, then (SiftPyramid.cpp:83-89, 129-147, 167-177):
+//       GenerateFeatureListTex (PyramidCU.cpp:454-504): each key goes to the level whose
+//         [sigma / 2^(0.5/d), sigma * 2^(0.5/d)) holds its scale (below the first / above the
+//         last level: the first / last level), in octave coordinates;
+//       ComputeOrientation with existing_keypoint (strongest orientation only) unless the keys
+//         carry orientations; DownloadKeypoints (PyramidCU.cpp:701-751) then rewrites the keys;
+//       GetFeatureDescriptors (PyramidCU.cpp:413-450) per level, put back into input order.
+std::vector<float> describe_keys(const uint8_t* img, int w, int h, int stride,
+                                 const sgpu_options& opt, const float* keys, int num,
+                                 int has_orientation, std::vector<float>* keys_out) {
+    sgpu_options o2 = opt;
+    o2.descriptors = 0;
+    Result R = extract(img, w, h, stride, o2, true);
+    sgp::Options po;
+    po.filter_width_factor = opt.filter_width_factor;
+    po.dog_level_num = opt.dog_level_num;
+    po.dog_threshold = opt.dog_threshold;
+    po.edge_threshold = opt.edge_threshold;
+    const sgp::Schedule S = sgp::make_schedule(po);
+    const int d = S.dog_level_num, noct = (int)R.octaves.size();
+    const double twopi = 2.0 * 3.14159265358979323846;
+    const float sigma_half_step = powf(2.0f, 0.5f / d);
+    const float offset = opt.lowe_origin ? 0.0f : 0.5f;
+    struct Entry { float k[4]; int index, octave, level; };
+    std::vector<Entry> list;
+    float octave_sigma = 1.0f;
+    for (int i = 0; i < noct; i++, octave_sigma *= 2.0f)
+        for (int j = 0; j < d; j++) {
+            const float level_sigma = sgp::level_sigma(S, j + S.level_min + 1) * octave_sigma;
+            const float sigma_min = level_sigma / sigma_half_step;
+            const float sigma_max = level_sigma * sigma_half_step;
+            for (int k = 0; k < num; k++) {
+                const float* key = keys + 4 * k;
+                const float sigmak = key[2];
+                if ((sigmak >= sigma_min && sigmak < sigma_max) ||
+                    (sigmak < sigma_min && i == 0 && j == 0) ||
+                    (sigmak > sigma_max && i == noct - 1 && j == d - 1)) {
+                    Entry e;
+                    e.k[0] = (key[0] - offset) / octave_sigma + 0.5f;
+                    e.k[1] = (key[1] - offset) / octave_sigma + 0.5f;
+                    e.k[2] = key[2] / octave_sigma;
+                    e.k[3] = (float)std::fmod(twopi - key[3], twopi);
+                    e.index = k;
+                    e.octave = i;
+                    e.level = j;
+                    list.push_back(e);
+                }
+            }
+        }
+    // gradients of G[1+j] of every octave
+    std::vector<std::vector<std::vector<float>>> grad(noct, std::vector<std::vector<float>>(d));
+    for (int o = 0; o < noct; o++)
+        for (int j = 0; j < d; j++) {
+            Image dog;
+            compute_dog(R.gauss[o][1 + j], R.gauss[o][j], &dog, &grad[o][j]);
+        }
+    const int num_orientation = opt.fixed_orientation ? 0 : opt.max_orientation;
+    if (!has_orientation) {
+        for (Entry& e : list) {
+            const sgp::Octave& oc = R.octaves[e.octave];
+            Key4 key{e.k[0], e.k[1], e.k[2], e.k[3]};
+            float out[4];
+            orientation_key(key, grad[e.octave][e.level], oc.wa, oc.h,
+                            opt.orientation_gaussian_factor,
+                            opt.orientation_gaussian_factor * opt.orientation_window_factor,
+                            num_orientation, 1, opt.circular_window, out);
+            e.k[3] = out[3];
+        }
+    }
+    // DownloadKeypoints + the descriptor re-ordering: list position i goes back to
+    // keypoint_index[i] for i < _featureNum (= num)
+    keys_out->assign(keys, keys + 4 * (size_t)num);
+    std::vector<float> desc((size_t)num * 128, 0.0f);
+    const int m = std::min<int>(num, (int)list.size());
+    for (int i = 0; i < m; i++) {
+        const Entry& e = list[i];
+        const float os = (float)(1 << e.octave);
+        if (!has_orientation) {
+            float* kk = keys_out->data() + 4 * (size_t)e.index;
+            kk[0] = os * (e.k[0] - 0.5f) + offset;
+            kk[1] = os * (e.k[1] - 0.5f) + offset;
+            kk[2] = os * e.k[2];
+            kk[3] = (float)std::fmod(twopi - e.k[3], twopi);
+        }
+        if (opt.descriptors) {
+            const sgp::Octave& oc = R.octaves[e.octave];
+            descriptor(e.k, grad[e.octave][e.level], oc.wa, oc.h, opt.descriptor_window_factor,
+                       opt.normalized, desc.data() + 128 * (size_t)e.index);
+        }
+    }
+    return desc;
+}
+
 float match_distance(int dot) {
     // RowMatch_Kernel / ColMatch_Kernel (ProgramCU.cu:1838-1839, 1884-1885):
     // float product, min with 1.0 in double, acos in double, stored as float.
@@ -702,6 +811,19 @@ int oracle_features_oct(const uint8_t* img, int w, int h, int stride, const sgpu
     }
     *n_out = n;
     return n > cap ? -4 : 0;
+}
+
+// SiftGPU::RunSIFT(num, keys, keys_have_orientation) on image img: keys_out [num][4],
+// desc [num][128] in input order.
+int oracle_describe_keys(const uint8_t* img, int w, int h, int stride, const sgpu_options* opt,
+                         const float* keys, int num, int has_orientation, float* keys_out,
+                         float* desc) {
+    std::vector<float> ko;
+    std::vector<float> d = oracle::describe_keys(img, w, h, stride, *opt, keys, num,
+                                                 has_orientation, &ko);
+    if (keys_out) memcpy(keys_out, ko.data(), ko.size() * sizeof(float));
+    if (desc && opt->descriptors) memcpy(desc, d.data(), d.size() * sizeof(float));
+    return 0;
 }
 
 int oracle_match(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float distmax,

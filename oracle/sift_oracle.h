@@ -52,6 +52,13 @@ struct Result {
 Result extract(const uint8_t* img, int w, int h, int stride, const sgpu_options& opt,
                bool keep_intermediates = true);
 
+// Descriptors (and, without orientations, the strongest orientation) of caller-supplied
+// keypoints on image img (SiftGPU::RunSIFT(num, keys, keys_have_orientation)).  Returns the
+// descriptors [num][128] in input order; *keys_out gets the keys as the reference returns them.
+std::vector<float> describe_keys(const uint8_t* img, int w, int h, int stride,
+                                 const sgpu_options& opt, const float* keys, int num,
+                                 int has_orientation, std::vector<float>* keys_out);
+
 // Matcher (SiftMatchCU::GetSiftMatch + GetBestMatch).  Returns pairs {i, j}, ascending i.
 std::vector<int> match(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float distmax,
                        float ratiomax, int mbm, int max_match);

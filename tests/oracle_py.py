@@ -36,6 +36,10 @@ def lib():
         L.oracle_features_oct.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, P(SgpuOptions), ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_int, P(ctypes.c_int)]
+        L.oracle_describe_keys.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, P(SgpuOptions), ctypes.c_void_p,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_void_p]
         L.oracle_match.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                    ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_void_p]
@@ -118,6 +122,19 @@ def features_oct(img, opts=None):
     lib().oracle_features_oct(p, w, h, w, ctypes.byref(opts), feat.ctypes.data, lvl.ctypes.data,
                               n.value, ctypes.byref(n))
     return feat[:n.value], lvl[:n.value]
+
+
+def describe_keys(img, keys, has_orientation=True, opts=None):
+    """Reference RunSIFT(num, keys, keys_have_orientation): (keys_out [n,4], desc [n,128])."""
+    opts = opts or default_options()
+    img, p = _img(img)
+    h, w = img.shape
+    k = np.ascontiguousarray(keys, np.float32).reshape(-1, 4)
+    ko = np.zeros_like(k)
+    d = np.zeros((len(k), 128), np.float32)
+    lib().oracle_describe_keys(p, w, h, w, ctypes.byref(opts), k.ctypes.data, len(k),
+                               1 if has_orientation else 0, ko.ctypes.data, d.ctypes.data)
+    return ko, d
 
 
 def match(d1: np.ndarray, d2: np.ndarray, distmax=0.7, ratiomax=0.8, mbm=1, max_match=None):

@@ -370,3 +370,57 @@ def test_rccl_single_rank_collectives(gpu_ctx):
     assert np.array_equal(gpu_ctx.allgather_i32(counts, 1), counts)
     assert gpu_ctx.allreduce_f64([1.5, -2.0], op_max=True).tolist() == [1.5, -2.0]
     assert gpu_ctx.allreduce_f64(4.25, op_max=False).tolist() == [4.25]
+
+
+# ---- caller-supplied keypoints (SiftGPU::RunSIFT(num, keys, keys_have_orientation)) ----------
+
+def _synth_keys(w, h, n, seed):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    k = np.zeros((n, 4), np.float32)
+    k[:, 0] = rng.uniform(0, w, n)
+    k[:, 1] = rng.uniform(0, h, n)
+    k[:, 2] = np.exp(rng.uniform(np.log(0.5), np.log(60.0), n))   # below the first / above the last level too
+    k[:, 3] = rng.uniform(0, 2 * np.pi, n)
+    return k
+
+
+@pytest.mark.parametrize("has_orientation", [True, False])
+@pytest.mark.parametrize("over", [{}, {"fixed_orientation": 1}, {"max_orientation": 1},
+                                  {"normalized": 0, "lowe_origin": 1}])
+def test_keypoints_vs_oracle(gpu_ctx, has_orientation, over):
+    img = synth_image(480, 360, 71)
+    opts = default_options(**over)
+    keys = _synth_keys(480, 360, 300, 72)
+    gpu_ctx.set_options(opts)
+    gpu_ctx.extract(img)
+    gpu_ctx.extract_keypoints(keys, has_orientation)
+    assert gpu_ctx.count(0) == len(keys) and gpu_ctx.total() == len(keys)
+    k, d = gpu_ctx.features(0)
+    rk, rd = O.describe_keys(img, keys, has_orientation, opts)
+    assert np.array_equal(_bits(k), _bits(rk))
+    assert np.array_equal(_bits(d), _bits(rd))
+
+
+def test_detected_keypoints_fed_back(gpu_ctx):
+    """Keys from the detector itself, described again as a caller-supplied list."""
+    img = synth_image(400, 300, 73)
+    gpu_ctx.set_options(default_options())
+    gpu_ctx.extract(img)
+    keys, _ = gpu_ctx.features(0)
+    gpu_ctx.extract_keypoints(keys, True)
+    k, d = gpu_ctx.features(0)
+    rk, rd = O.describe_keys(img, keys, True)
+    assert np.array_equal(_bits(k), _bits(keys))
+    assert np.array_equal(_bits(d), _bits(rd))
+
+
+def test_keypoints_on_batch_image(gpu_ctx):
+    imgs = np.stack([synth_image(320, 240, 80 + i) for i in range(3)])
+    keys = _synth_keys(320, 240, 50, 83)
+    gpu_ctx.set_options(default_options())
+    gpu_ctx.extract(imgs)
+    gpu_ctx.extract_keypoints(keys, False, image=2)
+    assert [gpu_ctx.count(i) for i in range(3)] == [0, 0, 50]
+    k, d = gpu_ctx.features(2)
+    rk, rd = O.describe_keys(imgs[2], keys, False)
+    assert np.array_equal(_bits(k), _bits(rk)) and np.array_equal(_bits(d), _bits(rd))
