@@ -48,6 +48,11 @@ struct Runtime {
     int verbose = 1;
     int feature_num = 0;
     std::vector<float> keys, desc;
+    // SetKeypointList (SiftPyramid::SetKeypointList, SiftPyramid.cpp:293-310): applied by the
+    // next RunSIFT on a new image, then cleared (SiftPyramid.cpp:204)
+    std::vector<float> pending;
+    int pending_orientation = 1;
+    bool have_image = false;    // a pyramid of the current image exists on the device
     Runtime() { sgpu_default_options(&opt); }
 };
 
@@ -328,8 +333,36 @@ void SiftGPU::SaveSIFT(const char* szFileName) {
     }
 }
 
-void SiftGPU::SetKeypointList(int, const SiftKeypoint*, int) {
-    std::cerr << "SiftGPU (MI355X): SetKeypointList is not implemented yet\n";
+void SiftGPU::SetKeypointList(int num, const SiftKeypoint* keys, int keys_have_orientation) {
+    if (num <= 0 || !keys) return;
+    Runtime* rt = RT(_pyramid);
+    rt->pending.assign((const float*)keys, (const float*)keys + 4 * (size_t)num);
+    rt->pending_orientation = keys_have_orientation;
+}
+
+// Copy the context's current features (image 0) into the object's host buffers.
+static int fetch_features(Runtime* rt) {
+    rt->feature_num = sgpu_feature_count(rt->ctx, 0);
+    rt->keys.resize((size_t)rt->feature_num * 4);
+    rt->desc.resize(rt->opt.descriptors ? (size_t)rt->feature_num * 128 : 0);
+    return sgpu_copy_features(rt->ctx, 0, rt->keys.data(),
+                              rt->opt.descriptors ? rt->desc.data() : nullptr);
+}
+
+// Descriptors of a keypoint list on the current image (SiftGPU::RunSIFT(num, keys, ...)).
+static int describe_keys(Runtime* rt, const float* keys, int num, int has_orientation) {
+    if (has_orientation < 0) {
+        // keys_have_orientation == -1: the rectangle description hack (SIFT_RECT_DESCRIPTION,
+        // SiftPyramid.cpp:309, ProgramCU.cu:1104-1171)
+        std::cerr << "SiftGPU (MI355X): rectangle descriptors (keys_have_orientation = -1) are "
+                     "not implemented\n";
+        return 0;
+    }
+    if (sgpu_extract_keypoints(rt->ctx, 0, keys, num, has_orientation) != SGPU_OK) {
+        std::cerr << "SiftGPU: " << sgpu_last_error(rt->ctx) << "\n";
+        return 0;
+    }
+    return fetch_features(rt) == SGPU_OK ? 1 : 0;
 }
 
 int SiftGPU::CreateContextGL() { return VerifyContextGL(); }
@@ -428,13 +461,20 @@ int SiftGPU::RunSIFT() {
     if (rc != SGPU_OK) {
         std::cerr << "SiftGPU: " << sgpu_last_error(rt->ctx) << "\n";
         rt->feature_num = 0;
+        rt->have_image = false;
+        rt->pending.clear();
         return 0;
     }
-    rt->feature_num = sgpu_feature_count(rt->ctx, 0);
-    rt->keys.resize((size_t)rt->feature_num * 4);
-    rt->desc.resize(rt->opt.descriptors ? (size_t)rt->feature_num * 128 : 0);
-    rc = sgpu_copy_features(rt->ctx, 0, rt->keys.data(), rt->opt.descriptors ? rt->desc.data() : nullptr);
-    if (rc != SGPU_OK) return 0;
+    rt->have_image = true;
+    if (!rt->pending.empty()) {
+        // a list from SetKeypointList replaces detection on this image
+        std::vector<float> keys;
+        keys.swap(rt->pending);
+        if (!describe_keys(rt, keys.data(), (int)(keys.size() / 4), rt->pending_orientation))
+            return 0;
+    } else if (fetch_features(rt) != SGPU_OK) {
+        return 0;
+    }
     float t[9] = {0};
     sgpu_last_timing(rt->ctx, t, 9);
     for (int i = 0; i < 10; i++) _timing[i] = 0;
@@ -449,10 +489,13 @@ int SiftGPU::RunSIFT() {
     return 1;
 }
 
-int SiftGPU::RunSIFT(int num, const SiftKeypoint*, int) {
-    if (num <= 0) return 0;
-    std::cerr << "SiftGPU (MI355X): descriptors for user keypoints are not implemented yet\n";
-    return 0;
+// SiftGPU::RunSIFT(num, keys, keys_have_orientation) (SiftGPU.cpp:287-291): the list is
+// described on the current image's pyramid (run_on_current: no new filtering).
+int SiftGPU::RunSIFT(int num, const SiftKeypoint* keys, int keys_have_orientation) {
+    if (num <= 0 || !keys) return 0;
+    Runtime* rt = RT(_pyramid);
+    if (!_initialized || !rt->have_image) return 0;
+    return describe_keys(rt, (const float*)keys, num, keys_have_orientation);
 }
 
 int SiftGPU::GetImageCount() { return (int)LIST(_list)->size(); }

@@ -424,3 +424,28 @@ def test_keypoints_on_batch_image(gpu_ctx):
     k, d = gpu_ctx.features(2)
     rk, rd = O.describe_keys(imgs[2], keys, False)
     assert np.array_equal(_bits(k), _bits(rk)) and np.array_equal(_bits(d), _bits(rd))
+
+
+def test_keypoint_api_replica(tmp_path):
+    """SiftGPU::RunSIFT(num, keys, 1) and SetKeypointList + RunSIFT(image) through the C++ API."""
+    lib = os.path.join(ROOT, "modify-sift-gpu_amd", "lib", "libsiftgpu.so")
+    exe = tmp_path / "keypoint_replica"
+    r = subprocess.run(["g++", "-std=c++11", "-O1", "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "tests", "abi", "keypoint_replica.cpp"),
+                        "-o", str(exe), "-ldl"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    img = synth_image(512, 384, 91)
+    _write_pgm(tmp_path / "a.pgm", img)
+    keys = _synth_keys(512, 384, 120, 92)
+    keys.tofile(tmp_path / "keys.f32")
+    r = subprocess.run([str(exe), lib, str(tmp_path / "a.pgm"), str(tmp_path / "keys.f32"),
+                        str(len(keys)), str(tmp_path / "A.f32"), str(tmp_path / "B.f32")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    n = len(keys)
+    for name, has_o in (("A.f32", True), ("B.f32", False)):
+        raw = np.fromfile(tmp_path / name, np.float32)
+        k, d = raw[: 4 * n].reshape(n, 4), raw[4 * n:].reshape(n, 128)
+        rk, rd = O.describe_keys(img, keys, has_o)
+        assert np.array_equal(_bits(k), _bits(rk)), name
+        assert np.array_equal(_bits(d), _bits(rd)), name
