@@ -126,6 +126,19 @@ int sgpu_match(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d2, int 
                float distmax, float ratiomax, int mutual_best_match, int max_match,
                int* out_pairs, int flags);
 
+/* Guided matcher: SiftMatchGPU::SetFeautreLocation + GetGuidedSiftMatch (SiftGPU.h:313-321;
+ * SiftMatch.cpp:663-677; SiftMatchCU.cpp:104-136; kernel MultiplyDescriptorG_Kernel
+ * ProgramCU.cu:1607-1777).  loc1 [n1][2], loc2 [n2][2] feature (x, y) (packed: the reference's
+ * `gap` is applied by the caller); H, F row-major 3x3.  A pair passes when
+ * |H x1 - x2| < hdistmax in both coordinates and its Sampson error under F is < fdistmax; the
+ * dot of every pair of an 8-row block with a passing row enters the row/column decisions as
+ * MultiplyDescriptorG_Kernel defines them.  H == NULL and F == NULL: plain sgpu_match; one of
+ * them NULL: the identity with threshold 1e20.  SGPU_INPUT_DEVICE covers the locations too. */
+int sgpu_match_guided(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d2, int n2,
+                      const float* loc1, const float* loc2, const float* H, const float* F,
+                      float distmax, float ratiomax, float hdistmax, float fdistmax,
+                      int mutual_best_match, int max_match, int* out_pairs, int flags);
+
 /* float -> u8 quantization of SiftMatchCU::SetDescriptors (SiftMatchCU.cpp:94-99), host side. */
 void sgpu_quantize_descriptors(const float* d, size_t count, uint8_t* out);
 

@@ -106,7 +106,7 @@ struct sgpu_ctx {
     hipEvent_t ev[T_N + 1] = {};
     float timing[T_N] = {};
     // matcher
-    DevBuf m_d1, m_d2, m_part, m_terms, m_match, m_dist;
+    DevBuf m_d1, m_d2, m_part, m_terms, m_match, m_dist, m_mask, m_loc;
     std::vector<int> h_match;
     bool dist_ready = false;
     // multi-GPU: RCCL communicator of this context's device (sgpu_comm_*)
@@ -292,7 +292,8 @@ int sgpu_ctx_destroy(sgpu_ctx* ctx) {
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     ctx->comm = nullptr;
     DevBuf* bufs[] = {&ctx->input, &ctx->all_keys, &ctx->all_desc, &ctx->m_d1, &ctx->m_d2,
-                      &ctx->m_part, &ctx->m_terms, &ctx->m_match, &ctx->m_dist, &ctx->c_buf};
+                      &ctx->m_part, &ctx->m_terms, &ctx->m_match, &ctx->m_dist, &ctx->m_mask, &ctx->m_loc,
+                      &ctx->c_buf};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i <= T_N; i++)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
@@ -674,13 +675,16 @@ int sgpu_extract_keypoints(sgpu_ctx* ctx, int image, const float* keys, int num,
     return SGPU_OK;
 }
 
-// SiftMatchGPU::SetDescriptors + GetSiftMatch (SiftMatchCU.cpp:71-179) in one call.
-int sgpu_match(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d2, int n2,
-               float distmax, float ratiomax, int mbm, int max_match, int* out_pairs,
-               int flags) {
+// SiftMatchGPU::SetDescriptors + GetSiftMatch (SiftMatchCU.cpp:71-179) in one call; with
+// `guided`, SetFeautreLocation + GetGuidedSiftMatch (SiftMatchCU.cpp:104-136).
+static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d2, int n2,
+                      float distmax, float ratiomax, int mbm, int max_match, int* out_pairs,
+                      int flags, const float* loc1, const float* loc2,
+                      const sgk::GuidedParams* guided) {
     if (!ctx) return SGPU_EINVAL;
     if (n1 <= 0 || n2 <= 0) return 0;   // SiftMatchCU.cpp:142
     if (!d1 || !d2 || (max_match > 0 && !out_pairs)) return ctx->fail(SGPU_EINVAL, "bad match arguments");
+    if (guided && (!loc1 || !loc2)) return ctx->fail(SGPU_EINVAL, "guided match needs locations");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     if (!ctx->dist_ready) {
@@ -703,6 +707,24 @@ int sgpu_match(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d2, int 
         a = ctx->m_d1.as<uint8_t>();
         b = ctx->m_d2.as<uint8_t>();
     }
+    // guided: locations (float2 per feature) and the two geometric masks
+    const int pitch_r = (n2 + 3) & ~3, pitch_c = (n1 + 7) & ~7;
+    const size_t rmask_bytes = (size_t)2 * ((n1 + 7) / 8) * pitch_r;
+    const size_t cmask_bytes = mbm ? (size_t)((n2 + 3) / 4) * pitch_c : 0;
+    const float* l1 = loc1;
+    const float* l2 = loc2;
+    if (guided) {
+        ALLOCCHK(ctx, ctx->m_mask.ensure(rmask_bytes + cmask_bytes));
+        if (!(flags & SGPU_INPUT_DEVICE)) {
+            ALLOCCHK(ctx, ctx->m_loc.ensure((size_t)(n1 + n2) * 2 * sizeof(float)));
+            float* dl = ctx->m_loc.as<float>();
+            HIPCHK(ctx, hipMemcpyAsync(dl, loc1, (size_t)n1 * 2 * sizeof(float), hipMemcpyHostToDevice, st));
+            HIPCHK(ctx, hipMemcpyAsync(dl + 2 * n1, loc2, (size_t)n2 * 2 * sizeof(float),
+                                       hipMemcpyHostToDevice, st));
+            l1 = dl;
+            l2 = dl + 2 * n1;
+        }
+    }
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], st));
     const int ca = sgk::match_chunks(n1, n2), cb = mbm ? sgk::match_chunks(n2, n1) : 0;
     const size_t part_n = std::max((size_t)ca * n1, (size_t)cb * n2);
@@ -716,17 +738,27 @@ int sgpu_match(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d2, int 
     int* match1 = ctx->m_match.as<int>();
     int* match2 = match1 + n1;
     sgk::Top2* part = ctx->m_part.as<sgk::Top2>();
+    uint8_t* rmask = guided ? ctx->m_mask.as<uint8_t>() : nullptr;
+    uint8_t* cmask = guided && mbm ? rmask + rmask_bytes : nullptr;
+    if (guided)
+        HIPCHK(ctx, sgk::launch_guided_mask(l1, n1, l2, n2, *guided, rmask, pitch_r, cmask,
+                                            pitch_c, st));
+    // guided: the row term goes into the accumulators and the finish adds none
     HIPCHK(ctx, sgk::launch_rowsums(a, n1, row1, 128, 0, st));
     HIPCHK(ctx, sgk::launch_rowsums(b, n2, col2, 128, -2097152, st));
-    HIPCHK(ctx, sgk::launch_match_rows(a, n1, b, n2, col2, ca, part, st));
-    HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, row1, ctx->m_dist.as<float>(), distmax,
-                                         ratiomax, match1, nullptr, st));
+    HIPCHK(ctx, sgk::launch_match_rows(a, n1, b, n2, col2, ca, part, st, guided ? 1 : 0, row1,
+                                       rmask, pitch_r));
+    HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, guided ? nullptr : row1,
+                                         ctx->m_dist.as<float>(), distmax, ratiomax, match1,
+                                         nullptr, st));
     if (mbm) {
         HIPCHK(ctx, sgk::launch_rowsums(b, n2, row2, 128, 0, st));
         HIPCHK(ctx, sgk::launch_rowsums(a, n1, col1, 128, -2097152, st));
-        HIPCHK(ctx, sgk::launch_match_rows(b, n2, a, n1, col1, cb, part, st));
-        HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, row2, ctx->m_dist.as<float>(), distmax,
-                                             ratiomax, match2, nullptr, st));
+        HIPCHK(ctx, sgk::launch_match_rows(b, n2, a, n1, col1, cb, part, st, guided ? 2 : 0, row2,
+                                           cmask, pitch_c));
+        HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, guided ? nullptr : row2,
+                                             ctx->m_dist.as<float>(), distmax, ratiomax, match2,
+                                             nullptr, st));
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
     ctx->h_match.resize((size_t)n1 + n2);
@@ -747,6 +779,33 @@ int sgpu_match(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d2, int 
         }
     }
     return nmatch;
+}
+
+int sgpu_match(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d2, int n2,
+               float distmax, float ratiomax, int mbm, int max_match, int* out_pairs,
+               int flags) {
+    return match_impl(ctx, d1, n1, d2, n2, distmax, ratiomax, mbm, max_match, out_pairs, flags,
+                      nullptr, nullptr, nullptr);
+}
+
+// SiftMatchGPU::GetGuidedSiftMatch (SiftMatch.cpp:663-677 defaults, SiftMatchCU.cpp:126-136).
+int sgpu_match_guided(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d2, int n2,
+                      const float* loc1, const float* loc2, const float* H, const float* F,
+                      float distmax, float ratiomax, float hdistmax, float fdistmax, int mbm,
+                      int max_match, int* out_pairs, int flags) {
+    if (!ctx) return SGPU_EINVAL;
+    if (!H && !F)
+        return match_impl(ctx, d1, n1, d2, n2, distmax, ratiomax, mbm, max_match, out_pairs,
+                          flags, nullptr, nullptr, nullptr);
+    // a missing matrix is the identity with its threshold at 1e20 (SiftMatch.cpp:667-675)
+    static const float kIdentity[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    sgk::GuidedParams gp;
+    memcpy(gp.H, H ? H : kIdentity, sizeof(gp.H));
+    memcpy(gp.F, F ? F : kIdentity, sizeof(gp.F));
+    gp.hdistmax = H ? hdistmax : 1.0e+20f;
+    gp.fdistmax = F ? fdistmax : 1.0e+20f;
+    return match_impl(ctx, d1, n1, d2, n2, distmax, ratiomax, mbm, max_match, out_pairs, flags,
+                      loc1, loc2, &gp);
 }
 
 // ---- multi-GPU: one process per GPU, RCCL over xGMI ----

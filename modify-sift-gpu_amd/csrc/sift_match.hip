@@ -60,10 +60,23 @@ __device__ __forceinline__ v4i load16_s8(const uint8_t* p) {
 
 // One row panel of A against columns [c_begin, c_end) of B.
 // part[chunk * nA + row] = running top-2 of row over those columns (dot without the row term).
+//
+// Guided matching (MODE 1: A = set 1, the row decision; MODE 2: A = set 2, the column
+// decision) folds the guided value of MultiplyDescriptorG_Kernel (ProgramCU.cu:1683-1733)
+// instead of the dot: the accumulators then start at row term + column term (the exact dot, the
+// masking below is not monotone in it), and `mask` (k_guided_mask) holds one byte per (4-row
+// group of A, column): bit i = pair (4g+i, col) passes the geometric test, bit 4+i = some row of
+// that pair's 8-row block of set 1 passes at that column (good_count > 0).
+//   MODE 1: pass ? dot : good ? max(dot - 2^18, 0) : 0      (d_result = max(results, 0))
+//   MODE 2: pass ? dot : good ? dot - 2^18 : -2^18          (the raw results of d_temp)
+template <int MODE>
 __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ A, int nA,
                                                     const uint8_t* __restrict__ B, int nB,
                                                     const int* __restrict__ col_term,
-                                                    int cols_per_chunk, Top2* __restrict__ part) {
+                                                    int cols_per_chunk, Top2* __restrict__ part,
+                                                    const int* __restrict__ row_term,
+                                                    const uint8_t* __restrict__ mask,
+                                                    int mask_pitch) {
     __shared__ __attribute__((aligned(16))) uint8_t s_b[2][kTile * kLdsRow];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int panel = blockIdx.x, chunk = blockIdx.y;
@@ -80,6 +93,18 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         for (int kh = 0; kh < 2; kh++) {
             if (row < nA) afrag[rb][kh] = load16_s8(A + (size_t)row * 128 + kh * 64 + quad * 16);
             else afrag[rb][kh] = v4i{0, 0, 0, 0};
+        }
+    }
+    // guided: the row terms of this lane's rows and their 4-row mask groups
+    int rterm[2][4] = {};
+    int mgroup[2] = {};
+    if constexpr (MODE != 0) {
+#pragma unroll
+        for (int rb = 0; rb < 2; rb++) {
+            const int r0 = panel * kPanel + wave * 32 + rb * 16 + quad * 4;
+            mgroup[rb] = r0 < nA ? r0 >> 2 : -1;
+#pragma unroll
+            for (int i = 0; i < 4; i++) rterm[rb][i] = r0 + i < nA ? row_term[r0 + i] : 0;
         }
     }
     // running state for this lane's 8 output rows: (rb, i) -> row wave*32 + rb*16 + quad*4 + i
@@ -119,12 +144,23 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         if (has_next) stage_load(tb + kTile, stg);
         // accumulators start at the column term (invalid columns: -inf)
         v4i acc[2][8];
+        uint32_t mb[2][8];
 #pragma unroll
         for (int cb = 0; cb < 8; cb++) {
             const int col = tb + cb * 16 + l16;
             const int ct = col < c_end ? col_term[col] : kNegCol;
-            acc[0][cb] = v4i{ct, ct, ct, ct};
-            acc[1][cb] = acc[0][cb];
+            if constexpr (MODE == 0) {
+                acc[0][cb] = v4i{ct, ct, ct, ct};
+                acc[1][cb] = acc[0][cb];
+            } else {
+#pragma unroll
+                for (int rb = 0; rb < 2; rb++) {
+                    acc[rb][cb] = v4i{ct + rterm[rb][0], ct + rterm[rb][1], ct + rterm[rb][2],
+                                      ct + rterm[rb][3]};
+                    mb[rb][cb] = (col < c_end && mgroup[rb] >= 0)
+                                     ? mask[(size_t)mgroup[rb] * mask_pitch + col] : 0u;
+                }
+            }
         }
         const uint8_t* sb = s_b[buf];
 #pragma unroll
@@ -151,7 +187,14 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
                 int m = m0, sv = S[rb][i];
 #pragma unroll
                 for (int cb = 0; cb < 8; cb++) {
-                    const int key = (acc[rb][cb][i] << 3) | (7 - cb);
+                    int v = acc[rb][cb][i];
+                    if constexpr (MODE != 0) {
+                        const bool pass = (mb[rb][cb] >> i) & 1u;
+                        const bool good = (mb[rb][cb] >> (4 + i)) & 1u;
+                        const int off = MODE == 1 ? max(v - 262144, 0) : v - 262144;
+                        v = pass ? v : (good ? off : (MODE == 1 ? 0 : -262144));
+                    }
+                    const int key = (v << 3) | (7 - cb);
                     sv = med3i(sv, m, key);
                     m = max(m, key);
                 }
@@ -221,7 +264,7 @@ __global__ __launch_bounds__(256) void k_match_finish(const Top2* __restrict__ p
         const int id = u.max > t.max ? u.idx : (t.max > u.max ? t.idx : min((unsigned)t.idx, (unsigned)u.idx));
         t = Top2{m, id, s};
     }
-    const int rt = row_term[r];
+    const int rt = row_term ? row_term[r] : 0;   // guided: folded in the accumulators
     // the reference's running maxima start at 0 with index -1 (ProgramCU.cu:1803)
     int mx = t.max + rt, sc = t.second + rt;
     int idx = t.idx;
@@ -232,7 +275,103 @@ __global__ __launch_bounds__(256) void k_match_finish(const Top2* __restrict__ p
     out[r] = (d1 < distmax) && (d1 < d2 * ratiomax) ? idx : -1;
 }
 
+// Geometric test of MultiplyDescriptorG_Kernel (ProgramCU.cu:1648-1681), once per pair, in
+// the operation order of oracle::guided_pass (row-only and column-only terms are hoisted, which
+// does not change any value; FDIV(a, b) = a * (1 / b)).  One thread per (8-row block of set 1,
+// 4 columns of set 2); it writes both masks k_match_rows<1/2> read:
+//   rmask[g][j] (4-row groups g of set 1, pitch pitch_r): bit i = pass(4g+i, j), bits 4-7 = good
+//   cmask[q][r] (4-row groups q of set 2, pitch pitch_c): bit c = pass(r, 4q+c), bit 4+c = good
+// where good(r, j) = some row of r's 8-row block passes at j (good_count > 0, :1682).
+__global__ __launch_bounds__(256) void k_guided_mask(const float2* __restrict__ loc1, int n1,
+                                                     const float2* __restrict__ loc2, int n2,
+                                                     GuidedParams gp, uint8_t* __restrict__ rmask,
+                                                     int pitch_r, uint8_t* __restrict__ cmask,
+                                                     int pitch_c) {
+    const int nq = (n2 + 3) >> 2, nblk = (n1 + 7) >> 3;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (int64_t)nq * nblk) return;
+    const int q = (int)(t % nq), blk = (int)(t / nq);
+    const float* H = gp.H;
+    const float* F = gp.F;
+    float x2[4], y2[4], t0[4], t1[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const int j = q * 4 + c;
+        const float2 l = j < n2 ? loc2[j] : make_float2(0.f, 0.f);
+        x2[c] = l.x;
+        y2[c] = l.y;
+        t0[c] = __builtin_fmaf(F[0], l.x, __builtin_fmaf(F[3], l.y, F[6]));
+        t1[c] = __builtin_fmaf(F[1], l.x, __builtin_fmaf(F[4], l.y, F[7]));
+    }
+    uint32_t pass = 0;   // bit k * 4 + c
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int r = blk * 8 + k;
+        if (r >= n1) break;
+        const float2 l = loc1[r];
+        const float h0 = __builtin_fmaf(H[0], l.x, __builtin_fmaf(H[1], l.y, H[2]));
+        const float h1 = __builtin_fmaf(H[3], l.x, __builtin_fmaf(H[4], l.y, H[5]));
+        const float h2 = __builtin_fmaf(H[6], l.x, __builtin_fmaf(H[7], l.y, H[8]));
+        const float rh = 1.0f / h2;
+        const float u = h0 * rh, v = h1 * rh;
+        const float f0 = __builtin_fmaf(F[0], l.x, __builtin_fmaf(F[1], l.y, F[2]));
+        const float f1 = __builtin_fmaf(F[3], l.x, __builtin_fmaf(F[4], l.y, F[5]));
+        const float f2 = __builtin_fmaf(F[6], l.x, __builtin_fmaf(F[7], l.y, F[8]));
+        const float d0 = __builtin_fmaf(f1, f1, f0 * f0);
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            if (q * 4 + c >= n2) break;
+            if (!(__builtin_fabsf(u - x2[c]) < gp.hdistmax && __builtin_fabsf(v - y2[c]) < gp.hdistmax))
+                continue;
+            const float x2fx1 = __builtin_fmaf(x2[c], f0, __builtin_fmaf(y2[c], f1, f2));
+            const float den = __builtin_fmaf(t1[c], t1[c], __builtin_fmaf(t0[c], t0[c], d0));
+            const float se = (x2fx1 * x2fx1) * (1.0f / den);
+            if (se < gp.fdistmax) pass |= 1u << (k * 4 + c);
+        }
+    }
+    uint32_t good = 0;   // bit c
+#pragma unroll
+    for (int c = 0; c < 4; c++) good |= ((pass & (0x11111111u << c)) != 0) << c;
+    // rmask: groups 2 blk + h, bytes for columns 4q .. 4q+3
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            uint32_t b = ((good >> c) & 1u) ? 0xf0u : 0u;
+#pragma unroll
+            for (int i = 0; i < 4; i++) b |= ((pass >> ((4 * h + i) * 4 + c)) & 1u) << i;
+            w |= b << (8 * c);
+        }
+        *reinterpret_cast<uint32_t*>(rmask + (size_t)(2 * blk + h) * pitch_r + q * 4) = w;
+    }
+    // cmask: group q, bytes for rows 8 blk .. 8 blk + 7
+    if (cmask) {
+        uint32_t w[2] = {0, 0};
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t b = ((pass >> (k * 4)) & 0xfu) | (good << 4);
+            w[k >> 2] |= b << (8 * (k & 3));
+        }
+        *reinterpret_cast<uint2*>(cmask + (size_t)q * pitch_c + blk * 8) = make_uint2(w[0], w[1]);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_guided_mask(const float* loc1, int n1, const float* loc2, int n2,
+                              const GuidedParams& gp, uint8_t* rmask, int pitch_r,
+                              uint8_t* cmask, int pitch_c, hipStream_t stream) {
+    if (n1 <= 0 || n2 <= 0) return hipSuccess;
+    if ((pitch_r & 3) || pitch_r < n2 || (cmask && ((pitch_c & 7) || pitch_c < n1)))
+        return hipErrorInvalidValue;
+    const int64_t threads = (int64_t)((n2 + 3) / 4) * ((n1 + 7) / 8);
+    hipLaunchKernelGGL(k_guided_mask, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream,
+                       reinterpret_cast<const float2*>(loc1), n1,
+                       reinterpret_cast<const float2*>(loc2), n2, gp, rmask, pitch_r, cmask,
+                       pitch_c);
+    return hipGetLastError();
+}
 
 hipError_t launch_rowsums(const uint8_t* d, int n, int* out, int scale, int bias,
                           hipStream_t stream) {
@@ -250,12 +389,23 @@ int match_chunks(int nA, int nB) {
 }
 
 hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
-                             const int* col_term, int chunks, Top2* part, hipStream_t stream) {
+                             const int* col_term, int chunks, Top2* part, hipStream_t stream,
+                             int guided_mode, const int* row_term, const uint8_t* mask,
+                             int mask_pitch) {
     if (nA <= 0 || nB <= 0) return hipSuccess;
     int per = (nB + chunks - 1) / chunks;
     per = (per + kTile - 1) / kTile * kTile;
     dim3 grid((nA + kPanel - 1) / kPanel, chunks);
-    hipLaunchKernelGGL(k_match_rows, grid, dim3(256), 0, stream, A, nA, B, nB, col_term, per, part);
+    if (guided_mode != 0 && (!row_term || !mask || mask_pitch < nB)) return hipErrorInvalidValue;
+    if (guided_mode == 0)
+        hipLaunchKernelGGL(k_match_rows<0>, grid, dim3(256), 0, stream, A, nA, B, nB, col_term,
+                           per, part, row_term, mask, mask_pitch);
+    else if (guided_mode == 1)
+        hipLaunchKernelGGL(k_match_rows<1>, grid, dim3(256), 0, stream, A, nA, B, nB, col_term,
+                           per, part, row_term, mask, mask_pitch);
+    else
+        hipLaunchKernelGGL(k_match_rows<2>, grid, dim3(256), 0, stream, A, nA, B, nB, col_term,
+                           per, part, row_term, mask, mask_pitch);
     return hipGetLastError();
 }
 

@@ -512,6 +512,8 @@ struct MatchState {
     int num[2] = {0, 0};
     int id[2] = {0, 0};
     std::vector<uint8_t> des[2];
+    int have_loc[2] = {0, 0};
+    std::vector<float> loc[2];   // packed (x, y) per feature
 };
 MatchState* MS(SiftMatchGPU* p) { return reinterpret_cast<MatchState*>(p); }
 }  // namespace
@@ -577,6 +579,7 @@ void SiftMatchGPU::SetDescriptors(int index, int num, const unsigned char* descr
     MatchState* m = MS(__matcher);
     if (!m || !m->ctx) return;
     index = std::min(std::max(index, 0), 1);
+    m->have_loc[index] = 0;   // SiftMatchCU.cpp:77
     if (id != -1 && id == m->id[index]) return;
     m->id[index] = id;
     if (num > m->max_sift) num = m->max_sift;
@@ -604,16 +607,37 @@ int SiftMatchGPU::GetSiftMatch(int max_match, int match_buffer[][2], float distm
     return r < 0 ? 0 : r;
 }
 
-void SiftMatchGPU::SetFeautreLocation(int, const float*, int) {}
+// SiftMatchCU::SetFeautreLocation (SiftMatchCU.cpp:104-122): (x, y) then `gap` skipped floats
+// per feature, for the current descriptor count of that set.
+void SiftMatchGPU::SetFeautreLocation(int index, const float* locations, int gap) {
+    MatchState* m = MS(__matcher);
+    if (!m || !m->ctx || !locations) return;
+    index = std::min(std::max(index, 0), 1);
+    const int n = m->num[index];
+    if (n <= 0) return;
+    std::vector<float>& l = m->loc[index];
+    l.resize((size_t)n * 2);
+    for (int i = 0; i < n; i++) {
+        l[2 * i] = locations[(size_t)i * (2 + gap)];
+        l[2 * i + 1] = locations[(size_t)i * (2 + gap) + 1];
+    }
+    m->have_loc[index] = 1;
+}
 
-// SiftMatch.cpp:663-677: without H and F this is GetSiftMatch.
+// SiftMatch.cpp:663-677 (NULL matrices) + SiftMatchCU::GetGuidedSiftMatch (:126-136).
 int SiftMatchGPU::GetGuidedSiftMatch(int max_match, int match_buffer[][2], float H[3][3],
-                                     float F[3][3], float distmax, float ratiomax, float, float,
-                                     int mutual_best_match) {
+                                     float F[3][3], float distmax, float ratiomax,
+                                     float hdistmax, float fdistmax, int mutual_best_match) {
     if (H == NULL && F == NULL)
         return GetSiftMatch(max_match, match_buffer, distmax, ratiomax, mutual_best_match);
-    std::cerr << "SiftMatchGPU (MI355X): guided matching is not implemented yet\n";
-    return 0;
+    MatchState* m = MS(__matcher);
+    if (!m || !m->ctx || m->num[0] <= 0 || m->num[1] <= 0) return 0;
+    if (!m->have_loc[0] || !m->have_loc[1]) return 0;
+    int r = sgpu_match_guided(m->ctx, m->des[0].data(), m->num[0], m->des[1].data(), m->num[1],
+                              m->loc[0].data(), m->loc[1].data(), H ? &H[0][0] : nullptr,
+                              F ? &F[0][0] : nullptr, distmax, ratiomax, hdistmax, fdistmax,
+                              mutual_best_match, max_match, &match_buffer[0][0], SGPU_INPUT_HOST);
+    return r < 0 ? 0 : r;
 }
 
 // ---------------------------------------------------------------------------------- factories

@@ -26,7 +26,7 @@ C_API = [
     "sgpu_device_features", "sgpu_match", "sgpu_quantize_descriptors", "sgpu_last_timing",
     "sgpu_debug_geometry", "sgpu_debug_gaussian", "sgpu_debug_candidates",
     "sgpu_debug_set_variant", "sgpu_comm_unique_id", "sgpu_comm_init", "sgpu_comm_allgather_i32",
-    "sgpu_comm_allreduce_f64", "sgpu_extract_keypoints",
+    "sgpu_comm_allreduce_f64", "sgpu_extract_keypoints", "sgpu_match_guided",
 ]
 
 _LIB = None
@@ -61,6 +61,9 @@ def lib():
         L.sgpu_device_features.argtypes = [vp, P(vp), P(vp), P(vp)]
         L.sgpu_match.argtypes = [vp, vp, c.c_int, vp, c.c_int, c.c_float, c.c_float, c.c_int,
                                  c.c_int, vp, c.c_int]
+        L.sgpu_match_guided.argtypes = [vp, vp, c.c_int, vp, c.c_int, vp, vp, vp, vp, c.c_float,
+                                        c.c_float, c.c_float, c.c_float, c.c_int, c.c_int, vp,
+                                        c.c_int]
         L.sgpu_quantize_descriptors.argtypes = [vp, c.c_size_t, vp]
         L.sgpu_last_timing.argtypes = [vp, vp, c.c_int]
         L.sgpu_debug_set_variant.argtypes = [c.c_int]
@@ -212,6 +215,31 @@ class SiftContext:
                              distmax, ratiomax, mbm, max_match, out.ctypes.data, flags)
         if m < 0:
             self._check(m, "sgpu_match")
+        return out[:m]
+
+    def match_guided(self, d1: np.ndarray, d2: np.ndarray, loc1: np.ndarray, loc2: np.ndarray,
+                     H=None, F=None, distmax=0.7, ratiomax=0.8, hdistmax=32.0, fdistmax=16.0,
+                     mbm=1, max_match=None):
+        """SiftMatchGPU::GetGuidedSiftMatch (SiftMatch.cpp:663-677): loc1/loc2 [n][2] (x, y),
+        H/F 3x3 or None (defaults of SiftGPU.h:318-321)."""
+        d1 = np.ascontiguousarray(d1, np.uint8)
+        d2 = np.ascontiguousarray(d2, np.uint8)
+        l1 = np.ascontiguousarray(loc1, np.float32)
+        l2 = np.ascontiguousarray(loc2, np.float32)
+        n1, n2 = d1.shape[0], d2.shape[0]
+        if l1.shape != (n1, 2) or l2.shape != (n2, 2):
+            raise ValueError("locations must be [n][2] per descriptor set")
+        hm = None if H is None else np.ascontiguousarray(H, np.float32).reshape(9)
+        fm = None if F is None else np.ascontiguousarray(F, np.float32).reshape(9)
+        max_match = n1 if max_match is None else max_match
+        out = np.zeros((max(max_match, 1), 2), np.int32)
+        m = lib().sgpu_match_guided(
+            self._ctx, d1.ctypes.data, n1, d2.ctypes.data, n2, l1.ctypes.data, l2.ctypes.data,
+            None if hm is None else hm.ctypes.data, None if fm is None else fm.ctypes.data,
+            distmax, ratiomax, hdistmax, fdistmax, mbm, max_match, out.ctypes.data,
+            SGPU_INPUT_HOST)
+        if m < 0:
+            self._check(m, "sgpu_match_guided")
         return out[:m]
 
     # ---- multi-GPU (RCCL inside libsiftgpu)

@@ -78,3 +78,37 @@ def quantize(d: np.ndarray) -> np.ndarray:
     truncation, modulo-256 narrowing)."""
     v = (np.float32(512.0) * d.astype(np.float32)).astype(np.float64) + 0.5
     return (np.trunc(v).astype(np.int64) & 0xFF).astype(np.uint8)
+
+
+def synth_guided_scene(n1: int, n2: int, seed: int, n_dup: int | None = None,
+                       n_exact: int = 8, width: float = 1920.0, height: float = 1080.0):
+    """Two descriptor sets with locations for guided matching (SiftMatchGPU::GetGuidedSiftMatch).
+
+    Set 2's first n_dup features are near-duplicates of set 1's that sit at H x1 (plus < 1 px),
+    every third of those is then moved far away (a descriptor match the geometry must reject),
+    and n_exact exact copies give dots above 2^18 (the reference's max(dot - 2^18, 0) branch).
+    H is a similarity-plus-perspective homography; F = [e]_x H, so x2' F x1 = 0 for x2 = H x1.
+    Returns (q1, q2, loc1, loc2, H, F) with u8 descriptors and float32 [n][2] locations."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    n_dup = min(n1, n2, n_dup if n_dup is not None else min(n1, n2) // 2)
+    d1 = synth_descriptors(n1, seed * 7 + 1)
+    d2 = synth_descriptors(n2, seed * 7 + 2, base=d1, n_dup=n_dup)
+    q1, q2 = quantize(d1), quantize(d2)
+    k = min(n_exact, n_dup)
+    q2[:k] = q1[:k]
+    loc1 = np.stack([rng.uniform(0, width, n1), rng.uniform(0, height, n1)], 1)
+    a = rng.uniform(-0.2, 0.2)
+    s = rng.uniform(0.9, 1.1)
+    H = np.array([[s * np.cos(a), -s * np.sin(a), rng.uniform(-50, 50)],
+                  [s * np.sin(a), s * np.cos(a), rng.uniform(-50, 50)],
+                  [rng.uniform(-1e-5, 1e-5), rng.uniform(-1e-5, 1e-5), 1.0]])
+    e = np.array([rng.uniform(-1, 1), rng.uniform(-1, 1), 1e-3])
+    ex = np.array([[0, -e[2], e[1]], [e[2], 0, -e[0]], [-e[1], e[0], 0]])
+    F = ex @ H
+    F /= np.linalg.norm(F)
+    loc2 = np.stack([rng.uniform(0, width, n2), rng.uniform(0, height, n2)], 1)
+    x1 = np.concatenate([loc1[:n_dup], np.ones((n_dup, 1))], 1) @ H.T
+    loc2[:n_dup] = x1[:, :2] / x1[:, 2:] + rng.uniform(-0.5, 0.5, (n_dup, 2))
+    loc2[2:n_dup:3] += rng.uniform(200, 400, (len(range(2, n_dup, 3)), 2))
+    return (q1, q2, loc1.astype(np.float32), loc2.astype(np.float32), H.astype(np.float32),
+            F.astype(np.float32))

@@ -706,6 +706,99 @@ std::vector<float> describe_keys(const uint8_t* img, int w, int h, int stride,
     return desc;
 }
 
+// --- Geometric test of MultiplyDescriptorG_Kernel (ProgramCU.cu:1648-1681) for one pair:
+//     |H x1 - x2| (both coordinates) < hdistmax, then the Sampson error of x2' F x1 < fdistmax.
+//     Contractions (nvcc's choice is not observable) are fixed as written out below on both
+//     sides; FDIV(a, b) = a * (1 / b).
+bool guided_pass(const float* H, const float* F, float x1, float y1, float x2, float y2,
+                 float hdistmax, float fdistmax) {
+    auto fdiv = [](float a, float b) { return a * (1.0f / b); };
+    const float h0 = fma_(H[0], x1, fma_(H[1], y1, H[2]));
+    const float h1 = fma_(H[3], x1, fma_(H[4], y1, H[5]));
+    const float h2 = fma_(H[6], x1, fma_(H[7], y1, H[8]));
+    const float d0 = fabs_(fdiv(h0, h2) - x2), d1 = fabs_(fdiv(h1, h2) - y2);
+    if (!(d0 < hdistmax && d1 < hdistmax)) return false;
+    const float f0 = fma_(F[0], x1, fma_(F[1], y1, F[2]));
+    const float f1 = fma_(F[3], x1, fma_(F[4], y1, F[5]));
+    const float f2 = fma_(F[6], x1, fma_(F[7], y1, F[8]));
+    const float t0 = fma_(F[0], x2, fma_(F[3], y2, F[6]));
+    const float t1 = fma_(F[1], x2, fma_(F[4], y2, F[7]));
+    const float x2fx1 = fma_(x2, f0, fma_(y2, f1, f2));
+    float den = f0 * f0;
+    den = fma_(f1, f1, den);
+    den = fma_(t0, t0, den);
+    den = fma_(t1, t1, den);
+    const float se = fdiv(x2fx1 * x2fx1, den);
+    return se < fdistmax;
+}
+
+// SiftMatchCU::GetGuidedSiftMatch (SiftMatchCU.cpp:126-136) = MultiplyDescriptorG_Kernel
+// (ProgramCU.cu:1607-1735) + the RowMatch / ColMatch decisions.  The guided dot of a pair is
+// its dot when the pair passes the geometric test; otherwise -262144, plus the dot when any
+// other row of its 8-row block (MULT_BLOCK_DIMY) passes at that column.  Rows: running top-2
+// from (0, -1, 0) with strict '>'; columns: the per-block (max, idx, second) of :1709-1721
+// merged over blocks as ColMatch_Kernel (:1874-1882).
+std::vector<int> match_guided(const uint8_t* d1, int n1, const uint8_t* d2, int n2,
+                              const float* loc1, const float* loc2, const float* H,
+                              const float* F, float distmax, float ratiomax, float hdistmax,
+                              float fdistmax, int mbm, int max_match) {
+    struct Top2 { int max = 0, idx = -1, second = 0; };
+    std::vector<Top2> rows(n1), cols(n2);
+    const int nblk = (n1 + 7) / 8;
+    for (int j = 0; j < n2; j++) {
+        Top2 colacc;
+        for (int blk = 0; blk < nblk; blk++) {
+            int res[8];
+            int good = 0;
+            for (int i = 0; i < 8; i++) {
+                const int r = blk * 8 + i;
+                res[i] = -262144;
+                if (r < n1 && guided_pass(H, F, loc1[2 * r], loc1[2 * r + 1], loc2[2 * j],
+                                          loc2[2 * j + 1], hdistmax, fdistmax))
+                    res[i] = 0;
+                good += res[i] >= 0;
+            }
+            if (good > 0)
+                for (int i = 0; i < 8; i++) {
+                    const int r = blk * 8 + i;
+                    if (r >= n1) break;
+                    int dot = 0;
+                    for (int k = 0; k < 128; k++) dot += (int)d1[r * 128 + k] * (int)d2[j * 128 + k];
+                    res[i] += dot;
+                }
+            Top2 cmp;   // (0, -1, 0)
+            for (int i = 0; i < 8; i++) {
+                const int r = blk * 8 + i;
+                if (r >= n1) break;
+                if (res[i] > cmp.max) { cmp.second = cmp.max; cmp.max = res[i]; cmp.idx = r; }
+                else cmp.second = std::max(cmp.second, res[i]);
+                const int v = std::max(res[i], 0);   // d_result = max(results, 0)
+                Top2& t = rows[r];
+                if (v > t.max) { t.second = t.max; t.max = v; t.idx = j; }
+                else t.second = std::max(t.second, v);
+            }
+            if (blk == 0) colacc = cmp;
+            else if (colacc.max < cmp.max) colacc = Top2{cmp.max, cmp.idx, std::max(colacc.max, cmp.second)};
+            else colacc.second = std::max(colacc.second, cmp.max);
+        }
+        cols[j] = colacc;
+    }
+    auto accept = [&](const Top2& t) {
+        float dist = match_distance(std::min(t.max, 262144));
+        float distn = match_distance(std::min(t.second, 262144));
+        return (dist < distmax) && (dist < distn * ratiomax) ? t.idx : -1;
+    };
+    std::vector<int> out;
+    for (int i = 0; i < n1 && (int)out.size() / 2 < max_match; ++i) {
+        int j = accept(rows[i]);
+        if (j >= 0 && (!mbm || accept(cols[j]) == i)) {
+            out.push_back(i);
+            out.push_back(j);
+        }
+    }
+    return out;
+}
+
 float match_distance(int dot) {
     // RowMatch_Kernel / ColMatch_Kernel (ProgramCU.cu:1838-1839, 1884-1885):
     // float product, min with 1.0 in double, acos in double, stored as float.
@@ -834,6 +927,21 @@ int oracle_match(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float dis
 }
 
 float oracle_match_distance(int dot) { return oracle::match_distance(dot); }
+
+int oracle_match_guided(const uint8_t* d1, int n1, const uint8_t* d2, int n2, const float* loc1,
+                        const float* loc2, const float* H, const float* F, float distmax,
+                        float ratiomax, float hdistmax, float fdistmax, int mbm, int max_match,
+                        int* out_pairs) {
+    std::vector<int> m = oracle::match_guided(d1, n1, d2, n2, loc1, loc2, H, F, distmax, ratiomax,
+                                              hdistmax, fdistmax, mbm, max_match);
+    memcpy(out_pairs, m.data(), m.size() * sizeof(int));
+    return (int)m.size() / 2;
+}
+
+int oracle_guided_pass(const float* H, const float* F, float x1, float y1, float x2, float y2,
+                       float hdistmax, float fdistmax) {
+    return oracle::guided_pass(H, F, x1, y1, x2, y2, hdistmax, fdistmax) ? 1 : 0;
+}
 
 void oracle_schedule(int dog_level_num, float* sigma0, float* sigma_skip0, float* sigmas,
                      int* widths) {

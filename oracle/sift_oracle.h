@@ -63,6 +63,15 @@ std::vector<float> describe_keys(const uint8_t* img, int w, int h, int stride,
 std::vector<int> match(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float distmax,
                        float ratiomax, int mbm, int max_match);
 
+// Guided matching (SiftMatchCU::GetGuidedSiftMatch): loc1/loc2 (x, y) per feature, H and F
+// row-major 3x3.
+std::vector<int> match_guided(const uint8_t* d1, int n1, const uint8_t* d2, int n2,
+                              const float* loc1, const float* loc2, const float* H,
+                              const float* F, float distmax, float ratiomax, float hdistmax,
+                              float fdistmax, int mbm, int max_match);
+bool guided_pass(const float* H, const float* F, float x1, float y1, float x2, float y2,
+                 float hdistmax, float fdistmax);
+
 // acos distance table shared with the HIP path's definition: dist[v] for dot v in [0, 262144].
 float match_distance(int dot);
 

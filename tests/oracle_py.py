@@ -43,6 +43,12 @@ def lib():
         L.oracle_match.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                    ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_void_p]
+        L.oracle_match_guided.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
+                                          ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        L.oracle_guided_pass.argtypes = [ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_float] * 6
         L.oracle_match_distance.argtypes = [ctypes.c_int]
         L.oracle_match_distance.restype = ctypes.c_float
         L.oracle_schedule.argtypes = [ctypes.c_int, P(ctypes.c_float), P(ctypes.c_float),
@@ -146,6 +152,39 @@ def match(d1: np.ndarray, d2: np.ndarray, distmax=0.7, ratiomax=0.8, mbm=1, max_
     m = lib().oracle_match(d1.ctypes.data, n1, d2.ctypes.data, n2, distmax, ratiomax, mbm,
                            max_match, out.ctypes.data)
     return out[:m]
+
+
+_IDENTITY = np.eye(3, dtype=np.float32)
+
+
+def match_guided(d1, d2, loc1, loc2, H=None, F=None, distmax=0.7, ratiomax=0.8, hdistmax=32.0,
+                 fdistmax=16.0, mbm=1, max_match=None):
+    """SiftMatchGPU::GetGuidedSiftMatch (SiftMatch.cpp:663-677) including its NULL-matrix
+    defaults; None/None is plain matching."""
+    if H is None and F is None:
+        return match(d1, d2, distmax, ratiomax, mbm, max_match)
+    hdistmax = hdistmax if H is not None else 1.0e20
+    fdistmax = fdistmax if F is not None else 1.0e20
+    H = np.ascontiguousarray(_IDENTITY if H is None else H, np.float32)
+    F = np.ascontiguousarray(_IDENTITY if F is None else F, np.float32)
+    d1 = np.ascontiguousarray(d1, np.uint8)
+    d2 = np.ascontiguousarray(d2, np.uint8)
+    l1 = np.ascontiguousarray(loc1, np.float32)
+    l2 = np.ascontiguousarray(loc2, np.float32)
+    n1, n2 = d1.shape[0], d2.shape[0]
+    max_match = n1 if max_match is None else max_match
+    out = np.zeros((max(max_match, 1), 2), np.int32)
+    m = lib().oracle_match_guided(d1.ctypes.data, n1, d2.ctypes.data, n2, l1.ctypes.data,
+                                  l2.ctypes.data, H.ctypes.data, F.ctypes.data, distmax, ratiomax,
+                                  hdistmax, fdistmax, mbm, max_match, out.ctypes.data)
+    return out[:m]
+
+
+def guided_pass(H, F, x1, y1, x2, y2, hdistmax, fdistmax):
+    H = np.ascontiguousarray(H, np.float32)
+    F = np.ascontiguousarray(F, np.float32)
+    return bool(lib().oracle_guided_pass(H.ctypes.data, F.ctypes.data, x1, y1, x2, y2,
+                                         hdistmax, fdistmax))
 
 
 def bench_extract(images: np.ndarray, opts=None, threads=1):

@@ -19,7 +19,8 @@ import pytest
 import oracle_py as O
 import sgpu
 from sgpu_types import default_options
-from sift_synth import synth_batch, synth_descriptors, synth_image, quantize
+from sift_synth import (synth_batch, synth_descriptors, synth_guided_scene, synth_image,
+                        quantize)
 
 pytestmark = pytest.mark.gpu
 
@@ -449,3 +450,82 @@ def test_keypoint_api_replica(tmp_path):
         rk, rd = O.describe_keys(img, keys, has_o)
         assert np.array_equal(_bits(k), _bits(rk)), name
         assert np.array_equal(_bits(d), _bits(rd)), name
+
+
+# ---- guided matching (SiftMatchGPU::SetFeautreLocation + GetGuidedSiftMatch) -----------------
+@pytest.mark.parametrize("n1,n2,hd,fd,mbm", [(1, 1, 32.0, 16.0, 1), (7, 9, 1e3, 1e3, 1),
+                                             (300, 250, 32.0, 16.0, 1), (301, 257, 8.0, 1.0, 0),
+                                             (1000, 1300, 32.0, 16.0, 1),
+                                             (4097, 3001, 16.0, 4.0, 1)])
+def test_match_guided_vs_oracle(gpu_ctx, n1, n2, hd, fd, mbm):
+    q1, q2, l1, l2, H, F = synth_guided_scene(n1, n2, n1 * 3 + n2)
+    for Hm, Fm in ((H, F), (H, None), (None, F)):
+        a = gpu_ctx.match_guided(q1, q2, l1, l2, Hm, Fm, hdistmax=hd, fdistmax=fd, mbm=mbm)
+        b = O.match_guided(q1, q2, l1, l2, Hm, Fm, hdistmax=hd, fdistmax=fd, mbm=mbm)
+        assert np.array_equal(a, b), (Hm is None, Fm is None, len(a), len(b))
+    if n1 >= 300:
+        assert len(b) > 10
+
+
+def test_match_guided_block_rule(gpu_ctx):
+    """The 8-row block rule of MultiplyDescriptorG_Kernel (see test_oracle's planted case)."""
+    q1, q2, l1, l2, H, F = synth_guided_scene(64, 40, 9, n_dup=0)
+    self_dot = (q1.astype(np.int64) ** 2).sum(1)
+    r = int(next(i for i in range(1, 64) if self_dot[i] > 262144 and i % 8))
+    mate, j = r - r % 8 + (0 if r % 8 else 1), 17
+    q2[j] = q1[r]
+    x = H.astype(np.float64) @ np.array([l1[mate, 0], l1[mate, 1], 1.0])
+    l2[j] = (x[:2] / x[2]).astype(np.float32)
+    for dm, rm, mbm in ((2.0, 1.0, 0), (2.0, 1.0, 1), (0.7, 0.8, 1)):
+        a = gpu_ctx.match_guided(q1, q2, l1, l2, H, F, distmax=dm, ratiomax=rm, mbm=mbm)
+        b = O.match_guided(q1, q2, l1, l2, H, F, distmax=dm, ratiomax=rm, mbm=mbm)
+        assert np.array_equal(a, b)
+        if mbm == 0:
+            assert [r, j] in a.tolist()
+
+
+def test_match_guided_accept_all_is_plain_match(gpu_ctx):
+    """Size-independent property at 8k x 8k: an all-accepting geometry (identity, 1e20) and no
+    geometry at all both give exactly the plain matches (SiftMatch.cpp:663-677)."""
+    q1, q2, l1, l2, H, F = synth_guided_scene(8192, 8000, 77)
+    plain = gpu_ctx.match(q1, q2)
+    assert len(plain) > 1000
+    assert np.array_equal(gpu_ctx.match_guided(q1, q2, l1, l2, None, None), plain)
+    eye = np.eye(3, dtype=np.float32)
+    assert np.array_equal(gpu_ctx.match_guided(q1, q2, l1, l2, eye, None, hdistmax=1e20), plain)
+    g = gpu_ctx.match_guided(q1, q2, l1, l2, H, F)
+    assert 0 < len(g) < len(plain)
+
+
+def test_guided_api_replica(tmp_path):
+    """SetDescriptors + SetFeatureLocation (gap 2) + GetGuidedSiftMatch through our SiftGPU.h."""
+    lib = os.path.join(ROOT, "modify-sift-gpu_amd", "lib", "libsiftgpu.so")
+    exe = tmp_path / "guided_replica"
+    r = subprocess.run(["g++", "-std=c++11", "-O1", "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "tests", "abi", "guided_replica.cpp"),
+                        "-o", str(exe), "-ldl"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    n1, n2 = 700, 650
+    q1, q2, l1, l2, H, F = synth_guided_scene(n1, n2, 41)
+    k1 = np.concatenate([l1, np.ones((n1, 2), np.float32)], 1)   # SiftKeypoint (x, y, s, o)
+    k2 = np.concatenate([l2, np.ones((n2, 2), np.float32)], 1)
+    th = np.array([0.7, 0.8, 32.0, 16.0], np.float32)
+    with open(tmp_path / "scene.bin", "wb") as f:
+        f.write(np.array([n1, n2], np.int32).tobytes())
+        for a in (q1, q2, k1, k2, H, F, th):
+            f.write(np.ascontiguousarray(a).tobytes())
+        f.write(np.array([1], np.int32).tobytes())
+    r = subprocess.run([str(exe), lib, str(tmp_path / "scene.bin")], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    cases, cur = [], None
+    for line in r.stdout.splitlines():
+        if line.startswith("CASE"):
+            cur = []
+            cases.append(cur)
+        elif line.startswith("PAIR"):
+            cur.append([int(v) for v in line.split()[1:]])
+    assert len(cases) == 4
+    for got, (Hm, Fm) in zip(cases, ((H, F), (H, None), (None, F), (None, None))):
+        want = O.match_guided(q1, q2, l1, l2, Hm, Fm)
+        assert np.array_equal(np.array(got, np.int32).reshape(-1, 2), want)

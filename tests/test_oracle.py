@@ -10,7 +10,7 @@ import pytest
 
 import oracle_py as O
 from sgpu_types import default_options
-from sift_synth import synth_image, synth_descriptors, quantize
+from sift_synth import synth_image, synth_descriptors, quantize, synth_guided_scene
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -114,25 +114,29 @@ def test_extract_deterministic_and_sane():
     assert np.all(d1 <= 0.2 / np.float32(0.2 * np.sqrt(1) ) + 1)   # finite
 
 
+def _np_top(dm, distmax, ratiomax):
+    """RowMatch_Kernel decision (ProgramCU.cu:1795-1841) on a dense value matrix: running maximum
+    from (0, -1, 0), first index on ties, second = the largest remaining value."""
+    arg = np.argmax(dm, axis=1)
+    mx = dm[np.arange(dm.shape[0]), arg]
+    srt = np.sort(dm, axis=1)
+    sec = srt[:, -2] if dm.shape[1] > 1 else np.zeros_like(mx)
+    mx, sec = np.maximum(mx, 0), np.maximum(sec, 0)
+    dist = lambda v: np.arccos(np.minimum((np.minimum(v, 262144).astype(np.float32) * np.float32(2 ** -18)).astype(np.float64), 1.0)).astype(np.float32)
+    d1, d2 = dist(mx), dist(sec)
+    ok = (d1 < np.float32(distmax)) & (d1 < d2 * np.float32(ratiomax))
+    return np.where(ok & (mx > 0), arg, -1)
+
+
+def _np_pairs(r, c, mbm):
+    out = [(i, j) for i, j in enumerate(r) if j >= 0 and (not mbm or c[j] == i)]
+    return np.array(out, np.int32).reshape(-1, 2)
+
+
 def _numpy_match(q1, q2, distmax=0.7, ratiomax=0.8, mbm=1):
     """Independent float64 restatement of RowMatch/ColMatch + GetBestMatch."""
     dot = q1.astype(np.int64) @ q2.astype(np.int64).T
-
-    def top(dm):
-        arg = np.argmax(dm, axis=1)
-        mx = dm[np.arange(dm.shape[0]), arg]
-        srt = np.sort(dm, axis=1)
-        sec = srt[:, -2] if dm.shape[1] > 1 else np.zeros_like(mx)
-        mx, sec = np.maximum(mx, 0), np.maximum(sec, 0)
-        dist = lambda v: np.arccos(np.minimum((v.astype(np.float32) * np.float32(2 ** -18)).astype(np.float64), 1.0)).astype(np.float32)
-        d1, d2 = dist(mx), dist(sec)
-        ok = (d1 < np.float32(distmax)) & (d1 < d2 * np.float32(ratiomax))
-        return np.where(ok & (mx > 0), arg, -1)
-
-    r = top(dot)
-    c = top(dot.T)
-    out = [(i, j) for i, j in enumerate(r) if j >= 0 and (not mbm or c[j] == i)]
-    return np.array(out, np.int32).reshape(-1, 2)
+    return _np_pairs(_np_top(dot, distmax, ratiomax), _np_top(dot.T, distmax, ratiomax), mbm)
 
 
 @pytest.mark.parametrize("mbm", [1, 0])
@@ -196,3 +200,91 @@ def test_u8_scale_is_exact_division():
         r = _round_f32(-Fraction(float(q)) * 255 + Fraction(float(x)))
         q2 = _round_f32(Fraction(float(r)) * Fraction(float(c)) + Fraction(float(q)))
         assert q2 == np.float32(x / np.float32(255.0)), p
+
+
+# ---- guided matching (SiftMatchGPU::GetGuidedSiftMatch) ---------------------------------------
+def _pass_matrix(l1, l2, H, F, hd, fd):
+    return np.array([[O.guided_pass(H, F, float(a[0]), float(a[1]), float(b[0]), float(b[1]), hd, fd)
+                      for b in l2] for a in l1], bool)
+
+
+def _numpy_guided(q1, q2, passm, distmax=0.7, ratiomax=0.8, mbm=1):
+    """Dense restatement of MultiplyDescriptorG_Kernel (ProgramCU.cu:1607-1735): a failed pair
+    gets -2^18, plus its dot when its 8-row block has a passing row; rows see max(v, 0)."""
+    dot = q1.astype(np.int64) @ q2.astype(np.int64).T
+    n1 = q1.shape[0]
+    nb = (n1 + 7) // 8
+    pad = np.zeros((nb * 8, q2.shape[0]), bool)
+    pad[:n1] = passm
+    good = pad.reshape(nb, 8, -1).any(axis=1)[np.arange(n1) // 8]
+    res = np.where(passm, dot, np.where(good, dot - 262144, -262144))
+    return _np_pairs(_np_top(np.maximum(res, 0), distmax, ratiomax),
+                     _np_top(res.T, distmax, ratiomax), mbm)
+
+
+def test_guided_pass_vs_float64():
+    """The geometric test against a float64 evaluation, away from the thresholds."""
+    q1, q2, l1, l2, H, F = synth_guided_scene(60, 50, 11)
+    H64, F64 = H.astype(np.float64), F.astype(np.float64)
+    checked = 0
+    for a in l1[:30]:
+        for b in l2:
+            x1 = np.array([a[0], a[1], 1.0])
+            hx = H64 @ x1
+            diff = np.abs(hx[:2] / hx[2] - b.astype(np.float64))
+            fx1 = F64 @ x1
+            ftx2 = F64.T @ np.array([b[0], b[1], 1.0])
+            se = (b[0] * fx1[0] + b[1] * fx1[1] + fx1[2]) ** 2 / (fx1[0] ** 2 + fx1[1] ** 2 + ftx2[0] ** 2 + ftx2[1] ** 2)
+            for hd, fd in ((32.0, 16.0), (4.0, 0.5), (1e20, 1e20)):
+                if np.min(np.abs(diff - hd)) < 1e-2 * hd or abs(se - fd) < 1e-2 * fd:
+                    continue
+                want = bool(diff.max() < hd and se < fd)
+                assert O.guided_pass(H, F, float(a[0]), float(a[1]), float(b[0]), float(b[1]), hd, fd) == want
+                checked += 1
+    assert checked > 3000
+
+
+@pytest.mark.parametrize("n1,n2,hd,fd,mbm", [(300, 250, 32.0, 16.0, 1), (301, 257, 8.0, 1.0, 1),
+                                             (173, 190, 32.0, 16.0, 0), (9, 7, 64.0, 1e3, 1)])
+def test_guided_oracle_vs_numpy(n1, n2, hd, fd, mbm):
+    q1, q2, l1, l2, H, F = synth_guided_scene(n1, n2, n1 + n2)
+    passm = _pass_matrix(l1, l2, H, F, hd, fd)
+    got = O.match_guided(q1, q2, l1, l2, H, F, hdistmax=hd, fdistmax=fd, mbm=mbm)
+    want = _numpy_guided(q1, q2, passm, mbm=mbm)
+    np.testing.assert_array_equal(got, want)
+    if n1 > 100:
+        assert len(want) > 10
+
+
+def test_guided_block_rule_matters():
+    """A failed pair whose 8-row block has a passing row keeps max(dot - 2^18, 0).  Plant one:
+    set-2 feature j copies row r's descriptor (self dot > 2^18) but sits at H x1 of r's block mate,
+    so only the block rule gives row r a positive value at j; with distmax 2, ratiomax 1 and one-way
+    matching it is accepted, and a per-pair mask would not accept it."""
+    q1, q2, l1, l2, H, F = synth_guided_scene(64, 40, 9, n_dup=0)
+    self_dot = (q1.astype(np.int64) ** 2).sum(1)
+    r = int(next(i for i in range(1, 64) if self_dot[i] > 262144 and i % 8))
+    mate, j = r - r % 8 + (0 if r % 8 else 1), 17
+    q2[j] = q1[r]
+    x = H.astype(np.float64) @ np.array([l1[mate, 0], l1[mate, 1], 1.0])
+    l2[j] = (x[:2] / x[2]).astype(np.float32)
+    passm = _pass_matrix(l1, l2, H, F, 32.0, 16.0)
+    assert passm[mate, j] and not passm[r, j]
+    got = O.match_guided(q1, q2, l1, l2, H, F, distmax=2.0, ratiomax=1.0, mbm=0)
+    np.testing.assert_array_equal(got, _numpy_guided(q1, q2, passm, 2.0, 1.0, 0))
+    assert [r, j] in got.tolist()
+    dot = q1.astype(np.int64) @ q2.astype(np.int64).T
+    per_pair = _np_top(np.where(passm, dot, 0), 2.0, 1.0)
+    assert per_pair[r] != j
+
+
+def test_guided_defaults():
+    """SiftMatch.cpp:663-677: no matrices = plain matching; an all-accepting geometry (identity,
+    thresholds 1e20) gives the plain matches too."""
+    q1, q2, l1, l2, H, F = synth_guided_scene(200, 180, 5)
+    plain = O.match(q1, q2)
+    np.testing.assert_array_equal(O.match_guided(q1, q2, l1, l2, None, None), plain)
+    np.testing.assert_array_equal(O.match_guided(q1, q2, l1, l2, np.eye(3), None, hdistmax=1e20), plain)
+    np.testing.assert_array_equal(O.match_guided(q1, q2, l1, l2, None, np.eye(3), fdistmax=1e20), plain)
+    g = O.match_guided(q1, q2, l1, l2, H, F)
+    assert 0 < len(g) < len(plain)
