@@ -26,7 +26,7 @@ import numpy as np  # noqa: E402
 
 import sgpu  # noqa: E402  (loads libsiftgpu.so before torch: one HIP runtime, /opt/rocm's)
 from sgpu_types import default_options  # noqa: E402
-from sift_synth import synth_batch, synth_descriptors, quantize  # noqa: E402
+from sift_synth import synth_batch, synth_descriptors, synth_guided_scene, quantize  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters (spec)
 I8_MFMA_PEAK_TOPS = 5000.0     # dense i8 MFMA = 2x the ~2.5 PF bf16 rate (same guide)
@@ -227,10 +227,19 @@ def bench_match(ctx, n):
         ms += ctx.timing()["match"]
     ms /= reps
     ops = 2.0 * 128 * n * n * 2      # both directions (rows and columns) are computed
+    # guided matching (GetGuidedSiftMatch) on a synthetic two-view scene of the same size
+    g1, g2, l1, l2, H, F = synth_guided_scene(n, n, 5002)
+    ctx.match_guided(g1, g2, l1, l2, H, F)
+    gms, gm = 0.0, None
+    for _ in range(reps):
+        gm = ctx.match_guided(g1, g2, l1, l2, H, F)
+        gms += ctx.timing()["match"]
+    gms /= reps
     return {"workload": f"C5 {n}x{n} u8 descriptors, mutual best match",
             "ms": ms, "matches": int(len(m)),
             "tops": ops / (ms * 1e-3) / 1e12,
-            "mfma_util": ops / (ms * 1e-3) / 1e12 / I8_MFMA_PEAK_TOPS}
+            "mfma_util": ops / (ms * 1e-3) / 1e12 / I8_MFMA_PEAK_TOPS,
+            "guided_ms": gms, "guided_matches": int(len(gm))}
 
 
 def cpu_baseline(imgs, opts):

@@ -708,9 +708,8 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
         b = ctx->m_d2.as<uint8_t>();
     }
     // guided: locations (float2 per feature) and the two geometric masks
-    const int pitch_r = (n2 + 3) & ~3, pitch_c = (n1 + 7) & ~7;
-    const size_t rmask_bytes = (size_t)2 * ((n1 + 7) / 8) * pitch_r;
-    const size_t cmask_bytes = mbm ? (size_t)((n2 + 3) / 4) * pitch_c : 0;
+    const size_t rmask_bytes = sgk::guided_mask_bytes(n1, n2);
+    const size_t cmask_bytes = mbm ? sgk::guided_mask_bytes(n2, n1) : 0;
     const float* l1 = loc1;
     const float* l2 = loc2;
     if (guided) {
@@ -741,24 +740,18 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     uint8_t* rmask = guided ? ctx->m_mask.as<uint8_t>() : nullptr;
     uint8_t* cmask = guided && mbm ? rmask + rmask_bytes : nullptr;
     if (guided)
-        HIPCHK(ctx, sgk::launch_guided_mask(l1, n1, l2, n2, *guided, rmask, pitch_r, cmask,
-                                            pitch_c, st));
-    // guided: the row term goes into the accumulators and the finish adds none
+        HIPCHK(ctx, sgk::launch_guided_mask(l1, n1, l2, n2, *guided, rmask, cmask, st));
     HIPCHK(ctx, sgk::launch_rowsums(a, n1, row1, 128, 0, st));
     HIPCHK(ctx, sgk::launch_rowsums(b, n2, col2, 128, -2097152, st));
-    HIPCHK(ctx, sgk::launch_match_rows(a, n1, b, n2, col2, ca, part, st, guided ? 1 : 0, row1,
-                                       rmask, pitch_r));
-    HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, guided ? nullptr : row1,
-                                         ctx->m_dist.as<float>(), distmax, ratiomax, match1,
-                                         nullptr, st));
+    HIPCHK(ctx, sgk::launch_match_rows(a, n1, b, n2, col2, ca, part, st, rmask));
+    HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, row1, ctx->m_dist.as<float>(), distmax,
+                                         ratiomax, match1, nullptr, st));
     if (mbm) {
         HIPCHK(ctx, sgk::launch_rowsums(b, n2, row2, 128, 0, st));
         HIPCHK(ctx, sgk::launch_rowsums(a, n1, col1, 128, -2097152, st));
-        HIPCHK(ctx, sgk::launch_match_rows(b, n2, a, n1, col1, cb, part, st, guided ? 2 : 0, row2,
-                                           cmask, pitch_c));
-        HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, guided ? nullptr : row2,
-                                             ctx->m_dist.as<float>(), distmax, ratiomax, match2,
-                                             nullptr, st));
+        HIPCHK(ctx, sgk::launch_match_rows(b, n2, a, n1, col1, cb, part, st, cmask));
+        HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, row2, ctx->m_dist.as<float>(), distmax,
+                                             ratiomax, match2, nullptr, st));
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
     ctx->h_match.resize((size_t)n1 + n2);

@@ -112,19 +112,20 @@ struct Top2 { int max, idx, second; };
 hipError_t launch_rowsums(const uint8_t* d, int n, int* s, int scale, int bias, hipStream_t stream);
 int match_chunks(int nA, int nB);
 // part[chunk][nA]: per-row top-2 of (A_i . B_j + col_term[j]) over each column chunk.
-// guided_mode 1 / 2: the guided values of the row / column decision (k_match_rows), with the
-// row term folded in (row_term) and the geometric mask of launch_guided_mask.
+// With a mask (launch_guided_mask, this side's lane records): the guided values
+// (k_match_rows<true>).
 hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
                              const int* col_term, int chunks, Top2* part, hipStream_t stream,
-                             int guided_mode = 0, const int* row_term = nullptr,
-                             const uint8_t* mask = nullptr, int mask_pitch = 0);
+                             const uint8_t* mask = nullptr);
 // Guided matching geometry (SiftMatchGPU::GetGuidedSiftMatch): H, F row-major 3x3.
 struct GuidedParams { float H[9]; float F[9]; float hdistmax, fdistmax; };
-// loc1 [n1][2], loc2 [n2][2].  rmask: (2 * ceil(n1 / 8)) x pitch_r bytes, pitch_r % 4 == 0,
-// pitch_r >= n2; cmask (optional): ceil(n2 / 4) x pitch_c bytes, pitch_c % 8 == 0, >= n1.
+// bytes of one side's guided mask records (A rows, B columns)
+size_t guided_mask_bytes(int nA, int nB);
+// loc1 [n1][2], loc2 [n2][2]; rec1 = guided_mask_bytes(n1, n2) bytes (row decision), rec2
+// (optional) = guided_mask_bytes(n2, n1) bytes (column decision).
 hipError_t launch_guided_mask(const float* loc1, int n1, const float* loc2, int n2,
-                              const GuidedParams& gp, uint8_t* rmask, int pitch_r,
-                              uint8_t* cmask, int pitch_c, hipStream_t stream);
+                              const GuidedParams& gp, uint8_t* rec1, uint8_t* rec2,
+                              hipStream_t stream);
 // merge chunks, add row_term, apply distmax / ratiomax -> out[i] = matched index or -1
 hipError_t launch_match_finish(const Top2* part, int n, int chunks, const int* row_term,
                                const float* dist, float distmax, float ratiomax, int* out,

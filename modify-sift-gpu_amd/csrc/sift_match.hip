@@ -61,22 +61,25 @@ __device__ __forceinline__ v4i load16_s8(const uint8_t* p) {
 // One row panel of A against columns [c_begin, c_end) of B.
 // part[chunk * nA + row] = running top-2 of row over those columns (dot without the row term).
 //
-// Guided matching (MODE 1: A = set 1, the row decision; MODE 2: A = set 2, the column
-// decision) folds the guided value of MultiplyDescriptorG_Kernel (ProgramCU.cu:1683-1733)
-// instead of the dot: the accumulators then start at row term + column term (the exact dot, the
-// masking below is not monotone in it), and `mask` (k_guided_mask) holds one byte per (4-row
-// group of A, column): bit i = pair (4g+i, col) passes the geometric test, bit 4+i = some row of
-// that pair's 8-row block of set 1 passes at that column (good_count > 0).
-//   MODE 1: pass ? dot : good ? max(dot - 2^18, 0) : 0      (d_result = max(results, 0))
-//   MODE 2: pass ? dot : good ? dot - 2^18 : -2^18          (the raw results of d_temp)
-template <int MODE>
+// Guided matching (GUIDED: the guided values of MultiplyDescriptorG_Kernel, ProgramCU.cu:
+// 1683-1733, for the row decision with A = set 1 or the column decision with A = set 2).  The
+// reference's value of a pair is dot (pass), dot - 2^18 (fail, but its 8-row block of set 1 has
+// a passing row: good_count > 0) or -2^18 (no passing row); rows see max(v, 0).  Both decisions
+// only ask which values are > 0 and how they order (running top-2 from (0, -1, 0); the finish
+// clamps at 0), so dot - bias with bias = 2^18 * fail + 2^23 * !good decides identically
+// (dot < 2^23 for u8 descriptors).  The bias goes into the accumulator's initial value, the row
+// term stays in the finish as in the plain matcher: two VALU per value more than plain.
+// `mask` (k_guided_mask) holds, per (32-row block of A, 128-column tile of B, lane), the lane's
+// 16-byte record: byte rb * 8 + cb covers rows 32 R + 16 rb + 4 quad + i and column
+// 128 T + 16 cb + l16 of this lane's accumulators; bit i = that pair fails the geometric test,
+// bit 4+i = no row of its 8-row block of set 1 passes.  One dwordx4 load per lane and tile.
+template <bool GUIDED>
 __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ A, int nA,
                                                     const uint8_t* __restrict__ B, int nB,
                                                     const int* __restrict__ col_term,
                                                     int cols_per_chunk, Top2* __restrict__ part,
-                                                    const int* __restrict__ row_term,
-                                                    const uint8_t* __restrict__ mask,
-                                                    int mask_pitch) {
+                                                    const uint4* __restrict__ mask,
+                                                    int mask_tiles) {
     __shared__ __attribute__((aligned(16))) uint8_t s_b[2][kTile * kLdsRow];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int panel = blockIdx.x, chunk = blockIdx.y;
@@ -95,18 +98,11 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
             else afrag[rb][kh] = v4i{0, 0, 0, 0};
         }
     }
-    // guided: the row terms of this lane's rows and their 4-row mask groups
-    int rterm[2][4] = {};
-    int mgroup[2] = {};
-    if constexpr (MODE != 0) {
-#pragma unroll
-        for (int rb = 0; rb < 2; rb++) {
-            const int r0 = panel * kPanel + wave * 32 + rb * 16 + quad * 4;
-            mgroup[rb] = r0 < nA ? r0 >> 2 : -1;
-#pragma unroll
-            for (int i = 0; i < 4; i++) rterm[rb][i] = r0 + i < nA ? row_term[r0 + i] : 0;
-        }
-    }
+    // guided: this lane's mask records (rows past nA read none)
+    const bool rec_ok = GUIDED && panel * kPanel + wave * 32 < nA;
+    const uint4* rec_p = rec_ok ? mask + (size_t)(panel * 4 + wave) * mask_tiles * 64 + lane : nullptr;
+    uint4 rec = make_uint4(0, 0, 0, 0);
+    if (rec_ok && c_begin < c_end) rec = rec_p[(c_begin / kTile) * 64];
     // running state for this lane's 8 output rows: (rb, i) -> row wave*32 + rb*16 + quad*4 + i
     int M[2][4], S[2][4], I[2][4];
 #pragma unroll
@@ -142,23 +138,25 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
     for (int tb = c_begin; tb < c_end; tb += kTile) {
         const bool has_next = tb + kTile < c_end;
         if (has_next) stage_load(tb + kTile, stg);
+        uint4 rec_next = rec;
+        if (rec_ok && has_next) rec_next = rec_p[(tb / kTile + 1) * 64];
         // accumulators start at the column term (invalid columns: -inf)
         v4i acc[2][8];
-        uint32_t mb[2][8];
 #pragma unroll
         for (int cb = 0; cb < 8; cb++) {
             const int col = tb + cb * 16 + l16;
             const int ct = col < c_end ? col_term[col] : kNegCol;
-            if constexpr (MODE == 0) {
+            if constexpr (!GUIDED) {
                 acc[0][cb] = v4i{ct, ct, ct, ct};
                 acc[1][cb] = acc[0][cb];
             } else {
 #pragma unroll
                 for (int rb = 0; rb < 2; rb++) {
-                    acc[rb][cb] = v4i{ct + rterm[rb][0], ct + rterm[rb][1], ct + rterm[rb][2],
-                                      ct + rterm[rb][3]};
-                    mb[rb][cb] = (col < c_end && mgroup[rb] >= 0)
-                                     ? mask[(size_t)mgroup[rb] * mask_pitch + col] : 0u;
+                    const uint32_t w = rb == 0 ? (cb < 4 ? rec.x : rec.y) : (cb < 4 ? rec.z : rec.w);
+                    const int mb = (int)(w >> ((cb & 3) * 8));
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        acc[rb][cb][i] = ct - (((mb >> i) & 1) << 18) - (((mb >> (4 + i)) & 1) << 23);
                 }
             }
         }
@@ -187,14 +185,7 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
                 int m = m0, sv = S[rb][i];
 #pragma unroll
                 for (int cb = 0; cb < 8; cb++) {
-                    int v = acc[rb][cb][i];
-                    if constexpr (MODE != 0) {
-                        const bool pass = (mb[rb][cb] >> i) & 1u;
-                        const bool good = (mb[rb][cb] >> (4 + i)) & 1u;
-                        const int off = MODE == 1 ? max(v - 262144, 0) : v - 262144;
-                        v = pass ? v : (good ? off : (MODE == 1 ? 0 : -262144));
-                    }
-                    const int key = (v << 3) | (7 - cb);
+                    const int key = (acc[rb][cb][i] << 3) | (7 - cb);
                     sv = med3i(sv, m, key);
                     m = max(m, key);
                 }
@@ -207,6 +198,7 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
             buf ^= 1;
             stage_store(buf, stg);
         }
+        rec = rec_next;
         __syncthreads();
     }
     // keys -> (dot, column): column = tile + 16 * (7 - low bits) + l16
@@ -264,7 +256,7 @@ __global__ __launch_bounds__(256) void k_match_finish(const Top2* __restrict__ p
         const int id = u.max > t.max ? u.idx : (t.max > u.max ? t.idx : min((unsigned)t.idx, (unsigned)u.idx));
         t = Top2{m, id, s};
     }
-    const int rt = row_term ? row_term[r] : 0;   // guided: folded in the accumulators
+    const int rt = row_term[r];
     // the reference's running maxima start at 0 with index -1 (ProgramCU.cu:1803)
     int mx = t.max + rt, sc = t.second + rt;
     int idx = t.idx;
@@ -277,99 +269,156 @@ __global__ __launch_bounds__(256) void k_match_finish(const Top2* __restrict__ p
 
 // Geometric test of MultiplyDescriptorG_Kernel (ProgramCU.cu:1648-1681), once per pair, in
 // the operation order of oracle::guided_pass (row-only and column-only terms are hoisted, which
-// does not change any value; FDIV(a, b) = a * (1 / b)).  One thread per (8-row block of set 1,
-// 4 columns of set 2); it writes both masks k_match_rows<1/2> read:
-//   rmask[g][j] (4-row groups g of set 1, pitch pitch_r): bit i = pass(4g+i, j), bits 4-7 = good
-//   cmask[q][r] (4-row groups q of set 2, pitch pitch_c): bit c = pass(r, 4q+c), bit 4+c = good
-// where good(r, j) = some row of r's 8-row block passes at j (good_count > 0, :1682).
+// does not change any value; FDIV(a, b) = a * (1 / b)).  One workgroup per 128 x 128 block of
+// pairs at a time (set-1 tile a = blockIdx.y; kMaskTiles set-2 tiles b in turn from
+// blockIdx.x * kMaskTiles): each thread tests one set-1 row
+// against 64 columns (the homography branch-free, the Sampson error only for the pairs that
+// passed it) into an LDS bit matrix, which is then read out as both sides' 16-byte lane records
+// (k_match_rows): rec1 for the row decision (A = set 1, tiles of set 2), rec2 for the column
+// decision (A = set 2, tiles of set 1), both written coalesced.
+// good(r, j) = some row of r's 8-row block of set 1 passes at j (good_count > 0, :1682).
+constexpr int kPassPitch = 5;   // words per LDS bit row (4 + 1 against bank conflicts)
+
+constexpr int kMaskTiles = 8;   // set-2 tiles per workgroup (amortises the row set-up)
+
 __global__ __launch_bounds__(256) void k_guided_mask(const float2* __restrict__ loc1, int n1,
                                                      const float2* __restrict__ loc2, int n2,
-                                                     GuidedParams gp, uint8_t* __restrict__ rmask,
-                                                     int pitch_r, uint8_t* __restrict__ cmask,
-                                                     int pitch_c) {
-    const int nq = (n2 + 3) >> 2, nblk = (n1 + 7) >> 3;
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= (int64_t)nq * nblk) return;
-    const int q = (int)(t % nq), blk = (int)(t / nq);
+                                                     GuidedParams gp, uint4* __restrict__ rec1,
+                                                     int tiles2, uint4* __restrict__ rec2,
+                                                     int tiles1) {
+    __shared__ uint32_t s_pass[128 * kPassPitch];   // [set-1 row][set-2 column word]
+    __shared__ uint32_t s_good[16 * kPassPitch];    // [8-row block of set 1][column word]
+    __shared__ __attribute__((aligned(16))) float2 s_loc2[128];
+    const int tid = threadIdx.x;
+    const int a = blockIdx.y;
     const float* H = gp.H;
     const float* F = gp.F;
-    float x2[4], y2[4], t0[4], t1[4];
+    const int il = tid >> 1, h = tid & 1;
+    const int r = a * 128 + il;
+    const float2 l = loc1[min(r, n1 - 1)];
+    const float h0 = __builtin_fmaf(H[0], l.x, __builtin_fmaf(H[1], l.y, H[2]));
+    const float h1 = __builtin_fmaf(H[3], l.x, __builtin_fmaf(H[4], l.y, H[5]));
+    const float h2 = __builtin_fmaf(H[6], l.x, __builtin_fmaf(H[7], l.y, H[8]));
+    const float rh = 1.0f / h2;
+    const float u = h0 * rh, v = h1 * rh;
+    const int rr = tid >> 6, lane = tid & 63, quad = lane >> 4, l16 = lane & 15;
+    const int b_end = min(tiles2, (int)(blockIdx.x + 1) * kMaskTiles);
+    float2 next = make_float2(0.f, 0.f);
+    int b = blockIdx.x * kMaskTiles;
+    if (tid < 128 && b * 128 + tid < n2) next = loc2[b * 128 + tid];
+    for (; b < b_end; b++) {
+        if (tid < 128) s_loc2[tid] = next;
+        __syncthreads();
+        if (tid < 128 && b + 1 < b_end && (b + 1) * 128 + tid < n2) next = loc2[(b + 1) * 128 + tid];
+        uint32_t w[2];
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-        const int j = q * 4 + c;
-        const float2 l = j < n2 ? loc2[j] : make_float2(0.f, 0.f);
-        x2[c] = l.x;
-        y2[c] = l.y;
-        t0[c] = __builtin_fmaf(F[0], l.x, __builtin_fmaf(F[3], l.y, F[6]));
-        t1[c] = __builtin_fmaf(F[1], l.x, __builtin_fmaf(F[4], l.y, F[7]));
-    }
-    uint32_t pass = 0;   // bit k * 4 + c
+        for (int q = 0; q < 2; q++) {
+            // 32 columns' (x, y) as 16 ds_read_b128, then a branch-free test per pair (bitwise
+            // '&': a short-circuit '&&' compiles to a branch per pair)
+            const float4* c4 = reinterpret_cast<const float4*>(s_loc2 + h * 64 + q * 32);
+            float4 cc[16];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const int r = blk * 8 + k;
-        if (r >= n1) break;
-        const float2 l = loc1[r];
-        const float h0 = __builtin_fmaf(H[0], l.x, __builtin_fmaf(H[1], l.y, H[2]));
-        const float h1 = __builtin_fmaf(H[3], l.x, __builtin_fmaf(H[4], l.y, H[5]));
-        const float h2 = __builtin_fmaf(H[6], l.x, __builtin_fmaf(H[7], l.y, H[8]));
-        const float rh = 1.0f / h2;
-        const float u = h0 * rh, v = h1 * rh;
-        const float f0 = __builtin_fmaf(F[0], l.x, __builtin_fmaf(F[1], l.y, F[2]));
-        const float f1 = __builtin_fmaf(F[3], l.x, __builtin_fmaf(F[4], l.y, F[5]));
-        const float f2 = __builtin_fmaf(F[6], l.x, __builtin_fmaf(F[7], l.y, F[8]));
-        const float d0 = __builtin_fmaf(f1, f1, f0 * f0);
+            for (int k = 0; k < 16; k++) cc[k] = c4[k];
+            uint32_t bits = 0;
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
-            if (q * 4 + c >= n2) break;
-            if (!(__builtin_fabsf(u - x2[c]) < gp.hdistmax && __builtin_fabsf(v - y2[c]) < gp.hdistmax))
-                continue;
-            const float x2fx1 = __builtin_fmaf(x2[c], f0, __builtin_fmaf(y2[c], f1, f2));
-            const float den = __builtin_fmaf(t1[c], t1[c], __builtin_fmaf(t0[c], t0[c], d0));
-            const float se = (x2fx1 * x2fx1) * (1.0f / den);
-            if (se < gp.fdistmax) pass |= 1u << (k * 4 + c);
+            for (int k = 0; k < 16; k++) {
+                const bool ok0 = (__builtin_fabsf(u - cc[k].x) < gp.hdistmax) &
+                                 (__builtin_fabsf(v - cc[k].y) < gp.hdistmax);
+                const bool ok1 = (__builtin_fabsf(u - cc[k].z) < gp.hdistmax) &
+                                 (__builtin_fabsf(v - cc[k].w) < gp.hdistmax);
+                bits |= ((uint32_t)ok0 << (2 * k)) | ((uint32_t)ok1 << (2 * k + 1));
+            }
+            const int c0 = b * 128 + h * 64 + q * 32;   // first column of this word
+            const int nvalid = min(max(n2 - c0, 0), 32);
+            w[q] = r < n1 ? bits & (nvalid == 32 ? 0xffffffffu : ((1u << nvalid) - 1u)) : 0u;
         }
-    }
-    uint32_t good = 0;   // bit c
+        if (w[0] | w[1]) {
+            const float f0 = __builtin_fmaf(F[0], l.x, __builtin_fmaf(F[1], l.y, F[2]));
+            const float f1 = __builtin_fmaf(F[3], l.x, __builtin_fmaf(F[4], l.y, F[5]));
+            const float f2 = __builtin_fmaf(F[6], l.x, __builtin_fmaf(F[7], l.y, F[8]));
+            const float d0 = __builtin_fmaf(f1, f1, f0 * f0);
 #pragma unroll
-    for (int c = 0; c < 4; c++) good |= ((pass & (0x11111111u << c)) != 0) << c;
-    // rmask: groups 2 blk + h, bytes for columns 4q .. 4q+3
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            uint32_t b = ((good >> c) & 1u) ? 0xf0u : 0u;
-#pragma unroll
-            for (int i = 0; i < 4; i++) b |= ((pass >> ((4 * h + i) * 4 + c)) & 1u) << i;
-            w |= b << (8 * c);
+            for (int q = 0; q < 2; q++) {
+                for (uint32_t rest = w[q]; rest; rest &= rest - 1) {
+                    const int jj = __builtin_ctz(rest);
+                    const float2 p2 = s_loc2[h * 64 + q * 32 + jj];
+                    const float t0 = __builtin_fmaf(F[0], p2.x, __builtin_fmaf(F[3], p2.y, F[6]));
+                    const float t1 = __builtin_fmaf(F[1], p2.x, __builtin_fmaf(F[4], p2.y, F[7]));
+                    const float x2fx1 = __builtin_fmaf(p2.x, f0, __builtin_fmaf(p2.y, f1, f2));
+                    const float den = __builtin_fmaf(t1, t1, __builtin_fmaf(t0, t0, d0));
+                    const float se = (x2fx1 * x2fx1) * (1.0f / den);
+                    if (!(se < gp.fdistmax)) w[q] &= ~(1u << jj);
+                }
+            }
         }
-        *reinterpret_cast<uint32_t*>(rmask + (size_t)(2 * blk + h) * pitch_r + q * 4) = w;
-    }
-    // cmask: group q, bytes for rows 8 blk .. 8 blk + 7
-    if (cmask) {
-        uint32_t w[2] = {0, 0};
+        s_pass[il * kPassPitch + h * 2] = w[0];
+        s_pass[il * kPassPitch + h * 2 + 1] = w[1];
+        __syncthreads();
+        if (tid < 64) {
+            const int blk = tid >> 2, wd = tid & 3;
+            uint32_t g = 0;
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint32_t b = ((pass >> (k * 4)) & 0xfu) | (good << 4);
-            w[k >> 2] |= b << (8 * (k & 3));
+            for (int k = 0; k < 8; k++) g |= s_pass[(blk * 8 + k) * kPassPitch + wd];
+            s_good[blk * kPassPitch + wd] = g;
         }
-        *reinterpret_cast<uint2*>(cmask + (size_t)q * pitch_c + blk * 8) = make_uint2(w[0], w[1]);
+        __syncthreads();
+        // rec1: rows 32 (4a + rr) + 16 rb + 4 quad + i of set 1, columns 128 b + 16 cb + l16
+        if ((a * 4 + rr) * 32 < n1) {
+            uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int rb = 0; rb < 2; rb++) {
+                const int row0 = rr * 32 + rb * 16 + quad * 4;
+                const int blk = row0 >> 3;
+#pragma unroll
+                for (int cb = 0; cb < 8; cb++) {
+                    const int col = cb * 16 + l16, wd = col >> 5, bit = col & 31;
+                    uint32_t byte = ((s_good[blk * kPassPitch + wd] >> bit) & 1u) ? 0u : 0xf0u;
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        byte |= (((s_pass[(row0 + i) * kPassPitch + wd] >> bit) & 1u) ^ 1u) << i;
+                    o[rb * 2 + (cb >> 2)] |= byte << ((cb & 3) * 8);
+                }
+            }
+            rec1[((size_t)(a * 4 + rr) * tiles2 + b) * 64 + lane] = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        // rec2: rows 32 (4b + rr) + 16 rb + 4 quad + c of set 2, columns 128 a + 16 cb + l16 of
+        // set 1
+        if (rec2 && (b * 4 + rr) * 32 < n2) {
+            uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int cb = 0; cb < 8; cb++) {
+                const int rl = cb * 16 + l16;
+                const uint32_t pw = s_pass[rl * kPassPitch + rr];
+                const uint32_t gw = s_good[(rl >> 3) * kPassPitch + rr];
+#pragma unroll
+                for (int rb = 0; rb < 2; rb++) {
+                    const int sh = rb * 16 + quad * 4;
+                    const uint32_t byte = (~(pw >> sh) & 0xfu) | ((~(gw >> sh) & 0xfu) << 4);
+                    o[rb * 2 + (cb >> 2)] |= byte << ((cb & 3) * 8);
+                }
+            }
+            rec2[((size_t)(b * 4 + rr) * tiles1 + a) * 64 + lane] = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        // the next tile's s_loc2 / s_pass writes wait for every read of this one
+        __syncthreads();
     }
 }
 
 }  // namespace
 
+size_t guided_mask_bytes(int nA, int nB) {
+    return (size_t)((nA + 31) / 32) * ((nB + kTile - 1) / kTile) * 64 * 16;
+}
+
 hipError_t launch_guided_mask(const float* loc1, int n1, const float* loc2, int n2,
-                              const GuidedParams& gp, uint8_t* rmask, int pitch_r,
-                              uint8_t* cmask, int pitch_c, hipStream_t stream) {
+                              const GuidedParams& gp, uint8_t* rec1, uint8_t* rec2,
+                              hipStream_t stream) {
     if (n1 <= 0 || n2 <= 0) return hipSuccess;
-    if ((pitch_r & 3) || pitch_r < n2 || (cmask && ((pitch_c & 7) || pitch_c < n1)))
-        return hipErrorInvalidValue;
-    const int64_t threads = (int64_t)((n2 + 3) / 4) * ((n1 + 7) / 8);
-    hipLaunchKernelGGL(k_guided_mask, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream,
+    const int t1 = (n1 + kTile - 1) / kTile, t2 = (n2 + kTile - 1) / kTile;
+    hipLaunchKernelGGL(k_guided_mask, dim3((t2 + kMaskTiles - 1) / kMaskTiles, t1), dim3(256), 0, stream,
                        reinterpret_cast<const float2*>(loc1), n1,
-                       reinterpret_cast<const float2*>(loc2), n2, gp, rmask, pitch_r, cmask,
-                       pitch_c);
+                       reinterpret_cast<const float2*>(loc2), n2, gp,
+                       reinterpret_cast<uint4*>(rec1), t2, reinterpret_cast<uint4*>(rec2), t1);
     return hipGetLastError();
 }
 
@@ -390,22 +439,19 @@ int match_chunks(int nA, int nB) {
 
 hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
                              const int* col_term, int chunks, Top2* part, hipStream_t stream,
-                             int guided_mode, const int* row_term, const uint8_t* mask,
-                             int mask_pitch) {
+                             const uint8_t* mask) {
     if (nA <= 0 || nB <= 0) return hipSuccess;
     int per = (nB + chunks - 1) / chunks;
     per = (per + kTile - 1) / kTile * kTile;
     dim3 grid((nA + kPanel - 1) / kPanel, chunks);
-    if (guided_mode != 0 && (!row_term || !mask || mask_pitch < nB)) return hipErrorInvalidValue;
-    if (guided_mode == 0)
-        hipLaunchKernelGGL(k_match_rows<0>, grid, dim3(256), 0, stream, A, nA, B, nB, col_term,
-                           per, part, row_term, mask, mask_pitch);
-    else if (guided_mode == 1)
-        hipLaunchKernelGGL(k_match_rows<1>, grid, dim3(256), 0, stream, A, nA, B, nB, col_term,
-                           per, part, row_term, mask, mask_pitch);
+    const int tiles = (nB + kTile - 1) / kTile;
+    const uint4* rec = reinterpret_cast<const uint4*>(mask);
+    if (!mask)
+        hipLaunchKernelGGL(k_match_rows<false>, grid, dim3(256), 0, stream, A, nA, B, nB,
+                           col_term, per, part, rec, tiles);
     else
-        hipLaunchKernelGGL(k_match_rows<2>, grid, dim3(256), 0, stream, A, nA, B, nB, col_term,
-                           per, part, row_term, mask, mask_pitch);
+        hipLaunchKernelGGL(k_match_rows<true>, grid, dim3(256), 0, stream, A, nA, B, nB,
+                           col_term, per, part, rec, tiles);
     return hipGetLastError();
 }
 
