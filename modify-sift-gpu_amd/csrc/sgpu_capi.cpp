@@ -743,15 +743,15 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
         HIPCHK(ctx, sgk::launch_guided_mask(l1, n1, l2, n2, *guided, rmask, cmask, st));
     HIPCHK(ctx, sgk::launch_rowsums(a, n1, row1, 128, 0, st));
     HIPCHK(ctx, sgk::launch_rowsums(b, n2, col2, 128, -2097152, st));
-    HIPCHK(ctx, sgk::launch_match_rows(a, n1, b, n2, col2, ca, part, st, rmask));
+    HIPCHK(ctx, sgk::launch_match_rows(a, n1, b, n2, col2, ca, part, st, rmask, true));
     HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, row1, ctx->m_dist.as<float>(), distmax,
-                                         ratiomax, match1, nullptr, st));
+                                         ratiomax, match1, nullptr, st, true));
     if (mbm) {
         HIPCHK(ctx, sgk::launch_rowsums(b, n2, row2, 128, 0, st));
         HIPCHK(ctx, sgk::launch_rowsums(a, n1, col1, 128, -2097152, st));
-        HIPCHK(ctx, sgk::launch_match_rows(b, n2, a, n1, col1, cb, part, st, cmask));
+        HIPCHK(ctx, sgk::launch_match_rows(b, n2, a, n1, col1, cb, part, st, cmask, false));
         HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, row2, ctx->m_dist.as<float>(), distmax,
-                                             ratiomax, match2, nullptr, st));
+                                             ratiomax, match2, nullptr, st, false));
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
     ctx->h_match.resize((size_t)n1 + n2);

@@ -112,11 +112,12 @@ struct Top2 { int max, idx, second; };
 hipError_t launch_rowsums(const uint8_t* d, int n, int* s, int scale, int bias, hipStream_t stream);
 int match_chunks(int nA, int nB);
 // part[chunk][nA]: per-row top-2 of (A_i . B_j + col_term[j]) over each column chunk.
+// row_side: equal maxima resolve as RowMatch_Kernel does (A = set 1); else in column order.
 // With a mask (launch_guided_mask, this side's lane records): the guided values
 // (k_match_rows<true>).
 hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
                              const int* col_term, int chunks, Top2* part, hipStream_t stream,
-                             const uint8_t* mask = nullptr);
+                             const uint8_t* mask, bool row_side);
 // Guided matching geometry (SiftMatchGPU::GetGuidedSiftMatch): H, F row-major 3x3.
 struct GuidedParams { float H[9]; float F[9]; float hdistmax, fdistmax; };
 // bytes of one side's guided mask records (A rows, B columns)
@@ -129,6 +130,6 @@ hipError_t launch_guided_mask(const float* loc1, int n1, const float* loc2, int 
 // merge chunks, add row_term, apply distmax / ratiomax -> out[i] = matched index or -1
 hipError_t launch_match_finish(const Top2* part, int n, int chunks, const int* row_term,
                                const float* dist, float distmax, float ratiomax, int* out,
-                               Top2* best, hipStream_t stream);
+                               Top2* best, hipStream_t stream, bool row_side);
 
 }  // namespace sgk

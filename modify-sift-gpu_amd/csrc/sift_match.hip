@@ -24,9 +24,13 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr int kPanel = 128;      // A rows per workgroup (4 waves x 32)
 constexpr int kTile = 128;       // B columns per LDS tile
 constexpr int kLdsRow = 128 + 16;// bytes per staged B row (padding against bank conflicts)
-constexpr int kNeg = -(1 << 29); // "minus infinity" for running maxima (no overflow with offsets)
-constexpr int kNegCol = -(1 << 26);  // column term of a missing column: its dot stays far below
-                                     // every real one (|dot| < 2^23) and (dot << 3) fits in int32
+// Running maxima hold keys (acc << 7) | low, acc = dot - row term (- guided bias) in
+// [-2^23 - 2^22, 2^23]: every key fits in int32 and INT_MIN is below all of them.
+constexpr int kNeg = INT_MIN;
+// Column term of a missing column: its acc stays <= 0 (a staged zero column adds at most 2^21),
+// so with the row term >= 0 added in the finish it can neither win nor raise a second maximum,
+// and (acc << 7) does not overflow.
+constexpr int kNegCol = -(1 << 22);
 
 // v_med3_i32: the median of three.  With s <= m, med3(s, m, v) is the new second maximum after
 // seeing v (v > m -> m; s < v <= m -> v; v <= s -> s).
@@ -46,6 +50,15 @@ __global__ __launch_bounds__(256) void k_rowsum(const uint8_t* __restrict__ d, i
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
     if (lane == 0) s[i] = scale * t + bias;
+}
+
+// Equal-dot order of the two decisions: does column a come before column b (-1 = none)?
+template <bool TIE32>
+__device__ __forceinline__ bool tie_before(int a, int b) {
+    if (a < 0) return false;
+    if (b < 0) return true;
+    if (TIE32 && (a & 31) != (b & 31)) return (a & 31) < (b & 31);
+    return a < b;
 }
 
 __device__ __forceinline__ v4i load16_s8(const uint8_t* p) {
@@ -73,7 +86,14 @@ __device__ __forceinline__ v4i load16_s8(const uint8_t* p) {
 // 16-byte record: byte rb * 8 + cb covers rows 32 R + 16 rb + 4 quad + i and column
 // 128 T + 16 cb + l16 of this lane's accumulators; bit i = that pair fails the geometric test,
 // bit 4+i = no row of its 8-row block of set 1 passes.  One dwordx4 load per lane and tile.
-template <bool GUIDED>
+//
+// Equal dots: the column side (A = set 2) takes the lowest column (ColMatch's row order); the
+// row side (A = set 1, TIE32) takes the column lowest mod 32, then the lowest, as RowMatch_Kernel's
+// 32 strided threads and tree reduction do (ProgramCU.cu:1803-1835).  Inside a tile the key's 7
+// low bits order equal dots that way, so the tile's maximum key is its winner.  Across tiles a
+// later tile may only take over when the key's tie-relevant prefix grows (the dot; TIE32: the dot
+// and col % 32), and the key is recorded with its tile at that moment.
+template <bool GUIDED, bool TIE32>
 __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ A, int nA,
                                                     const uint8_t* __restrict__ B, int nB,
                                                     const int* __restrict__ col_term,
@@ -103,12 +123,14 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
     const uint4* rec_p = rec_ok ? mask + (size_t)(panel * 4 + wave) * mask_tiles * 64 + lane : nullptr;
     uint4 rec = make_uint4(0, 0, 0, 0);
     if (rec_ok && c_begin < c_end) rec = rec_p[(c_begin / kTile) * 64];
-    // running state for this lane's 8 output rows: (rb, i) -> row wave*32 + rb*16 + quad*4 + i
-    int M[2][4], S[2][4], I[2][4];
+    // running state for this lane's 8 output rows: (rb, i) -> row wave*32 + rb*16 + quad*4 + i:
+    // max key, second key, tile of the winner and the winner's key when it was taken
+    int M[2][4], S[2][4], I[2][4], W[2][4];
 #pragma unroll
     for (int rb = 0; rb < 2; rb++)
 #pragma unroll
-        for (int i = 0; i < 4; i++) { M[rb][i] = kNeg; S[rb][i] = kNeg; I[rb][i] = -1; }
+        for (int i = 0; i < 4; i++) { M[rb][i] = kNeg; S[rb][i] = kNeg; I[rb][i] = -1; W[rb][i] = 0; }
+    constexpr uint32_t kPrefix = TIE32 ? 4u : 128u;   // keys differing below this bit tie
 
     // staging: thread t copies 64 bytes: column t>>1, half (t&1)
     auto stage_load = [&](int tbase, uint4* r) {
@@ -127,6 +149,15 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
             reinterpret_cast<uint4*>(dst)[q] = v;
         }
     };
+
+    // the key's low 7 bits per column block: a larger value = an earlier column in the
+    // reference's tie order (TIE32: (31 - col % 32) << 2 | (3 - col / 32 in the tile); else
+    // 127 - col in the tile)
+    int low[8];
+#pragma unroll
+    for (int cb = 0; cb < 8; cb++)
+        low[cb] = TIE32 ? ((31 - ((cb & 1) * 16 + l16)) << 2) | (3 - (cb >> 1))
+                        : 127 - (cb * 16 + l16);
 
     uint4 stg[4];
     int buf = 0;
@@ -173,10 +204,9 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         }
         // epilogue: fold the 2x8 tiles into the running top-2 (C layout: col = l16,
         // row = quad*4 + i within the 16-row block).  Values are folded as keys
-        // (dot << 3) | (7 - cb): one v_lshl_or, one v_max and one v_med3 per value; the key's
-        // low bits name the column block and the tile is recorded once per tile when the
-        // maximum moved.  Equal dots order by lower column first (the reference's strict '>'
-        // scan); the second key of an equal pair carries the same dot, so ties still reject.
+        // (acc << 7) | low[cb]: one v_lshl_or, one v_max and one v_med3 per value; the tile is
+        // recorded once per tile when the maximum moved.  The second key of an equal pair
+        // carries the same dot, so exact ties still reach the ratio test as the reference's do.
 #pragma unroll
         for (int rb = 0; rb < 2; rb++)
 #pragma unroll
@@ -185,11 +215,13 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
                 int m = m0, sv = S[rb][i];
 #pragma unroll
                 for (int cb = 0; cb < 8; cb++) {
-                    const int key = (acc[rb][cb][i] << 3) | (7 - cb);
+                    const int key = (acc[rb][cb][i] << 7) | low[cb];
                     sv = med3i(sv, m, key);
                     m = max(m, key);
                 }
-                I[rb][i] = m != m0 ? tb : I[rb][i];
+                const bool took = (uint32_t)(m ^ m0) >= kPrefix;
+                I[rb][i] = took ? tb : I[rb][i];
+                W[rb][i] = took ? m : W[rb][i];
                 M[rb][i] = m;
                 S[rb][i] = sv;
             }
@@ -201,17 +233,19 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         rec = rec_next;
         __syncthreads();
     }
-    // keys -> (dot, column): column = tile + 16 * (7 - low bits) + l16
+    // keys -> (acc, column)
 #pragma unroll
     for (int rb = 0; rb < 2; rb++)
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            const int k = M[rb][i];
-            I[rb][i] = I[rb][i] < 0 ? -1 : I[rb][i] + 16 * (7 - (k & 7)) + l16;
-            M[rb][i] = k >> 3;
-            S[rb][i] = S[rb][i] >> 3;
+            const int k = W[rb][i] & 127;
+            const int in_tile = TIE32 ? (3 - (k & 3)) * 32 + (31 - (k >> 2)) : 127 - k;
+            I[rb][i] = I[rb][i] < 0 ? -1 : I[rb][i] + in_tile;
+            M[rb][i] >>= 7;
+            S[rb][i] >>= 7;
         }
-    // merge the 16 lanes that share a row (same quad): xor 1, 2, 4, 8
+    // merge the 16 lanes that share a row (same quad): xor 1, 2, 4, 8; equal dots resolve in the
+    // side's tie order
 #pragma unroll
     for (int off = 1; off < 16; off <<= 1) {
 #pragma unroll
@@ -224,7 +258,7 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
                 const int m1 = M[rb][i], s1 = S[rb][i], i1 = I[rb][i];
                 M[rb][i] = max(m1, m2);
                 S[rb][i] = max(min(m1, m2), max(s1, s2));
-                I[rb][i] = m2 > m1 ? i2 : (m1 > m2 ? i1 : min((unsigned)i1, (unsigned)i2));
+                I[rb][i] = (m2 > m1 || (m2 == m1 && tie_before<TIE32>(i2, i1))) ? i2 : i1;
             }
     }
     if (l16 == 0) {
@@ -240,12 +274,14 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
 
 // Merge the column chunks of one side, add the row term, apply the distance/ratio test
 // (RowMatch_Kernel / ColMatch_Kernel decision, ProgramCU.cu:1838-1841, 1884-1887).
+// Equal maxima of two chunks resolve in the side's tie order (tie32: RowMatch_Kernel's, see
+// k_match_rows).
 __global__ __launch_bounds__(256) void k_match_finish(const Top2* __restrict__ part, int n,
                                                       int chunks, const int* __restrict__ row_term,
                                                       const float* __restrict__ dist,
                                                       float distmax, float ratiomax,
                                                       int* __restrict__ out,
-                                                      Top2* __restrict__ best) {
+                                                      Top2* __restrict__ best, int tie32) {
     const int r = blockIdx.x * 256 + threadIdx.x;
     if (r >= n) return;
     Top2 t = part[r];
@@ -253,8 +289,10 @@ __global__ __launch_bounds__(256) void k_match_finish(const Top2* __restrict__ p
         const Top2 u = part[(size_t)c * n + r];
         const int m = max(t.max, u.max);
         const int s = max(min(t.max, u.max), max(t.second, u.second));
-        const int id = u.max > t.max ? u.idx : (t.max > u.max ? t.idx : min((unsigned)t.idx, (unsigned)u.idx));
-        t = Top2{m, id, s};
+        const bool later = u.max > t.max ||
+                           (u.max == t.max && (tie32 ? tie_before<true>(u.idx, t.idx)
+                                                     : tie_before<false>(u.idx, t.idx)));
+        t = Top2{m, later ? u.idx : t.idx, s};
     }
     const int rt = row_term[r];
     // the reference's running maxima start at 0 with index -1 (ProgramCU.cu:1803)
@@ -439,28 +477,34 @@ int match_chunks(int nA, int nB) {
 
 hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
                              const int* col_term, int chunks, Top2* part, hipStream_t stream,
-                             const uint8_t* mask) {
+                             const uint8_t* mask, bool row_side) {
     if (nA <= 0 || nB <= 0) return hipSuccess;
     int per = (nB + chunks - 1) / chunks;
     per = (per + kTile - 1) / kTile * kTile;
     dim3 grid((nA + kPanel - 1) / kPanel, chunks);
     const int tiles = (nB + kTile - 1) / kTile;
     const uint4* rec = reinterpret_cast<const uint4*>(mask);
-    if (!mask)
-        hipLaunchKernelGGL(k_match_rows<false>, grid, dim3(256), 0, stream, A, nA, B, nB,
+    if (!mask && row_side)
+        hipLaunchKernelGGL((k_match_rows<false, true>), grid, dim3(256), 0, stream, A, nA, B, nB,
+                           col_term, per, part, rec, tiles);
+    else if (!mask)
+        hipLaunchKernelGGL((k_match_rows<false, false>), grid, dim3(256), 0, stream, A, nA, B,
+                           nB, col_term, per, part, rec, tiles);
+    else if (row_side)
+        hipLaunchKernelGGL((k_match_rows<true, true>), grid, dim3(256), 0, stream, A, nA, B, nB,
                            col_term, per, part, rec, tiles);
     else
-        hipLaunchKernelGGL(k_match_rows<true>, grid, dim3(256), 0, stream, A, nA, B, nB,
+        hipLaunchKernelGGL((k_match_rows<true, false>), grid, dim3(256), 0, stream, A, nA, B, nB,
                            col_term, per, part, rec, tiles);
     return hipGetLastError();
 }
 
 hipError_t launch_match_finish(const Top2* part, int n, int chunks, const int* row_term,
                                const float* dist, float distmax, float ratiomax, int* out,
-                               Top2* best, hipStream_t stream) {
+                               Top2* best, hipStream_t stream, bool row_side) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_match_finish, dim3((n + 255) / 256), dim3(256), 0, stream, part, n,
-                       chunks, row_term, dist, distmax, ratiomax, out, best);
+                       chunks, row_term, dist, distmax, ratiomax, out, best, row_side ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -112,3 +112,28 @@ def synth_guided_scene(n1: int, n2: int, seed: int, n_dup: int | None = None,
     loc2[2:n_dup:3] += rng.uniform(200, 400, (len(range(2, n_dup, 3)), 2))
     return (q1, q2, loc1.astype(np.float32), loc2.astype(np.float32), H.astype(np.float32),
             F.astype(np.float32))
+
+
+def synth_tie_scene(n1: int, n2: int, seed: int, col_pairs, row_pairs=()):
+    """Descriptor sets with exact ties at row maxima: for each (c_a, c_b) in col_pairs one row of
+    set 1 (self dot < 2^18, so distances stay > 0) is copied to set-2 columns c_a and c_b; for each
+    (r_a, r_b) in row_pairs rows r_a and r_b of set 1 copy one set-2 column (a column-side tie).
+    Matches on ties are accepted only with ratiomax > 1.  Returns (q1, q2, tied rows of set 1)."""
+    q1 = quantize(synth_descriptors(n1, seed))
+    q2 = quantize(synth_descriptors(n2, seed + 1))
+    used = {r for pair in row_pairs for r in pair}
+    rows = [i for i in range(n1) if i not in used and
+            int((q1[i].astype(np.int64) ** 2).sum()) < 262144][:len(col_pairs)]
+    for i, (ca, cb) in zip(rows, col_pairs):
+        q2[ca] = q1[i]
+        q2[cb] = q1[i]
+    for k, (ra, rb) in enumerate(row_pairs):
+        c = (k * 7919 + 11) % n2
+        q1[ra] = q2[c]
+        q1[rb] = q2[c]
+    return q1, q2, rows
+
+
+def tie_winner(ca: int, cb: int) -> int:
+    """RowMatch_Kernel's choice between two equal maxima: lowest column mod 32, then lowest."""
+    return min((ca, cb), key=lambda c: (c % 32, c))

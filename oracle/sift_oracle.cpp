@@ -706,6 +706,26 @@ std::vector<float> describe_keys(const uint8_t* img, int w, int h, int stride,
     return desc;
 }
 
+struct Top2 { int max = 0, idx = -1, second = 0; };
+
+// RowMatch_Kernel (ProgramCU.cu:1785-1835): 32 threads, thread t scans columns t, t+32, ... with
+// a running (max, second, idx) from (0, 0, -1) and strict '>'; a tree reduction then keeps the
+// lower thread on equal maxima, and the second is the largest value except the winner.  In
+// column order that is: a larger value wins; an equal value takes the index when its column is
+// lower mod 32 (same thread: the first occurrence stays); the second collects every other value.
+inline void row_fold(Top2& t, int v, int col) {
+    if (v > t.max) { t.second = t.max; t.max = v; t.idx = col; return; }
+    t.second = std::max(t.second, v);
+    if (v == t.max && t.idx >= 0 && (col & 31) < (t.idx & 31)) t.idx = col;
+}
+
+// MultiplyDescriptor(G)_Kernel's column partials + ColMatch_Kernel (ProgramCU.cu:1540-1552,
+// 1874-1882): the same running top-2 in row order, ties keep the earlier row.
+inline void col_fold(Top2& t, int v, int row) {
+    if (v > t.max) { t.second = t.max; t.max = v; t.idx = row; }
+    else t.second = std::max(t.second, v);
+}
+
 // --- Geometric test of MultiplyDescriptorG_Kernel (ProgramCU.cu:1648-1681) for one pair:
 //     |H x1 - x2| (both coordinates) < hdistmax, then the Sampson error of x2' F x1 < fdistmax.
 //     Contractions (nvcc's choice is not observable) are fixed as written out below on both
@@ -735,14 +755,13 @@ bool guided_pass(const float* H, const float* F, float x1, float y1, float x2, f
 // SiftMatchCU::GetGuidedSiftMatch (SiftMatchCU.cpp:126-136) = MultiplyDescriptorG_Kernel
 // (ProgramCU.cu:1607-1735) + the RowMatch / ColMatch decisions.  The guided dot of a pair is
 // its dot when the pair passes the geometric test; otherwise -262144, plus the dot when any
-// other row of its 8-row block (MULT_BLOCK_DIMY) passes at that column.  Rows: running top-2
-// from (0, -1, 0) with strict '>'; columns: the per-block (max, idx, second) of :1709-1721
-// merged over blocks as ColMatch_Kernel (:1874-1882).
+// other row of its 8-row block (MULT_BLOCK_DIMY) passes at that column.  Rows: row_fold over
+// max(v, 0); columns: the per-block (max, idx, second) of :1709-1721 merged over blocks as
+// ColMatch_Kernel (:1874-1882).
 std::vector<int> match_guided(const uint8_t* d1, int n1, const uint8_t* d2, int n2,
                               const float* loc1, const float* loc2, const float* H,
                               const float* F, float distmax, float ratiomax, float hdistmax,
                               float fdistmax, int mbm, int max_match) {
-    struct Top2 { int max = 0, idx = -1, second = 0; };
     std::vector<Top2> rows(n1), cols(n2);
     const int nblk = (n1 + 7) / 8;
     for (int j = 0; j < n2; j++) {
@@ -772,10 +791,7 @@ std::vector<int> match_guided(const uint8_t* d1, int n1, const uint8_t* d2, int 
                 if (r >= n1) break;
                 if (res[i] > cmp.max) { cmp.second = cmp.max; cmp.max = res[i]; cmp.idx = r; }
                 else cmp.second = std::max(cmp.second, res[i]);
-                const int v = std::max(res[i], 0);   // d_result = max(results, 0)
-                Top2& t = rows[r];
-                if (v > t.max) { t.second = t.max; t.max = v; t.idx = j; }
-                else t.second = std::max(t.second, v);
+                row_fold(rows[r], std::max(res[i], 0), j);   // d_result = max(results, 0)
             }
             if (blk == 0) colacc = cmp;
             else if (colacc.max < cmp.max) colacc = Top2{cmp.max, cmp.idx, std::max(colacc.max, cmp.second)};
@@ -807,21 +823,14 @@ float match_distance(int dot) {
 
 std::vector<int> match(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float distmax,
                        float ratiomax, int mbm, int max_match) {
-    struct Top2 { int max = 0, idx = -1, second = 0; };
     std::vector<Top2> rows(n1), cols(n2);
     // MultiplyDescriptor_Kernel (ProgramCU.cu:1466-1564): exact int dot products
     for (int i = 0; i < n1; i++)
         for (int j = 0; j < n2; j++) {
             int dot = 0;
             for (int k = 0; k < 128; k++) dot += (int)d1[i * 128 + k] * (int)d2[j * 128 + k];
-            // RowMatch (ProgramCU.cu:1803-1835) and the texCRT / ColMatch merge (:1540-1552,
-            // 1874-1882): running top-2 with strict '>', ties push the old max to second
-            Top2& r = rows[i];
-            if (dot > r.max) { r.second = r.max; r.max = dot; r.idx = j; }
-            else r.second = std::max(r.second, dot);
-            Top2& c = cols[j];
-            if (dot > c.max) { c.second = c.max; c.max = dot; c.idx = i; }
-            else c.second = std::max(c.second, dot);
+            row_fold(rows[i], dot, j);
+            col_fold(cols[j], dot, i);
         }
     auto accept = [&](const Top2& t) {
         float dist = match_distance(std::min(t.max, 262144));

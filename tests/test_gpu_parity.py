@@ -20,7 +20,7 @@ import oracle_py as O
 import sgpu
 from sgpu_types import default_options
 from sift_synth import (synth_batch, synth_descriptors, synth_guided_scene, synth_image,
-                        quantize)
+                        synth_tie_scene, tie_winner, quantize)
 
 pytestmark = pytest.mark.gpu
 
@@ -259,6 +259,23 @@ def test_match_ties_and_duplicates(gpu_ctx):
     assert np.array_equal(gpu_ctx.match(base, q2), O.match(base, q2))
     zeros = np.zeros((50, 128), np.uint8)
     assert np.array_equal(gpu_ctx.match(zeros, zeros), O.match(zeros, zeros))
+
+
+@pytest.mark.parametrize("n1,n2,cols", [
+    (70, 100, [(5, 34), (40, 66), (3, 99), (31, 32), (7, 39)]),
+    # across 128-column tiles (same and different col % 32) and across column chunks
+    (3000, 9000, [(200, 129), (130, 2), (4000, 33), (8999, 1), (640, 4064), (7000, 5000)]),
+])
+def test_match_exact_ties(gpu_ctx, n1, n2, cols):
+    """ratiomax > 1 accepts exact ties, so the winner's index shows: RowMatch_Kernel's order on
+    the row side, the first row on the column side (oracle pinned by test_oracle)."""
+    q1, q2, rows = synth_tie_scene(n1, n2, n1 + n2, cols, [(60, 61), (1, n1 - 5)])
+    for mbm in (0, 1):
+        a = gpu_ctx.match(q1, q2, distmax=2.0, ratiomax=1.5, mbm=mbm)
+        b = O.match(q1, q2, distmax=2.0, ratiomax=1.5, mbm=mbm)
+        assert np.array_equal(a, b), mbm
+    pairs = dict(map(tuple, gpu_ctx.match(q1, q2, distmax=2.0, ratiomax=1.5, mbm=0).tolist()))
+    assert [pairs.get(i) for i in rows] == [tie_winner(x, y) for x, y in cols]
 
 
 def test_match_max_match_truncates(gpu_ctx):

@@ -10,7 +10,8 @@ import pytest
 
 import oracle_py as O
 from sgpu_types import default_options
-from sift_synth import synth_image, synth_descriptors, quantize, synth_guided_scene
+from sift_synth import (synth_image, synth_descriptors, quantize, synth_guided_scene,
+                        synth_tie_scene, tie_winner)
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -114,11 +115,17 @@ def test_extract_deterministic_and_sane():
     assert np.all(d1 <= 0.2 / np.float32(0.2 * np.sqrt(1) ) + 1)   # finite
 
 
-def _np_top(dm, distmax, ratiomax):
-    """RowMatch_Kernel decision (ProgramCU.cu:1795-1841) on a dense value matrix: running maximum
-    from (0, -1, 0), first index on ties, second = the largest remaining value."""
+def _np_top(dm, distmax, ratiomax, mod32=False):
+    """Row/column decision on a dense value matrix: maximum from (0, -1, 0), second = the largest
+    remaining value.  Equal maxima: the first index (ColMatch order), or with mod32 the index
+    lowest mod 32, then lowest (RowMatch_Kernel's 32 strided threads + tree reduction,
+    ProgramCU.cu:1803-1835)."""
     arg = np.argmax(dm, axis=1)
     mx = dm[np.arange(dm.shape[0]), arg]
+    if mod32:
+        cols = np.arange(dm.shape[1])
+        rank = np.where(dm == mx[:, None], (cols % 32) * dm.shape[1] + cols, np.iinfo(np.int64).max)
+        arg = np.argmin(rank, axis=1)
     srt = np.sort(dm, axis=1)
     sec = srt[:, -2] if dm.shape[1] > 1 else np.zeros_like(mx)
     mx, sec = np.maximum(mx, 0), np.maximum(sec, 0)
@@ -136,7 +143,7 @@ def _np_pairs(r, c, mbm):
 def _numpy_match(q1, q2, distmax=0.7, ratiomax=0.8, mbm=1):
     """Independent float64 restatement of RowMatch/ColMatch + GetBestMatch."""
     dot = q1.astype(np.int64) @ q2.astype(np.int64).T
-    return _np_pairs(_np_top(dot, distmax, ratiomax), _np_top(dot.T, distmax, ratiomax), mbm)
+    return _np_pairs(_np_top(dot, distmax, ratiomax, True), _np_top(dot.T, distmax, ratiomax), mbm)
 
 
 @pytest.mark.parametrize("mbm", [1, 0])
@@ -160,6 +167,21 @@ def test_matcher_ties_and_wrap():
     np.testing.assert_array_equal(got, want)
     assert 0 not in got[:, 0]
     assert quantize(np.array([[0.5]], np.float32))[0, 0] == 0      # int(256.5) -> 256 -> 0
+
+
+# tied column pairs: within a 32-column group, across threads, same thread (first occurrence)
+TIE_COLS = [(5, 34), (40, 66), (3, 99), (31, 32), (7, 39)]
+
+
+@pytest.mark.parametrize("mbm", [0, 1])
+def test_matcher_tie_rules(mbm):
+    q1, q2, rows = synth_tie_scene(70, 100, 21, TIE_COLS, [(60, 61)])
+    got = O.match(q1, q2, distmax=2.0, ratiomax=1.5, mbm=mbm)
+    np.testing.assert_array_equal(got, _numpy_match(q1, q2, 2.0, 1.5, mbm))
+    if not mbm:
+        pairs = dict(map(tuple, got.tolist()))
+        assert [pairs[i] for i in rows] == [tie_winner(a, b) for a, b in TIE_COLS]
+        assert [pairs[i] for i in rows] == [34, 66, 3, 32, 7]
 
 
 def test_golden_fixtures():
@@ -218,7 +240,7 @@ def _numpy_guided(q1, q2, passm, distmax=0.7, ratiomax=0.8, mbm=1):
     pad[:n1] = passm
     good = pad.reshape(nb, 8, -1).any(axis=1)[np.arange(n1) // 8]
     res = np.where(passm, dot, np.where(good, dot - 262144, -262144))
-    return _np_pairs(_np_top(np.maximum(res, 0), distmax, ratiomax),
+    return _np_pairs(_np_top(np.maximum(res, 0), distmax, ratiomax, True),
                      _np_top(res.T, distmax, ratiomax), mbm)
 
 
