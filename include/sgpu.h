@@ -35,7 +35,7 @@ typedef struct sgpu_options {
     int subpixel;                      /* -s   (1)                                          */
     int max_orientation;               /* -m   (2)                                          */
     int fixed_orientation;             /* -ofix (0)                                         */
-    int octave_min;                    /* -fo  (0; only 0 is implemented)                   */
+    int octave_min;                    /* -fo  first octave, >= -2 (0)                       */
     int octave_num;                    /* -no  (-1 = floor(log2(min(w,h)))-3)                */
     int dog_level_num;                 /* -d   (3)                                          */
     int lowe_origin;                   /* -loweo (0)                                        */

@@ -231,7 +231,11 @@ int sgpu_ctx_set_options(sgpu_ctx* ctx, const sgpu_options* opt) {
     if (!ctx) return SGPU_EINVAL;
     sgpu_options o;
     if (opt) o = *opt; else sgpu_default_options(&o);
-    if (o.octave_min != 0) return ctx->fail(SGPU_EINVAL, "only first octave 0 (-fo 0) is implemented");
+    // -fo -2 is accepted by the reference's parser (SiftGPU.cpp:1075) but its initial smoothing
+    // sigma is then 0 (sqrt only when 1.6 > 0.5 * 4 + 0.001, SiftGPU.cpp:446-452) and
+    // CreateFilterKernel(0) yields NaN taps (ProgramCU.cu:391-398): a NaN pyramid.  Rejected.
+    if (o.octave_min < -1)
+        return ctx->fail(SGPU_EINVAL, "first octave must be >= -1 (-fo -2 gives the reference a NaN pyramid)");
     if (o.dog_level_num < 1 || o.dog_level_num > 6) return ctx->fail(SGPU_EINVAL, "dog_level_num must be 1..6");
     ctx->opt = o;
     sgp::Options po;
@@ -239,6 +243,7 @@ int sgpu_ctx_set_options(sgpu_ctx* ctx, const sgpu_options* opt) {
     po.dog_level_num = o.dog_level_num;
     po.dog_threshold = o.dog_threshold;
     po.edge_threshold = o.edge_threshold;
+    po.octave_min = o.octave_min;
     ctx->sched = sgp::make_schedule(po);
     return SGPU_OK;
 }
@@ -356,6 +361,7 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     fp.circular = O.circular_window;
     fp.normalize = O.normalized;
     fp.origin_offset = O.lowe_origin ? 0.0f : 0.5f;
+    fp.octave_min = O.octave_min;
 
     // candidate capacity: grow-only, first guess one per 256 octave pixels
     const size_t sum_px = (size_t)goff / (size_t)std::max(1, nlev) / (size_t)n;
@@ -404,8 +410,19 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
         float* lvl0 = pyr + od.gauss_off;
         if (o == 0) {
             int fw = sgp::make_filter(S.initial_smooth, O.filter_width_factor, taps.k);
-            HIPCHK(ctx, sgk::launch_gauss(srcf, src8, stride, (long long)img_elems, lvl0, npx,
-                                          od.wa, od.h, fw, taps, n, nullptr, 0, 0, 0, st));
+            if (O.octave_min == 0) {
+                HIPCHK(ctx, sgk::launch_gauss(srcf, src8, stride, (long long)img_elems, lvl0, npx,
+                                              od.wa, od.h, fw, taps, n, nullptr, 0, 0, 0, st));
+            } else {
+                // -fo != 0: resample the input into level 1's storage (free until level 1 is
+                // filtered), then the initial smoothing as for a float input
+                float* tmp = lvl0 + od.level_stride;
+                HIPCHK(ctx, sgk::launch_first_octave_input(srcf, src8, stride, (long long)img_elems,
+                                                           ctx->w & ~3, h, O.octave_min, tmp,
+                                                           od.wa, od.h, npx, n, st));
+                HIPCHK(ctx, sgk::launch_gauss(tmp, nullptr, od.wa, npx, lvl0, npx, od.wa, od.h,
+                                              fw, taps, n, nullptr, 0, 0, 0, st));
+            }
         }
         for (int k = 1; k < nlev; k++) {
             int fw = sgp::make_filter(S.sigma[k - 1], O.filter_width_factor, taps.k);
@@ -496,7 +513,7 @@ static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
         return ctx->fail(SGPU_EINVAL, "staged input does not match the batch");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     const sgpu_options& O = ctx->opt;
-    ctx->oct = sgp::make_octaves(w, h, O.octave_num, 0);
+    ctx->oct = sgp::make_octaves(w, h, O.octave_num, O.octave_min);
     const int noct = (int)ctx->oct.size();
     if (noct > sgk::kMaxOctaves) return ctx->fail(SGPU_EINVAL, "too many octaves");
     for (const auto& oc : ctx->oct)
@@ -612,7 +629,7 @@ int sgpu_extract_keypoints(sgpu_ctx* ctx, int image, const float* keys, int num,
     std::vector<float4> lf;
     std::vector<int2> li;
     std::vector<int> lidx;
-    float octave_sigma = 1.0f;
+    float octave_sigma = ldexpf(1.0f, O.octave_min);   // PyramidCU.cpp:461
     for (int i = 0; i < noct; i++, octave_sigma *= 2.0f)
         for (int j = 0; j < d; j++) {
             const float level_sigma = sgp::level_sigma(S, j + S.level_min + 1) * octave_sigma;

@@ -38,6 +38,7 @@ struct FeatureParams {
     float window_factor;                 // descriptor (3.0)
     int subpixel, num_orientation, keep_sign, circular, normalize;
     float origin_offset;                 // 0.5 (or 0 with -loweo)
+    int octave_min;                      // -fo: octave o of the pyramid is octave o + octave_min
     OctaveDesc oct[kMaxOctaves];
 };
 
@@ -50,6 +51,15 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         int w, int h, int fw, const Taps& taps, int batch,
                         float* ds_dst, int ds_w, int ds_h, long long ds_img_stride,
                         hipStream_t stream);
+
+// First octave of -fo != 0 (BuildPyramid, PyramidCU.cpp:1011-1016): the batch's input
+// (u8 p/255 or f32; tw = w & ~3 columns used, rows `stride` apart) resampled into dst
+// (dw x dh per image, dst_img_stride apart): SampleImageD by 2^fo for fo > 0, UpsampleKernel
+// by 2^-fo for fo < 0 (then dw = tw << -fo).
+hipError_t launch_first_octave_input(const float* src, const uint8_t* src_u8, int stride,
+                                     long long src_img_stride, int tw, int h, int fo, float* dst,
+                                     int dw, int dh, long long dst_img_stride, int batch,
+                                     hipStream_t stream);
 
 // Extremum detection for all octaves, all d levels and all images (one launch): sets the
 // keypoint bits in the zeroed mask and adds per-row keypoint counts into the zeroed row_count

@@ -1544,6 +1544,74 @@ __global__ __launch_bounds__(256) void k_orientation(const float* __restrict__ p
 }
 
 // ------------------------------------------------------------------------------------------
+// -fo != 0: the first octave's input.  src value of input pixel k of the flat tw x h buffer
+// the reference binds (_inputTex, PyramidCU.cpp:949-958): u8 -> p / 255.0f as the host
+// conversion (GLTexImage.cpp:818); indices past the buffer read 0 (tex1Dfetch).
+template <bool U8>
+__device__ __forceinline__ float input_at(const float* sf, const uint8_t* s8, int stride, int tw,
+                                          int h, long long k) {
+    if (k >= (long long)tw * h) return 0.0f;
+    const int r = (int)(k / tw), c = (int)(k - (long long)r * tw);
+    return U8 ? u8_to_unit(s8[(long long)r * stride + c]) : sf[(long long)r * stride + c];
+}
+
+// DownsampleKernel (ProgramCU.cu:287-311): dst(r, c) = src(r << fo, min(c << fo, tw - 1)).
+template <bool U8>
+__global__ __launch_bounds__(256) void k_input_down(const float* __restrict__ src,
+                                                    const uint8_t* __restrict__ src8, int stride,
+                                                    long long src_img_stride, int tw, int h,
+                                                    int fo, float* __restrict__ dst, int dw, int dh,
+                                                    long long dst_img_stride) {
+    const int b = blockIdx.z, r = blockIdx.y;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= dw || r >= dh) return;
+    const long long so = (long long)b * src_img_stride;
+    const int sc = min(c << fo, tw - 1), sr = r << fo;
+    const float v = U8 ? u8_to_unit(src8[so + (long long)sr * stride + sc])
+                       : src[so + (long long)sr * stride + sc];
+    dst[(long long)b * dst_img_stride + (long long)r * dw + c] = v;
+}
+
+// UpsampleKernel<s> (ProgramCU.cu:225-270): output row R blends source rows R >> s and
+// (R >> s) + 1 with w1 = (R & (S-1)) / S; each source column c writes S outputs at
+// (tw R + c) S interpolating c and c + 1 of the flat buffer.  a*b + c*d -> fma(a, b, c*d).
+template <bool U8>
+__global__ __launch_bounds__(256) void k_input_up(const float* __restrict__ src,
+                                                  const uint8_t* __restrict__ src8, int stride,
+                                                  long long src_img_stride, int tw, int h, int s,
+                                                  float* __restrict__ dst,
+                                                  long long dst_img_stride) {
+    const int b = blockIdx.z, R = blockIdx.y;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= tw) return;
+    const int S = 1 << s;
+    const float inv = 1.0f / float(S);
+    const float* sf = U8 ? nullptr : src + (long long)b * src_img_stride;
+    const uint8_t* s8 = U8 ? src8 + (long long)b * src_img_stride : nullptr;
+    const int row = R >> s, helper = R & (S - 1);
+    const long long index = (long long)row * tw + c;
+    float v1, v2;
+    if (helper) {
+        const float v11 = input_at<U8>(sf, s8, stride, tw, h, index);
+        const float v12 = input_at<U8>(sf, s8, stride, tw, h, index + 1);
+        const float v21 = input_at<U8>(sf, s8, stride, tw, h, index + tw);
+        const float v22 = input_at<U8>(sf, s8, stride, tw, h, index + tw + 1);
+        const float w1 = inv * (float)helper, w2 = 1.0f - w1;   // (float)(1.0 - w1): exact
+        v1 = fma_(v21, w1, w2 * v11);
+        v2 = fma_(v22, w1, w2 * v12);
+    } else {
+        v1 = input_at<U8>(sf, s8, stride, tw, h, index);
+        v2 = input_at<U8>(sf, s8, stride, tw, h, index + 1);
+    }
+    float* o = dst + (long long)b * dst_img_stride + ((long long)tw * R + c) * S;
+    o[0] = v1;
+    for (int i = 1; i < S; i++) {
+        const float r2 = (float)i * inv, r1 = 1.0f - r2;
+        o[i] = fma_(v1, r1, v2 * r2);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Feature expansion + image coordinates (PyramidCU.cpp:521-606 / 701-751).
 __global__ __launch_bounds__(256) void k_expand(const float4* __restrict__ cand,
                                                 const int2* __restrict__ info,
@@ -1559,7 +1627,7 @@ __global__ __launch_bounds__(256) void k_expand(const float4* __restrict__ cand,
     const float4 c = cand[f];
     const int2 in = info[f];
     const int o = in.y / fp.d;
-    const float oss = (float)(1 << o);
+    const float oss = ldexpf(1.0f, o + fp.octave_min);   // os * 2^o, os = 2^octave_min
     const double twopi = 2.0 * 3.14159265358979323846;
     float ang[2];
     if (fp.num_orientation >= 2) {
@@ -1805,7 +1873,7 @@ __global__ __launch_bounds__(256) void k_orient_keys(const float* __restrict__ p
         }
         if (sub == 0) {
             feat[e].w = angle;
-            const float os = (float)(1 << o);
+            const float os = ldexpf(1.0f, o + fp.octave_min);
             keys_out[index[e]] = make_float4(os * (k.x - 0.5f) + fp.origin_offset,
                                              os * (k.y - 0.5f) + fp.origin_offset, os * k.z,
                                              (float)fmod(twopi - (double)angle, twopi));
@@ -1859,6 +1927,35 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
         default: return hipErrorInvalidValue;
     }
 #undef SGK_GAUSS
+}
+
+hipError_t launch_first_octave_input(const float* src, const uint8_t* src_u8, int stride,
+                                     long long src_img_stride, int tw, int h, int fo, float* dst,
+                                     int dw, int dh, long long dst_img_stride, int batch,
+                                     hipStream_t stream) {
+    if (fo > 0) {
+        if (dw > (tw >> fo) + 3 || dh > (h >> fo)) return hipErrorInvalidValue;
+        const dim3 grid((dw + 255) / 256, dh, batch);
+        if (src_u8)
+            hipLaunchKernelGGL(k_input_down<true>, grid, dim3(256), 0, stream, src, src_u8, stride,
+                               src_img_stride, tw, h, fo, dst, dw, dh, dst_img_stride);
+        else
+            hipLaunchKernelGGL(k_input_down<false>, grid, dim3(256), 0, stream, src, src_u8,
+                               stride, src_img_stride, tw, h, fo, dst, dw, dh, dst_img_stride);
+    } else if (fo < 0) {
+        const int s = -fo;
+        if (s > 3 || dw != (tw << s) || dh != (h << s)) return hipErrorInvalidValue;
+        const dim3 grid((tw + 255) / 256, h << s, batch);
+        if (src_u8)
+            hipLaunchKernelGGL(k_input_up<true>, grid, dim3(256), 0, stream, src, src_u8, stride,
+                               src_img_stride, tw, h, s, dst, dst_img_stride);
+        else
+            hipLaunchKernelGGL(k_input_up<false>, grid, dim3(256), 0, stream, src, src_u8, stride,
+                               src_img_stride, tw, h, s, dst, dst_img_stride);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,

@@ -25,7 +25,7 @@ struct Options {
     int subpixel = 1;                       // -s   GlobalUtil.cpp:63
     int max_orientation = 2;                // -m   GlobalUtil.cpp:64
     int fixed_orientation = 0;              // -ofix GlobalUtil.cpp:117
-    int octave_min = 0;                     // -fo  GlobalUtil.cpp:111 (only >= 0 supported)
+    int octave_min = 0;                     // -fo  GlobalUtil.cpp:111, -2 .. (SiftGPU.cpp:1074-1077)
     int octave_num = -1;                    // -no  GlobalUtil.cpp:112
     int dog_level_num = 3;                  // -d   SiftGPU.cpp:436
     float dog_threshold = 0.0f;             // -t   0 -> 0.02/d (SiftGPU.cpp:495)
@@ -105,11 +105,15 @@ inline int make_filter(float sigma, float factor, float* taps) {
 // every level image is wa x h floats with wa = ((w+3)/4)*4.
 struct Octave { int w, h, wa; };
 
-// Octave geometry for an input of w x h pixels (first octave 0, no -maxd clamping).
-// octave_num <= 0 selects floor(log2(min(w,h))) - 3 (PyramidCU.cpp:206-210).
+// Octave geometry for an input of w x h pixels (no -maxd clamping).  The first octave is
+// octave_min (-fo): its size is the truncated input shifted by octave_min, up-sampled for
+// octave_min < 0 (PyramidCU::InitPyramid, PyramidCU.cpp:89-112; SiftGPU::AllocatePyramid,
+// SiftGPU.cpp:1435-1448).  octave_num <= 0 selects floor(log2(min(w,h))) - 3 of that size
+// (SiftPyramid::GetRequiredOctaveNum, SiftPyramid.cpp:279-285).
 inline std::vector<Octave> make_octaves(int w, int h, int octave_num, int octave_min = 0) {
     w &= ~3;  // TruncateWidthCU (GLTexImage.h:125) via PyramidCU::InitPyramid:95
-    int wp = w >> octave_min, hp = h >> octave_min;
+    int wp = octave_min >= 0 ? w >> octave_min : w << -octave_min;
+    int hp = octave_min >= 0 ? h >> octave_min : h << -octave_min;
     int n = octave_num;
     if (n < 1) {
         int m = wp < hp ? wp : hp;

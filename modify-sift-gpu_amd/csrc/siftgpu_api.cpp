@@ -245,7 +245,7 @@ SiftGPU::~SiftGPU() {
 
 void SiftGPU::PrintUsage() {
     std::cout << "SiftGPU (MI355X) usage: -i <files> -o <file> -f <float> -w <float> -dw <float>\n"
-                 "  -fo 0 -no <int> -d <int> -t <float> -e <float> -m [int] -s [int] -sd -unn -b\n"
+                 "  -fo <int> -no <int> -d <int> -t <float> -e <float> -m [int] -s [int] -sd -unn -b\n"
                  "  -loweo -ofix -sign -cuda [device] -v <int>\n";
 }
 

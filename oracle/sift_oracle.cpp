@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <stdexcept>
 
 #include "../modify-sift-gpu_amd/csrc/sift_math.h"
 
@@ -77,6 +78,58 @@ Image downsample(const Image& src, int wdst, int hdst) {
     for (int r = 0; r < hdst; r++)
         for (int c = 0; c < wdst; c++)
             d.px[(size_t)r * wdst + c] = src.at(std::min(c << 1, src.w - 1), r << 1);
+    return d;
+}
+
+// --- SampleImageD (ProgramCU.cu:300-328) from the input for -fo > 0: dst(r, c) =
+//     src(r << s, min(c << s, Wsrc - 1)) into the first octave's wa x h.
+Image downsample_input(const Image& src, int s, int wdst, int hdst) {
+    Image d;
+    d.w = wdst;
+    d.h = hdst;
+    d.px.resize((size_t)wdst * hdst);
+    for (int r = 0; r < hdst; r++)
+        for (int c = 0; c < wdst; c++)
+            d.px[(size_t)r * wdst + c] = src.at(std::min(c << s, src.w - 1), r << s);
+    return d;
+}
+
+// --- UpsampleKernel<s> (ProgramCU.cu:225-285) for -fo < 0, on the input as the flat W x H
+//     buffer it is bound as (tex1Dfetch: index + 1 at the end of a row is the next row's first
+//     pixel, indices past the buffer read 0).  Output row R, source row R >> s, blend weight
+//     w1 = (R & (S-1)) / S; every source column c writes S consecutive outputs at (W R + c) S.
+//     Contractions as elsewhere: a*b + c*d -> fma(a, b, c*d).
+Image upsample_input(const Image& src, int s) {
+    const int S = 1 << s, W = src.w, H = src.h;
+    const float inv = 1.0f / float(S);
+    Image d;
+    d.w = W * S;
+    d.h = H * S;
+    d.px.resize((size_t)d.w * d.h);
+    auto in = [&](long k) { return k < (long)src.px.size() ? src.px[(size_t)k] : 0.0f; };
+    for (int R = 0; R < d.h; R++) {
+        const int row = R >> s, helper = R & (S - 1);
+        for (int c = 0; c < W; c++) {
+            const long index = (long)row * W + c;
+            float v1, v2;
+            if (helper) {
+                const float v11 = in(index), v12 = in(index + 1);
+                const float v21 = in(index + W), v22 = in(index + W + 1);
+                const float w1 = inv * helper, w2 = (float)(1.0 - (double)w1);
+                v1 = fma_(v21, w1, w2 * v11);
+                v2 = fma_(v22, w1, w2 * v12);
+            } else {
+                v1 = in(index);
+                v2 = in(index + 1);
+            }
+            float* o = &d.px[((size_t)W * R + c) * S];
+            o[0] = v1;
+            for (int i = 1; i < S; i++) {
+                const float r2 = i * inv, r1 = 1.0f - r2;
+                o[i] = fma_(v1, r1, v2 * r2);
+            }
+        }
+    }
     return d;
 }
 
@@ -502,11 +555,14 @@ Result extract(const uint8_t* img, int w, int h, int stride, const sgpu_options&
     po.dog_level_num = opt.dog_level_num;
     po.dog_threshold = opt.dog_threshold;
     po.edge_threshold = opt.edge_threshold;
-    po.octave_min = 0;
+    po.octave_min = opt.octave_min;
     const sgp::Schedule S = sgp::make_schedule(po);
     const int d = S.dog_level_num, nlev = S.level_num;
+    const int fo = opt.octave_min;
+    if (fo < -1 || !(S.initial_smooth > 0.0f))   // NaN filter taps (see sgpu_ctx_set_options)
+        throw std::invalid_argument("first octave must be >= -1");
     Result R;
-    R.octaves = sgp::make_octaves(w, h, opt.octave_num, 0);
+    R.octaves = sgp::make_octaves(w, h, opt.octave_num, fo);
     const int noct = (int)R.octaves.size();
 
     // ResizeFeatureStorage (PyramidCU.cpp:341-347): histopyramid depth from the base level
@@ -529,7 +585,9 @@ Result extract(const uint8_t* img, int w, int h, int stride, const sgpu_options&
         // BuildPyramid (PyramidCU.cpp:979-1044)
         if (o == 0) {
             int fw = sgp::make_filter(S.initial_smooth, opt.filter_width_factor, taps);
-            g[0] = filter(input, taps, fw);
+            if (fo == 0) g[0] = filter(input, taps, fw);
+            else if (fo > 0) g[0] = filter(downsample_input(input, fo, oc.wa, oc.h), taps, fw);
+            else g[0] = filter(upsample_input(input, -fo), taps, fw);
         } else {
             g[0] = downsample(prev[S.level_ds - S.level_min], oc.wa, oc.h);
             if (S.sigma_skip1 > 0) {
@@ -569,7 +627,7 @@ Result extract(const uint8_t* img, int w, int h, int stride, const sgpu_options&
                 }
             }
             // feature expansion + image coordinates
-            const float oss = (float)(1 << o);
+            const float oss = ldexpf(1.0f, o + fo);   // os * 2^o, os = 2^octave_min
             auto emit = [&](const float* src, float ang) {
                 R.feat_oct.insert(R.feat_oct.end(), {src[0], src[1], src[2], ang});
                 R.keys.push_back(oss * (src[0] - 0.5f) + offset);
@@ -631,6 +689,7 @@ std::vector<float> describe_keys(const uint8_t* img, int w, int h, int stride,
     po.dog_level_num = opt.dog_level_num;
     po.dog_threshold = opt.dog_threshold;
     po.edge_threshold = opt.edge_threshold;
+    po.octave_min = opt.octave_min;
     const sgp::Schedule S = sgp::make_schedule(po);
     const int d = S.dog_level_num, noct = (int)R.octaves.size();
     const double twopi = 2.0 * 3.14159265358979323846;
@@ -638,7 +697,7 @@ std::vector<float> describe_keys(const uint8_t* img, int w, int h, int stride,
     const float offset = opt.lowe_origin ? 0.0f : 0.5f;
     struct Entry { float k[4]; int index, octave, level; };
     std::vector<Entry> list;
-    float octave_sigma = 1.0f;
+    float octave_sigma = ldexpf(1.0f, opt.octave_min);   // PyramidCU.cpp:461
     for (int i = 0; i < noct; i++, octave_sigma *= 2.0f)
         for (int j = 0; j < d; j++) {
             const float level_sigma = sgp::level_sigma(S, j + S.level_min + 1) * octave_sigma;
@@ -689,7 +748,7 @@ std::vector<float> describe_keys(const uint8_t* img, int w, int h, int stride,
     const int m = std::min<int>(num, (int)list.size());
     for (int i = 0; i < m; i++) {
         const Entry& e = list[i];
-        const float os = (float)(1 << e.octave);
+        const float os = ldexpf(1.0f, e.octave + opt.octave_min);
         if (!has_orientation) {
             float* kk = keys_out->data() + 4 * (size_t)e.index;
             kk[0] = os * (e.k[0] - 0.5f) + offset;
@@ -856,63 +915,79 @@ extern "C" {
 
 int oracle_extract(const uint8_t* img, int w, int h, int stride, const sgpu_options* opt,
                    float* keys, float* desc, int cap, int* n_out) {
-    oracle::Result R = oracle::extract(img, w, h, stride, *opt, false);
-    int n = (int)R.feat_level.size();
-    *n_out = n;
-    if (n > cap) return -4;
-    if (keys) memcpy(keys, R.keys.data(), sizeof(float) * 4 * n);
-    if (desc && opt->descriptors) memcpy(desc, R.desc.data(), sizeof(float) * 128 * n);
-    return 0;
+    try {
+        oracle::Result R = oracle::extract(img, w, h, stride, *opt, false);
+        int n = (int)R.feat_level.size();
+        *n_out = n;
+        if (n > cap) return -4;
+        if (keys) memcpy(keys, R.keys.data(), sizeof(float) * 4 * n);
+        if (desc && opt->descriptors) memcpy(desc, R.desc.data(), sizeof(float) * 128 * n);
+        return 0;
+    } catch (const std::invalid_argument&) {
+        return -2;   // options the reference cannot run (see oracle::extract)
+    }
 }
 
 // Gaussian level (octave o, level k) of the oracle pyramid.
 int oracle_gaussian(const uint8_t* img, int w, int h, int stride, const sgpu_options* opt,
                     int octave, int level, float* out, int cap) {
-    sgpu_options o2 = *opt;
-    o2.descriptors = 0;
-    oracle::Result R = oracle::extract(img, w, h, stride, o2, true);
-    if (octave >= (int)R.gauss.size()) return -1;
-    const oracle::Image& g = R.gauss[octave][level];
-    if ((int)g.px.size() > cap) return -4;
-    memcpy(out, g.px.data(), g.px.size() * sizeof(float));
-    return (int)g.px.size();
+    try {
+        sgpu_options o2 = *opt;
+        o2.descriptors = 0;
+        oracle::Result R = oracle::extract(img, w, h, stride, o2, true);
+        if (octave >= (int)R.gauss.size()) return -1;
+        const oracle::Image& g = R.gauss[octave][level];
+        if ((int)g.px.size() > cap) return -4;
+        memcpy(out, g.px.data(), g.px.size() * sizeof(float));
+        return (int)g.px.size();
+    } catch (const std::invalid_argument&) {
+        return -2;   // options the reference cannot run (see oracle::extract)
+    }
 }
 
 // Candidates in reference order: ints {col,row,level_id,0}, floats {dx,dy,ds,0}.
 int oracle_candidates(const uint8_t* img, int w, int h, int stride, const sgpu_options* opt,
                       int* ints, float* floats, int cap, int* n_out) {
-    sgpu_options o2 = *opt;
-    o2.descriptors = 0;
-    oracle::Result R = oracle::extract(img, w, h, stride, o2, false);
-    int n = 0, d = opt->dog_level_num;
-    for (const auto& L : R.levels)
-        for (const auto& c : L.candidates) {
-            if (n < cap) {
-                int* p = ints + 4 * n;
-                p[0] = c.col; p[1] = c.row; p[2] = L.octave * d + L.level; p[3] = 0;
-                float* q = floats + 4 * n;
-                q[0] = c.dx; q[1] = c.dy; q[2] = c.ds; q[3] = 0;
+    try {
+        sgpu_options o2 = *opt;
+        o2.descriptors = 0;
+        oracle::Result R = oracle::extract(img, w, h, stride, o2, false);
+        int n = 0, d = opt->dog_level_num;
+        for (const auto& L : R.levels)
+            for (const auto& c : L.candidates) {
+                if (n < cap) {
+                    int* p = ints + 4 * n;
+                    p[0] = c.col; p[1] = c.row; p[2] = L.octave * d + L.level; p[3] = 0;
+                    float* q = floats + 4 * n;
+                    q[0] = c.dx; q[1] = c.dy; q[2] = c.ds; q[3] = 0;
+                }
+                n++;
             }
-            n++;
-        }
-    *n_out = n;
-    return n > cap ? -4 : 0;
+        *n_out = n;
+        return n > cap ? -4 : 0;
+    } catch (const std::invalid_argument&) {
+        return -2;   // options the reference cannot run (see oracle::extract)
+    }
 }
 
 // Features in octave coordinates (x, y, s, o: the descriptor's input) with their level id
 // (octave*d + j), in output order.  For the independent float64 cross-check (tests/ref_numpy.py).
 int oracle_features_oct(const uint8_t* img, int w, int h, int stride, const sgpu_options* opt,
                         float* feat, int* level, int cap, int* n_out) {
-    sgpu_options o2 = *opt;
-    o2.descriptors = 0;
-    oracle::Result R = oracle::extract(img, w, h, stride, o2, false);
-    const int n = (int)R.feat_level.size();
-    for (int i = 0; i < n && i < cap; i++) {
-        memcpy(feat + 4 * i, &R.feat_oct[4 * (size_t)i], 4 * sizeof(float));
-        level[i] = R.feat_level[i];
+    try {
+        sgpu_options o2 = *opt;
+        o2.descriptors = 0;
+        oracle::Result R = oracle::extract(img, w, h, stride, o2, false);
+        const int n = (int)R.feat_level.size();
+        for (int i = 0; i < n && i < cap; i++) {
+            memcpy(feat + 4 * i, &R.feat_oct[4 * (size_t)i], 4 * sizeof(float));
+            level[i] = R.feat_level[i];
+        }
+        *n_out = n;
+        return n > cap ? -4 : 0;
+    } catch (const std::invalid_argument&) {
+        return -2;   // options the reference cannot run (see oracle::extract)
     }
-    *n_out = n;
-    return n > cap ? -4 : 0;
 }
 
 // SiftGPU::RunSIFT(num, keys, keys_have_orientation) on image img: keys_out [num][4],
@@ -920,12 +995,16 @@ int oracle_features_oct(const uint8_t* img, int w, int h, int stride, const sgpu
 int oracle_describe_keys(const uint8_t* img, int w, int h, int stride, const sgpu_options* opt,
                          const float* keys, int num, int has_orientation, float* keys_out,
                          float* desc) {
-    std::vector<float> ko;
-    std::vector<float> d = oracle::describe_keys(img, w, h, stride, *opt, keys, num,
-                                                 has_orientation, &ko);
-    if (keys_out) memcpy(keys_out, ko.data(), ko.size() * sizeof(float));
-    if (desc && opt->descriptors) memcpy(desc, d.data(), d.size() * sizeof(float));
-    return 0;
+    try {
+        std::vector<float> ko;
+        std::vector<float> d = oracle::describe_keys(img, w, h, stride, *opt, keys, num,
+                                                     has_orientation, &ko);
+        if (keys_out) memcpy(keys_out, ko.data(), ko.size() * sizeof(float));
+        if (desc && opt->descriptors) memcpy(desc, d.data(), d.size() * sizeof(float));
+        return 0;
+    } catch (const std::invalid_argument&) {
+        return -2;   // options the reference cannot run (see oracle::extract)
+    }
 }
 
 int oracle_match(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float distmax,
@@ -968,8 +1047,23 @@ void oracle_schedule(int dog_level_num, float* sigma0, float* sigma_skip0, float
 }
 
 // Octave geometry (w, h, wa per octave) for an input of w x h (PyramidCU.cpp:89-271).
-int oracle_geometry(int w, int h, int octave_num, int* dims, int max) {
-    std::vector<sgp::Octave> oc = sgp::make_octaves(w, h, octave_num, 0);
+// The first octave's resampled input for -fo != 0 (before the initial smoothing): returns the
+// element count, dims[0..1] = width, height.
+int oracle_first_octave_input(const uint8_t* img, int w, int h, int stride, int fo, float* out,
+                              int cap, int* dims) {
+    oracle::Image in = oracle::ingest(img, w, h, stride);
+    std::vector<sgp::Octave> oc = sgp::make_octaves(w, h, 1, fo);
+    oracle::Image r = fo > 0 ? oracle::downsample_input(in, fo, oc[0].wa, oc[0].h)
+                             : oracle::upsample_input(in, -fo);
+    if ((int)r.px.size() > cap) return -4;
+    memcpy(out, r.px.data(), r.px.size() * sizeof(float));
+    dims[0] = r.w;
+    dims[1] = r.h;
+    return (int)r.px.size();
+}
+
+int oracle_geometry(int w, int h, int octave_num, int* dims, int max, int octave_min) {
+    std::vector<sgp::Octave> oc = sgp::make_octaves(w, h, octave_num, octave_min);
     for (int o = 0; o < (int)oc.size() && o < max; o++) {
         dims[3 * o] = oc[o].w; dims[3 * o + 1] = oc[o].h; dims[3 * o + 2] = oc[o].wa;
     }

@@ -49,12 +49,14 @@ def lib():
                                           ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.oracle_guided_pass.argtypes = [ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_float] * 6
+        L.oracle_first_octave_input.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 4 + [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         L.oracle_match_distance.argtypes = [ctypes.c_int]
         L.oracle_match_distance.restype = ctypes.c_float
         L.oracle_schedule.argtypes = [ctypes.c_int, P(ctypes.c_float), P(ctypes.c_float),
                                       ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_geometry.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
-                                      ctypes.c_int]
+                                      ctypes.c_int, ctypes.c_int]
         L.oracle_hist_widths.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_void_p, ctypes.c_int]
         L.oracle_exp.argtypes = [ctypes.c_float]
@@ -96,7 +98,7 @@ def gaussian(img, octave, level, opts=None):
     opts = opts or default_options()
     img, p = _img(img)
     h, w = img.shape
-    cap = (w + 4) * h
+    cap = (w + 4) * h * (1 << (2 * max(0, -opts.octave_min)))
     out = np.zeros(cap, np.float32)
     n = lib().oracle_gaussian(p, w, h, w, ctypes.byref(opts), octave, level, out.ctypes.data, cap)
     assert n > 0, n
@@ -152,6 +154,19 @@ def match(d1: np.ndarray, d2: np.ndarray, distmax=0.7, ratiomax=0.8, mbm=1, max_
     m = lib().oracle_match(d1.ctypes.data, n1, d2.ctypes.data, n2, distmax, ratiomax, mbm,
                            max_match, out.ctypes.data)
     return out[:m]
+
+
+def first_octave_input(img, fo):
+    """The resampled first-octave input of -fo != 0 (SampleImageD / UpsampleKernel)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    cap = (w << 3) * (h << 3) + 16
+    out = np.zeros(cap, np.float32)
+    dims = np.zeros(2, np.int32)
+    n = lib().oracle_first_octave_input(img.ctypes.data, w, h, w, fo, out.ctypes.data, cap,
+                                        dims.ctypes.data)
+    assert n >= 0
+    return out[:n].reshape(dims[1], dims[0])
 
 
 _IDENTITY = np.eye(3, dtype=np.float32)

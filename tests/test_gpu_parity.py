@@ -80,6 +80,44 @@ def test_gaussian_levels_bitwise(gpu_ctx, w, h, seed):
             assert np.array_equal(_bits(g), _bits(r)), (o, lvl)
 
 
+@pytest.mark.parametrize("fo,w,h", [(1, 203, 97), (-1, 203, 97), (-1, 96, 64), (2, 321, 241)])
+def test_first_octave_levels_bitwise(gpu_ctx, fo, w, h):
+    """-fo != 0: the resampled first octave (SampleImageD / UpsampleKernel) and its levels."""
+    img = synth_image(w, h, 17 + fo)
+    opts = default_options(octave_min=fo)
+    gpu_ctx.set_options(opts)
+    gpu_ctx.extract(img)
+    geo = gpu_ctx.geometry()
+    for o in range(min(len(geo), 2)):
+        for lvl in range(opts.dog_level_num + 3):
+            g = gpu_ctx.gaussian(0, o, lvl)
+            r = O.gaussian(img, o, lvl, opts)
+            assert np.array_equal(_bits(g), _bits(r)), (o, lvl)
+
+
+def test_first_octave_minus_two_rejected(gpu_ctx):
+    """-fo -2: the reference's initial smoothing sigma is 0, its filter taps NaN."""
+    with pytest.raises(Exception):
+        gpu_ctx.set_options(default_options(octave_min=-2))
+    gpu_ctx.set_options(default_options())
+
+
+def test_first_octave_on_a_batch(gpu_ctx):
+    """-fo 1 and -fo -1 on a batch equal the single-image results (u8 and f32 input)."""
+    imgs = np.stack([synth_image(256, 192, 40 + i) for i in range(3)])
+    for fo in (1, -1):
+        opts = default_options(octave_min=fo)
+        gpu_ctx.set_options(opts)
+        gpu_ctx.extract(imgs)
+        batch = [gpu_ctx.features(i) for i in range(3)]
+        for i in range(3):
+            rk, rd = O.extract(imgs[i], opts)
+            _assert_features_equal(batch[i][0], batch[i][1], rk, rd, f"fo{fo} image {i}")
+        gpu_ctx.extract(imgs.astype(np.float32) / np.float32(255.0))
+        k, d = gpu_ctx.features(1)
+        _assert_features_equal(k, d, batch[1][0], batch[1][1], f"fo{fo} f32")
+
+
 @pytest.mark.parametrize("w,h,seed", [(160, 120, 1), (640, 480, 1000), (333, 251, 9)])
 def test_candidates_bitwise(gpu_ctx, w, h, seed):
     img = synth_image(w, h, seed)
@@ -105,6 +143,10 @@ OPTION_CASES = [
     {"edge_threshold": 5},
     {"filter_width_factor": 3},
     {"descriptor_window_factor": 2},
+    {"octave_min": 1},
+    {"octave_min": 2},
+    {"octave_min": -1},
+    {"octave_min": -1, "dog_level_num": 4},
 ]
 
 

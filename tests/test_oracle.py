@@ -40,15 +40,15 @@ def test_sigma_schedule_kat():
 def test_octave_geometry_kat():
     # PyramidCU.cpp:985: 800*600---400*300--200*150--100*75--52*37--28*18
     dims = np.zeros(48, np.int32)
-    n = O.lib().oracle_geometry(800, 600, -1, dims.ctypes.data, 16)
+    n = O.lib().oracle_geometry(800, 600, -1, dims.ctypes.data, 16, 0)
     got = [(dims[3 * i + 2], dims[3 * i + 1]) for i in range(n)]
     assert got == [(800, 600), (400, 300), (200, 150), (100, 75), (52, 37), (28, 18)]
     # 1080p with -no 4 (config C2): sum of wa*h = 2,754,000
-    n = O.lib().oracle_geometry(1920, 1080, 4, dims.ctypes.data, 16)
+    n = O.lib().oracle_geometry(1920, 1080, 4, dims.ctypes.data, 16, 0)
     assert n == 4
     assert sum(int(dims[3 * i + 2]) * int(dims[3 * i + 1]) for i in range(n)) == 2754000
     # 4096^2 with -no 6 (config C4): 22,364,160 px
-    n = O.lib().oracle_geometry(4096, 4096, 6, dims.ctypes.data, 16)
+    n = O.lib().oracle_geometry(4096, 4096, 6, dims.ctypes.data, 16, 0)
     assert sum(int(dims[3 * i + 2]) * int(dims[3 * i + 1]) for i in range(n)) == 22364160
 
 
@@ -310,3 +310,68 @@ def test_guided_defaults():
     np.testing.assert_array_equal(O.match_guided(q1, q2, l1, l2, None, np.eye(3), fdistmax=1e20), plain)
     g = O.match_guided(q1, q2, l1, l2, H, F)
     assert 0 < len(g) < len(plain)
+
+
+# ---- first octave -fo != 0 ---------------------------------------------------------------------
+def test_first_octave_geometry():
+    """InitPyramid (PyramidCU.cpp:89-112) + GetRequiredOctaveNum (SiftPyramid.cpp:279-285)."""
+    dims = np.zeros(48, np.int32)
+    def geo(w, h, fo):
+        n = O.lib().oracle_geometry(w, h, -1, dims.ctypes.data, 16, fo)
+        return [(int(dims[3 * i]), int(dims[3 * i + 1]), int(dims[3 * i + 2])) for i in range(n)]
+    # -fo 1: 800x600 -> 400x300 first, floor(log2(300)) - 3 = 5 octaves
+    assert geo(800, 600, 1) == [(400, 300, 400), (200, 150, 200), (100, 75, 100), (50, 37, 52),
+                                (25, 18, 28)]
+    # -fo -1: 1600x1200, 7 octaves; the width is truncated to a multiple of 4 before scaling
+    g = geo(803, 600, -1)
+    assert g[0] == (1600, 1200, 1600) and len(g) == 7
+    assert geo(1920, 1080, 2)[0] == (480, 270, 480)
+
+
+def _np_upsample(img_f, s):
+    """UpsampleKernel<s> (ProgramCU.cu:225-270) on the flat buffer: independent restatement,
+    a*b + c*d as fma(a, b, c*d) (fma in float64 then rounded: a*b is exact in float64)."""
+    def fma(a, b, c):
+        return (a.astype(np.float64) * np.float64(b) + c.astype(np.float64)).astype(np.float32)
+    H, W = img_f.shape
+    S = 1 << s
+    flat = np.concatenate([img_f.reshape(-1), np.zeros(W + 2, np.float32)])
+    out = np.zeros((H * S, W * S), np.float32)
+    inv = np.float32(1.0 / S)
+    for R in range(H * S):
+        row, helper = R >> s, R & (S - 1)
+        idx = row * W + np.arange(W)
+        if helper:
+            w1 = np.float32(inv * np.float32(helper))
+            w2 = np.float32(1.0) - w1
+            v1 = fma(flat[idx + W], w1, w2 * flat[idx])
+            v2 = fma(flat[idx + W + 1], w1, w2 * flat[idx + 1])
+        else:
+            v1, v2 = flat[idx], flat[idx + 1]
+        o = out.reshape(-1)[(W * R) * S:(W * R + W) * S].reshape(W, S)
+        o[:, 0] = v1
+        for i in range(1, S):
+            r2 = np.float32(i) * inv
+            o[:, i] = fma(v1, np.float32(1.0) - r2, v2 * r2)
+    return out
+
+
+@pytest.mark.parametrize("fo", [-1, -2, -3, 1, 2])
+def test_first_octave_input_vs_numpy(fo):
+    img = synth_image(37 * 4 + 3, 29, 5)          # width truncated to a multiple of 4
+    got = O.first_octave_input(img, fo)
+    f = (img[:, : img.shape[1] & ~3].astype(np.float32) / np.float32(255.0))
+    if fo < 0:
+        want = _np_upsample(f, -fo)
+    else:
+        h2, w2 = f.shape[0] >> fo, f.shape[1] >> fo
+        wa = (w2 + 3) // 4 * 4
+        cols = np.minimum(np.arange(wa) << fo, f.shape[1] - 1)
+        want = f[(np.arange(h2) << fo)][:, cols]
+    np.testing.assert_array_equal(got, want)
+
+
+def test_first_octave_minus_two_is_refused():
+    """-fo -2 makes the reference's initial sigma 0 and CreateFilterKernel's taps NaN."""
+    with pytest.raises(AssertionError):
+        O.extract(synth_image(64, 48, 1), default_options(octave_min=-2))
