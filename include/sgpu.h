@@ -90,6 +90,18 @@ int sgpu_extract(sgpu_ctx* ctx, const uint8_t* images, int n, int w, int h, int 
 int sgpu_extract_f32(sgpu_ctx* ctx, const float* images, int n, int w, int h, int stride,
                      int flags);
 
+/* Color input, converted to luminance on the device with the reference's formula
+ * (GLTexInput::SetImageData -> DownSamplePixelDataI2F<u8>, GLTexImage.cpp:834-858:
+ * (19595 r + 38470 g + 7471 b) / (65535 * 255); BGR swaps r and b; alpha ignored).  `format`
+ * is one of SGPU_RGB, SGPU_BGR, SGPU_RGBA, SGPU_BGRA; `stride` in bytes.  Replaces
+ * RunSIFT(w, h, data, GL_RGB | GL_BGR | GL_RGBA | GL_BGRA, GL_UNSIGNED_BYTE), batched. */
+#define SGPU_RGB  1
+#define SGPU_BGR  2
+#define SGPU_RGBA 3
+#define SGPU_BGRA 4
+int sgpu_extract_color(sgpu_ctx* ctx, const uint8_t* images, int n, int w, int h, int stride,
+                       int format, int flags);
+
 /* Feature count of image i of the last extract (SiftGPU::GetFeatureNum, SiftGPU.cpp:1411). */
 int sgpu_feature_count(const sgpu_ctx* ctx, int image);
 /* Total over the batch. */

@@ -101,7 +101,7 @@ struct sgpu_ctx {
     size_t staged_bytes = 0;
     std::vector<int64_t> img_off;          // global per-image offsets [batch + 1]
     Part part[kMaxParts];
-    DevBuf input, all_keys, all_desc;      // all_*: lazily gathered multi-part outputs
+    DevBuf input, all_keys, all_desc, gray;      // all_*: lazily gathered multi-part outputs
     bool gathered = false;
     hipEvent_t ev[T_N + 1] = {};
     float timing[T_N] = {};
@@ -296,7 +296,7 @@ int sgpu_ctx_destroy(sgpu_ctx* ctx) {
     }
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     ctx->comm = nullptr;
-    DevBuf* bufs[] = {&ctx->input, &ctx->all_keys, &ctx->all_desc, &ctx->m_d1, &ctx->m_d2,
+    DevBuf* bufs[] = {&ctx->input, &ctx->all_keys, &ctx->all_desc, &ctx->gray, &ctx->m_d1, &ctx->m_d2,
                       &ctx->m_part, &ctx->m_terms, &ctx->m_match, &ctx->m_dist, &ctx->m_mask, &ctx->m_loc,
                       &ctx->c_buf};
     for (DevBuf* b : bufs) b->release();
@@ -504,11 +504,14 @@ static int enqueue_readback(sgpu_ctx* ctx, Part& pt) {
 }
 
 static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, int w, int h,
-                        int stride, int flags) {
+                        int stride, int flags, int color = 0) {
     if (!ctx) return SGPU_EINVAL;
     const bool staged = (flags & SGPU_INPUT_STAGED) != 0;
-    if ((!images && !staged) || n <= 0 || w < 8 || h < 8 || stride < w)
+    const int channels = color == SGPU_RGB || color == SGPU_BGR ? 3 : color ? 4 : 1;
+    if ((!images && !staged) || n <= 0 || w < 8 || h < 8 || stride < w * channels)
         return ctx->fail(SGPU_EINVAL, "bad image arguments");
+    if (color && (staged || is_f32 || color > SGPU_BGRA))
+        return ctx->fail(SGPU_EINVAL, "bad color input");
     if (staged && (is_f32 || ctx->staged_bytes < (size_t)n * h * stride))
         return ctx->fail(SGPU_EINVAL, "staged input does not match the batch");
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -548,6 +551,17 @@ static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
         ALLOCCHK(ctx, ctx->input.ensure(in_bytes));
         HIPCHK(ctx, hipMemcpyAsync(ctx->input.p, images, in_bytes, hipMemcpyHostToDevice, ctx->stream));
         src_in = ctx->input.p;
+    }
+    if (color) {
+        // luminance on the device; the pipeline then takes it as float input, tw floats a row
+        const int tw = w & ~3;
+        ALLOCCHK(ctx, ctx->gray.ensure((size_t)n * h * tw * sizeof(float)));
+        HIPCHK(ctx, sgk::launch_color_to_gray((const uint8_t*)src_in, n, w, h, stride, channels,
+                                              color == SGPU_BGR || color == SGPU_BGRA,
+                                              ctx->gray.as<float>(), ctx->stream));
+        src_in = ctx->gray.p;
+        is_f32 = true;
+        stride = tw;
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
 
@@ -891,6 +905,13 @@ int sgpu_extract(sgpu_ctx* ctx, const uint8_t* images, int n, int w, int h, int 
 int sgpu_extract_f32(sgpu_ctx* ctx, const float* images, int n, int w, int h, int stride,
                      int flags) {
     return extract_impl(ctx, images, true, n, w, h, stride, flags);
+}
+
+int sgpu_extract_color(sgpu_ctx* ctx, const uint8_t* images, int n, int w, int h, int stride,
+                       int format, int flags) {
+    if (!ctx) return SGPU_EINVAL;
+    if (format < SGPU_RGB || format > SGPU_BGRA) return ctx->fail(SGPU_EINVAL, "bad color format");
+    return extract_impl(ctx, images, false, n, w, h, stride, flags, format);
 }
 
 int sgpu_feature_count(const sgpu_ctx* ctx, int image) {

@@ -61,6 +61,12 @@ hipError_t launch_first_octave_input(const float* src, const uint8_t* src_u8, in
                                      int dw, int dh, long long dst_img_stride, int batch,
                                      hipStream_t stream);
 
+// Color ingest (DownSamplePixelDataI2F<u8>, GLTexImage.cpp:834-858): n images of w x h
+// pixels with `channels` (3 or 4) bytes each, rows `stride` bytes apart; bgr swaps the red and
+// blue weights.  dst gets tw = w & ~3 floats per row (the truncated width), images tw*h apart.
+hipError_t launch_color_to_gray(const uint8_t* src, int n, int w, int h, int stride,
+                                int channels, bool bgr, float* dst, hipStream_t stream);
+
 // Extremum detection for all octaves, all d levels and all images (one launch): sets the
 // keypoint bits in the zeroed mask and adds per-row keypoint counts into the zeroed row_count
 // (rows ordered image, octave, level, row).

@@ -1612,6 +1612,22 @@ __global__ __launch_bounds__(256) void k_input_up(const float* __restrict__ src,
 }
 
 // ------------------------------------------------------------------------------------------
+// Color -> luminance: (19595 r + 38470 g + 7471 b) / (65535.0f * 255.0f).  The numerator is an
+// exact integer below 2^24 and the denominator an exact float, so the IEEE division on the
+// device gives the host conversion's bits.
+template <int CH, bool BGR>
+__global__ __launch_bounds__(256) void k_color_gray(const uint8_t* __restrict__ src, int tw, int h,
+                                                    int stride, float* __restrict__ dst) {
+    const int b = blockIdx.z, y = blockIdx.y;
+    const int x = blockIdx.x * 256 + threadIdx.x;
+    if (x >= tw) return;
+    const uint8_t* p = src + ((long long)b * h + y) * stride + (long long)x * CH;
+    const int r = BGR ? p[2] : p[0], g = p[1], bl = BGR ? p[0] : p[2];
+    const int num = 19595 * r + 38470 * g + 7471 * bl;
+    dst[((long long)b * h + y) * tw + x] = (float)num / (65535.0f * 255.0f);
+}
+
+// ------------------------------------------------------------------------------------------
 // Feature expansion + image coordinates (PyramidCU.cpp:521-606 / 701-751).
 __global__ __launch_bounds__(256) void k_expand(const float4* __restrict__ cand,
                                                 const int2* __restrict__ info,
@@ -1927,6 +1943,22 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
         default: return hipErrorInvalidValue;
     }
 #undef SGK_GAUSS
+}
+
+hipError_t launch_color_to_gray(const uint8_t* src, int n, int w, int h, int stride,
+                                int channels, bool bgr, float* dst, hipStream_t stream) {
+    const int tw = w & ~3;
+    if (n <= 0 || tw <= 0 || (channels != 3 && channels != 4) || stride < w * channels)
+        return hipErrorInvalidValue;
+    const dim3 grid((tw + 255) / 256, h, n);
+#define SGK_COLOR(CH, B) \
+    hipLaunchKernelGGL((k_color_gray<CH, B>), grid, dim3(256), 0, stream, src, tw, h, stride, dst)
+    if (channels == 3 && !bgr) SGK_COLOR(3, false);
+    else if (channels == 3) SGK_COLOR(3, true);
+    else if (!bgr) SGK_COLOR(4, false);
+    else SGK_COLOR(4, true);
+#undef SGK_COLOR
+    return hipGetLastError();
 }
 
 hipError_t launch_first_octave_input(const float* src, const uint8_t* src_u8, int stride,

@@ -35,6 +35,7 @@ constexpr unsigned kGL_UNSIGNED_BYTE = 0x1401, kGL_UNSIGNED_SHORT = 0x1403, kGL_
 struct HostImage {
     int w = 0, h = 0;
     bool is_float = false;
+    int color = 0;                 // SGPU_RGB.. for u8 color data, 0 for luminance
     std::vector<uint8_t> u8;
     std::vector<float> f32;
 };
@@ -114,8 +115,9 @@ bool load_pnm(const char* path, HostImage* img) {
 }
 
 // GLTexInput::SetImageData for the CUDA path (GLTexImage.cpp:918-1009) with down-sampling 1:
-// u8 luminance stays u8 (converted to float on the GPU, value / 255.0f); every other format is
-// converted to float luminance on the host with the reference's formulas (:808-916).
+// u8 luminance and u8 RGB/BGR/RGBA/BGRA stay u8 (converted to float luminance on the GPU with
+// the reference's formulas); u16, float and luminance-alpha input is converted on the host
+// (:808-916).
 template <class T>
 void to_float(const T* p, unsigned fmt, int w, int h, float factor, std::vector<float>* out) {
     out->resize((size_t)w * h);
@@ -152,9 +154,19 @@ bool set_image(HostImage* img, int w, int h, const void* data, unsigned fmt, uns
     }
     img->w = w;
     img->h = h;
+    img->color = 0;
     if (fmt == kGL_LUMINANCE && type == kGL_UNSIGNED_BYTE) {
         img->is_float = false;
         img->u8.assign((const uint8_t*)data, (const uint8_t*)data + (size_t)w * h);
+        return true;
+    }
+    if (type == kGL_UNSIGNED_BYTE && fmt != kGL_LUMINANCE_ALPHA) {
+        // RGB / BGR / RGBA / BGRA u8: converted to luminance on the device (sgpu_extract_color)
+        const int ch = (fmt == kGL_RGB || fmt == kGL_BGR) ? 3 : 4;
+        img->is_float = false;
+        img->color = fmt == kGL_RGB ? SGPU_RGB : fmt == kGL_BGR ? SGPU_BGR
+                   : fmt == kGL_RGBA ? SGPU_RGBA : SGPU_BGRA;
+        img->u8.assign((const uint8_t*)data, (const uint8_t*)data + (size_t)w * h * ch);
         return true;
     }
     img->is_float = true;
@@ -455,8 +467,12 @@ int SiftGPU::RunSIFT() {
         }
         _image_loaded = 1;
     }
+    const int ch = img->color == SGPU_RGB || img->color == SGPU_BGR ? 3 : 4;
     int rc = img->is_float
                  ? sgpu_extract_f32(rt->ctx, img->f32.data(), 1, img->w, img->h, img->w, SGPU_INPUT_HOST)
+             : img->color
+                 ? sgpu_extract_color(rt->ctx, img->u8.data(), 1, img->w, img->h, img->w * ch,
+                                      img->color, SGPU_INPUT_HOST)
                  : sgpu_extract(rt->ctx, img->u8.data(), 1, img->w, img->h, img->w, SGPU_INPUT_HOST);
     if (rc != SGPU_OK) {
         std::cerr << "SiftGPU: " << sgpu_last_error(rt->ctx) << "\n";

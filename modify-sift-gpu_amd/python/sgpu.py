@@ -26,7 +26,7 @@ C_API = [
     "sgpu_device_features", "sgpu_match", "sgpu_quantize_descriptors", "sgpu_last_timing",
     "sgpu_debug_geometry", "sgpu_debug_gaussian", "sgpu_debug_candidates",
     "sgpu_debug_set_variant", "sgpu_comm_unique_id", "sgpu_comm_init", "sgpu_comm_allgather_i32",
-    "sgpu_comm_allreduce_f64", "sgpu_extract_keypoints", "sgpu_match_guided",
+    "sgpu_comm_allreduce_f64", "sgpu_extract_keypoints", "sgpu_match_guided", "sgpu_extract_color",
 ]
 
 _LIB = None
@@ -64,6 +64,7 @@ def lib():
         L.sgpu_match_guided.argtypes = [vp, vp, c.c_int, vp, c.c_int, vp, vp, vp, vp, c.c_float,
                                         c.c_float, c.c_float, c.c_float, c.c_int, c.c_int, vp,
                                         c.c_int]
+        L.sgpu_extract_color.argtypes = [vp, vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int]
         L.sgpu_quantize_descriptors.argtypes = [vp, c.c_size_t, vp]
         L.sgpu_last_timing.argtypes = [vp, vp, c.c_int]
         L.sgpu_debug_set_variant.argtypes = [c.c_int]
@@ -168,6 +169,22 @@ class SiftContext:
         self._check(rc, "sgpu_extract")
         self.batch = n
         return self
+
+    COLOR_FORMATS = {"rgb": 1, "bgr": 2, "rgba": 3, "bgra": 4}
+
+    def extract_color(self, images: np.ndarray, fmt: str = "rgb"):
+        """u8 color images [n, h, w, 3|4] (or [h, w, c]): luminance on the device with the
+        reference's formula (GLTexImage.cpp:834-858), then the usual pipeline."""
+        a = np.ascontiguousarray(images, np.uint8)
+        if a.ndim == 3:
+            a = a[None]
+        n, h, w, c = a.shape
+        if c != (3 if fmt in ("rgb", "bgr") else 4):
+            raise ValueError("channel count does not match the format")
+        self._check(lib().sgpu_extract_color(self._ctx, a.ctypes.data, n, w, h, w * c,
+                                             self.COLOR_FORMATS[fmt], SGPU_INPUT_HOST),
+                    "extract_color")
+        self.batch = n
 
     def extract_keypoints(self, keys: np.ndarray, has_orientation: bool = True, image: int = 0):
         """Descriptors of caller-supplied keys [n, 4] (x, y, scale, orientation) on image

@@ -36,6 +36,17 @@ Image ingest(const uint8_t* img, int w, int h, int stride) {
     return o;
 }
 
+// --- float luminance input: the same truncated width, values as given.
+Image ingest_f32(const float* img, int w, int h, int stride) {
+    Image o;
+    o.w = w & ~3;
+    o.h = h;
+    o.px.resize((size_t)o.w * h);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < o.w; x++) o.px[(size_t)y * o.w + x] = img[(size_t)y * stride + x];
+    return o;
+}
+
 // --- FilterH<FW> + FilterV<FW> (ProgramCU.cu:115-222, driven by FilterImage :406-446):
 //     horizontal pass clamps within the row, vertical pass clamps to rows 0..H-1; each output
 //     sums taps i = 0..FW-1 in order (value += data[..]*k[i] -> fma).
@@ -549,7 +560,7 @@ void descriptor(const float* key, const std::vector<float>& grad, int W, int H,
 }  // namespace
 
 Result extract(const uint8_t* img, int w, int h, int stride, const sgpu_options& opt,
-               bool keep) {
+               bool keep, const float* img_f32) {
     sgp::Options po;
     po.filter_width_factor = opt.filter_width_factor;
     po.dog_level_num = opt.dog_level_num;
@@ -569,7 +580,7 @@ Result extract(const uint8_t* img, int w, int h, int stride, const sgpu_options&
     int whmax = std::max(R.octaves[0].wa, R.octaves[0].h);
     int hp_levels = (int)std::ceil(std::log(double(whmax)) / std::log(4.0));
 
-    Image input = ingest(img, w, h, stride);
+    Image input = img_f32 ? ingest_f32(img_f32, w, h, stride) : ingest(img, w, h, stride);
     float taps[sgp::kMaxFilterWidth];
     std::vector<Image> prev;  // previous octave's Gaussian levels
     const float sigma_step = powf(2.0f, 1.0f / d);  // PyramidCU.cpp:1200
@@ -929,6 +940,21 @@ int oracle_extract(const uint8_t* img, int w, int h, int stride, const sgpu_opti
 }
 
 // Gaussian level (octave o, level k) of the oracle pyramid.
+int oracle_extract_f32(const float* img, int w, int h, int stride, const sgpu_options* opt,
+                       float* keys, float* desc, int cap, int* n_out) {
+    try {
+        oracle::Result R = oracle::extract(nullptr, w, h, stride, *opt, false, img);
+        int n = (int)R.feat_level.size();
+        *n_out = n;
+        if (n > cap) return -4;
+        if (keys) memcpy(keys, R.keys.data(), sizeof(float) * 4 * n);
+        if (desc && opt->descriptors) memcpy(desc, R.desc.data(), sizeof(float) * 128 * n);
+        return 0;
+    } catch (const std::invalid_argument&) {
+        return -2;
+    }
+}
+
 int oracle_gaussian(const uint8_t* img, int w, int h, int stride, const sgpu_options* opt,
                     int octave, int level, float* out, int cap) {
     try {

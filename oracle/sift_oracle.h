@@ -49,8 +49,10 @@ struct Result {
 };
 
 // Runs the whole pipeline on one gray u8 image.  keep_intermediates=false drops the pyramid.
+// With img_f32 (and img == nullptr) the input is float luminance, row stride `stride` floats
+// (the GL_FLOAT / host-converted path of GLTexInput::SetImageData, GLTexImage.cpp:981-1006).
 Result extract(const uint8_t* img, int w, int h, int stride, const sgpu_options& opt,
-               bool keep_intermediates = true);
+               bool keep_intermediates = true, const float* img_f32 = nullptr);
 
 // Descriptors (and, without orientations, the strongest orientation) of caller-supplied
 // keypoints on image img (SiftGPU::RunSIFT(num, keys, keys_have_orientation)).  Returns the

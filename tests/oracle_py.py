@@ -51,6 +51,9 @@ def lib():
         L.oracle_guided_pass.argtypes = [ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_float] * 6
         L.oracle_first_octave_input.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 4 + [
             ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        L.oracle_extract_f32.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_int, ctypes.c_void_p]
         L.oracle_match_distance.argtypes = [ctypes.c_int]
         L.oracle_match_distance.restype = ctypes.c_float
         L.oracle_schedule.argtypes = [ctypes.c_int, P(ctypes.c_float), P(ctypes.c_float),
@@ -92,6 +95,33 @@ def extract(img: np.ndarray, opts: SgpuOptions | None = None):
                               desc.ctypes.data, n.value, ctypes.byref(n))
     assert rc == 0, rc
     return keys[:n.value], desc[:n.value]
+
+
+def extract_f32(img: np.ndarray, opts: SgpuOptions | None = None):
+    """Float luminance input [h, w] (the GL_FLOAT / converted-RGB ingest path)."""
+    opts = opts or default_options()
+    img = np.ascontiguousarray(img, np.float32)
+    h, w = img.shape
+    n = ctypes.c_int(0)
+    lib().oracle_extract_f32(img.ctypes.data, w, h, w, ctypes.byref(opts), None, None, 0,
+                             ctypes.byref(n))
+    keys = np.zeros((max(n.value, 1), 4), np.float32)
+    desc = np.zeros((max(n.value, 1), 128), np.float32)
+    rc = lib().oracle_extract_f32(img.ctypes.data, w, h, w, ctypes.byref(opts), keys.ctypes.data,
+                                  desc.ctypes.data, n.value, ctypes.byref(n))
+    assert rc == 0, rc
+    return keys[:n.value], desc[:n.value]
+
+
+def gray_from_color(img: np.ndarray, fmt: str) -> np.ndarray:
+    """DownSamplePixelDataI2F<u8> for GL_RGB/RGBA/BGR/BGRA (GLTexImage.cpp:834-858): the exact
+    integer numerator over 65535 * 255 as one float division; width truncated to 4."""
+    h, w, c = img.shape
+    tw = w & ~3
+    p = img[:, :tw].astype(np.int64)
+    r, g, b = (p[..., 0], p[..., 1], p[..., 2]) if fmt in ("rgb", "rgba") else (p[..., 2], p[..., 1], p[..., 0])
+    num = (19595 * r + 38470 * g + 7471 * b).astype(np.float32)
+    return num / np.float32(65535.0 * 255.0)
 
 
 def gaussian(img, octave, level, opts=None):

@@ -200,6 +200,48 @@ def test_float_input_matches_u8(gpu_ctx):
     assert np.array_equal(_bits(k8), _bits(kf)) and np.array_equal(_bits(d8), _bits(df))
 
 
+def _synth_color(w, h, seed, ch):
+    rng = np.random.default_rng(seed)
+    base = synth_image(w, h, seed).astype(np.int32)
+    img = np.stack([np.clip(base + rng.integers(-40, 41, (h, w)), 0, 255) for _ in range(ch)], -1)
+    return img.astype(np.uint8)
+
+
+@pytest.mark.parametrize("fmt", ["rgb", "bgr", "rgba", "bgra"])
+def test_color_ingest_vs_oracle(gpu_ctx, fmt):
+    """Device luminance conversion (GLTexImage.cpp:834-858) then the float-input pipeline,
+    against the oracle run on the host-converted luminance."""
+    ch = 3 if fmt in ("rgb", "bgr") else 4
+    imgs = np.stack([_synth_color(322, 241, 60 + i, ch) for i in range(2)])
+    gpu_ctx.set_options(default_options())
+    gpu_ctx.extract_color(imgs, fmt)
+    for i in range(2):
+        k, d = gpu_ctx.features(i)
+        rk, rd = O.extract_f32(O.gray_from_color(imgs[i], fmt))
+        _assert_features_equal(k, d, rk, rd, f"{fmt} image {i}")
+    # -fo 1 on color input: conversion first, then SampleImageD (GLTexImage.cpp:931-935 keeps
+    # the device down-sampling path for images within the texture limit)
+    opts = default_options(octave_min=1)
+    gpu_ctx.set_options(opts)
+    gpu_ctx.extract_color(imgs[:1], fmt)
+    k, d = gpu_ctx.features(0)
+    rk, rd = O.extract_f32(O.gray_from_color(imgs[0], fmt), opts)
+    _assert_features_equal(k, d, rk, rd, f"{fmt} -fo 1")
+    gpu_ctx.set_options(default_options())
+
+
+def test_float_input_vs_oracle(gpu_ctx):
+    """Float luminance that is not u8 / 255 (GL_FLOAT input)."""
+    rng = np.random.default_rng(3)
+    img = (synth_image(300, 200, 5).astype(np.float32) / 300.0 +
+           rng.uniform(0, 0.1, (200, 300)).astype(np.float32))
+    gpu_ctx.set_options(default_options())
+    gpu_ctx.extract(img)
+    k, d = gpu_ctx.features(0)
+    rk, rd = O.extract_f32(img)
+    _assert_features_equal(k, d, rk, rd, "f32")
+
+
 def test_batch_equals_single_images(gpu_ctx):
     imgs = np.stack([synth_image(256, 192, 500 + i) for i in range(5)])
     gpu_ctx.set_options(default_options())

@@ -375,3 +375,22 @@ def test_first_octave_minus_two_is_refused():
     """-fo -2 makes the reference's initial sigma 0 and CreateFilterKernel's taps NaN."""
     with pytest.raises(AssertionError):
         O.extract(synth_image(64, 48, 1), default_options(octave_min=-2))
+
+
+def test_float_ingest_equals_u8_ingest():
+    """u8 p and float p/255.0f are the same input (GLTexImage.cpp:818)."""
+    img = synth_image(160, 120, 4)
+    k8, d8 = O.extract(img)
+    kf, df = O.extract_f32(img.astype(np.float32) / np.float32(255.0))
+    np.testing.assert_array_equal(k8, kf)
+    np.testing.assert_array_equal(d8, df)
+
+
+def test_color_formula_kat():
+    """(19595 r + 38470 g + 7471 b) / (65535 * 255): the weights sum to 65536, so white is
+    65536/65535 (slightly above 1) as in the reference; BGR swaps r and b."""
+    px = np.array([[[255, 255, 255, 0], [255, 0, 0, 0], [0, 0, 255, 0], [10, 20, 30, 0]]], np.uint8)
+    g = O.gray_from_color(px, "rgba")
+    assert g[0, 0] == np.float32(65536 * 255) / np.float32(65535.0 * 255.0) > 1.0
+    assert g[0, 1] == np.float32(19595 * 255) / np.float32(65535.0 * 255.0)
+    assert O.gray_from_color(px, "bgra")[0, 2] == g[0, 1]
