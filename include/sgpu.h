@@ -122,7 +122,10 @@ int sgpu_device_features(sgpu_ctx* ctx, const float** keys, const float** descri
  * SiftPyramid::SetKeypointList SiftPyramid.cpp:293-310, GenerateFeatureListTex
  * PyramidCU.cpp:454-504).  keys: num x (x, y, scale, orientation) in image coordinates.  With
  * has_orientation == 0 the strongest orientation is computed (ComputeOrientation_Kernel with
- * existing_keypoint) and the keys are rewritten as DownloadKeypoints does.  Results (input order)
+ * existing_keypoint) and the keys are rewritten as DownloadKeypoints does.  has_orientation ==
+ * -1 is the rectangle mode (SIFT_RECT_DESCRIPTION, SiftPyramid.cpp:308-309): keys are
+ * (x, y, width, height) and ComputeDescriptorRECT_Kernel (ProgramCU.cu:1104-1171) describes the
+ * rectangle; keys come back unchanged.  Results (input order)
  * replace the context's features: image `image` reports num features (sgpu_copy_features),
  * every other image none. */
 int sgpu_extract_keypoints(sgpu_ctx* ctx, int image, const float* keys, int num,

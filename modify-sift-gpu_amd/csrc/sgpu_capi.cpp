@@ -640,6 +640,7 @@ int sgpu_extract_keypoints(sgpu_ctx* ctx, int image, const float* keys, int num,
     const double twopi = 2.0 * 3.14159265358979323846;
     const float sigma_half_step = powf(2.0f, 0.5f / d);
     const float offset = O.lowe_origin ? 0.0f : 0.5f;
+    const bool rect = has_orientation == -1;
     std::vector<float4> lf;
     std::vector<int2> li;
     std::vector<int> lidx;
@@ -651,14 +652,17 @@ int sgpu_extract_keypoints(sgpu_ctx* ctx, int image, const float* keys, int num,
             const float sigma_max = level_sigma * sigma_half_step;
             for (int k = 0; k < num; k++) {
                 const float* key = keys + 4 * (size_t)k;
-                const float sigmak = key[2];
+                // RECT (keys_have_orientation == -1, SiftPyramid.cpp:308-309): (x, y, width,
+                // height) rectangles, levelled by min(width, height) / 12 (PyramidCU.cpp:480)
+                const float sigmak = rect ? std::min(key[2], key[3]) / 12.0f : key[2];
                 if ((sigmak >= sigma_min && sigmak < sigma_max) ||
                     (sigmak < sigma_min && i == 0 && j == 0) ||
                     (sigmak > sigma_max && i == noct - 1 && j == d - 1)) {
                     lf.push_back(make_float4((key[0] - offset) / octave_sigma + 0.5f,
                                              (key[1] - offset) / octave_sigma + 0.5f,
                                              key[2] / octave_sigma,
-                                             (float)std::fmod(twopi - key[3], twopi)));
+                                             rect ? key[3] / octave_sigma
+                                                  : (float)std::fmod(twopi - key[3], twopi)));
                     li.push_back(make_int2(b, i * d + j));
                     lidx.push_back(k);
                 }
@@ -692,7 +696,7 @@ int sgpu_extract_keypoints(sgpu_ctx* ctx, int image, const float* keys, int num,
         HIPCHK(ctx, hipMemsetAsync(pt.desc.p, 0, (size_t)num * 128 * sizeof(float), st));
         HIPCHK(ctx, sgk::launch_descriptor(pt.pyr.as<float>(), pt.feat.as<float4>(),
                                            pt.feat_info.as<int2>(), d_m, std::max(m, 1), pt.fp,
-                                           pt.desc.as<float>(), st, d_index));
+                                           pt.desc.as<float>(), st, d_index, rect));
     }
     HIPCHK(ctx, hipStreamSynchronize(st));
     // the described image now owns the context's feature list

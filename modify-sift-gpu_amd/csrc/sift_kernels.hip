@@ -1676,6 +1676,10 @@ __device__ __forceinline__ float sq4(float a, float b, float c, float d) {
     return fma_(d, d, t);
 }
 
+// RECT: ComputeDescriptorRECT_Kernel<false> (ProgramCU.cu:1104-1171) for keys given with
+// keys_have_orientation == -1: the 4 x 4 grid spans the rectangle [x, x+z] x [y, y+w], cells
+// are axis-aligned (nx = dx / sptx), no Gaussian window, theta = -angle.
+template <bool RECT>
 __device__ __forceinline__ void descriptor_one(uint32_t e, int lane,
                                                const float* __restrict__ pyr,
                                                const float4* __restrict__ feat,
@@ -1700,22 +1704,35 @@ __device__ __forceinline__ void descriptor_one(uint32_t e, int lane,
     const float* g = pyr + od.gauss_off + (long long)(1 + j) * od.level_stride +
                      (long long)in.x * W * H;
     const float rpi = (float)(4.0 / 3.14159265358979323846);
-    const float spt = fabs_(key.z * fp.window_factor);
-    float s, c;
-    sincos_(key.w, &s, &c);
-    const float anglef = (double)key.w > 3.14159265358979323846
-                             ? (float)((double)key.w - (2.0 * 3.14159265358979323846))
-                             : key.w;
-    const float cspt = c * spt, sspt = s * spt;
-    const float crspt = c / spt, srspt = s / spt;
-    const float ox = ix - 1.5f, oy = iy - 1.5f;
-    const float ptx = fma_(cspt, ox, -(sspt * oy)) + key.x;
-    const float pty = fma_(cspt, oy, sspt * ox) + key.y;
-    const float bsz = fabs_(cspt) + fabs_(sspt);
-    const float xmin = fmax_(1.5f, floor_(ptx - bsz) + 0.5f);
-    const float ymin = fmax_(1.5f, floor_(pty - bsz) + 0.5f);
-    const float xmax = fmin_(W - 1.5f, floor_(ptx + bsz) + 0.5f);
-    const float ymax = fmin_(H - 1.5f, floor_(pty + bsz) + 0.5f);
+    float spt = 0.f, anglef = 0.f, cspt = 0.f, sspt = 0.f, crspt = 0.f, srspt = 0.f;
+    float ox = 0.f, oy = 0.f, ptx, pty, bszx, bszy;
+    const float sptx = key.z * 0.25f, spty = key.w * 0.25f;   // RECT (exact: key * 0.25 double)
+    if (RECT) {
+        ptx = fma_(sptx, ix + 0.5f, key.x);
+        pty = fma_(spty, iy + 0.5f, key.y);
+        bszx = sptx;
+        bszy = spty;
+    } else {
+        spt = fabs_(key.z * fp.window_factor);
+        float s, c;
+        sincos_(key.w, &s, &c);
+        anglef = (double)key.w > 3.14159265358979323846
+                     ? (float)((double)key.w - (2.0 * 3.14159265358979323846))
+                     : key.w;
+        cspt = c * spt;
+        sspt = s * spt;
+        crspt = c / spt;
+        srspt = s / spt;
+        ox = ix - 1.5f;
+        oy = iy - 1.5f;
+        ptx = fma_(cspt, ox, -(sspt * oy)) + key.x;
+        pty = fma_(cspt, oy, sspt * ox) + key.y;
+        bszx = bszy = fabs_(cspt) + fabs_(sspt);
+    }
+    const float xmin = fmax_(1.5f, floor_(ptx - bszx) + 0.5f);
+    const float ymin = fmax_(1.5f, floor_(pty - bszy) + 0.5f);
+    const float xmax = fmin_(W - 1.5f, floor_(ptx + bszx) + 0.5f);
+    const float ymax = fmin_(H - 1.5f, floor_(pty + bszy) + 0.5f);
     const int ncols = xmax >= xmin ? (int)(xmax - xmin) + 1 : 0;
     const int nrows = ymax >= ymin ? (int)(ymax - ymin) + 1 : 0;
     // The reference visits every sample of the cell's axis-aligned box and keeps those with
@@ -1723,7 +1740,9 @@ __device__ __forceinline__ void descriptor_one(uint32_t e, int lane,
     // quad walks, row by row, a column span that covers the square with a 0.01-pixel margin
     // (the float bounds and the float test differ by ~1e-5 pixel; the exact test below still
     // decides each sample) -- same samples, same (y, x) order, ~45% fewer iterations.
-    const bool use_c = fabs_(crspt) > 1e-4f / spt, use_s = fabs_(srspt) > 1e-4f / spt;
+    // (RECT: every column of the box; the exact test below decides)
+    const bool use_c = !RECT && fabs_(crspt) > 1e-4f / spt;
+    const bool use_s = !RECT && fabs_(srspt) > 1e-4f / spt;
     const float icr = use_c ? 1.0f / crspt : 0.0f, isr = use_s ? 1.0f / srspt : 0.0f;
     const float kInf = as_float(0x7f800000u);
     auto row_span = [&](int r, int& lo, int& len) {
@@ -1763,18 +1782,30 @@ __device__ __forceinline__ void descriptor_one(uint32_t e, int lane,
         if (wr < nrows) {
             const float x = xmin + (float)(wlo + wc), y = ymin + (float)wr;
             const float dx = x - ptx, dy = y - pty;
-            const float nx = fma_(crspt, dx, srspt * dy);
-            const float ny = fma_(crspt, dy, -(srspt * dx));
+            float nx, ny;
+            if (RECT) {
+                nx = dx / sptx;
+                ny = dy / spty;
+            } else {
+                nx = fma_(crspt, dx, srspt * dy);
+                ny = fma_(crspt, dy, -(srspt * dx));
+            }
             const float nxn = fabs_(nx), nyn = fabs_(ny);
             if (nxn < 1.0f && nyn < 1.0f) {
                 const float2 cc = grad_at(g, W, (int)x, (int)y);
-                const float dnx = nx + ox, dny = ny + oy;
-                const float ww = exp_mid_(-0.125f * fma_(dnx, dnx, dny * dny));   // in [-1.6, 0]
                 // (float)(1.0 - (double)n) of the reference: 1 - n is exact in double, so the
                 // single float subtraction rounds to the same value
                 const float wx = 1.0f - nxn, wy = 1.0f - nyn;
-                weight = ww * wx * wy * cc.x;
-                float theta = (anglef - cc.y) * rpi;
+                float theta;
+                if (RECT) {
+                    weight = wx * wy * cc.x;
+                    theta = (-cc.y) * rpi;
+                } else {
+                    const float dnx = nx + ox, dny = ny + oy;
+                    const float ww = exp_mid_(-0.125f * fma_(dnx, dnx, dny * dny));   // in [-1.6, 0]
+                    weight = ww * wx * wy * cc.x;
+                    theta = (anglef - cc.y) * rpi;
+                }
                 if (theta < 0) theta += 8.0f;
                 const float fo = floor_(theta);
                 fidx = (int)fo;
@@ -1844,6 +1875,7 @@ __device__ __forceinline__ void descriptor_one(uint32_t e, int lane,
 }
 
 // One wave per feature, grid-stride over the features (count read on the device).
+template <bool RECT>
 __global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ pyr,
                                                     const float4* __restrict__ feat,
                                                     const int2* __restrict__ feat_info,
@@ -1854,8 +1886,8 @@ __global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ py
     const int lane = threadIdx.x & 63;
     const uint32_t n = *n_feat_dev;
     for (uint32_t e = blockIdx.x * 4 + (threadIdx.x >> 6); e < n; e += gridDim.x * 4)   // uniform per wave
-        descriptor_one(e, lane, pyr, feat, feat_info, fp, desc,
-                       out_index ? (uint32_t)out_index[e] : e);
+        descriptor_one<RECT>(e, lane, pyr, feat, feat_info, fp, desc,
+                             out_index ? (uint32_t)out_index[e] : e);
 }
 
 // Caller-supplied keypoints (SiftGPU::RunSIFT(num, keys, keys_have_orientation),
@@ -2123,11 +2155,16 @@ hipError_t launch_orient_keys(const float* pyr, float4* feat, const int2* feat_i
 
 hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* feat_info,
                              const uint32_t* n_feat_dev, int n_feat_cap, const FeatureParams& fp,
-                             float* desc, hipStream_t stream, const int* out_index) {
+                             float* desc, hipStream_t stream, const int* out_index,
+                             bool rect) {
     if (n_feat_cap <= 0) return hipSuccess;
     const unsigned grid = (unsigned)std::min(((long long)n_feat_cap + 3) / 4, 65536LL);
-    hipLaunchKernelGGL(k_descriptor, dim3(grid), dim3(256), 0, stream, pyr, feat, feat_info,
-                       n_feat_dev, fp, desc, out_index);
+    if (rect)
+        hipLaunchKernelGGL(k_descriptor<true>, dim3(grid), dim3(256), 0, stream, pyr, feat,
+                           feat_info, n_feat_dev, fp, desc, out_index);
+    else
+        hipLaunchKernelGGL(k_descriptor<false>, dim3(grid), dim3(256), 0, stream, pyr, feat,
+                           feat_info, n_feat_dev, fp, desc, out_index);
     return hipGetLastError();
 }
 

@@ -362,14 +362,10 @@ static int fetch_features(Runtime* rt) {
 }
 
 // Descriptors of a keypoint list on the current image (SiftGPU::RunSIFT(num, keys, ...)).
+// keys_have_orientation: 0 computes the strongest orientation, -1 is the rectangle description
+// (SIFT_RECT_DESCRIPTION, SiftPyramid.cpp:307-309, ProgramCU.cu:1104-1171), anything else keeps
+// the given orientations.
 static int describe_keys(Runtime* rt, const float* keys, int num, int has_orientation) {
-    if (has_orientation < 0) {
-        // keys_have_orientation == -1: the rectangle description hack (SIFT_RECT_DESCRIPTION,
-        // SiftPyramid.cpp:309, ProgramCU.cu:1104-1171)
-        std::cerr << "SiftGPU (MI355X): rectangle descriptors (keys_have_orientation = -1) are "
-                     "not implemented\n";
-        return 0;
-    }
     if (sgpu_extract_keypoints(rt->ctx, 0, keys, num, has_orientation) != SGPU_OK) {
         std::cerr << "SiftGPU: " << sgpu_last_error(rt->ctx) << "\n";
         return 0;

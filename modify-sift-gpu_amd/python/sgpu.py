@@ -186,12 +186,13 @@ class SiftContext:
                     "extract_color")
         self.batch = n
 
-    def extract_keypoints(self, keys: np.ndarray, has_orientation: bool = True, image: int = 0):
+    def extract_keypoints(self, keys: np.ndarray, has_orientation=True, image: int = 0):
         """Descriptors of caller-supplied keys [n, 4] (x, y, scale, orientation) on image
-        `image` of the last extract (SiftGPU::RunSIFT(num, keys, keys_have_orientation))."""
+        `image` of the last extract (SiftGPU::RunSIFT(num, keys, keys_have_orientation)).
+        has_orientation = -1: rectangles (x, y, width, height), the RECT description."""
         k = np.ascontiguousarray(keys, np.float32).reshape(-1, 4)
-        self._check(lib().sgpu_extract_keypoints(self._ctx, image, k.ctypes.data, len(k),
-                                                 1 if has_orientation else 0),
+        ho = -1 if has_orientation == -1 else (1 if has_orientation else 0)
+        self._check(lib().sgpu_extract_keypoints(self._ctx, image, k.ctypes.data, len(k), ho),
                     "sgpu_extract_keypoints")
         return self
 

@@ -490,6 +490,26 @@ void orientation_key(Key4 key, const std::vector<float>& grad, int W, int H,
 
 // --- ComputeDescriptor_Kernel<false> (ProgramCU.cu:1013-1101) + NormalizeDescriptor_Kernel
 //     (:1173-1208) for one feature (fx, fy, s, o) in octave coordinates.
+// --- NormalizeDescriptor_Kernel (ProgramCU.cu:1173-1208): sums of the 32 float4 in order,
+//     rsqrt, clip 0.2, renormalise.
+void normalize_descriptor(float* des128, int normalize) {
+    if (!normalize) return;
+    auto sq4 = [](const float* p) {
+        float t = p[0] * p[0];
+        t = fma_(p[1], p[1], t);
+        t = fma_(p[2], p[2], t);
+        t = fma_(p[3], p[3], t);
+        return t;
+    };
+    float norm1 = 0, norm2 = 0;
+    for (int i = 0; i < 32; ++i) norm1 += sq4(des128 + 4 * i);
+    norm1 = rsqrt_(norm1);
+    for (int i = 0; i < 128; ++i) des128[i] = fmin_(0.2f, des128[i] * norm1);
+    for (int i = 0; i < 32; ++i) norm2 += sq4(des128 + 4 * i);
+    norm2 = rsqrt_(norm2);
+    for (int i = 0; i < 128; ++i) des128[i] *= norm2;
+}
+
 void descriptor(const float* key, const std::vector<float>& grad, int W, int H,
                 float window_factor, int normalize, float* des128) {
     const float rpi = (float)(4.0 / 3.14159265358979323846);
@@ -540,22 +560,53 @@ void descriptor(const float* key, const std::vector<float>& grad, int W, int H,
         des[0] += des[8];
         for (int i = 0; i < 8; i++) des128[bidx * 8 + i] = des[i];
     }
-    if (!normalize) return;
-    auto sq4 = [](const float* p) {
-        float t = p[0] * p[0];
-        t = fma_(p[1], p[1], t);
-        t = fma_(p[2], p[2], t);
-        t = fma_(p[3], p[3], t);
-        return t;
-    };
-    float norm1 = 0, norm2 = 0;
-    for (int i = 0; i < 32; ++i) norm1 += sq4(des128 + 4 * i);
-    norm1 = rsqrt_(norm1);
-    for (int i = 0; i < 128; ++i) des128[i] = fmin_(0.2f, des128[i] * norm1);
-    for (int i = 0; i < 32; ++i) norm2 += sq4(des128 + 4 * i);
-    norm2 = rsqrt_(norm2);
-    for (int i = 0; i < 128; ++i) des128[i] *= norm2;
+    normalize_descriptor(des128, normalize);
 }
+
+// --- ComputeDescriptorRECT_Kernel<false> (ProgramCU.cu:1104-1171): keys passed with
+//     keys_have_orientation == -1 (SIFT_RECT_DESCRIPTION, SiftPyramid.cpp:307-309) describe the
+//     axis-aligned rectangle [x, x + z] x [y, y + w] (octave coordinates) as a 4 x 4 grid, with
+//     bilinear cell weights, no Gaussian window and the gradient angle taken as is.
+void descriptor_rect(const float* key, const std::vector<float>& grad, int W, int H,
+                     int normalize, float* des128) {
+    const float rpi = (float)(4.0 / 3.14159265358979323846);
+    for (int bidx = 0; bidx < 16; bidx++) {
+        const int ix = bidx & 3, iy = bidx >> 2;
+        const float sptx = (float)(key[2] * 0.25), spty = (float)(key[3] * 0.25);
+        const float ptx = fma_(sptx, ix + 0.5f, key[0]);
+        const float pty = fma_(spty, iy + 0.5f, key[1]);
+        const float xmin = fmax_(1.5f, floor_(ptx - sptx) + 0.5f);
+        const float ymin = fmax_(1.5f, floor_(pty - spty) + 0.5f);
+        const float xmax = fmin_(W - 1.5f, floor_(ptx + sptx) + 0.5f);
+        const float ymax = fmin_(H - 1.5f, floor_(pty + spty) + 0.5f);
+        float des[9];
+        for (int i = 0; i < 9; ++i) des[i] = 0.0f;
+        for (float y = ymin; y <= ymax; y += 1.0f)
+            for (float x = xmin; x <= xmax; x += 1.0f) {
+                const float nx = (x - ptx) / sptx, ny = (y - pty) / spty;
+                const float nxn = fabs_(nx), nyn = fabs_(ny);
+                if (nxn < 1.0f && nyn < 1.0f) {
+                    const size_t t = ((size_t)(int)y * W + (int)x) * 2;
+                    const float gm = grad[t], ga = grad[t + 1];
+                    const float wx = (float)(1.0 - nxn), wy = (float)(1.0 - nyn);
+                    const float weight = wx * wy * gm;
+                    float theta = (-ga) * rpi;
+                    if (theta < 0) theta += 8.0f;
+                    const float fo = floor_(theta);
+                    const int fidx = (int)fo;
+                    const float weight1 = fo + 1.0f - theta, weight2 = theta - fo;
+                    if (fidx >= 0 && fidx < 8) {
+                        des[fidx] = fma_(weight1, weight, des[fidx]);
+                        des[fidx + 1] = fma_(weight2, weight, des[fidx + 1]);
+                    }
+                }
+            }
+        des[0] += des[8];
+        for (int i = 0; i < 8; i++) des128[bidx * 8 + i] = des[i];
+    }
+    normalize_descriptor(des128, normalize);
+}
+
 
 }  // namespace
 
@@ -716,7 +767,8 @@ std::vector<float> describe_keys(const uint8_t* img, int w, int h, int stride,
             const float sigma_max = level_sigma * sigma_half_step;
             for (int k = 0; k < num; k++) {
                 const float* key = keys + 4 * k;
-                const float sigmak = key[2];
+                const bool rect = has_orientation == -1;   // SIFT_RECT_DESCRIPTION
+                const float sigmak = rect ? fmin_(key[2], key[3]) / 12.0f : key[2];
                 if ((sigmak >= sigma_min && sigmak < sigma_max) ||
                     (sigmak < sigma_min && i == 0 && j == 0) ||
                     (sigmak > sigma_max && i == noct - 1 && j == d - 1)) {
@@ -724,7 +776,8 @@ std::vector<float> describe_keys(const uint8_t* img, int w, int h, int stride,
                     e.k[0] = (key[0] - offset) / octave_sigma + 0.5f;
                     e.k[1] = (key[1] - offset) / octave_sigma + 0.5f;
                     e.k[2] = key[2] / octave_sigma;
-                    e.k[3] = (float)std::fmod(twopi - key[3], twopi);
+                    e.k[3] = rect ? key[3] / octave_sigma
+                                  : (float)std::fmod(twopi - key[3], twopi);
                     e.index = k;
                     e.octave = i;
                     e.level = j;
@@ -769,8 +822,12 @@ std::vector<float> describe_keys(const uint8_t* img, int w, int h, int stride,
         }
         if (opt.descriptors) {
             const sgp::Octave& oc = R.octaves[e.octave];
-            descriptor(e.k, grad[e.octave][e.level], oc.wa, oc.h, opt.descriptor_window_factor,
-                       opt.normalized, desc.data() + 128 * (size_t)e.index);
+            if (has_orientation == -1)
+                descriptor_rect(e.k, grad[e.octave][e.level], oc.wa, oc.h, opt.normalized,
+                                &desc[(size_t)e.index * 128]);
+            else
+                descriptor(e.k, grad[e.octave][e.level], oc.wa, oc.h, opt.descriptor_window_factor,
+                           opt.normalized, desc.data() + 128 * (size_t)e.index);
         }
     }
     return desc;

@@ -170,8 +170,9 @@ def describe_keys(img, keys, has_orientation=True, opts=None):
     k = np.ascontiguousarray(keys, np.float32).reshape(-1, 4)
     ko = np.zeros_like(k)
     d = np.zeros((len(k), 128), np.float32)
-    lib().oracle_describe_keys(p, w, h, w, ctypes.byref(opts), k.ctypes.data, len(k),
-                               1 if has_orientation else 0, ko.ctypes.data, d.ctypes.data)
+    ho = -1 if has_orientation == -1 else (1 if has_orientation else 0)
+    lib().oracle_describe_keys(p, w, h, w, ctypes.byref(opts), k.ctypes.data, len(k), ho,
+                               ko.ctypes.data, d.ctypes.data)
     return ko, d
 
 

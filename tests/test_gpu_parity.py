@@ -503,6 +503,32 @@ def test_keypoints_vs_oracle(gpu_ctx, has_orientation, over):
     assert np.array_equal(_bits(d), _bits(rd))
 
 
+def _synth_rects(w, h, n, seed):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    k = np.zeros((n, 4), np.float32)
+    k[:, 2] = np.exp(rng.uniform(np.log(4.0), np.log(300.0), n))     # width
+    k[:, 3] = k[:, 2] * rng.uniform(0.3, 3.0, n).astype(np.float32)  # height
+    k[:, 0] = rng.uniform(-20, w, n)                                 # left (may leave the image)
+    k[:, 1] = rng.uniform(-20, h, n)
+    return k
+
+
+@pytest.mark.parametrize("over", [{}, {"normalized": 0}, {"octave_min": 1}])
+def test_rect_keypoints_vs_oracle(gpu_ctx, over):
+    """keys_have_orientation == -1: rectangle descriptors (ComputeDescriptorRECT_Kernel)."""
+    img = synth_image(480, 360, 73)
+    opts = default_options(**over)
+    keys = _synth_rects(480, 360, 250, 74)
+    gpu_ctx.set_options(opts)
+    gpu_ctx.extract(img)
+    gpu_ctx.extract_keypoints(keys, -1)
+    k, d = gpu_ctx.features(0)
+    rk, rd = O.describe_keys(img, keys, -1, opts)
+    assert np.array_equal(_bits(k), _bits(keys)) and np.array_equal(_bits(rk), _bits(keys))
+    assert np.array_equal(_bits(d), _bits(rd))
+    gpu_ctx.set_options(default_options())
+
+
 def test_detected_keypoints_fed_back(gpu_ctx):
     """Keys from the detector itself, described again as a caller-supplied list."""
     img = synth_image(400, 300, 73)
