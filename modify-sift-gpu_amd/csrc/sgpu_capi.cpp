@@ -402,12 +402,51 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     float* pyr = pt.pyr.as<float>();
     sgk::Taps taps;
     const bool two = noct > 1 && (sgk::get_variant() & 16384);
+    // One launch per level (k_gauss_pk2) is the shipped path.  Variant bit 8388608 (test hook)
+    // runs each octave of the default schedule (d = 3, filter factor 4) as ONE fused launch
+    // instead (sift_octave.hip: all levels streamed through LDS, 25-26 B of HBM traffic per
+    // octave pixel instead of 48) -- bit-identical, but slower on MI355X.
+    sgk::Taps ltaps[sgk::kMaxLevels], taps0;
+    int lfw[sgk::kMaxLevels] = {0};
+    for (int k = 1; k < nlev; k++)
+        lfw[k] = sgp::make_filter(S.sigma[k - 1], O.filter_width_factor, ltaps[k].k);
+    const int fw0 = sgp::make_filter(S.initial_smooth, O.filter_width_factor, taps0.k);
+    const bool fused = !two && (sgk::get_variant() & 8388608) &&
+                       sgk::octave_fused_supported(nlev, lfw, S.level_ds - S.level_min);
     for (int o = 0; o < noct; o++) {
         if (o == 1 && two) HIPCHK(ctx, hipStreamWaitEvent(pt.stream_aux, pt.ev[7], 0));
         st = (o >= 1 && two) ? pt.stream_aux : pt.stream;
         const sgk::OctaveDesc& od = fp.oct[o];
         const long long npx = (long long)od.wa * od.h;
         float* lvl0 = pyr + od.gauss_off;
+        if (fused && (o > 0 || O.octave_min == 0)) {
+            sgk::OctaveLaunch L{};
+            if (o == 0) {
+                L.src8 = src8;
+                L.srcf = srcf;
+                L.src_stride = stride;
+                L.src_img_stride = (long long)img_elems;
+                L.fw0 = fw0;
+                L.taps0 = taps0.k;
+            }
+            L.pyr = lvl0;
+            L.level_stride = od.level_stride;
+            L.w = od.wa;
+            L.h = od.h;
+            L.batch = n;
+            for (int k = 1; k < nlev; k++) L.taps[k] = ltaps[k].k;
+            if (o + 1 < noct) {
+                const sgk::OctaveDesc& nd = fp.oct[o + 1];
+                L.ds = pyr + nd.gauss_off;
+                L.dsw = nd.wa;
+                L.dsh = nd.h;
+                L.ds_img_stride = (long long)nd.wa * nd.h;
+            }
+            const hipError_t e = sgk::launch_octave(L, st);
+            if (e == hipSuccess) continue;
+            if (e != hipErrorNotSupported) HIPCHK(ctx, e);
+            (void)hipGetLastError();   // unsupported input layout: per-level path below
+        }
         if (o == 0) {
             int fw = sgp::make_filter(S.initial_smooth, O.filter_width_factor, taps.k);
             if (O.octave_min == 0) {

@@ -52,6 +52,29 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         float* ds_dst, int ds_w, int ds_h, long long ds_img_stride,
                         hipStream_t stream);
 
+// Fused octave pyramid (sift_octave.hip): all d+3 = 6 levels of one octave in one launch,
+// for the default schedule (d = 3, filter factor 4: level filters 11, 13, 17, 21, 25).
+// Octave 0: src8 (u8, value p/255) or srcf (f32) is the input, filtered with taps0 (fw0 11 or
+// 13) into level 0.  Octave > 0: src8 = srcf = nullptr and level 0 is already in the pyramid.
+// ds != nullptr: level 3 also writes its 2x point-downsample there (next octave level 0).
+struct OctaveLaunch {
+    const uint8_t* src8;
+    const float* srcf;
+    int src_stride;
+    long long src_img_stride;
+    int fw0;
+    const float* taps0;
+    float* pyr;              // level 0 of image 0
+    long long level_stride;  // floats between levels (images are w * h apart)
+    int w, h, batch;
+    const float* taps[6];    // taps[l], l = 1..5
+    float* ds;
+    int dsw, dsh;
+    long long ds_img_stride;
+};
+bool octave_fused_supported(int nlev, const int* fw, int level_ds);
+hipError_t launch_octave(const OctaveLaunch& L, hipStream_t stream);
+
 // First octave of -fo != 0 (BuildPyramid, PyramidCU.cpp:1011-1016): the batch's input
 // (u8 p/255 or f32; tw = w & ~3 columns used, rows `stride` apart) resampled into dst
 // (dw x dh per image, dst_img_stride apart): SampleImageD by 2^fo for fo > 0, UpsampleKernel

@@ -80,6 +80,35 @@ def test_gaussian_levels_bitwise(gpu_ctx, w, h, seed):
             assert np.array_equal(_bits(g), _bits(r)), (o, lvl)
 
 
+@pytest.mark.parametrize("w,h,n", [(16, 16, 1), (256, 97, 1), (1000, 300, 3), (96, 1500, 1),
+                                   (484, 250, 2), (1920, 1080, 2), (203, 97, 1)])
+def test_fused_octave_matches_per_level(gpu_ctx, w, h, n):
+    """The fused one-launch-per-octave pyramid (sift_octave.hip, variant 8388608) against the
+    shipped per-level kernels, bit for bit, on every level of every octave: one and several
+    column strips, row bands (tall images, batch 1), odd heights, a ragged last strip, u8 rows
+    whose stride is not a multiple of 4 (octave 0 then falls back to the per-level kernel)."""
+    imgs = np.stack([synth_image(w, h, 40 + i) for i in range(n)])
+    opts = default_options()
+    gpu_ctx.set_options(opts)
+    gpu_ctx.extract(imgs)
+    geo = gpu_ctx.geometry()
+    ref = [[gpu_ctx.gaussian(i, o, l) for o in range(len(geo)) for l in range(6)]
+           for i in range(n)]
+    rk, rd = gpu_ctx.features(n - 1)
+    try:
+        sgpu.lib().sgpu_debug_set_variant(8388608)
+        gpu_ctx.extract(imgs)
+        fused = [[gpu_ctx.gaussian(i, o, l) for o in range(len(geo)) for l in range(6)]
+                 for i in range(n)]
+        k, d = gpu_ctx.features(n - 1)
+    finally:
+        sgpu.lib().sgpu_debug_set_variant(0)
+    for i in range(n):
+        for q, (g, r) in enumerate(zip(fused[i], ref[i])):
+            assert np.array_equal(_bits(g), _bits(r)), (i, divmod(q, 6))
+    assert np.array_equal(_bits(k), _bits(rk)) and np.array_equal(_bits(d), _bits(rd))
+
+
 @pytest.mark.parametrize("fo,w,h", [(1, 203, 97), (-1, 203, 97), (-1, 96, 64), (2, 321, 241)])
 def test_first_octave_levels_bitwise(gpu_ctx, fo, w, h):
     """-fo != 0: the resampled first octave (SampleImageD / UpsampleKernel) and its levels."""
