@@ -67,6 +67,10 @@ def main():
         print(f"note: WORLD_SIZE={world} differs from --gpus {args.gpus}", file=sys.stderr)
     sgpu.lib()   # libsiftgpu (and /opt/rocm's HIP runtime) before torch: torch never touches
                  # the GPU here -- torch.distributed (gloo, host) is only the rendezvous
+    # Initialise /opt/rocm's HIP runtime now, before `import torch` maps torch's own copy of
+    # libamdhip64: a context created after the torch import and the gloo rendezvous otherwise
+    # finds no device (observed on the box with two ranks).
+    n_dev = sgpu.device_count()
     dist = None
     device = local
     if world > 1:
@@ -83,7 +87,7 @@ def main():
             os.dup2(saved, 1)
             os.close(saved)
         if args.dist_backend == "gloo":
-            device = local % max(1, sgpu.device_count())
+            device = local % max(1, n_dev)
 
     B, W, H = args.batch, args.width, args.height
     opts = default_options(octave_num=args.octaves)
@@ -187,6 +191,10 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_match:
         result["match"] = bench_match(ctx, args.match_n)
+    if world > 1 and not args.no_match:
+        sm = bench_match_sharded(ctx, args.match_n, rank, world, None if rccl else dist)
+        if rank == 0:
+            result["match_sharded"] = sm
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(imgs, opts)
     if rank == 0:
@@ -240,6 +248,49 @@ def bench_match(ctx, n):
             "tops": ops / (ms * 1e-3) / 1e12,
             "mfma_util": ops / (ms * 1e-3) / 1e12 / I8_MFMA_PEAK_TOPS,
             "guided_ms": gms, "guided_matches": int(len(gm))}
+
+
+def bench_match_sharded(ctx, n, rank, world, host_dist=None):
+    """Config C5 with set 1 sharded over the ranks: each rank matches its rows
+    against all of set 2, the per-column states travel by one RCCL all-gather, and the rank
+    keeps its rows' mutual pairs (sgpu_match_sharded).  Reported: the slowest rank's device
+    time and wall time per call, and the total pair count (equal to the 1-GPU count).
+    host_dist (gloo rehearsal, ranks sharing a GPU): the same exchange over torch.distributed."""
+    from sift_dist import match_sharded_host, shard
+    try:
+        d1 = synth_descriptors(n, 5000)
+        d2 = synth_descriptors(n, 5001, base=d1, n_dup=min(20000, n // 2))
+        q1, q2 = quantize(d1), quantize(d2)
+        s, e = shard(n, rank, world)
+        def one():
+            if host_dist is None:
+                return ctx.match_sharded(q1[s:e], s, q2)
+            rows, cols = ctx.match_shard_begin(q1[s:e], s, q2)
+            return match_sharded_host(rows, cols, s, host_dist)
+
+        one()   # warm-up
+        reps, dev, wall, m = 5, 0.0, 0.0, None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            m = one()
+            wall += time.perf_counter() - t0
+            dev += ctx.timing()["match"]
+        v = [dev / reps, wall / reps * 1e3, float(len(m))]
+        if host_dist is None:
+            v[:2] = ctx.allreduce_f64(v[:2], op_max=True).tolist()
+            v[2] = float(ctx.allreduce_f64(v[2], op_max=False)[0])
+        else:
+            import torch
+            t = torch.tensor(v[:2], dtype=torch.float64)
+            host_dist.all_reduce(t, op=host_dist.ReduceOp.MAX)
+            c = torch.tensor([v[2]], dtype=torch.float64)
+            host_dist.all_reduce(c)
+            v = t.tolist() + c.tolist()
+        return {"workload": f"C5 {n}x{n}, set 1 sharded over {world} ranks, "
+                            f"{'RCCL' if host_dist is None else 'gloo'} all-gather of the column "
+                            f"states", "device_ms": v[0], "wall_ms": v[1], "matches": int(v[2])}
+    except Exception as ex:   # never costs the main measurement
+        return {"error": str(ex)}
 
 
 def cpu_baseline(imgs, opts):

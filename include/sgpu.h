@@ -154,6 +154,29 @@ int sgpu_match_guided(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
                       float distmax, float ratiomax, float hdistmax, float fdistmax,
                       int mutual_best_match, int max_match, int* out_pairs, int flags);
 
+/* Sharded matcher (multi-GPU extension of SiftMatchGPU::GetSiftMatch):
+ * this rank holds rows [row_begin, row_begin + ns) of set 1 (d1 = those rows) and all n2 rows
+ * of set 2.  The result over all ranks equals sgpu_match on the whole of set 1.
+ * sgpu_match_shard_begin: row_match[ns] = the row decision of each local row (matched set-2
+ * row or -1; RowMatch_Kernel, ProgramCU.cu:1785-1841) and, with mutual_best_match, col_best
+ * [n2][3] = this shard's clamped column state (max dot, global set-1 row, second dot) of
+ * ColMatch_Kernel (ProgramCU.cu:1844-1900).
+ * sgpu_match_shard_end (host only, no device): merges the nshards column states (rank order),
+ * applies the column decision and the mutual check (SiftMatchCU.cpp:166-176) and writes this
+ * shard's pairs {global i, j} in ascending i; returns their count.  Concatenated in rank order
+ * the shards' pairs are sgpu_match's (max_match applies per call).
+ * sgpu_match_sharded: both, with the exchange as an RCCL all-gather over the context's
+ * communicator (sgpu_comm_init; without one it is a single shard). */
+int sgpu_match_shard_begin(sgpu_ctx* ctx, const uint8_t* d1, int ns, int row_begin,
+                           const uint8_t* d2, int n2, float distmax, float ratiomax,
+                           int mutual_best_match, int* row_match, int* col_best, int flags);
+int sgpu_match_shard_end(const int* col_best_all, int nshards, int n2, const int* row_match,
+                         int ns, int row_begin, float distmax, float ratiomax,
+                         int mutual_best_match, int max_match, int* out_pairs);
+int sgpu_match_sharded(sgpu_ctx* ctx, const uint8_t* d1, int ns, int row_begin,
+                       const uint8_t* d2, int n2, float distmax, float ratiomax,
+                       int mutual_best_match, int max_match, int* out_pairs, int flags);
+
 /* float -> u8 quantization of SiftMatchCU::SetDescriptors (SiftMatchCU.cpp:94-99), host side. */
 void sgpu_quantize_descriptors(const float* d, size_t count, uint8_t* out);
 

@@ -855,6 +855,157 @@ int sgpu_match(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d2, int 
                       nullptr, nullptr, nullptr);
 }
 
+// ---- sharded matcher: rows of set 1 split over ranks, set 2 replicated ----
+// The row decision of a set-1 row needs only its own dots, so it stays local.  The column
+// decision of a set-2 row j needs the best / second-best over ALL set-1 rows: every rank
+// reduces its shard to the clamped running state (max, argmax, second) that
+// RowMatch_Kernel / ColMatch_Kernel keep (ProgramCU.cu:1803, 1850: running maxima start at 0
+// with index -1), the ranks exchange those n2 x 3 ints, and the merge -- max, the column
+// side's tie order (lowest set-1 row first), second = max(min of the maxima, seconds) -- gives
+// exactly the single-device state, because clamping at 0 commutes with max.
+
+// float(acos(min(v * 2^-18, 1.0))) -- the expression of RowMatch_Kernel (ProgramCU.cu:1838)
+// and of the device distance table
+static float match_dist(int v) {
+    v = std::min(std::max(v, 0), sgk::kDistTable - 1);
+    return (float)std::acos(std::min((double)(v * 0.000003814697265625f), 1.0));
+}
+
+int sgpu_match_shard_begin(sgpu_ctx* ctx, const uint8_t* d1, int ns, int row_begin,
+                           const uint8_t* d2, int n2, float distmax, float ratiomax, int mbm,
+                           int* row_match, int* col_best, int flags) {
+    if (!ctx) return SGPU_EINVAL;
+    if (ns < 0 || n2 < 0 || row_begin < 0 || (ns > 0 && (!d1 || !row_match)) ||
+        (n2 > 0 && !d2) || (mbm && n2 > 0 && !col_best))
+        return ctx->fail(SGPU_EINVAL, "bad shard-match arguments");
+    if (mbm)   // an empty shard contributes the initial state (0, -1, 0) to every column
+        for (int j = 0; j < n2; j++) {
+            col_best[3 * j] = 0;
+            col_best[3 * j + 1] = -1;
+            col_best[3 * j + 2] = 0;
+        }
+    if (ns == 0 || n2 == 0) {
+        for (int i = 0; i < ns; i++) row_match[i] = -1;
+        return SGPU_OK;
+    }
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    if (!ctx->dist_ready) {
+        std::vector<float> t(sgk::kDistTable);
+        for (int v = 0; v < sgk::kDistTable; v++) t[v] = match_dist(v);
+        ALLOCCHK(ctx, ctx->m_dist.ensure(t.size() * sizeof(float)));
+        HIPCHK(ctx, hipMemcpy(ctx->m_dist.p, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
+        ctx->dist_ready = true;
+    }
+    const uint8_t* a = d1;
+    const uint8_t* b = d2;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[0], st));
+    if (!(flags & SGPU_INPUT_DEVICE)) {
+        ALLOCCHK(ctx, ctx->m_d1.ensure((size_t)ns * 128));
+        ALLOCCHK(ctx, ctx->m_d2.ensure((size_t)n2 * 128));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->m_d1.p, d1, (size_t)ns * 128, hipMemcpyHostToDevice, st));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->m_d2.p, d2, (size_t)n2 * 128, hipMemcpyHostToDevice, st));
+        a = ctx->m_d1.as<uint8_t>();
+        b = ctx->m_d2.as<uint8_t>();
+    }
+    HIPCHK(ctx, hipEventRecord(ctx->ev[1], st));
+    const int ca = sgk::match_chunks(ns, n2), cb = mbm ? sgk::match_chunks(n2, ns) : 0;
+    const size_t part_n = std::max((size_t)ca * ns, (size_t)cb * n2);
+    ALLOCCHK(ctx, ctx->m_part.ensure(part_n * sizeof(sgk::Top2) + (size_t)n2 * sizeof(sgk::Top2)));
+    ALLOCCHK(ctx, ctx->m_terms.ensure((size_t)2 * (ns + n2) * sizeof(int)));
+    ALLOCCHK(ctx, ctx->m_match.ensure((size_t)(ns + n2) * sizeof(int)));
+    int* row1 = ctx->m_terms.as<int>();
+    int* col1 = row1 + ns;
+    int* row2 = col1 + ns;
+    int* col2 = row2 + n2;
+    int* match1 = ctx->m_match.as<int>();
+    int* match2 = match1 + ns;
+    sgk::Top2* part = ctx->m_part.as<sgk::Top2>();
+    sgk::Top2* best2 = part + part_n;
+    const float* dist = ctx->m_dist.as<float>();
+    HIPCHK(ctx, sgk::launch_rowsums(a, ns, row1, 128, 0, st));
+    HIPCHK(ctx, sgk::launch_rowsums(b, n2, col2, 128, -2097152, st));
+    HIPCHK(ctx, sgk::launch_match_rows(a, ns, b, n2, col2, ca, part, st, nullptr, true));
+    HIPCHK(ctx, sgk::launch_match_finish(part, ns, ca, row1, dist, distmax, ratiomax, match1,
+                                         nullptr, st, true));
+    if (mbm) {
+        HIPCHK(ctx, sgk::launch_rowsums(b, n2, row2, 128, 0, st));
+        HIPCHK(ctx, sgk::launch_rowsums(a, ns, col1, 128, -2097152, st));
+        HIPCHK(ctx, sgk::launch_match_rows(b, n2, a, ns, col1, cb, part, st, nullptr, false));
+        HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, row2, dist, distmax, ratiomax, match2,
+                                             best2, st, false));
+    }
+    HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
+    HIPCHK(ctx, hipMemcpyAsync(row_match, match1, (size_t)ns * sizeof(int), hipMemcpyDeviceToHost, st));
+    if (mbm) {
+        static_assert(sizeof(sgk::Top2) == 3 * sizeof(int), "Top2 = 3 ints");
+        HIPCHK(ctx, hipMemcpyAsync(col_best, best2, (size_t)n2 * sizeof(sgk::Top2),
+                                   hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    (void)hipEventElapsedTime(&ctx->timing[T_MATCH], ctx->ev[1], ctx->ev[2]);
+    if (mbm)   // Top2 is (max, idx, second); the shard's row index becomes the global one
+        for (int j = 0; j < n2; j++)
+            if (col_best[3 * j + 1] >= 0) col_best[3 * j + 1] += row_begin;
+    return SGPU_OK;
+}
+
+int sgpu_match_shard_end(const int* col_best_all, int nshards, int n2, const int* row_match,
+                         int ns, int row_begin, float distmax, float ratiomax, int mbm,
+                         int max_match, int* out_pairs) {
+    if (ns < 0 || n2 < 0 || (ns > 0 && !row_match) || (max_match > 0 && !out_pairs) ||
+        (mbm && (nshards < 1 || (n2 > 0 && !col_best_all))))
+        return SGPU_EINVAL;
+    std::vector<int> col_match;
+    if (mbm) {
+        col_match.assign((size_t)n2, -1);
+        for (int j = 0; j < n2; j++) {
+            // shards in rank order: rank r's rows precede rank r+1's (lowest row wins ties)
+            int m = col_best_all[3 * j], idx = col_best_all[3 * j + 1], sc = col_best_all[3 * j + 2];
+            for (int r = 1; r < nshards; r++) {
+                const int* u = col_best_all + ((size_t)r * n2 + j) * 3;
+                const bool later = u[0] > m || (u[0] == m && u[1] >= 0 && (idx < 0 || u[1] < idx));
+                sc = std::max(std::min(m, u[0]), std::max(sc, u[2]));
+                if (later) idx = u[1];
+                m = std::max(m, u[0]);
+            }
+            const float d1 = match_dist(m), d2 = match_dist(sc);
+            col_match[j] = (d1 < distmax) && (d1 < d2 * ratiomax) ? idx : -1;
+        }
+    }
+    int nmatch = 0;
+    for (int i = 0; i < ns && nmatch < max_match; ++i) {
+        const int j = row_match[i];
+        if (j >= 0 && j < n2 && (!mbm || col_match[j] == row_begin + i)) {
+            out_pairs[2 * nmatch] = row_begin + i;
+            out_pairs[2 * nmatch + 1] = j;
+            nmatch++;
+        }
+    }
+    return nmatch;
+}
+
+int sgpu_match_sharded(sgpu_ctx* ctx, const uint8_t* d1, int ns, int row_begin,
+                       const uint8_t* d2, int n2, float distmax, float ratiomax, int mbm,
+                       int max_match, int* out_pairs, int flags) {
+    if (!ctx) return SGPU_EINVAL;
+    const int ranks = ctx->comm ? ctx->comm_ranks : 1;
+    std::vector<int> rows((size_t)std::max(ns, 1)), mine((size_t)3 * std::max(n2, 1));
+    int rc = sgpu_match_shard_begin(ctx, d1, ns, row_begin, d2, n2, distmax, ratiomax, mbm,
+                                    rows.data(), mine.data(), flags);
+    if (rc != SGPU_OK) return rc;
+    std::vector<int> all;
+    if (mbm && ctx->comm && n2 > 0) {   // RCCL all-gather of the n2 x 3 column states
+        all.resize((size_t)3 * n2 * ranks);
+        rc = sgpu_comm_allgather_i32(ctx, mine.data(), 3 * n2, all.data());
+        if (rc != SGPU_OK) return rc;
+    } else {
+        all = mine;
+    }
+    return sgpu_match_shard_end(all.data(), ranks, n2, rows.data(), ns, row_begin, distmax,
+                                ratiomax, mbm, max_match, out_pairs);
+}
+
 // SiftMatchGPU::GetGuidedSiftMatch (SiftMatch.cpp:663-677 defaults, SiftMatchCU.cpp:126-136).
 int sgpu_match_guided(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d2, int n2,
                       const float* loc1, const float* loc2, const float* H, const float* F,

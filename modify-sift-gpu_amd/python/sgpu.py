@@ -27,6 +27,7 @@ C_API = [
     "sgpu_debug_geometry", "sgpu_debug_gaussian", "sgpu_debug_candidates",
     "sgpu_debug_set_variant", "sgpu_comm_unique_id", "sgpu_comm_init", "sgpu_comm_allgather_i32",
     "sgpu_comm_allreduce_f64", "sgpu_extract_keypoints", "sgpu_match_guided", "sgpu_extract_color",
+    "sgpu_match_shard_begin", "sgpu_match_shard_end", "sgpu_match_sharded",
 ]
 
 _LIB = None
@@ -76,8 +77,33 @@ def lib():
         L.sgpu_comm_init.argtypes = [vp, c.c_int, c.c_int, vp, c.c_int]
         L.sgpu_comm_allgather_i32.argtypes = [vp, vp, c.c_int, vp]
         L.sgpu_comm_allreduce_f64.argtypes = [vp, vp, c.c_int, c.c_int]
+        L.sgpu_match_shard_begin.argtypes = [vp, vp, c.c_int, c.c_int, vp, c.c_int, c.c_float,
+                                             c.c_float, c.c_int, vp, vp, c.c_int]
+        L.sgpu_match_shard_end.argtypes = [vp, c.c_int, c.c_int, vp, c.c_int, c.c_int, c.c_float,
+                                           c.c_float, c.c_int, c.c_int, vp]
+        L.sgpu_match_sharded.argtypes = [vp, vp, c.c_int, c.c_int, vp, c.c_int, c.c_float,
+                                         c.c_float, c.c_int, c.c_int, vp, c.c_int]
         _LIB = L
     return _LIB
+
+
+def match_shard_end(col_best_all: np.ndarray, row_match: np.ndarray, row_begin: int,
+                    distmax=0.7, ratiomax=0.8, mbm=1, max_match=None) -> np.ndarray:
+    """Host-side merge of the shards' column states ([nshards][n2][3] int32, rank order) plus
+    this shard's row decisions -> this shard's pairs {global i, j} (sgpu_match_shard_end; no
+    device involved)."""
+    cb = np.ascontiguousarray(col_best_all, np.int32)
+    if cb.ndim == 2:
+        cb = cb[None]
+    rm = np.ascontiguousarray(row_match, np.int32)
+    ns, n2 = len(rm), cb.shape[1]
+    max_match = ns if max_match is None else max_match
+    out = np.zeros((max(max_match, 1), 2), np.int32)
+    m = lib().sgpu_match_shard_end(cb.ctypes.data, cb.shape[0], n2, rm.ctypes.data, ns,
+                                   row_begin, distmax, ratiomax, mbm, max_match, out.ctypes.data)
+    if m < 0:
+        raise RuntimeError(f"sgpu_match_shard_end failed ({m})")
+    return out[:m].copy()
 
 
 def comm_unique_id() -> bytes:
@@ -216,6 +242,37 @@ class SiftContext:
         lib().sgpu_last_timing(self._ctx, t.ctypes.data, 9)
         return dict(zip(["upload", "pyramid", "detect", "orientation", "expand", "descriptor",
                          "download", "total", "match"], t.tolist()))
+
+    def match_shard_begin(self, d1_shard: np.ndarray, row_begin: int, d2: np.ndarray,
+                          distmax=0.7, ratiomax=0.8, mbm=1):
+        """Rows [row_begin, row_begin + len(d1_shard)) of set 1 against all of set 2
+        (sgpu_match_shard_begin): (row decisions [ns], column state [n2][3])."""
+        d1 = np.ascontiguousarray(d1_shard, np.uint8)
+        d2 = np.ascontiguousarray(d2, np.uint8)
+        ns, n2 = d1.shape[0], d2.shape[0]
+        rows = np.zeros(max(ns, 1), np.int32)
+        cols = np.zeros((max(n2, 1), 3), np.int32)
+        self._check(lib().sgpu_match_shard_begin(self._ctx, d1.ctypes.data, ns, row_begin,
+                                                 d2.ctypes.data, n2, distmax, ratiomax, mbm,
+                                                 rows.ctypes.data, cols.ctypes.data,
+                                                 SGPU_INPUT_HOST), "sgpu_match_shard_begin")
+        return rows[:ns].copy(), cols[:n2].copy()
+
+    def match_sharded(self, d1_shard: np.ndarray, row_begin: int, d2: np.ndarray,
+                      distmax=0.7, ratiomax=0.8, mbm=1, max_match=None):
+        """This rank's pairs of the sharded matcher; the column states travel by RCCL over the
+        context's communicator (comm_init), or stay local without one (sgpu_match_sharded)."""
+        d1 = np.ascontiguousarray(d1_shard, np.uint8)
+        d2 = np.ascontiguousarray(d2, np.uint8)
+        ns = d1.shape[0]
+        max_match = ns if max_match is None else max_match
+        out = np.zeros((max(max_match, 1), 2), np.int32)
+        m = lib().sgpu_match_sharded(self._ctx, d1.ctypes.data, ns, row_begin, d2.ctypes.data,
+                                     d2.shape[0], distmax, ratiomax, mbm, max_match,
+                                     out.ctypes.data, SGPU_INPUT_HOST)
+        if m < 0:
+            self._check(m, "sgpu_match_sharded")
+        return out[:m].copy()
 
     def match(self, d1: np.ndarray, d2: np.ndarray, distmax=0.7, ratiomax=0.8, mbm=1,
               max_match=None, device_ptrs=None):

@@ -43,3 +43,19 @@ def global_offsets(counts: np.ndarray) -> np.ndarray:
     off = np.zeros(len(counts) + 1, np.int64)
     np.cumsum(counts, out=off[1:])
     return off
+
+
+def match_sharded_host(row_match: np.ndarray, col_best: np.ndarray, row_begin: int, dist,
+                       distmax=0.7, ratiomax=0.8, mbm=1) -> np.ndarray:
+    """Sharded SiftMatch exchange over torch.distributed (gloo on the host): all-gather every
+    rank's column state ([n2][3] int32 from SiftContext.match_shard_begin) and finish this
+    rank's rows (sgpu_match_shard_end).  The RCCL form of the same exchange is
+    SiftContext.match_sharded."""
+    import torch
+    import sgpu
+    world = dist.get_world_size()
+    mine = torch.from_numpy(np.ascontiguousarray(col_best, np.int32).reshape(-1))
+    out = torch.zeros(mine.numel() * world, dtype=torch.int32)
+    dist.all_gather_into_tensor(out, mine)
+    allc = out.numpy().reshape(world, -1, 3)
+    return sgpu.match_shard_end(allc, row_match, row_begin, distmax, ratiomax, mbm)

@@ -685,3 +685,25 @@ def test_guided_api_replica(tmp_path):
     for got, (Hm, Fm) in zip(cases, ((H, F), (H, None), (None, F), (None, None))):
         want = O.match_guided(q1, q2, l1, l2, Hm, Fm)
         assert np.array_equal(np.array(got, np.int32).reshape(-1, 2), want)
+
+
+@pytest.mark.parametrize("bounds", [[0, 5000], [0, 1234, 1235, 3100, 5000], [0, 0, 2500, 5000]])
+def test_sharded_match_equals_full(gpu_ctx, bounds):
+    """Sharded matcher on the device: sgpu_match_shard_begin per shard, the
+    column states merged by sgpu_match_shard_end; the concatenated pairs equal sgpu_match and
+    the oracle, ties between rows of different shards included."""
+    d1 = synth_descriptors(5000, 7000)
+    d2 = synth_descriptors(4100, 7001, base=d1, n_dup=2000)
+    q1, q2 = quantize(d1), quantize(d2)
+    q1[4000] = q1[17]
+    q1[2600] = q1[1300]
+    full = gpu_ctx.match(q1, q2)
+    np.testing.assert_array_equal(full, O.match(q1, q2))
+    shards = list(zip(bounds[:-1], bounds[1:]))
+    begun = [gpu_ctx.match_shard_begin(q1[a:b], a, q2) for a, b in shards]
+    allc = np.stack([c for _, c in begun])
+    got = np.concatenate([sgpu.match_shard_end(allc, r, a) for (a, _), (r, _) in zip(shards, begun)])
+    np.testing.assert_array_equal(got, full)
+    # the convenience call: column states all-gathered by RCCL (one rank on this box)
+    gpu_ctx.comm_init(1, 0, sgpu.comm_unique_id())
+    np.testing.assert_array_equal(gpu_ctx.match_sharded(q1, 0, q2), full)

@@ -157,6 +157,52 @@ def test_matcher_oracle_vs_numpy(mbm):
     np.testing.assert_array_equal(got, want)
 
 
+def np_shard_state(q1s, row_begin, q2, distmax=0.7, ratiomax=0.8):
+    """What a rank computes for rows [row_begin, row_begin + len(q1s)) of set 1 (restated with
+    NumPy): its rows' decisions (RowMatch_Kernel, local) and, per set-2 row, the clamped column
+    state (max dot, global set-1 row, second dot) of ColMatch_Kernel over its rows."""
+    dot = q1s.astype(np.int64) @ q2.astype(np.int64).T          # [ns][n2]
+    rows = _np_top(dot, distmax, ratiomax, True)
+    colv = dot.T                                                  # [n2][ns]
+    state = np.zeros((q2.shape[0], 3), np.int32)
+    state[:, 1] = -1
+    if q1s.shape[0]:
+        arg = np.argmax(colv, axis=1)                             # first (lowest) row on ties
+        mx = colv[np.arange(colv.shape[0]), arg]
+        sec = np.sort(colv, axis=1)[:, -2] if q1s.shape[0] > 1 else np.zeros_like(mx)
+        pos = mx > 0
+        state[:, 0] = np.maximum(mx, 0)
+        state[:, 1] = np.where(pos, arg + row_begin, -1)
+        state[:, 2] = np.maximum(sec, 0)
+    return rows.astype(np.int32), state
+
+
+@pytest.mark.parametrize("bounds", [[0, 400], [0, 131, 132, 290, 400], [0, 0, 200, 400]])
+def test_sharded_match_merge_equals_full(bounds):
+    """SURVEY.md §8e sharded matcher: rows of set 1 split over ranks; every rank's local row
+    decisions plus the merged column states (sgpu_match_shard_end, host code of libsiftgpu)
+    give exactly the single-device pairs -- including exact ties between rows of different
+    shards (duplicated rows: equal maxima -> second == max -> rejected)."""
+    import sgpu
+    d1 = synth_descriptors(400, 5100)
+    d2 = synth_descriptors(350, 5101, base=d1, n_dup=150)
+    q1, q2 = quantize(d1), quantize(d2)
+    q1[300] = q1[20]            # the same row in two shards: a cross-shard tie for its column
+    q1[399] = q1[3]
+    full = O.match(q1, q2)
+    assert len(full) > 50
+    shards = list(zip(bounds[:-1], bounds[1:]))
+    states = [np_shard_state(q1[a:b], a, q2) for a, b in shards]
+    allc = np.stack([st for _, st in states])
+    got = np.concatenate([sgpu.match_shard_end(allc, rows, a) for (a, b), (rows, _) in
+                          zip(shards, states)])
+    np.testing.assert_array_equal(got, full)
+    # without the mutual check the column states are not needed
+    got0 = np.concatenate([sgpu.match_shard_end(allc, rows, a, mbm=0) for (a, b), (rows, _) in
+                           zip(shards, states)])
+    np.testing.assert_array_equal(got0, O.match(q1, q2, mbm=0))
+
+
 def test_matcher_ties_and_wrap():
     # duplicated rows create exact ties (second == max -> rejected); 512*d wraps past 255
     q1 = np.zeros((4, 128), np.uint8)
