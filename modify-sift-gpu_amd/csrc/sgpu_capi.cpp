@@ -804,10 +804,8 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     ALLOCCHK(ctx, ctx->m_part.ensure(part_n * sizeof(sgk::Top2)));
     ALLOCCHK(ctx, ctx->m_terms.ensure((size_t)2 * (n1 + n2) * sizeof(int)));
     ALLOCCHK(ctx, ctx->m_match.ensure((size_t)(n1 + n2) * sizeof(int)));
-    int* row1 = ctx->m_terms.as<int>();          // 128 * sum(d1)
-    int* col1 = row1 + n1;                       // 128 * sum(d1) - 2^21
-    int* row2 = col1 + n1;
-    int* col2 = row2 + n2;
+    int* row1 = ctx->m_terms.as<int>();          // row terms 128 * sum(d1), 128 * sum(d2); the
+    int* row2 = row1 + n1;                       // column terms are formed in k_match_rows
     int* match1 = ctx->m_match.as<int>();
     int* match2 = match1 + n1;
     sgk::Top2* part = ctx->m_part.as<sgk::Top2>();
@@ -816,14 +814,12 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     if (guided)
         HIPCHK(ctx, sgk::launch_guided_mask(l1, n1, l2, n2, *guided, rmask, cmask, st));
     HIPCHK(ctx, sgk::launch_rowsums(a, n1, row1, 128, 0, st));
-    HIPCHK(ctx, sgk::launch_rowsums(b, n2, col2, 128, -2097152, st));
-    HIPCHK(ctx, sgk::launch_match_rows(a, n1, b, n2, col2, ca, part, st, rmask, true));
+    HIPCHK(ctx, sgk::launch_match_rows(a, n1, b, n2, ca, part, st, rmask, true));
     HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, row1, ctx->m_dist.as<float>(), distmax,
                                          ratiomax, match1, nullptr, st, true));
     if (mbm) {
         HIPCHK(ctx, sgk::launch_rowsums(b, n2, row2, 128, 0, st));
-        HIPCHK(ctx, sgk::launch_rowsums(a, n1, col1, 128, -2097152, st));
-        HIPCHK(ctx, sgk::launch_match_rows(b, n2, a, n1, col1, cb, part, st, cmask, false));
+        HIPCHK(ctx, sgk::launch_match_rows(b, n2, a, n1, cb, part, st, cmask, false));
         HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, row2, ctx->m_dist.as<float>(), distmax,
                                              ratiomax, match2, nullptr, st, false));
     }
@@ -915,23 +911,19 @@ int sgpu_match_shard_begin(sgpu_ctx* ctx, const uint8_t* d1, int ns, int row_beg
     ALLOCCHK(ctx, ctx->m_terms.ensure((size_t)2 * (ns + n2) * sizeof(int)));
     ALLOCCHK(ctx, ctx->m_match.ensure((size_t)(ns + n2) * sizeof(int)));
     int* row1 = ctx->m_terms.as<int>();
-    int* col1 = row1 + ns;
-    int* row2 = col1 + ns;
-    int* col2 = row2 + n2;
+    int* row2 = row1 + ns;
     int* match1 = ctx->m_match.as<int>();
     int* match2 = match1 + ns;
     sgk::Top2* part = ctx->m_part.as<sgk::Top2>();
     sgk::Top2* best2 = part + part_n;
     const float* dist = ctx->m_dist.as<float>();
     HIPCHK(ctx, sgk::launch_rowsums(a, ns, row1, 128, 0, st));
-    HIPCHK(ctx, sgk::launch_rowsums(b, n2, col2, 128, -2097152, st));
-    HIPCHK(ctx, sgk::launch_match_rows(a, ns, b, n2, col2, ca, part, st, nullptr, true));
+    HIPCHK(ctx, sgk::launch_match_rows(a, ns, b, n2, ca, part, st, nullptr, true));
     HIPCHK(ctx, sgk::launch_match_finish(part, ns, ca, row1, dist, distmax, ratiomax, match1,
                                          nullptr, st, true));
     if (mbm) {
         HIPCHK(ctx, sgk::launch_rowsums(b, n2, row2, 128, 0, st));
-        HIPCHK(ctx, sgk::launch_rowsums(a, ns, col1, 128, -2097152, st));
-        HIPCHK(ctx, sgk::launch_match_rows(b, n2, a, ns, col1, cb, part, st, nullptr, false));
+        HIPCHK(ctx, sgk::launch_match_rows(b, n2, a, ns, cb, part, st, nullptr, false));
         HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, row2, dist, distmax, ratiomax, match2,
                                              best2, st, false));
     }

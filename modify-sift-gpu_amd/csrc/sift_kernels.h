@@ -152,12 +152,13 @@ struct Top2 { int max, idx, second; };
 // s[i] = scale * sum_k d[i][k] + bias
 hipError_t launch_rowsums(const uint8_t* d, int n, int* s, int scale, int bias, hipStream_t stream);
 int match_chunks(int nA, int nB);
-// part[chunk][nA]: per-row top-2 of (A_i . B_j + col_term[j]) over each column chunk.
+// part[chunk][nA]: per-row top-2 of (A_i . B_j + col_term[j]) over each column chunk, with
+// col_term[j] = 128 * sum(B_j) - 2^21 formed in the kernel from the staged bytes.
 // row_side: equal maxima resolve as RowMatch_Kernel does (A = set 1); else in column order.
 // With a mask (launch_guided_mask, this side's lane records): the guided values
 // (k_match_rows<true>).
 hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
-                             const int* col_term, int chunks, Top2* part, hipStream_t stream,
+                             int chunks, Top2* part, hipStream_t stream,
                              const uint8_t* mask, bool row_side);
 // Guided matching geometry (SiftMatchGPU::GetGuidedSiftMatch): H, F row-major 3x3.
 struct GuidedParams { float H[9]; float F[9]; float hdistmax, fdistmax; };

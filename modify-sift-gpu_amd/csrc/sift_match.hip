@@ -96,11 +96,11 @@ __device__ __forceinline__ v4i load16_s8(const uint8_t* p) {
 template <bool GUIDED, bool TIE32>
 __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ A, int nA,
                                                     const uint8_t* __restrict__ B, int nB,
-                                                    const int* __restrict__ col_term,
                                                     int cols_per_chunk, Top2* __restrict__ part,
                                                     const uint4* __restrict__ mask,
                                                     int mask_tiles) {
     __shared__ __attribute__((aligned(16))) uint8_t s_b[2][kTile * kLdsRow];
+    __shared__ int s_ct[2][kTile];   // column terms of the staged tile (from its bytes)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int panel = blockIdx.x, chunk = blockIdx.y;
     const int c_begin = chunk * cols_per_chunk;
@@ -140,13 +140,27 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         for (int q = 0; q < 4; q++)
             r[q] = col < c_end ? reinterpret_cast<const uint4*>(src)[q] : make_uint4(0, 0, 0, 0);
     };
-    auto stage_store = [&](int buf, const uint4* r) {
+    // The column term 128 * sum(B[col]) - 2^21 is formed here from the staged bytes (byte sums
+    // by v_dot4_u32_u8, the two half-columns joined by one shuffle) instead of being loaded from
+    // global memory per tile: those loads sat between the next tile's staging loads and the
+    // MFMAs, and waiting for them waited for the whole prefetch.
+    auto stage_store = [&](int buf, const uint4* r, int tbase) {
         uint8_t* dst = &s_b[buf][(tid >> 1) * kLdsRow + (tid & 1) * 64];
+        uint32_t sum = 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             uint4 v = r[q];
+            sum = __builtin_amdgcn_udot4(v.x, 0x01010101u, sum, false);
+            sum = __builtin_amdgcn_udot4(v.y, 0x01010101u, sum, false);
+            sum = __builtin_amdgcn_udot4(v.z, 0x01010101u, sum, false);
+            sum = __builtin_amdgcn_udot4(v.w, 0x01010101u, sum, false);
             v.x ^= 0x80808080u; v.y ^= 0x80808080u; v.z ^= 0x80808080u; v.w ^= 0x80808080u;
             reinterpret_cast<uint4*>(dst)[q] = v;
+        }
+        sum += __shfl_xor(sum, 1, 64);
+        if (!(tid & 1)) {
+            const int col = tbase + (tid >> 1);
+            s_ct[buf][tid >> 1] = col < c_end ? 128 * (int)sum - 2097152 : kNegCol;
         }
     };
 
@@ -163,7 +177,7 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
     int buf = 0;
     if (c_begin < c_end) {
         stage_load(c_begin, stg);
-        stage_store(0, stg);
+        stage_store(0, stg, c_begin);
     }
     __syncthreads();
     for (int tb = c_begin; tb < c_end; tb += kTile) {
@@ -175,8 +189,7 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         v4i acc[2][8];
 #pragma unroll
         for (int cb = 0; cb < 8; cb++) {
-            const int col = tb + cb * 16 + l16;
-            const int ct = col < c_end ? col_term[col] : kNegCol;
+            const int ct = s_ct[buf][cb * 16 + l16];
             if constexpr (!GUIDED) {
                 acc[0][cb] = v4i{ct, ct, ct, ct};
                 acc[1][cb] = acc[0][cb];
@@ -228,7 +241,7 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         __syncthreads();
         if (has_next) {
             buf ^= 1;
-            stage_store(buf, stg);
+            stage_store(buf, stg, tb + kTile);
         }
         rec = rec_next;
         __syncthreads();
@@ -468,15 +481,16 @@ hipError_t launch_rowsums(const uint8_t* d, int n, int* out, int scale, int bias
 }
 
 int match_chunks(int nA, int nB) {
-    // enough workgroups to fill 256 CUs ~4 deep; each chunk at least two tiles wide
+    // ~4096 workgroups (about 5 per resident slot at 3 per CU) so that the last wave of
+    // workgroups is a small tail; each chunk at least two tiles wide
     const int panels = (nA + kPanel - 1) / kPanel;
-    int chunks = (1024 + panels - 1) / panels;
+    int chunks = (4096 + panels - 1) / panels;
     const int max_chunks = max(1, (nB + 2 * kTile - 1) / (2 * kTile));
     return max(1, min(chunks, max_chunks));
 }
 
 hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
-                             const int* col_term, int chunks, Top2* part, hipStream_t stream,
+                             int chunks, Top2* part, hipStream_t stream,
                              const uint8_t* mask, bool row_side) {
     if (nA <= 0 || nB <= 0) return hipSuccess;
     int per = (nB + chunks - 1) / chunks;
@@ -486,16 +500,16 @@ hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
     const uint4* rec = reinterpret_cast<const uint4*>(mask);
     if (!mask && row_side)
         hipLaunchKernelGGL((k_match_rows<false, true>), grid, dim3(256), 0, stream, A, nA, B, nB,
-                           col_term, per, part, rec, tiles);
+                           per, part, rec, tiles);
     else if (!mask)
         hipLaunchKernelGGL((k_match_rows<false, false>), grid, dim3(256), 0, stream, A, nA, B,
-                           nB, col_term, per, part, rec, tiles);
+                           nB, per, part, rec, tiles);
     else if (row_side)
         hipLaunchKernelGGL((k_match_rows<true, true>), grid, dim3(256), 0, stream, A, nA, B, nB,
-                           col_term, per, part, rec, tiles);
+                           per, part, rec, tiles);
     else
         hipLaunchKernelGGL((k_match_rows<true, false>), grid, dim3(256), 0, stream, A, nA, B, nB,
-                           col_term, per, part, rec, tiles);
+                           per, part, rec, tiles);
     return hipGetLastError();
 }
 

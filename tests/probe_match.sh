@@ -1,0 +1,5 @@
+# Matcher check on the GPU box: parity tests, then the C5 timing probe.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "match" > gpurun_out/t_match.log 2>&1; rc=$?; tail -2 gpurun_out/t_match.log
+[ $rc -eq 0 ] && timeout -k 10 200 python tests/match_probe.py > gpurun_out/match_probe.log 2>&1; cat gpurun_out/match_probe.log
