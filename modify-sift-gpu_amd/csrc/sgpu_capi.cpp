@@ -106,7 +106,7 @@ struct sgpu_ctx {
     hipEvent_t ev[T_N + 1] = {};
     float timing[T_N] = {};
     // matcher
-    DevBuf m_d1, m_d2, m_part, m_terms, m_match, m_dist, m_mask, m_loc;
+    DevBuf m_d1, m_d2, m_s1, m_s2, m_part, m_terms, m_match, m_dist, m_mask, m_loc;
     std::vector<int> h_match;
     bool dist_ready = false;
     // multi-GPU: RCCL communicator of this context's device (sgpu_comm_*)
@@ -296,7 +296,7 @@ int sgpu_ctx_destroy(sgpu_ctx* ctx) {
     }
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     ctx->comm = nullptr;
-    DevBuf* bufs[] = {&ctx->input, &ctx->all_keys, &ctx->all_desc, &ctx->gray, &ctx->m_d1, &ctx->m_d2,
+    DevBuf* bufs[] = {&ctx->input, &ctx->all_keys, &ctx->all_desc, &ctx->gray, &ctx->m_d1, &ctx->m_d2, &ctx->m_s1, &ctx->m_s2,
                       &ctx->m_part, &ctx->m_terms, &ctx->m_match, &ctx->m_dist, &ctx->m_mask, &ctx->m_loc,
                       &ctx->c_buf};
     for (DevBuf* b : bufs) b->release();
@@ -813,13 +813,20 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     uint8_t* cmask = guided && mbm ? rmask + rmask_bytes : nullptr;
     if (guided)
         HIPCHK(ctx, sgk::launch_guided_mask(l1, n1, l2, n2, *guided, rmask, cmask, st));
+    // s8 forms of both sets: the operands of the i8 MFMA
+    ALLOCCHK(ctx, ctx->m_s1.ensure((size_t)n1 * 128));
+    ALLOCCHK(ctx, ctx->m_s2.ensure((size_t)n2 * 128));
+    const uint8_t* s1 = ctx->m_s1.as<uint8_t>();
+    const uint8_t* s2 = ctx->m_s2.as<uint8_t>();
+    HIPCHK(ctx, sgk::launch_to_s8(a, n1, ctx->m_s1.as<uint8_t>(), st));
+    HIPCHK(ctx, sgk::launch_to_s8(b, n2, ctx->m_s2.as<uint8_t>(), st));
     HIPCHK(ctx, sgk::launch_rowsums(a, n1, row1, 128, 0, st));
-    HIPCHK(ctx, sgk::launch_match_rows(a, n1, b, n2, ca, part, st, rmask, true));
+    HIPCHK(ctx, sgk::launch_match_rows(s1, n1, s2, n2, ca, part, st, rmask, true));
     HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, row1, ctx->m_dist.as<float>(), distmax,
                                          ratiomax, match1, nullptr, st, true));
     if (mbm) {
         HIPCHK(ctx, sgk::launch_rowsums(b, n2, row2, 128, 0, st));
-        HIPCHK(ctx, sgk::launch_match_rows(b, n2, a, n1, cb, part, st, cmask, false));
+        HIPCHK(ctx, sgk::launch_match_rows(s2, n2, s1, n1, cb, part, st, cmask, false));
         HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, row2, ctx->m_dist.as<float>(), distmax,
                                              ratiomax, match2, nullptr, st, false));
     }
@@ -917,13 +924,19 @@ int sgpu_match_shard_begin(sgpu_ctx* ctx, const uint8_t* d1, int ns, int row_beg
     sgk::Top2* part = ctx->m_part.as<sgk::Top2>();
     sgk::Top2* best2 = part + part_n;
     const float* dist = ctx->m_dist.as<float>();
+    ALLOCCHK(ctx, ctx->m_s1.ensure((size_t)ns * 128));
+    ALLOCCHK(ctx, ctx->m_s2.ensure((size_t)n2 * 128));
+    const uint8_t* s1 = ctx->m_s1.as<uint8_t>();
+    const uint8_t* s2 = ctx->m_s2.as<uint8_t>();
+    HIPCHK(ctx, sgk::launch_to_s8(a, ns, ctx->m_s1.as<uint8_t>(), st));
+    HIPCHK(ctx, sgk::launch_to_s8(b, n2, ctx->m_s2.as<uint8_t>(), st));
     HIPCHK(ctx, sgk::launch_rowsums(a, ns, row1, 128, 0, st));
-    HIPCHK(ctx, sgk::launch_match_rows(a, ns, b, n2, ca, part, st, nullptr, true));
+    HIPCHK(ctx, sgk::launch_match_rows(s1, ns, s2, n2, ca, part, st, nullptr, true));
     HIPCHK(ctx, sgk::launch_match_finish(part, ns, ca, row1, dist, distmax, ratiomax, match1,
                                          nullptr, st, true));
     if (mbm) {
         HIPCHK(ctx, sgk::launch_rowsums(b, n2, row2, 128, 0, st));
-        HIPCHK(ctx, sgk::launch_match_rows(b, n2, a, ns, cb, part, st, nullptr, false));
+        HIPCHK(ctx, sgk::launch_match_rows(s2, n2, s1, ns, cb, part, st, nullptr, false));
         HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, row2, dist, distmax, ratiomax, match2,
                                              best2, st, false));
     }

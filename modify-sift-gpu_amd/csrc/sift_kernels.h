@@ -149,11 +149,14 @@ hipError_t launch_debug_candidates(const float* pyr, const uint32_t* mask,
 // host with the same expression as the oracle and uploaded once.
 constexpr int kDistTable = 262145;
 struct Top2 { int max, idx, second; };
+// dst = src xor 0x80 (u8 -> s8 descriptors, the operands of the i8 MFMA), n descriptors
+hipError_t launch_to_s8(const uint8_t* src, int n, uint8_t* dst, hipStream_t stream);
 // s[i] = scale * sum_k d[i][k] + bias
 hipError_t launch_rowsums(const uint8_t* d, int n, int* s, int scale, int bias, hipStream_t stream);
 int match_chunks(int nA, int nB);
 // part[chunk][nA]: per-row top-2 of (A_i . B_j + col_term[j]) over each column chunk, with
-// col_term[j] = 128 * sum(B_j) - 2^21 formed in the kernel from the staged bytes.
+// col_term[j] = 128 * sum(B_j) - 2^21 formed in the kernel from the staged bytes.  A and B are
+// the s8 forms of the descriptor sets (launch_to_s8).
 // row_side: equal maxima resolve as RowMatch_Kernel does (A = set 1); else in column order.
 // With a mask (launch_guided_mask, this side's lane records): the guided values
 // (k_match_rows<true>).

@@ -14,6 +14,8 @@
 // 2^21, all in int32.  The column term is the accumulator's initial value, the row term is added
 // once per row at the end (it does not change a row's ordering).  Results equal the reference's
 // integer dot products exactly.
+#include <algorithm>
+
 #include "sift_kernels.h"
 
 namespace sgk {
@@ -52,6 +54,16 @@ __global__ __launch_bounds__(256) void k_rowsum(const uint8_t* __restrict__ d, i
     if (lane == 0) s[i] = scale * t + bias;
 }
 
+// u8 descriptors -> s8 (s = u - 128, xor 0x80), once per match call for both sets
+__global__ __launch_bounds__(256) void k_to_s8(const uint4* __restrict__ src, size_t n16,
+                                               uint4* __restrict__ dst) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) {
+        uint4 v = src[i];
+        v.x ^= 0x80808080u; v.y ^= 0x80808080u; v.z ^= 0x80808080u; v.w ^= 0x80808080u;
+        dst[i] = v;
+    }
+}
+
 // Equal-dot order of the two decisions: does column a come before column b (-1 = none)?
 template <bool TIE32>
 __device__ __forceinline__ bool tie_before(int a, int b) {
@@ -59,16 +71,6 @@ __device__ __forceinline__ bool tie_before(int a, int b) {
     if (b < 0) return true;
     if (TIE32 && (a & 31) != (b & 31)) return (a & 31) < (b & 31);
     return a < b;
-}
-
-__device__ __forceinline__ v4i load16_s8(const uint8_t* p) {
-    const uint4 u = *reinterpret_cast<const uint4*>(p);
-    v4i r;
-    r[0] = (int)(u.x ^ 0x80808080u);
-    r[1] = (int)(u.y ^ 0x80808080u);
-    r[2] = (int)(u.z ^ 0x80808080u);
-    r[3] = (int)(u.w ^ 0x80808080u);
-    return r;
 }
 
 // One row panel of A against columns [c_begin, c_end) of B.
@@ -114,7 +116,7 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         const int row = panel * kPanel + wave * 32 + rb * 16 + l16;
 #pragma unroll
         for (int kh = 0; kh < 2; kh++) {
-            if (row < nA) afrag[rb][kh] = load16_s8(A + (size_t)row * 128 + kh * 64 + quad * 16);
+            if (row < nA) afrag[rb][kh] = *reinterpret_cast<const v4i*>(A + (size_t)row * 128 + kh * 64 + quad * 16);
             else afrag[rb][kh] = v4i{0, 0, 0, 0};
         }
     }
@@ -140,27 +142,27 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         for (int q = 0; q < 4; q++)
             r[q] = col < c_end ? reinterpret_cast<const uint4*>(src)[q] : make_uint4(0, 0, 0, 0);
     };
-    // The column term 128 * sum(B[col]) - 2^21 is formed here from the staged bytes (byte sums
-    // by v_dot4_u32_u8, the two half-columns joined by one shuffle) instead of being loaded from
-    // global memory per tile: those loads sat between the next tile's staging loads and the
-    // MFMAs, and waiting for them waited for the whole prefetch.
+    // The column term 128 * sum(u8 B[col]) - 2^21 is formed here from the staged s8 bytes
+    // (sum(u) = sum(s) + 128 * 128; byte sums by v_dot4_i32_i8, the two half-columns joined by
+    // one shuffle) instead of being loaded from global memory per tile: those loads sat between
+    // the next tile's staging loads and the MFMAs, and waiting for them waited for the whole
+    // prefetch.
     auto stage_store = [&](int buf, const uint4* r, int tbase) {
         uint8_t* dst = &s_b[buf][(tid >> 1) * kLdsRow + (tid & 1) * 64];
-        uint32_t sum = 0;
+        int sum = 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            uint4 v = r[q];
-            sum = __builtin_amdgcn_udot4(v.x, 0x01010101u, sum, false);
-            sum = __builtin_amdgcn_udot4(v.y, 0x01010101u, sum, false);
-            sum = __builtin_amdgcn_udot4(v.z, 0x01010101u, sum, false);
-            sum = __builtin_amdgcn_udot4(v.w, 0x01010101u, sum, false);
-            v.x ^= 0x80808080u; v.y ^= 0x80808080u; v.z ^= 0x80808080u; v.w ^= 0x80808080u;
+            const uint4 v = r[q];
+            sum = __builtin_amdgcn_sdot4((int)v.x, 0x01010101, sum, false);
+            sum = __builtin_amdgcn_sdot4((int)v.y, 0x01010101, sum, false);
+            sum = __builtin_amdgcn_sdot4((int)v.z, 0x01010101, sum, false);
+            sum = __builtin_amdgcn_sdot4((int)v.w, 0x01010101, sum, false);
             reinterpret_cast<uint4*>(dst)[q] = v;
         }
         sum += __shfl_xor(sum, 1, 64);
         if (!(tid & 1)) {
             const int col = tbase + (tid >> 1);
-            s_ct[buf][tid >> 1] = col < c_end ? 128 * (int)sum - 2097152 : kNegCol;
+            s_ct[buf][tid >> 1] = col < c_end ? 128 * (sum + 16384) - 2097152 : kNegCol;
         }
     };
 
@@ -185,15 +187,20 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         if (has_next) stage_load(tb + kTile, stg);
         uint4 rec_next = rec;
         if (rec_ok && has_next) rec_next = rec_p[(tb / kTile + 1) * 64];
-        // accumulators start at the column term (invalid columns: -inf)
+        // plain: the accumulators start at 0 and the column term enters the key,
+        // key = (acc << 7) + ((ct << 7) | low) = ((acc + ct) << 7) | low;
+        // guided: they start at the column term minus the geometric bias (invalid columns: -inf)
         v4i acc[2][8];
+        int ctlow[8];
 #pragma unroll
         for (int cb = 0; cb < 8; cb++) {
             const int ct = s_ct[buf][cb * 16 + l16];
             if constexpr (!GUIDED) {
-                acc[0][cb] = v4i{ct, ct, ct, ct};
+                ctlow[cb] = (ct << 7) | low[cb];
+                acc[0][cb] = v4i{0, 0, 0, 0};
                 acc[1][cb] = acc[0][cb];
             } else {
+                ctlow[cb] = low[cb];
 #pragma unroll
                 for (int rb = 0; rb < 2; rb++) {
                     const uint32_t w = rb == 0 ? (cb < 4 ? rec.x : rec.y) : (cb < 4 ? rec.z : rec.w);
@@ -228,7 +235,7 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
                 int m = m0, sv = S[rb][i];
 #pragma unroll
                 for (int cb = 0; cb < 8; cb++) {
-                    const int key = (acc[rb][cb][i] << 7) | low[cb];
+                    const int key = (acc[rb][cb][i] << 7) + ctlow[cb];
                     sv = med3i(sv, m, key);
                     m = max(m, key);
                 }
@@ -470,6 +477,15 @@ hipError_t launch_guided_mask(const float* loc1, int n1, const float* loc2, int 
                        reinterpret_cast<const float2*>(loc1), n1,
                        reinterpret_cast<const float2*>(loc2), n2, gp,
                        reinterpret_cast<uint4*>(rec1), t2, reinterpret_cast<uint4*>(rec2), t1);
+    return hipGetLastError();
+}
+
+hipError_t launch_to_s8(const uint8_t* src, int n, uint8_t* dst, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    const size_t n16 = (size_t)n * 8;   // 128 bytes = 8 uint4 per descriptor
+    const unsigned grid = (unsigned)std::min<size_t>((n16 + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_to_s8, dim3(grid), dim3(256), 0, stream,
+                       reinterpret_cast<const uint4*>(src), n16, reinterpret_cast<uint4*>(dst));
     return hipGetLastError();
 }
 
