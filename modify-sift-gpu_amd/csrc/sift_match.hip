@@ -227,23 +227,36 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         // (acc << 7) | low[cb]: one v_lshl_or, one v_max and one v_med3 per value; the tile is
         // recorded once per tile when the maximum moved.  The second key of an equal pair
         // carries the same dot, so exact ties still reach the ratio test as the reference's do.
+        // Column blocks 0..3 of every row first (their MFMAs finished earliest), then 4..7:
+        // each row still folds its keys in column order, and the first half's reads do not
+        // wait on the last MFMAs.
+        int mt[2][4], st[2][4];
+#pragma unroll
+        for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) { mt[rb][i] = M[rb][i]; st[rb][i] = S[rb][i]; }
+#pragma unroll
+        for (int half = 0; half < 2; half++)
+#pragma unroll
+            for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int cb = 4 * half; cb < 4 * half + 4; cb++) {
+                        const int key = (acc[rb][cb][i] << 7) + ctlow[cb];
+                        st[rb][i] = med3i(st[rb][i], mt[rb][i], key);
+                        mt[rb][i] = max(mt[rb][i], key);
+                    }
 #pragma unroll
         for (int rb = 0; rb < 2; rb++)
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const int m0 = M[rb][i];
-                int m = m0, sv = S[rb][i];
-#pragma unroll
-                for (int cb = 0; cb < 8; cb++) {
-                    const int key = (acc[rb][cb][i] << 7) + ctlow[cb];
-                    sv = med3i(sv, m, key);
-                    m = max(m, key);
-                }
-                const bool took = (uint32_t)(m ^ m0) >= kPrefix;
+                const int m = mt[rb][i];
+                const bool took = (uint32_t)(m ^ M[rb][i]) >= kPrefix;
                 I[rb][i] = took ? tb : I[rb][i];
                 W[rb][i] = took ? m : W[rb][i];
                 M[rb][i] = m;
-                S[rb][i] = sv;
+                S[rb][i] = st[rb][i];
             }
         __syncthreads();
         if (has_next) {
