@@ -447,39 +447,84 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
             if (e != hipErrorNotSupported) HIPCHK(ctx, e);
             (void)hipGetLastError();   // unsupported input layout: per-level path below
         }
-        if (o == 0) {
-            int fw = sgp::make_filter(S.initial_smooth, O.filter_width_factor, taps.k);
-            if (O.octave_min == 0) {
-                HIPCHK(ctx, sgk::launch_gauss(srcf, src8, stride, (long long)img_elems, lvl0, npx,
-                                              od.wa, od.h, fw, taps, n, nullptr, 0, 0, 0, st));
-            } else {
-                // -fo != 0: resample the input into level 1's storage (free until level 1 is
-                // filtered), then the initial smoothing as for a float input
-                float* tmp = lvl0 + od.level_stride;
-                HIPCHK(ctx, sgk::launch_first_octave_input(srcf, src8, stride, (long long)img_elems,
-                                                           ctx->w & ~3, h, O.octave_min, tmp,
-                                                           od.wa, od.h, npx, n, st));
-                HIPCHK(ctx, sgk::launch_gauss(tmp, nullptr, od.wa, npx, lvl0, npx, od.wa, od.h,
-                                              fw, taps, n, nullptr, 0, 0, 0, st));
-            }
+        // Filter ops of this octave: op 0 (octave 0 only) smooths the input into level 0, op k
+        // filters level k-1 into level k.  One launch per op (k_gauss_pk2) is the shipped path;
+        // variant 1024 (test hook) runs consecutive ops as one two-level launch instead
+        // (k_gauss_pair: level k-1 read once, levels k and k+1 written), bit-identical.
+        const int kds = S.level_ds - S.level_min;   // level d feeds the next octave (PyramidCU.cpp:1024)
+        float* ds = nullptr;
+        int dsw = 0, dsh = 0;
+        long long ds_stride = 0;
+        if (o + 1 < noct) {
+            const sgk::OctaveDesc& nd = fp.oct[o + 1];
+            ds = pyr + nd.gauss_off;
+            dsw = nd.wa;
+            dsh = nd.h;
+            ds_stride = (long long)nd.wa * nd.h;
         }
-        for (int k = 1; k < nlev; k++) {
-            int fw = sgp::make_filter(S.sigma[k - 1], O.filter_width_factor, taps.k);
-            float* ds = nullptr;
-            int dsw = 0, dsh = 0;
-            long long ds_stride = 0;
-            // level_ds - level_min (= d) feeds the next octave (PyramidCU.cpp:1024)
-            if (k == S.level_ds - S.level_min && o + 1 < noct) {
-                const sgk::OctaveDesc& nd = fp.oct[o + 1];
-                ds = pyr + nd.gauss_off;
-                dsw = nd.wa;
-                dsh = nd.h;
-                ds_stride = (long long)nd.wa * nd.h;
+        const float* in_f = srcf;                   // op 0 source
+        const uint8_t* in_8 = src8;
+        int in_stride = stride;
+        long long in_img = (long long)img_elems;
+        if (o == 0 && O.octave_min != 0) {
+            // -fo != 0: resample the input into level 1's storage (free until level 1 is
+            // filtered), then the initial smoothing as for a float input
+            float* tmp = lvl0 + od.level_stride;
+            HIPCHK(ctx, sgk::launch_first_octave_input(srcf, src8, stride, (long long)img_elems,
+                                                       ctx->w & ~3, h, O.octave_min, tmp,
+                                                       od.wa, od.h, npx, n, st));
+            in_f = tmp;
+            in_8 = nullptr;
+            in_stride = od.wa;
+            in_img = npx;
+        }
+        const bool pairs = (sgk::get_variant() & 1024) != 0;
+        for (int k = (o == 0 ? 0 : 1); k < nlev;) {
+            const int fwk = k == 0 ? fw0 : lfw[k];
+            const float* tk = k == 0 ? taps0.k : ltaps[k].k;
+            const float* sk_f = k == 0 ? in_f : lvl0 + (k - 1) * od.level_stride;
+            const uint8_t* sk_8 = k == 0 ? in_8 : nullptr;
+            const int sk_stride = k == 0 ? in_stride : od.wa;
+            const long long sk_img = k == 0 ? in_img : npx;
+            if (pairs && k + 1 < nlev && sgk::gauss_pair_supported(fwk, lfw[k + 1])) {
+                sgk::GaussPairLaunch L{};
+                L.src = sk_f;
+                L.src8 = sk_8;
+                L.src_stride = sk_stride;
+                L.src_img_stride = sk_img;
+                L.dst1 = lvl0 + k * od.level_stride;
+                L.dst2 = lvl0 + (k + 1) * od.level_stride;
+                L.dst_img_stride = npx;
+                L.w = od.wa;
+                L.h = od.h;
+                L.batch = n;
+                L.fw1 = fwk;
+                L.fw2 = lfw[k + 1];
+                L.taps1 = tk;
+                L.taps2 = ltaps[k + 1].k;
+                if (ds && (kds == k || kds == k + 1)) {
+                    L.ds = ds;
+                    L.ds_level = kds == k ? 1 : 2;
+                    L.dsw = dsw;
+                    L.dsh = dsh;
+                    L.ds_img_stride = ds_stride;
+                }
+                const hipError_t e = sgk::launch_gauss_pair(L, st);
+                if (e == hipSuccess) {
+                    if (o == 0 && L.ds) HIPCHK(ctx, hipEventRecord(pt.ev[7], st));
+                    k += 2;
+                    continue;
+                }
+                if (e != hipErrorNotSupported) HIPCHK(ctx, e);
+                (void)hipGetLastError();   // unaligned source or asymmetric taps: single levels
             }
-            HIPCHK(ctx, sgk::launch_gauss(lvl0 + (k - 1) * od.level_stride, nullptr, od.wa, npx,
-                                          lvl0 + k * od.level_stride, npx, od.wa, od.h, fw, taps,
-                                          n, ds, dsw, dsh, ds_stride, st));
-            if (o == 0 && ds) HIPCHK(ctx, hipEventRecord(pt.ev[7], st));
+            for (int i = 0; i < fwk; i++) taps.k[i] = tk[i];
+            const bool dk = ds && kds == k;
+            HIPCHK(ctx, sgk::launch_gauss(sk_f, sk_8, sk_stride, sk_img, lvl0 + k * od.level_stride,
+                                          npx, od.wa, od.h, fwk, taps, n, dk ? ds : nullptr,
+                                          dk ? dsw : 0, dk ? dsh : 0, dk ? ds_stride : 0, st));
+            if (o == 0 && dk) HIPCHK(ctx, hipEventRecord(pt.ev[7], st));
+            k += 1;
         }
     }
     st = pt.stream;

@@ -75,6 +75,33 @@ struct OctaveLaunch {
 bool octave_fused_supported(int nlev, const int* fw, int level_ds);
 hipError_t launch_octave(const OctaveLaunch& L, hipStream_t stream);
 
+// Two consecutive levels in one launch (sift_gauss_pair.hip): dst1 = V1(H1(src)),
+// dst2 = V2(H2(dst1)), both with the reference's clamp-to-edge semantics and bit-identical to two
+// launch_gauss calls.  src8 != nullptr selects the u8 ingest (value p/255).  ds != nullptr also
+// writes the 2x point-downsample of level ds_level (1 = dst1, 2 = dst2).  dst1 / dst2 / ds are
+// w x h (dsw x dsh) per image, dst_img_stride (ds_img_stride) apart.  Returns
+// hipErrorNotSupported for filter-width pairs without an instance or unaligned sources; the
+// caller then runs two launch_gauss calls.
+struct GaussPairLaunch {
+    const float* src;
+    const uint8_t* src8;
+    int src_stride;
+    long long src_img_stride;
+    float* dst1;
+    float* dst2;
+    long long dst_img_stride;
+    int w, h, batch;
+    int fw1, fw2;
+    const float* taps1;
+    const float* taps2;
+    float* ds;
+    int ds_level;
+    int dsw, dsh;
+    long long ds_img_stride;
+};
+bool gauss_pair_supported(int fw1, int fw2);
+hipError_t launch_gauss_pair(const GaussPairLaunch& L, hipStream_t stream);
+
 // First octave of -fo != 0 (BuildPyramid, PyramidCU.cpp:1011-1016): the batch's input
 // (u8 p/255 or f32; tw = w & ~3 columns used, rows `stride` apart) resampled into dst
 // (dw x dh per image, dst_img_stride apart): SampleImageD by 2^fo for fo > 0, UpsampleKernel

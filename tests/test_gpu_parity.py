@@ -109,6 +109,40 @@ def test_fused_octave_matches_per_level(gpu_ctx, w, h, n):
     assert np.array_equal(_bits(k), _bits(rk)) and np.array_equal(_bits(d), _bits(rd))
 
 
+@pytest.mark.parametrize("w,h,n,f32", [(16, 16, 1, False), (68, 40, 1, False),
+                                       (256, 97, 1, False), (1000, 300, 3, False),
+                                       (96, 1500, 1, False), (484, 250, 2, True),
+                                       (1920, 1080, 2, False), (203, 97, 1, True),
+                                       (130, 4000, 1, False)])
+def test_level_pairs_match_per_level(gpu_ctx, w, h, n, f32):
+    """The two-levels-per-launch pyramid (sift_gauss_pair.hip, variant 1024) against the shipped
+    one launch per level, bit for bit, on every level of every octave: strips clamped on both
+    sides (w <= 64 + halo), row bands (tall images, batch 1) where the middle level's clamped
+    rows sit inside a band boundary, odd heights, ragged last strips, f32 input, and u8 rows
+    whose stride is not a multiple of 4 (octave 0 then falls back to single levels)."""
+    imgs = np.stack([synth_image(w, h, 60 + i) for i in range(n)])
+    if f32:
+        imgs = imgs.astype(np.float32) / np.float32(255.0)
+    gpu_ctx.set_options(default_options())
+    gpu_ctx.extract(imgs)
+    geo = gpu_ctx.geometry()
+    single = [[gpu_ctx.gaussian(i, o, l) for o in range(len(geo)) for l in range(6)]
+              for i in range(n)]
+    rk, rd = gpu_ctx.features(n - 1)
+    try:
+        sgpu.lib().sgpu_debug_set_variant(1024)
+        gpu_ctx.extract(imgs)
+        pair = [[gpu_ctx.gaussian(i, o, l) for o in range(len(geo)) for l in range(6)]
+                for i in range(n)]
+        k, d = gpu_ctx.features(n - 1)
+    finally:
+        sgpu.lib().sgpu_debug_set_variant(0)
+    for i in range(n):
+        for q, (g, r) in enumerate(zip(pair[i], single[i])):
+            assert np.array_equal(_bits(g), _bits(r)), (i, divmod(q, 6))
+    assert np.array_equal(_bits(k), _bits(rk)) and np.array_equal(_bits(d), _bits(rd))
+
+
 @pytest.mark.parametrize("fo,w,h", [(1, 203, 97), (-1, 203, 97), (-1, 96, 64), (2, 321, 241)])
 def test_first_octave_levels_bitwise(gpu_ctx, fo, w, h):
     """-fo != 0: the resampled first octave (SampleImageD / UpsampleKernel) and its levels."""
