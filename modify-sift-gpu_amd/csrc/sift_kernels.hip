@@ -701,8 +701,18 @@ hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
         nsy = (h + rows - 1) / rows;
         dim3 grid((unsigned)(strips_x * nsy * batch));
         if (!(g_host_variant & (32 | 64))) {
-            // 32-row chunks: strip height a multiple of SR2
-            int nsy2 = (int)std::min<long long>((2048 + per_col - 1) / per_col, (h + SR2 - 1) / SR2);
+            // 32-row chunks: bands of at most 17 chunks (544 rows), and at least 1024 workgroups
+            // when the image is short (kernel traces: 2 bands of 540 rows beat 1 band of 1080 on
+            // 1080p, and 1 band beats 2 on the 540- and 270-row octaves).  Test hook: variant 512
+            // restores the former rule (about 2048 workgroups).
+            int nsy2;
+            if (g_host_variant & 512) {
+                nsy2 = (int)std::min<long long>((2048 + per_col - 1) / per_col, (h + SR2 - 1) / SR2);
+            } else {
+                nsy2 = (h + 17 * SR2 - 1) / (17 * SR2);
+                const int need = (int)std::min<long long>((1024 + per_col - 1) / per_col, (h + SR2 - 1) / SR2);
+                nsy2 = std::max(nsy2, need);
+            }
             nsy2 = std::max(nsy2, 1);
             int rows2 = (h + nsy2 - 1) / nsy2;
             rows2 = (rows2 + SR2 - 1) / SR2 * SR2;
