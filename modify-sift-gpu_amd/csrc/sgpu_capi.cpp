@@ -411,7 +411,11 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     for (int k = 1; k < nlev; k++)
         lfw[k] = sgp::make_filter(S.sigma[k - 1], O.filter_width_factor, ltaps[k].k);
     const int fw0 = sgp::make_filter(S.initial_smooth, O.filter_width_factor, taps0.k);
-    const bool fused = !two && (sgk::get_variant() & 8388608) &&
+    // Test hooks 4194304 / 2097152: the fused launch for octaves >= 1 / >= 2 only (the small
+    // octaves, where the per-level kernel is latency-bound).
+    const int vv0 = sgk::get_variant();
+    const int fused_from = (vv0 & 8388608) ? 0 : (vv0 & 4194304) ? 1 : (vv0 & 2097152) ? 2 : noct;
+    const bool fused = !two && fused_from < noct &&
                        sgk::octave_fused_supported(nlev, lfw, S.level_ds - S.level_min);
     for (int o = 0; o < noct; o++) {
         if (o == 1 && two) HIPCHK(ctx, hipStreamWaitEvent(pt.stream_aux, pt.ev[7], 0));
@@ -419,7 +423,7 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
         const sgk::OctaveDesc& od = fp.oct[o];
         const long long npx = (long long)od.wa * od.h;
         float* lvl0 = pyr + od.gauss_off;
-        if (fused && (o > 0 || O.octave_min == 0)) {
+        if (fused && o >= fused_from && (o > 0 || O.octave_min == 0)) {
             sgk::OctaveLaunch L{};
             if (o == 0) {
                 L.src8 = src8;

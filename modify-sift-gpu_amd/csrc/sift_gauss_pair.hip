@@ -82,15 +82,6 @@ __device__ __forceinline__ void lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// s_waitcnt vmcnt(N) (expcnt / lgkmcnt left at their maximum).
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-    static_assert(N >= 0 && N < 64, "vmcnt range");
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-
 // Gaussian taps are symmetric bit for bit (make_filter: exp(-i^2/2s^2) for i = -sz..sz, one
 // normalisation), so tap m is read as tap min(m, FW-1-m) and only the H+1 distinct values
 // occupy registers; the host checks the symmetry before launching.
@@ -238,13 +229,11 @@ __global__ __launch_bounds__(NT) void k_gauss_pair(
     // after the load would make the compiler wait for each prefetch as soon as it is issued,
     // and with two workgroups per CU nothing else hides that latency.
     struct Elem { float4 v0, v1; };
-    constexpr int NL = 2 * NLD;                        // loads per chunk and thread
     Elem stA[NLD], stB[NLD];
-    // The chunk loads are issued from inline asm, so the compiler does not track them: its own
-    // waits would be vmcnt(0) at the first use (the HBM stores in between have data-dependent
-    // counts), which also waits for every store of the step.  Instead every step issues exactly
-    // NL loads, unpredicated with clamped addresses, and the consumer waits for vmcnt <= NL: all
-    // memory operations older than the most recent chunk's loads have completed.
+    // Chunk loads keep the RAW quads; edge replication and the u8 conversion happen when the
+    // chunk is stored to LDS, so the compiler does not wait for a load right after issuing it.
+    // (Issuing them from inline asm with explicit vmcnt waits saved 2 %, but the compiler then
+    // copies and reuses the destination registers before the data lands: unsafe.)
     auto load_chunk = [&](Elem (&stage)[NLD], int c) {
 #pragma unroll
         for (int m = 0; m < NLD; m++) {
@@ -254,18 +243,11 @@ __global__ __launch_bounds__(NT) void k_gauss_pair(
             const int gy1 = clampi(iy0 + c * PC + 2 * p + 1, 0, H - 1);
             const int lq = clampi(a0 + 4 * j, 0, W - 4);
             if (U8) {
-                uint32_t w0, w1;
-                asm volatile("global_load_dword %0, %1, off" : "=v"(w0)
-                             : "v"(s8 + (long long)gy0 * src_stride + lq) : "memory");
-                asm volatile("global_load_dword %0, %1, off" : "=v"(w1)
-                             : "v"(s8 + (long long)gy1 * src_stride + lq) : "memory");
-                stage[m].v0.x = __uint_as_float(w0);
-                stage[m].v1.x = __uint_as_float(w1);
+                stage[m].v0.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(s8 + (long long)gy0 * src_stride + lq));
+                stage[m].v1.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(s8 + (long long)gy1 * src_stride + lq));
             } else {
-                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(stage[m].v0)
-                             : "v"(sf + (long long)gy0 * src_stride + lq) : "memory");
-                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(stage[m].v1)
-                             : "v"(sf + (long long)gy1 * src_stride + lq) : "memory");
+                stage[m].v0 = *reinterpret_cast<const float4*>(sf + (long long)gy0 * src_stride + lq);
+                stage[m].v1 = *reinterpret_cast<const float4*>(sf + (long long)gy1 * src_stride + lq);
             }
         }
     };
@@ -303,7 +285,6 @@ __global__ __launch_bounds__(NT) void k_gauss_pair(
     };
 
     load_chunk(stA, 0);
-    wait_vm<0>();
     store_chunk(stA);
     load_chunk(stA, 1);
     load_chunk(stB, 2);
@@ -333,8 +314,7 @@ __global__ __launch_bounds__(NT) void k_gauss_pair(
             }
         }
         lds_sync();
-        // chunk c+1 -> s_in (H1 has finished with it).  At least chunk c+2's NL loads are younger.
-        wait_vm<NL>();
+        // chunk c+1 -> s_in (H1 has finished with it)
         if (has_next) store_chunk(cur);
         const int km = c - 1;   // middle chunk of this step (parity 1 - P)
         if (km >= 0 && km < nchunk_mid) {
@@ -409,7 +389,7 @@ __global__ __launch_bounds__(NT) void k_gauss_pair(
                 }
             }
         }
-        // chunk c+3, issued before the V2 stores so that the next wait does not include them
+        // chunk c+3 (rows clamped, so always a valid address)
         load_chunk(cur, c + 3);
         if (do_v2) {
             const int x = x0 + vc;
@@ -430,7 +410,6 @@ __global__ __launch_bounds__(NT) void k_gauss_pair(
         step(c, IC<0>(), stA, stB);
         if (c + 1 < nsteps) step(c + 1, IC<1>(), stB, stA);
     }
-    wait_vm<0>();   // the last, unused prefetches land before the wave ends
 }
 
 template <int FW1, int FW2>
