@@ -32,6 +32,8 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 // instead of strips, 32 scalar-FMA strip Gaussian instead of the packed one, 64 16-row packed
 // strip Gaussian (k_gauss_pk) instead of the 32-row one (k_gauss_pk2), 128 timing probe (filters
 // replaced by copies, results wrong), 256 element-wise instead of quad loads in k_gauss_pk2,
+// 131072 / 262144 non-temporal stores / loads in k_gauss_pk2 (no effect / 25 % slower; with the
+// two hooks compiled in, the default path measured 1.5 % faster in the same process),
 // 4096 / 8192 two / four batch parts, 16384 pyramid octaves >= 1 on a second stream
 // (sgpu_capi.cpp), 65536 workgroup-tile strip extremum kernel instead of the wave-streaming one.
 __constant__ int g_variant;
@@ -549,8 +551,17 @@ __global__ __launch_bounds__(256) void k_gauss_pk2(
                         r1[t] = u8_to_unit((w1 >> (8 * t)) & 255u);
                     }
                 } else {
-                    const float4 v0 = *reinterpret_cast<const float4*>(sf + (long long)gy0 * src_stride + lq);
-                    const float4 v1 = *reinterpret_cast<const float4*>(sf + (long long)gy1 * src_stride + lq);
+                    float4 v0, v1;
+                    if (g_variant & 262144) {   // test hook: non-temporal loads (25 % slower)
+                        typedef float nt4 __attribute__((ext_vector_type(4)));
+                        const nt4 a = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(sf + (long long)gy0 * src_stride + lq));
+                        const nt4 c = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(sf + (long long)gy1 * src_stride + lq));
+                        v0 = make_float4(a.x, a.y, a.z, a.w);
+                        v1 = make_float4(c.x, c.y, c.z, c.w);
+                    } else {
+                        v0 = *reinterpret_cast<const float4*>(sf + (long long)gy0 * src_stride + lq);
+                        v1 = *reinterpret_cast<const float4*>(sf + (long long)gy1 * src_stride + lq);
+                    }
                     r0[0] = v0.x; r0[1] = v0.y; r0[2] = v0.z; r0[3] = v0.w;
                     r1[0] = v1.x; r1[1] = v1.y; r1[2] = v1.z; r1[3] = v1.w;
                 }
@@ -662,7 +673,10 @@ __global__ __launch_bounds__(256) void k_gauss_pk2(
                 for (int j = 0; j < 4; j++) {
                     const int y = yb + t0 + j;
                     if (y < ye) {
-                        *reinterpret_cast<f2v*>(&d[(long long)y * W + x]) = acc[j];
+                        if (g_variant & 131072)   // test hook: non-temporal stores (no effect)
+                            __builtin_nontemporal_store(acc[j], reinterpret_cast<f2v*>(&d[(long long)y * W + x]));
+                        else
+                            *reinterpret_cast<f2v*>(&d[(long long)y * W + x]) = acc[j];
                         // DownsampleKernel<1> (ProgramCU.cu:287-298) into the next octave's
                         // level 0: dst(r, c) = src(2r, min(2c, W-1)); x is even, W is even.
                         if (dd && !(y & 1) && (y >> 1) < dsh) {
