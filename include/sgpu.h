@@ -46,6 +46,20 @@ typedef struct sgpu_options {
                                           ProgramCU.cu:869-884; 1: circular window of
                                           ProgramCU-0.cu:834 / the GLSL path                */
     int verbose;                       /* -v   (0 here; the library prints nothing at 0)     */
+    int max_dimension;                 /* -maxd (13200, GlobalUtil.cpp:86; SiftGPU::SetMaxDimension):
+                                          while the first octave is wider or taller, octave_min
+                                          is raised by one (PyramidCU::InitPyramid,
+                                          PyramidCU.cpp:129-135)                              */
+    int preprocess_on_cpu;             /* -prep / -noprep (1, GlobalUtil.cpp:81): with -fo > 0
+                                          the input is first sampled by 2^fo and its width
+                                          truncated (GLTexInput::SetImageData,
+                                          GLTexImage.cpp:928-1009), then run from octave 0;
+                                          0: the first octave is SampleImageD of the full input  */
+    int feature_count_threshold;       /* -tc[1|2|3] <n> (-1 = off, GlobalUtil.cpp:135)         */
+    int truncate_method;               /* 0: -tc / -tc1, 1: -tc2, 2: -tc3 (SiftGPU.cpp:1185-1203;
+                                          SiftPyramid::LimitFeatureCount, SiftPyramid.cpp:219-260,
+                                          and the level skip of PyramidCU::GenerateFeatureList,
+                                          PyramidCU.cpp:829-853)                              */
 } sgpu_options;
 
 /* Defaults of GlobalUtil.cpp:50-135. */
@@ -202,8 +216,12 @@ int sgpu_comm_allgather_i32(sgpu_ctx* ctx, const int32_t* send, int n, int32_t* 
 int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
 
 /* ---- test hooks (parity tests read intermediate stages; not part of the drop-in surface) ---- */
-/* Select a kernel variant for in-process A/B timing (0 = shipped configuration). */
-int sgpu_debug_set_variant(int variant);
+/* Per-context debug flags (0 = shipped configuration). */
+#define SGPU_DEBUG_PARTS2   1   /* split a batch into 2 parts on separate streams              */
+#define SGPU_DEBUG_PARTS4   2   /* ... into 4 parts                                            */
+#define SGPU_DEBUG_TINY_CAP 4   /* start the keypoint capacity at 64 per part, so that the
+                                   capacity-overflow re-run of a part is exercised             */
+int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);
 /* Gaussian level (image, octave, level 0..level_num-1) as wa*h floats. */

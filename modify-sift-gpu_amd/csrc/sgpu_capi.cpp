@@ -53,7 +53,6 @@ enum { T_UPLOAD, T_PYRAMID, T_DETECT, T_ORIENT, T_EXPAND, T_DESC, T_DOWNLOAD, T_
 struct Part {
     hipStream_t stream = nullptr;      // high priority: pyramid + detection
     hipStream_t stream_lo = nullptr;   // low priority: orientation, descriptors, readback
-    hipStream_t stream_aux = nullptr;  // high priority: pyramid octaves >= 1 beside octave 0
     size_t cand_hint = 0, feat_hint = 0;   // counts of the previous call (launch-grid sizing)
     hipEvent_t ev[10] = {};  // start, pyramid, detect, orientation, expand, descriptor, end,
                              // octave-1 base ready, octaves >= 1 done, (spare)
@@ -80,8 +79,7 @@ struct Part {
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
         if (stream_lo) (void)hipStreamDestroy(stream_lo);
-        if (stream_aux) (void)hipStreamDestroy(stream_aux);
-        stream = stream_lo = stream_aux = nullptr;
+        stream = stream_lo = nullptr;
     }
 };
 
@@ -94,6 +92,8 @@ struct sgpu_ctx {
     hipStream_t stream = nullptr;   // matcher, uploads, gathers
     sgpu_options opt{};
     sgp::Schedule sched{};
+    sgp::InputPlan plan{};                 // first octave of the last extract (plan_input)
+    int debug_flags = 0;                   // SGPU_DEBUG_* test hooks
     std::string err;
     // last extract
     int batch = 0, w = 0, h = 0, nparts = 0;
@@ -101,7 +101,8 @@ struct sgpu_ctx {
     size_t staged_bytes = 0;
     std::vector<int64_t> img_off;          // global per-image offsets [batch + 1]
     Part part[kMaxParts];
-    DevBuf input, all_keys, all_desc, gray;      // all_*: lazily gathered multi-part outputs
+    DevBuf input, all_keys, all_desc, gray, pre;  // all_*: lazily gathered multi-part outputs;
+                                                  // pre: the 2^ds-sampled input (-fo > 0)
     bool gathered = false;
     hipEvent_t ev[T_N + 1] = {};
     float timing[T_N] = {};
@@ -162,6 +163,10 @@ void sgpu_default_options(sgpu_options* o) {
     o->keep_extremum_sign = 0;
     o->circular_window = 0;
     o->verbose = 0;
+    o->max_dimension = 13200;
+    o->preprocess_on_cpu = 1;
+    o->feature_count_threshold = -1;
+    o->truncate_method = 0;
 }
 
 // SiftGPU::ParseParam (SiftGPU.cpp:801-1246): options are matched on their first four
@@ -202,7 +207,16 @@ int sgpu_parse_args(sgpu_options* o, int argc, const char* const* argv, int* dev
         } else if (k == "ofix") o->fixed_orientation = (strcmp(arg + 1, "ofix") == 0);
         else if (k == "lowe") o->lowe_origin = 1;
         else if (k == "sign") o->keep_extremum_sign = 1;
+        else if (k == "prep") o->preprocess_on_cpu = 1;
+        else if (k == "nopr") o->preprocess_on_cpu = 0;
         else if (!param) continue;
+        else if (k == "tc" || k == "tc1" || k == "tc2" || k == "tc3") {
+            // SiftGPU.cpp:1185-1203: the method is set even when no count follows
+            o->truncate_method = k == "tc2" ? 1 : k == "tc3" ? 2 : 0;
+            if (sscanf(param, "%d", &iv) == 1 && iv > 0) { o->feature_count_threshold = iv; i++; }
+        } else if (k == "maxd") {   // SiftGPU.cpp:1213-1222
+            if (sscanf(param, "%d", &iv) == 1 && iv > 0) { o->max_dimension = iv; i++; }
+        }
         else if (k == "f") { if (sscanf(param, "%f", &fv) == 1 && fv > 0) { o->filter_width_factor = fv; i++; } }
         else if (k == "w") { if (sscanf(param, "%f", &fv) == 1 && fv > 0) { o->orientation_window_factor = fv; i++; } }
         else if (k == "dw") { if (sscanf(param, "%f", &fv) == 1 && fv > 0) { o->descriptor_window_factor = fv; i++; } }
@@ -231,12 +245,14 @@ int sgpu_ctx_set_options(sgpu_ctx* ctx, const sgpu_options* opt) {
     if (!ctx) return SGPU_EINVAL;
     sgpu_options o;
     if (opt) o = *opt; else sgpu_default_options(&o);
-    // -fo -2 is accepted by the reference's parser (SiftGPU.cpp:1075) but its initial smoothing
-    // sigma is then 0 (sqrt only when 1.6 > 0.5 * 4 + 0.001, SiftGPU.cpp:446-452) and
-    // CreateFilterKernel(0) yields NaN taps (ProgramCU.cu:391-398): a NaN pyramid.  Rejected.
-    if (o.octave_min < -1)
-        return ctx->fail(SGPU_EINVAL, "first octave must be >= -1 (-fo -2 gives the reference a NaN pyramid)");
+    // -fo -2 runs as in the reference: its initial smoothing sigma is 0 (sqrt only when
+    // 1.6 > 0.5 * 4 + 0.001, SiftGPU.cpp:446-452), CreateFilterKernel(0) yields NaN taps
+    // (ProgramCU.cu:391-398) and the NaN pyramid has no keypoint with an orientation: the call
+    // succeeds with 0 features.  -fo below -3 is clamped to -3
+    // (PyramidCU.cpp:106-107).
+    if (o.octave_min < -3) o.octave_min = -3;
     if (o.dog_level_num < 1 || o.dog_level_num > 6) return ctx->fail(SGPU_EINVAL, "dog_level_num must be 1..6");
+    if (o.max_dimension < 8) return ctx->fail(SGPU_EINVAL, "max_dimension must be >= 8");
     ctx->opt = o;
     sgp::Options po;
     po.filter_width_factor = o.filter_width_factor;
@@ -268,7 +284,6 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     for (Part& pt : ctx->part) {
         if (hipStreamCreateWithPriority(&pt.stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-            hipStreamCreateWithPriority(&pt.stream_aux, hipStreamNonBlocking, prio_hi) != hipSuccess ||
             hipStreamCreateWithPriority(&pt.stream_lo, hipStreamNonBlocking, prio_lo) != hipSuccess) {
             sgpu_ctx_destroy(ctx);
             return SGPU_ENODEV;
@@ -291,12 +306,11 @@ int sgpu_ctx_destroy(sgpu_ctx* ctx) {
     for (Part& pt : ctx->part) {
         if (pt.stream) (void)hipStreamSynchronize(pt.stream);
         if (pt.stream_lo) (void)hipStreamSynchronize(pt.stream_lo);
-        if (pt.stream_aux) (void)hipStreamSynchronize(pt.stream_aux);
         pt.release();
     }
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     ctx->comm = nullptr;
-    DevBuf* bufs[] = {&ctx->input, &ctx->all_keys, &ctx->all_desc, &ctx->gray, &ctx->m_d1, &ctx->m_d2, &ctx->m_s1, &ctx->m_s2,
+    DevBuf* bufs[] = {&ctx->input, &ctx->all_keys, &ctx->all_desc, &ctx->gray, &ctx->pre, &ctx->m_d1, &ctx->m_d2, &ctx->m_s1, &ctx->m_s2,
                       &ctx->m_part, &ctx->m_terms, &ctx->m_match, &ctx->m_dist, &ctx->m_mask, &ctx->m_loc,
                       &ctx->c_buf};
     for (DevBuf* b : bufs) b->release();
@@ -361,11 +375,13 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     fp.circular = O.circular_window;
     fp.normalize = O.normalized;
     fp.origin_offset = O.lowe_origin ? 0.0f : 0.5f;
-    fp.octave_min = O.octave_min;
+    fp.octave_min = ctx->plan.octave_min + ctx->plan.ds;   // coordinate scale 2^(om + ds)
 
     // candidate capacity: grow-only, first guess one per 256 octave pixels
     const size_t sum_px = (size_t)goff / (size_t)std::max(1, nlev) / (size_t)n;
-    pt.cand_cap = std::max(pt.cand_cap, std::max<size_t>(1024, sum_px / 256 * n));
+    pt.cand_cap = (ctx->debug_flags & SGPU_DEBUG_TINY_CAP)
+                      ? std::max<size_t>(pt.cand_cap, 64)
+                      : std::max(pt.cand_cap, std::max<size_t>(1024, sum_px / 256 * n));
     const size_t nc = pt.cand_cap, ne_cap = 2 * nc;
     ALLOCCHK(ctx, pt.pyr.ensure((size_t)goff * sizeof(float)));
     ALLOCCHK(ctx, pt.mask.ensure((size_t)moff * sizeof(uint32_t)));
@@ -394,68 +410,21 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     const uint8_t* src8 = is_f32 ? nullptr : (const uint8_t*)src_in + (size_t)pt.img0 * img_elems;
     const float* srcf = is_f32 ? (const float*)src_in + (size_t)pt.img0 * img_elems : nullptr;
 
-    // ---- Gaussian pyramid (BuildPyramid, PyramidCU.cpp:979-1044).  Optionally (test hook,
-    // variant 16384) octaves >= 1 run on the aux stream as soon as their base level (the
-    // decimated level d of octave 0) exists, overlapping octave 0's last two levels.  That
-    // saves ~2% of the pyramid time but makes per-kernel durations overlap, so the shipped
-    // configuration keeps one stream and kernel times that add up to the stage time.
+    // ---- Gaussian pyramid (BuildPyramid, PyramidCU.cpp:979-1044): one launch per level
+    // (k_gauss_pk2) for the whole part.  Level kds = level_ds - level_min of octave o also writes
+    // its 2x decimation as level 0 of octave o+1 (PyramidCU.cpp:1024).
     float* pyr = pt.pyr.as<float>();
     sgk::Taps taps;
-    const bool two = noct > 1 && (sgk::get_variant() & 16384);
-    // One launch per level (k_gauss_pk2) is the shipped path.  Variant bit 8388608 (test hook)
-    // runs each octave of the default schedule (d = 3, filter factor 4) as ONE fused launch
-    // instead (sift_octave.hip: all levels streamed through LDS, 25-26 B of HBM traffic per
-    // octave pixel instead of 48) -- bit-identical, but slower on MI355X.
     sgk::Taps ltaps[sgk::kMaxLevels], taps0;
     int lfw[sgk::kMaxLevels] = {0};
     for (int k = 1; k < nlev; k++)
         lfw[k] = sgp::make_filter(S.sigma[k - 1], O.filter_width_factor, ltaps[k].k);
     const int fw0 = sgp::make_filter(S.initial_smooth, O.filter_width_factor, taps0.k);
-    // Test hooks 4194304 / 2097152: the fused launch for octaves >= 1 / >= 2 only (the small
-    // octaves, where the per-level kernel is latency-bound).
-    const int vv0 = sgk::get_variant();
-    const int fused_from = (vv0 & 8388608) ? 0 : (vv0 & 4194304) ? 1 : (vv0 & 2097152) ? 2 : noct;
-    const bool fused = !two && fused_from < noct &&
-                       sgk::octave_fused_supported(nlev, lfw, S.level_ds - S.level_min);
+    const int kds = S.level_ds - S.level_min;
     for (int o = 0; o < noct; o++) {
-        if (o == 1 && two) HIPCHK(ctx, hipStreamWaitEvent(pt.stream_aux, pt.ev[7], 0));
-        st = (o >= 1 && two) ? pt.stream_aux : pt.stream;
         const sgk::OctaveDesc& od = fp.oct[o];
         const long long npx = (long long)od.wa * od.h;
         float* lvl0 = pyr + od.gauss_off;
-        if (fused && o >= fused_from && (o > 0 || O.octave_min == 0)) {
-            sgk::OctaveLaunch L{};
-            if (o == 0) {
-                L.src8 = src8;
-                L.srcf = srcf;
-                L.src_stride = stride;
-                L.src_img_stride = (long long)img_elems;
-                L.fw0 = fw0;
-                L.taps0 = taps0.k;
-            }
-            L.pyr = lvl0;
-            L.level_stride = od.level_stride;
-            L.w = od.wa;
-            L.h = od.h;
-            L.batch = n;
-            for (int k = 1; k < nlev; k++) L.taps[k] = ltaps[k].k;
-            if (o + 1 < noct) {
-                const sgk::OctaveDesc& nd = fp.oct[o + 1];
-                L.ds = pyr + nd.gauss_off;
-                L.dsw = nd.wa;
-                L.dsh = nd.h;
-                L.ds_img_stride = (long long)nd.wa * nd.h;
-            }
-            const hipError_t e = sgk::launch_octave(L, st);
-            if (e == hipSuccess) continue;
-            if (e != hipErrorNotSupported) HIPCHK(ctx, e);
-            (void)hipGetLastError();   // unsupported input layout: per-level path below
-        }
-        // Filter ops of this octave: op 0 (octave 0 only) smooths the input into level 0, op k
-        // filters level k-1 into level k.  One launch per op (k_gauss_pk2) is the shipped path;
-        // variant 1024 (test hook) runs consecutive ops as one two-level launch instead
-        // (k_gauss_pair: level k-1 read once, levels k and k+1 written), bit-identical.
-        const int kds = S.level_ds - S.level_min;   // level d feeds the next octave (PyramidCU.cpp:1024)
         float* ds = nullptr;
         int dsw = 0, dsh = 0;
         long long ds_stride = 0;
@@ -466,75 +435,35 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
             dsh = nd.h;
             ds_stride = (long long)nd.wa * nd.h;
         }
-        const float* in_f = srcf;                   // op 0 source
+        // filter op k: op 0 (octave 0 only) smooths the input into level 0, op k >= 1 filters
+        // level k-1 into level k
+        const float* in_f = srcf;
         const uint8_t* in_8 = src8;
         int in_stride = stride;
         long long in_img = (long long)img_elems;
-        if (o == 0 && O.octave_min != 0) {
+        if (o == 0 && ctx->plan.octave_min != 0) {
             // -fo != 0: resample the input into level 1's storage (free until level 1 is
             // filtered), then the initial smoothing as for a float input
             float* tmp = lvl0 + od.level_stride;
             HIPCHK(ctx, sgk::launch_first_octave_input(srcf, src8, stride, (long long)img_elems,
-                                                       ctx->w & ~3, h, O.octave_min, tmp,
+                                                       ctx->w & ~3, h, ctx->plan.octave_min, tmp,
                                                        od.wa, od.h, npx, n, st));
             in_f = tmp;
             in_8 = nullptr;
             in_stride = od.wa;
             in_img = npx;
         }
-        const bool pairs = (sgk::get_variant() & 1024) != 0;
-        for (int k = (o == 0 ? 0 : 1); k < nlev;) {
+        for (int k = (o == 0 ? 0 : 1); k < nlev; k++) {
             const int fwk = k == 0 ? fw0 : lfw[k];
             const float* tk = k == 0 ? taps0.k : ltaps[k].k;
-            const float* sk_f = k == 0 ? in_f : lvl0 + (k - 1) * od.level_stride;
-            const uint8_t* sk_8 = k == 0 ? in_8 : nullptr;
-            const int sk_stride = k == 0 ? in_stride : od.wa;
-            const long long sk_img = k == 0 ? in_img : npx;
-            if (pairs && k + 1 < nlev && sgk::gauss_pair_supported(fwk, lfw[k + 1])) {
-                sgk::GaussPairLaunch L{};
-                L.src = sk_f;
-                L.src8 = sk_8;
-                L.src_stride = sk_stride;
-                L.src_img_stride = sk_img;
-                L.dst1 = lvl0 + k * od.level_stride;
-                L.dst2 = lvl0 + (k + 1) * od.level_stride;
-                L.dst_img_stride = npx;
-                L.w = od.wa;
-                L.h = od.h;
-                L.batch = n;
-                L.fw1 = fwk;
-                L.fw2 = lfw[k + 1];
-                L.taps1 = tk;
-                L.taps2 = ltaps[k + 1].k;
-                if (ds && (kds == k || kds == k + 1)) {
-                    L.ds = ds;
-                    L.ds_level = kds == k ? 1 : 2;
-                    L.dsw = dsw;
-                    L.dsh = dsh;
-                    L.ds_img_stride = ds_stride;
-                }
-                const hipError_t e = sgk::launch_gauss_pair(L, st);
-                if (e == hipSuccess) {
-                    if (o == 0 && L.ds) HIPCHK(ctx, hipEventRecord(pt.ev[7], st));
-                    k += 2;
-                    continue;
-                }
-                if (e != hipErrorNotSupported) HIPCHK(ctx, e);
-                (void)hipGetLastError();   // unaligned source or asymmetric taps: single levels
-            }
             for (int i = 0; i < fwk; i++) taps.k[i] = tk[i];
             const bool dk = ds && kds == k;
-            HIPCHK(ctx, sgk::launch_gauss(sk_f, sk_8, sk_stride, sk_img, lvl0 + k * od.level_stride,
+            HIPCHK(ctx, sgk::launch_gauss(k == 0 ? in_f : lvl0 + (k - 1) * od.level_stride,
+                                          k == 0 ? in_8 : nullptr, k == 0 ? in_stride : od.wa,
+                                          k == 0 ? in_img : npx, lvl0 + k * od.level_stride,
                                           npx, od.wa, od.h, fwk, taps, n, dk ? ds : nullptr,
                                           dk ? dsw : 0, dk ? dsh : 0, dk ? ds_stride : 0, st));
-            if (o == 0 && dk) HIPCHK(ctx, hipEventRecord(pt.ev[7], st));
-            k += 1;
         }
-    }
-    st = pt.stream;
-    if (two) {
-        HIPCHK(ctx, hipEventRecord(pt.ev[8], pt.stream_aux));
-        HIPCHK(ctx, hipStreamWaitEvent(st, pt.ev[8], 0));
     }
     HIPCHK(ctx, hipEventRecord(pt.ev[1], st));
 
@@ -543,6 +472,9 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     HIPCHK(ctx, hipMemsetAsync(pt.mask.p, 0, (size_t)moff * sizeof(uint32_t), st));
     HIPCHK(ctx, sgk::launch_extrema(pyr, pt.mask.as<uint32_t>(), pt.row_count.as<uint32_t>(),
                                     fp, st));
+    if (O.feature_count_threshold > 0)   // -tc: GenerateFeatureList skip + LimitFeatureCount(0)
+        HIPCHK(ctx, sgk::launch_limit_rows(pt.row_count.as<uint32_t>(), fp,
+                                           O.feature_count_threshold, O.truncate_method, st));
     HIPCHK(ctx, sgk::launch_scan(pt.row_count.as<uint32_t>(), pt.row_base.as<uint32_t>(),
                                  pt.total_rows, pt.scan_tmp.as<uint32_t>(), st));
     HIPCHK(ctx, hipEventRecord(pt.ev[2], st));
@@ -560,6 +492,10 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
                                         pt.total_rows, n_cand_dev, (int)nc, cand_grid, fp,
                                         pt.cand.as<float4>(), pt.info.as<int2>(),
                                         pt.ocount.as<uint32_t>(), st));
+    if (O.feature_count_threshold > 0 && fp.num_orientation >= 2)   // LimitFeatureCount(1)
+        HIPCHK(ctx, sgk::launch_limit_oriented(pt.ocount.as<uint32_t>(), pt.row_base.as<uint32_t>(),
+                                               fp, O.feature_count_threshold, O.truncate_method,
+                                               (uint32_t)nc, st));
     HIPCHK(ctx, hipEventRecord(pt.ev[3], st));
     HIPCHK(ctx, sgk::launch_scan(pt.ocount.as<uint32_t>(), pt.eoff.as<uint32_t>(), nc,
                                  pt.scan_tmp.as<uint32_t>(), st));
@@ -604,24 +540,36 @@ static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
         return ctx->fail(SGPU_EINVAL, "staged input does not match the batch");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     const sgpu_options& O = ctx->opt;
-    ctx->oct = sgp::make_octaves(w, h, O.octave_num, O.octave_min);
+    // first octave (GLTexInput::SetImageData + PyramidCU::InitPyramid): -fo, -prep, -maxd
+    const sgp::InputPlan plan = sgp::plan_input(w, h, O.octave_min, O.max_dimension, O.preprocess_on_cpu);
+    if (plan.w < 8 || plan.h < 8) return ctx->fail(SGPU_EINVAL, "image too small for the first octave");
+    {
+        sgp::Options po;
+        po.filter_width_factor = O.filter_width_factor;
+        po.dog_level_num = O.dog_level_num;
+        po.dog_threshold = O.dog_threshold;
+        po.edge_threshold = O.edge_threshold;
+        po.octave_min = plan.octave_min + plan.ds;   // GetInitialSmoothSigma(_octave_min + ds)
+        ctx->sched = sgp::make_schedule(po);
+    }
+    ctx->plan = plan;
+    ctx->oct = sgp::make_octaves(plan.w, plan.h, O.octave_num, plan.octave_min);
     const int noct = (int)ctx->oct.size();
     if (noct > sgk::kMaxOctaves) return ctx->fail(SGPU_EINVAL, "too many octaves");
     for (const auto& oc : ctx->oct)
         if (oc.w < 4 || oc.h < 4) return ctx->fail(SGPU_EINVAL, "image too small for the octave count");
     ctx->batch = n;
-    ctx->w = w;
-    ctx->h = h;
+    ctx->w = plan.ds ? plan.w : w;
+    ctx->h = plan.h;
     ctx->gathered = false;
 
     // parts: one by default.  Measured on MI355X (profiles/): a second
     // part's pyramid starves beside the previous part's descriptor kernel (the dispatcher keeps
     // filling the CUs with descriptor workgroups despite the stream priorities), so splitting
-    // does not pay yet.  Test hook: variant 4096 -> 2 parts, 8192 -> 4 parts.
-    const int vv = sgk::get_variant();
+    // does not pay yet.  Test hook: SGPU_DEBUG_PARTS2 / SGPU_DEBUG_PARTS4.
     int np = 1;
-    if ((vv & 4096) && n >= 2) np = 2;
-    if ((vv & 8192) && n >= 4) np = 4;
+    if ((ctx->debug_flags & SGPU_DEBUG_PARTS2) && n >= 2) np = 2;
+    if ((ctx->debug_flags & SGPU_DEBUG_PARTS4) && n >= 4) np = 4;
     ctx->nparts = np;
     for (int p = 0, i0 = 0; p < np; p++) {
         const int cnt = n / np + (p < n % np ? 1 : 0);
@@ -650,6 +598,21 @@ static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
         src_in = ctx->gray.p;
         is_f32 = true;
         stride = tw;
+    }
+    if (plan.ds > 0) {
+        // -fo > 0 with -prep (GLTexInput::SetImageData -> DownSamplePixelDataI2F/F,
+        // GLTexImage.cpp:928-1009): pixel (r << ds, c << ds) of the input, plan.w x plan.h
+        // (the sampled columns never reach the truncated-away ones)
+        const size_t px = (size_t)plan.w * plan.h;
+        ALLOCCHK(ctx, ctx->pre.ensure((size_t)n * px * sizeof(float)));
+        HIPCHK(ctx, sgk::launch_first_octave_input(is_f32 ? (const float*)src_in : nullptr,
+                                                   is_f32 ? nullptr : (const uint8_t*)src_in,
+                                                   stride, (long long)stride * h, w & ~3, h, plan.ds,
+                                                   ctx->pre.as<float>(), plan.w, plan.h,
+                                                   (long long)px, n, ctx->stream));
+        src_in = ctx->pre.p;
+        is_f32 = true;
+        stride = plan.w;
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
 
@@ -732,7 +695,7 @@ int sgpu_extract_keypoints(sgpu_ctx* ctx, int image, const float* keys, int num,
     std::vector<float4> lf;
     std::vector<int2> li;
     std::vector<int> lidx;
-    float octave_sigma = ldexpf(1.0f, O.octave_min);   // PyramidCU.cpp:461
+    float octave_sigma = ldexpf(1.0f, ctx->plan.octave_min + ctx->plan.ds);   // PyramidCU.cpp:461-463
     for (int i = 0; i < noct; i++, octave_sigma *= 2.0f)
         for (int j = 0; j < d; j++) {
             const float level_sigma = sgp::level_sigma(S, j + S.level_min + 1) * octave_sigma;
@@ -1240,8 +1203,10 @@ int sgpu_last_timing(const sgpu_ctx* ctx, float* times, int n) {
     return SGPU_OK;
 }
 
-int sgpu_debug_set_variant(int variant) {
-    return sgk::set_variant(variant) == hipSuccess ? SGPU_OK : SGPU_ENODEV;
+int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags) {
+    if (!ctx) return SGPU_EINVAL;
+    ctx->debug_flags = flags;
+    return SGPU_OK;
 }
 
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims, int max) {

@@ -13,10 +13,6 @@ constexpr int kMaxOctaves = 16;
 
 struct Taps { float k[33]; };
 
-// In-process A/B switch for kernel variants (test hook; 0 = shipped configuration).
-hipError_t set_variant(int v);
-int get_variant();
-
 // Per-octave geometry and buffer offsets used by the feature kernels.
 struct OctaveDesc {
     int w, h, wa;          // wa = padded width = row stride of every level image
@@ -51,56 +47,6 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         int w, int h, int fw, const Taps& taps, int batch,
                         float* ds_dst, int ds_w, int ds_h, long long ds_img_stride,
                         hipStream_t stream);
-
-// Fused octave pyramid (sift_octave.hip): all d+3 = 6 levels of one octave in one launch,
-// for the default schedule (d = 3, filter factor 4: level filters 11, 13, 17, 21, 25).
-// Octave 0: src8 (u8, value p/255) or srcf (f32) is the input, filtered with taps0 (fw0 11 or
-// 13) into level 0.  Octave > 0: src8 = srcf = nullptr and level 0 is already in the pyramid.
-// ds != nullptr: level 3 also writes its 2x point-downsample there (next octave level 0).
-struct OctaveLaunch {
-    const uint8_t* src8;
-    const float* srcf;
-    int src_stride;
-    long long src_img_stride;
-    int fw0;
-    const float* taps0;
-    float* pyr;              // level 0 of image 0
-    long long level_stride;  // floats between levels (images are w * h apart)
-    int w, h, batch;
-    const float* taps[6];    // taps[l], l = 1..5
-    float* ds;
-    int dsw, dsh;
-    long long ds_img_stride;
-};
-bool octave_fused_supported(int nlev, const int* fw, int level_ds);
-hipError_t launch_octave(const OctaveLaunch& L, hipStream_t stream);
-
-// Two consecutive levels in one launch (sift_gauss_pair.hip): dst1 = V1(H1(src)),
-// dst2 = V2(H2(dst1)), both with the reference's clamp-to-edge semantics and bit-identical to two
-// launch_gauss calls.  src8 != nullptr selects the u8 ingest (value p/255).  ds != nullptr also
-// writes the 2x point-downsample of level ds_level (1 = dst1, 2 = dst2).  dst1 / dst2 / ds are
-// w x h (dsw x dsh) per image, dst_img_stride (ds_img_stride) apart.  Returns
-// hipErrorNotSupported for filter-width pairs without an instance or unaligned sources; the
-// caller then runs two launch_gauss calls.
-struct GaussPairLaunch {
-    const float* src;
-    const uint8_t* src8;
-    int src_stride;
-    long long src_img_stride;
-    float* dst1;
-    float* dst2;
-    long long dst_img_stride;
-    int w, h, batch;
-    int fw1, fw2;
-    const float* taps1;
-    const float* taps2;
-    float* ds;
-    int ds_level;
-    int dsw, dsh;
-    long long ds_img_stride;
-};
-bool gauss_pair_supported(int fw1, int fw2);
-hipError_t launch_gauss_pair(const GaussPairLaunch& L, hipStream_t stream);
 
 // First octave of -fo != 0 (BuildPyramid, PyramidCU.cpp:1011-1016): the batch's input
 // (u8 p/255 or f32; tw = w & ~3 columns used, rows `stride` apart) resampled into dst
@@ -157,6 +103,15 @@ hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* f
 hipError_t launch_orient_keys(const float* pyr, float4* feat, const int2* feat_info,
                               const int* index, int n, const FeatureParams& fp, float4* keys_out,
                               hipStream_t stream);
+
+// Feature-count limiting (-tc / -tc2 / -tc3, method 0 / 1 / 2), per image of the batch.
+// launch_limit_rows: on the detected keypoints' row counts (before the row scan);
+// launch_limit_oriented: on the oriented counts (after orientation, before the feature scan).
+hipError_t launch_limit_rows(uint32_t* row_count, const FeatureParams& fp, int threshold,
+                             int method, hipStream_t stream);
+hipError_t launch_limit_oriented(uint32_t* ocount, const uint32_t* row_base,
+                                 const FeatureParams& fp, int threshold, int method,
+                                 uint32_t cand_cap, hipStream_t stream);
 
 // Per-image feature offsets: off[b] = eoff[min(row_base[b * rows_per_image], cap)] for b in
 // [0, batch] (cap = candidate capacity; the clamp only matters when the candidates overflowed).

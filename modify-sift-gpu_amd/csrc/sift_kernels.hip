@@ -26,313 +26,23 @@ namespace {
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-// Kernel variant switch for in-process A/B measurements (sgpu_debug_set_variant; 0 = shipped).
-// Bits: 1 XCD remap in the tile Gaussian, 2 row-streaming loader in the tile Gaussian, 4 XCD
-// remap in the tile extremum kernel, 8 tile Gaussian instead of strips, 16 tile extremum kernel
-// instead of strips, 32 scalar-FMA strip Gaussian instead of the packed one, 64 16-row packed
-// strip Gaussian (k_gauss_pk) instead of the 32-row one (k_gauss_pk2), 128 timing probe (filters
-// replaced by copies, results wrong), 256 element-wise instead of quad loads in k_gauss_pk2,
-// 131072 / 262144 non-temporal stores / loads in k_gauss_pk2 (no effect / 25 % slower; with the
-// two hooks compiled in, the default path measured 1.5 % faster in the same process),
-// 4096 / 8192 two / four batch parts, 16384 pyramid octaves >= 1 on a second stream
-// (sgpu_capi.cpp), 65536 workgroup-tile strip extremum kernel instead of the wave-streaming one.
-__constant__ int g_variant;
-int g_host_variant = 0;   // host copy: selects launch configurations
-
 // ------------------------------------------------------------------------------------------
-// Gaussian level: FilterH<FW> then FilterV<FW> (ProgramCU.cu:115-222) fused in one tile.
-// Output tile 64 x 64, 256 threads.  The input tile (64+FW-1)^2 is loaded with the clamped
-// indices of both passes, so the H pass over the tile rows reproduces the reference's
-// per-row clamping and the V pass its row clamping.
+// Gaussian level: FilterH<FW> then FilterV<FW> (ProgramCU.cu:115-222) in one kernel.
+// A 256-thread workgroup owns a 64-column strip of `rows_per_strip` output rows and walks it top
+// to bottom in chunks of SR2 = 32 rows:
+//   * the input rows of chunk c+2 are loaded into registers while chunk c is filtered
+//     (register-staged prefetch, written to LDS after the V pass), so HBM loads overlap the
+//     filter arithmetic;
+//   * the input chunk is stored in LDS as row PAIRS, s_in[pair][col] = (row 2p, row 2p+1);
+//   * every FMA is a v_pk_fma_f32 on two independent outputs (gfx950 issues packed FP32 at twice
+//     the scalar rate): a thread's H pass covers 2 rows x 4 columns and its V pass 4 rows x 2
+//     columns, so every value read from LDS feeds 4 packed FMAs;
+//   * the H pass writes 32 filtered rows into a 64-row LDS ring; the V pass emits output chunk
+//     c-1 from the ring (lag one chunk: FW - 1 <= 32).
+// Each input row is read from HBM once per strip (vertical halo (FW-1)/rows_per_strip), the
+// horizontal halo (FW-1)/64 comes through L2.  Each packed lane is an IEEE fma and the taps are
+// summed i = 0..FW-1 in order, so the levels are bit-identical to the oracle.
 constexpr int GT = 64;
-
-template <int FW, bool U8>
-__global__ __launch_bounds__(256) void k_gauss(const float* __restrict__ src,
-                                               const uint8_t* __restrict__ src8, int src_stride,
-                                               long long src_img_stride, float* __restrict__ dst,
-                                               long long dst_img_stride, int W, int H, Taps taps,
-                                               float* __restrict__ ds, int dsw, int dsh,
-                                               long long ds_img_stride) {
-    constexpr int HALF = FW >> 1;
-    constexpr int IN_W = GT + FW - 1;
-    constexpr int IN_H = GT + FW - 1;
-    constexpr int NV4 = (FW + 3 + 3) / 4;          // float4 reads per H-pass thread
-    constexpr int IN_S = 60 + 4 * NV4 + 4;         // row stride (floats), multiple of 4
-    constexpr int HS = GT + 1;
-    __shared__ __attribute__((aligned(16))) float s_in[IN_H * IN_S];
-    __shared__ float s_h[IN_H * HS];
-
-    const int tid = threadIdx.x;
-    // XCD-aware tile order (cdna_hip_programming.md T1): workgroups are dealt round-robin to the
-    // 8 XCDs, so remap the linear id so that each XCD walks a contiguous run of tiles and
-    // neighbouring tiles (which share halo rows) meet in the same L2.
-    const int tiles_x = (W + GT - 1) / GT, tiles_y = (H + GT - 1) / GT;
-    const int nwg = gridDim.x;
-    int wid = blockIdx.x;
-    if (g_variant & 1) {
-        const int id = blockIdx.x, xcd = id & 7, q = nwg >> 3, r = nwg & 7;
-        wid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
-    }
-    const int bx = wid % tiles_x, rest = wid / tiles_x;
-    const int by = rest % tiles_y, b = rest / tiles_y;
-    const int x0 = bx * GT, y0 = by * GT;
-
-    // ---- load (clamped) input tile (bit 2 of the variant: row-streaming loader)
-    if (!(g_variant & 2)) {
-        if (U8) {
-            const uint8_t* s = src8 + (long long)b * src_img_stride;
-            for (int i = tid; i < IN_H * IN_W; i += 256) {
-                int ty = i / IN_W, tx = i - ty * IN_W;
-                int gy = clampi(y0 - HALF + ty, 0, H - 1), gx = clampi(x0 - HALF + tx, 0, W - 1);
-                s_in[ty * IN_S + tx] = (float)s[(long long)gy * src_stride + gx] / 255.0f;
-            }
-        } else {
-            const float* s = src + (long long)b * src_img_stride;
-            for (int i = tid; i < IN_H * IN_W; i += 256) {
-                int ty = i / IN_W, tx = i - ty * IN_W;
-                int gy = clampi(y0 - HALF + ty, 0, H - 1), gx = clampi(x0 - HALF + tx, 0, W - 1);
-                s_in[ty * IN_S + tx] = s[(long long)gy * src_stride + gx];
-            }
-        }
-    } else {
-        const int lane = tid & 63, wave = tid >> 6;
-        if (U8) {
-            const uint8_t* s = src8 + (long long)b * src_img_stride;
-            for (int ty = wave; ty < IN_H; ty += 4) {
-                const uint8_t* row = s + (long long)clampi(y0 - HALF + ty, 0, H - 1) * src_stride;
-                for (int tx = lane; tx < IN_W; tx += 64)
-                    s_in[ty * IN_S + tx] = (float)row[clampi(x0 - HALF + tx, 0, W - 1)] / 255.0f;
-            }
-        } else {
-            const float* s = src + (long long)b * src_img_stride;
-            for (int ty = wave; ty < IN_H; ty += 4) {
-                const float* row = s + (long long)clampi(y0 - HALF + ty, 0, H - 1) * src_stride;
-                for (int tx = lane; tx < IN_W; tx += 64)
-                    s_in[ty * IN_S + tx] = row[clampi(x0 - HALF + tx, 0, W - 1)];
-            }
-        }
-    }
-    __syncthreads();
-
-    float k[FW];
-#pragma unroll
-    for (int i = 0; i < FW; i++) k[i] = taps.k[i];
-
-    // ---- H pass: 4 consecutive outputs per thread, taps summed i = 0..FW-1 in order.
-    {
-        const int c0 = (tid & 15) * 4;
-        for (int ty = tid >> 4; ty < IN_H; ty += 16) {
-            const float4* row = reinterpret_cast<const float4*>(&s_in[ty * IN_S + c0]);
-            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-#pragma unroll
-            for (int q = 0; q < NV4; q++) {
-                float4 v4 = row[q];
-                float vv[4] = {v4.x, v4.y, v4.z, v4.w};
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const int m = q * 4 + e;
-                    const float v = vv[e];
-                    if (m < FW) a0 = fma_(v, k[m], a0);
-                    if (m >= 1 && m - 1 < FW) a1 = fma_(v, k[m - 1], a1);
-                    if (m >= 2 && m - 2 < FW) a2 = fma_(v, k[m - 2], a2);
-                    if (m >= 3 && m - 3 < FW) a3 = fma_(v, k[m - 3], a3);
-                }
-            }
-            float* o = &s_h[ty * HS + c0];
-            o[0] = a0; o[1] = a1; o[2] = a2; o[3] = a3;
-        }
-    }
-    __syncthreads();
-
-    // ---- V pass: column c, 8 consecutive rows per step.
-    const int c = tid & 63;
-    const int x = x0 + c;
-    float* d = dst + (long long)b * dst_img_stride;
-    float* dd = ds ? ds + (long long)b * ds_img_stride : nullptr;
-    for (int rb = (tid >> 6) * 8; rb < GT; rb += 32) {
-        float acc[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) acc[j] = 0.f;
-#pragma unroll
-        for (int m = 0; m < FW + 7; m++) {
-            const float v = s_h[(rb + m) * HS + c];
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int i = m - j;
-                if (i >= 0 && i < FW) acc[j] = fma_(v, k[i], acc[j]);
-            }
-        }
-        if (x < W) {
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int y = y0 + rb + j;
-                if (y < H) {
-                    d[(long long)y * W + x] = acc[j];
-                    // DownsampleKernel<1> (ProgramCU.cu:287-298) of this level into the next
-                    // octave's level 0: dst(r, c) = src(2r, min(2c, W-1)).
-                    if (dd && !(y & 1) && (y >> 1) < dsh) {
-                        float* drow = dd + (long long)(y >> 1) * dsw;
-                        if (!(x & 1) && (x >> 1) < dsw) drow[x >> 1] = acc[j];
-                        if (x == W - 1)
-                            for (int cc = W >> 1; cc < dsw; cc++) drow[cc] = acc[j];
-                    }
-                }
-            }
-        }
-    }
-}
-
-// ------------------------------------------------------------------------------------------
-// Gaussian level, strip-streaming form (the shipped one).  A workgroup owns a 64-column strip
-// of `rows_per_strip` output rows and walks it top to bottom in chunks of SR = 16 rows:
-//   * the input rows of chunk c+1 are loaded into registers while chunk c is filtered
-//     (register-staged prefetch, written to LDS after the next barrier), so HBM loads overlap
-//     the filter arithmetic instead of alternating with it;
-//   * the horizontal pass writes 16 filtered rows into a ring of (D+1)*16 rows in LDS,
-//     D = ceil((FW-1)/16); the vertical pass emits output chunk c-D from the ring;
-//   * every input row is read once per strip (vertical halo (FW-1)/rows_per_strip), the
-//     horizontal halo (FW-1)/64 goes through L2; ~12-25 KB of LDS, 4-6 workgroups per CU.
-// Arithmetic and clamping are exactly those of k_gauss (taps summed i = 0..FW-1 with fma).
-constexpr int SR = 16;
-
-template <int FW, bool U8>
-__global__ __launch_bounds__(256) void k_gauss_strip(
-    const float* __restrict__ src, const uint8_t* __restrict__ src8, int src_stride,
-    long long src_img_stride, float* __restrict__ dst, long long dst_img_stride, int W, int H,
-    Taps taps, float* __restrict__ ds, int dsw, int dsh, long long ds_img_stride,
-    int rows_per_strip) {
-    constexpr int HALF = FW >> 1;
-    constexpr int NV4 = (FW + 3 + 3) / 4;
-    constexpr int IN_S = 60 + 4 * NV4;               // >= 64 + FW - 1, multiple of 4
-    constexpr int D = (FW - 1 + SR - 1) / SR;        // output lag in chunks
-    constexpr int RS = (D + 1) * SR <= 32 ? 32 : 64;  // ring rows (power of two >= (D+1)*SR)
-    constexpr int HS = GT + 1;
-    constexpr int NLD = (SR * IN_S + 255) / 256;     // staged elements per thread per chunk
-    __shared__ __attribute__((aligned(16))) float s_in[2][SR * IN_S];
-    __shared__ float s_h[RS * HS];
-
-    const int tid = threadIdx.x;
-    const int strips_x = (W + GT - 1) / GT;
-    const int strips_y = (H + rows_per_strip - 1) / rows_per_strip;
-    const int id = blockIdx.x;
-    const int sx = id % strips_x, rest = id / strips_x;
-    const int sy = rest % strips_y, b = rest / strips_y;
-    const int x0 = sx * GT;
-    const int yb = sy * rows_per_strip;
-    const int ye = min(H, yb + rows_per_strip);
-    const int nin = (ye - yb) + FW - 1;              // input rows of this strip
-    const int nchunk_in = (nin + SR - 1) / SR;
-    const int nchunk_out = (ye - yb + SR - 1) / SR;
-
-    const float* sf = U8 ? nullptr : src + (long long)b * src_img_stride;
-    const uint8_t* s8 = U8 ? src8 + (long long)b * src_img_stride : nullptr;
-    float stage[NLD];
-    auto load_chunk = [&](int c) {
-#pragma unroll
-        for (int m = 0; m < NLD; m++) {
-            const int e = tid + 256 * m;
-            const int r = e / IN_S, col = e - r * IN_S;
-            const int gy = clampi(yb - HALF + c * SR + r, 0, H - 1);
-            const int gx = clampi(x0 - HALF + col, 0, W - 1);
-            if (e < SR * IN_S) {
-                if (U8) stage[m] = (float)s8[(long long)gy * src_stride + gx] / 255.0f;
-                else stage[m] = sf[(long long)gy * src_stride + gx];
-            }
-        }
-    };
-    auto store_chunk = [&](int buf) {
-#pragma unroll
-        for (int m = 0; m < NLD; m++) {
-            const int e = tid + 256 * m;
-            if (e < SR * IN_S) s_in[buf][e] = stage[m];
-        }
-    };
-
-    float k[FW];
-#pragma unroll
-    for (int i = 0; i < FW; i++) k[i] = taps.k[i];
-
-    load_chunk(0);
-    store_chunk(0);
-    __syncthreads();
-    float* d = dst + (long long)b * dst_img_stride;
-    float* dd = ds ? ds + (long long)b * ds_img_stride : nullptr;
-    const int c0 = (tid & 15) * 4, hr = tid >> 4;     // H pass: row hr, outputs c0..c0+3
-    const int vc = tid & 63, vr = (tid >> 6) * 4;      // V pass: column vc, rows vr..vr+3
-    const int x = x0 + vc;
-    for (int c = 0; c < nchunk_out + D; c++) {
-        const bool has_in = c < nchunk_in, has_next = c + 1 < nchunk_in;
-        if (has_next) load_chunk(c + 1);
-        if (has_in) {   // H pass of input chunk c -> ring rows c*SR .. c*SR+15
-            const float4* row = reinterpret_cast<const float4*>(&s_in[c & 1][hr * IN_S + c0]);
-            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-#pragma unroll
-            for (int q = 0; q < NV4; q++) {
-                const float4 v4 = row[q];
-                const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const int m = q * 4 + e;
-                    const float v = vv[e];
-                    if (m < FW) a0 = fma_(v, k[m], a0);
-                    if (m >= 1 && m - 1 < FW) a1 = fma_(v, k[m - 1], a1);
-                    if (m >= 2 && m - 2 < FW) a2 = fma_(v, k[m - 2], a2);
-                    if (m >= 3 && m - 3 < FW) a3 = fma_(v, k[m - 3], a3);
-                }
-            }
-            float* o = &s_h[((c * SR + hr) & (RS - 1)) * HS + c0];
-            o[0] = a0; o[1] = a1; o[2] = a2; o[3] = a3;
-        }
-        __syncthreads();
-        const int kout = c - D;
-        if (kout >= 0) {   // V pass of output chunk kout: needs ring rows kout*SR .. +SR+FW-2
-            const int t0 = kout * SR + vr;
-            float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int m = 0; m < FW + 3; m++) {
-                const float v = s_h[((t0 + m) & (RS - 1)) * HS + vc];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int i = m - j;
-                    if (i >= 0 && i < FW) acc[j] = fma_(v, k[i], acc[j]);
-                }
-            }
-            if (x < W) {
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int y = yb + t0 + j;
-                    if (y < ye) {
-                        d[(long long)y * W + x] = acc[j];
-                        // DownsampleKernel<1> (ProgramCU.cu:287-298) into the next octave's
-                        // level 0: dst(r, c) = src(2r, min(2c, W-1)).
-                        if (dd && !(y & 1) && (y >> 1) < dsh) {
-                            float* drow = dd + (long long)(y >> 1) * dsw;
-                            if (!(x & 1) && (x >> 1) < dsw) drow[x >> 1] = acc[j];
-                            if (x == W - 1)
-                                for (int cc = W >> 1; cc < dsw; cc++) drow[cc] = acc[j];
-                        }
-                    }
-                }
-            }
-        }
-        if (has_next) store_chunk((c + 1) & 1);
-        __syncthreads();
-    }
-}
-
-// ------------------------------------------------------------------------------------------
-// Gaussian level, strip-streaming with packed FP32 (the shipped form).  Same strip walk,
-// register-staged prefetch and LDS ring as k_gauss_strip, but every FMA is a v_pk_fma_f32 on
-// two independent outputs, which halves the VALU issue of the filter (gfx950 runs packed FP32 at
-// twice the scalar rate):
-//   * the input chunk is stored in LDS as row PAIRS, s_in[pair][col] = (row 2p, row 2p+1), so
-//     the H pass of a thread (rows 2p, 2p+1; columns c, c+1) reads two float2 per ds_read_b128
-//     and issues pk_fma((in[2p][c+k], in[2p+1][c+k]), k[k], acc_c) -- 2*FW packed FMAs for 4
-//     outputs;
-//   * the V pass of a thread (columns c, c+1; rows r, r+1) reads float2 ring rows and issues
-//     pk_fma((h[r+k][c], h[r+k][c+1]), k[k], acc_r) -- again 2*FW for 4 outputs, and its stores
-//     are float2.
-// Each packed lane is an IEEE fma: the sums are bit-identical to k_gauss / the oracle.
 typedef float f2v __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2v pk_fma(f2v a, float b, f2v c) {
@@ -348,142 +58,6 @@ __device__ __forceinline__ float u8_to_unit(uint32_t p) {
     return fma_(fma_(-q, 255.0f, x), c, q);
 }
 
-template <int FW, bool U8>
-__global__ __launch_bounds__(256) void k_gauss_pk(
-    const float* __restrict__ src, const uint8_t* __restrict__ src8, int src_stride,
-    long long src_img_stride, float* __restrict__ dst, long long dst_img_stride, int W, int H,
-    Taps taps, float* __restrict__ ds, int dsw, int dsh, long long ds_img_stride,
-    int rows_per_strip) {
-    constexpr int HALF = FW >> 1;
-    constexpr int IN_W = GT + FW - 1;                 // input columns of a strip
-    constexpr int NRD = (FW + 1) / 2;                 // ds_read_b128 per H-pass thread
-    constexpr int IN_S = (GT + FW + 1 + 3) & ~3;      // float2 per row pair (>= 64 + FW + 1)
-    constexpr int D = (FW - 1 + SR - 1) / SR;         // output lag in chunks
-    constexpr int RS = (D + 1) * SR <= 32 ? 32 : 64;  // ring rows (power of two)
-    constexpr int HS = GT + 4;                        // ring row stride (floats)
-    constexpr int NLD = ((SR / 2) * IN_W + 255) / 256;   // staged row-pair elements per thread
-    __shared__ __attribute__((aligned(16))) f2v s_in[2][(SR / 2) * IN_S];
-    __shared__ __attribute__((aligned(16))) float s_h[RS * HS];
-
-    const int tid = threadIdx.x;
-    const int strips_x = (W + GT - 1) / GT;
-    const int strips_y = (H + rows_per_strip - 1) / rows_per_strip;
-    const int id = blockIdx.x;
-    const int sx = id % strips_x, rest = id / strips_x;
-    const int sy = rest % strips_y, b = rest / strips_y;
-    const int x0 = sx * GT;
-    const int yb = sy * rows_per_strip;
-    const int ye = min(H, yb + rows_per_strip);
-    const int nin = (ye - yb) + FW - 1;
-    const int nchunk_in = (nin + SR - 1) / SR;
-    const int nchunk_out = (ye - yb + SR - 1) / SR;
-
-    const float* sf = U8 ? nullptr : src + (long long)b * src_img_stride;
-    const uint8_t* s8 = U8 ? src8 + (long long)b * src_img_stride : nullptr;
-    // two register stages: chunk c+1 waits in one while chunk c+2 is in flight in the other
-    f2v stA[NLD], stB[NLD];
-    auto load_chunk = [&](f2v (&stage)[NLD], int c) {
-#pragma unroll
-        for (int m = 0; m < NLD; m++) {
-            const int e = min(tid + 256 * m, (SR / 2) * IN_W - 1);
-            const int p = e / IN_W, col = e - p * IN_W;
-            const int gy0 = clampi(yb - HALF + c * SR + 2 * p, 0, H - 1);
-            const int gy1 = clampi(yb - HALF + c * SR + 2 * p + 1, 0, H - 1);
-            const int gx = clampi(x0 - HALF + col, 0, W - 1);
-            if (U8) {
-                stage[m] = f2v{u8_to_unit(s8[(long long)gy0 * src_stride + gx]),
-                               u8_to_unit(s8[(long long)gy1 * src_stride + gx])};
-            } else {
-                stage[m] = f2v{sf[(long long)gy0 * src_stride + gx],
-                               sf[(long long)gy1 * src_stride + gx]};
-            }
-        }
-    };
-    auto store_chunk = [&](const f2v (&stage)[NLD], int buf) {
-#pragma unroll
-        for (int m = 0; m < NLD; m++) {
-            const int e = tid + 256 * m;
-            if (e < (SR / 2) * IN_W) {
-                const int p = e / IN_W, col = e - p * IN_W;
-                s_in[buf][p * IN_S + col] = stage[m];
-            }
-        }
-    };
-
-    load_chunk(stA, 0);
-    store_chunk(stA, 0);
-    if (1 < nchunk_in) load_chunk(stA, 1);
-    __syncthreads();
-    float* d = dst + (long long)b * dst_img_stride;
-    float* dd = ds ? ds + (long long)b * ds_img_stride : nullptr;
-    const int pr = tid >> 5, pc = (tid & 31) * 2;     // rows 2pr, 2pr+1; columns pc, pc+1
-    const int x = x0 + pc;
-    // iteration c: chunk c is in LDS, chunk c+1 in `cur` registers; load chunk c+2 into `nxt`
-    auto step = [&](int c, f2v (&cur)[NLD], f2v (&nxt)[NLD]) {
-        const bool has_in = c < nchunk_in, has_next = c + 1 < nchunk_in;
-        if (c + 2 < nchunk_in) load_chunk(nxt, c + 2);
-        if (has_in) {   // H pass of input chunk c -> ring rows c*SR .. c*SR+15
-            const float4* row = reinterpret_cast<const float4*>(&s_in[c & 1][pr * IN_S + pc]);
-            f2v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};   // column pc / pc+1, (row 2pr, row 2pr+1)
-#pragma unroll
-            for (int q = 0; q < NRD; q++) {
-                const float4 v = row[q];             // pair columns pc+2q, pc+2q+1
-                const f2v e0 = {v.x, v.y}, e1 = {v.z, v.w};
-                const int m0 = 2 * q, m1 = 2 * q + 1;
-                if (m0 < FW) a0 = pk_fma(e0, taps.k[m0], a0);
-                if (m0 >= 1 && m0 - 1 < FW) a1 = pk_fma(e0, taps.k[m0 - 1], a1);
-                if (m1 < FW) a0 = pk_fma(e1, taps.k[m1], a0);
-                if (m1 - 1 < FW) a1 = pk_fma(e1, taps.k[m1 - 1], a1);
-            }
-            const int r0 = (c * SR + 2 * pr) & (RS - 1);
-            *reinterpret_cast<f2v*>(&s_h[r0 * HS + pc]) = f2v{a0.x, a1.x};
-            *reinterpret_cast<f2v*>(&s_h[(r0 + 1) * HS + pc]) = f2v{a0.y, a1.y};
-        }
-        __syncthreads();
-        const int kout = c - D;
-        if (kout >= 0) {   // V pass of output chunk kout
-            const int t0 = kout * SR + 2 * pr;
-            f2v acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};   // row t0 / t0+1, (col pc, col pc+1)
-#pragma unroll
-            for (int m = 0; m <= FW; m++) {
-                const f2v v = *reinterpret_cast<const f2v*>(&s_h[((t0 + m) & (RS - 1)) * HS + pc]);
-                if (m < FW) acc0 = pk_fma(v, taps.k[m], acc0);
-                if (m >= 1) acc1 = pk_fma(v, taps.k[m - 1], acc1);
-            }
-            if (x < W) {
-#pragma unroll
-                for (int j = 0; j < 2; j++) {
-                    const int y = yb + t0 + j;
-                    const f2v a = j ? acc1 : acc0;
-                    if (y < ye) {
-                        *reinterpret_cast<f2v*>(&d[(long long)y * W + x]) = a;
-                        // DownsampleKernel<1> (ProgramCU.cu:287-298) into the next octave's
-                        // level 0: dst(r, c) = src(2r, min(2c, W-1)); x is even, W is even.
-                        if (dd && !(y & 1) && (y >> 1) < dsh) {
-                            float* drow = dd + (long long)(y >> 1) * dsw;
-                            if ((x >> 1) < dsw) drow[x >> 1] = a.x;
-                            if (x + 1 == W - 1)
-                                for (int cc = W >> 1; cc < dsw; cc++) drow[cc] = a.y;
-                        }
-                    }
-                }
-            }
-        }
-        if (has_next) store_chunk(cur, (c + 1) & 1);
-        __syncthreads();
-    };
-    const int nsteps = nchunk_out + D;
-    for (int c = 0; c < nsteps; c += 2) {
-        step(c, stA, stB);
-        if (c + 1 < nsteps) step(c + 1, stB, stA);
-    }
-}
-
-// k_gauss_pk with 32-row chunks and 8 outputs per thread per pass (the shipped form).  A
-// thread's H pass covers 2 rows x 4 columns and its V pass 4 rows x 2 columns, so every value
-// read from LDS feeds 4 (instead of 2) packed FMAs: LDS traffic per output is halved and stays
-// below the FMA issue time even at FW = 25.  One s_in buffer suffices: the next chunk is
-// written after the V pass, when the H pass has finished reading.
 constexpr int SR2 = 32;
 
 // VEC: the input rows are fetched as 16-byte (f32) / 4-byte (u8) aligned quads instead of one
@@ -551,17 +125,8 @@ __global__ __launch_bounds__(256) void k_gauss_pk2(
                         r1[t] = u8_to_unit((w1 >> (8 * t)) & 255u);
                     }
                 } else {
-                    float4 v0, v1;
-                    if (g_variant & 262144) {   // test hook: non-temporal loads (25 % slower)
-                        typedef float nt4 __attribute__((ext_vector_type(4)));
-                        const nt4 a = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(sf + (long long)gy0 * src_stride + lq));
-                        const nt4 c = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(sf + (long long)gy1 * src_stride + lq));
-                        v0 = make_float4(a.x, a.y, a.z, a.w);
-                        v1 = make_float4(c.x, c.y, c.z, c.w);
-                    } else {
-                        v0 = *reinterpret_cast<const float4*>(sf + (long long)gy0 * src_stride + lq);
-                        v1 = *reinterpret_cast<const float4*>(sf + (long long)gy1 * src_stride + lq);
-                    }
+                    const float4 v0 = *reinterpret_cast<const float4*>(sf + (long long)gy0 * src_stride + lq);
+                    const float4 v1 = *reinterpret_cast<const float4*>(sf + (long long)gy1 * src_stride + lq);
                     r0[0] = v0.x; r0[1] = v0.y; r0[2] = v0.z; r0[3] = v0.w;
                     r1[0] = v1.x; r1[1] = v1.y; r1[2] = v1.z; r1[3] = v1.w;
                 }
@@ -623,9 +188,6 @@ __global__ __launch_bounds__(256) void k_gauss_pk2(
         if (has_in) {   // H pass of input chunk c -> ring rows c*SR2 .. c*SR2+31
             const f2v* rowp = &s_in[hp * IN_SV + hc + OFF];
             f2v a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};   // columns hc+i
-            if (g_variant & 128) {   // timing probe only: same memory traffic, no filter
-                a[0] = rowp[HALF]; a[1] = rowp[HALF + 1]; a[2] = rowp[HALF + 2]; a[3] = rowp[HALF + 3];
-            } else {
 #pragma unroll
             for (int q = 0; q < NRD; q++) {
                 f2v e[2];                            // pair columns hc+2q, hc+2q+1
@@ -645,7 +207,6 @@ __global__ __launch_bounds__(256) void k_gauss_pk2(
                         if (m - i >= 0 && m - i < FW) a[i] = pk_fma(e[u], taps.k[m - i], a[i]);
                 }
             }
-            }
             const int r0 = (c * SR2 + 2 * hp) & (RS - 1);
             *reinterpret_cast<float4*>(&s_h[r0 * HS + hc]) = make_float4(a[0].x, a[1].x, a[2].x, a[3].x);
             *reinterpret_cast<float4*>(&s_h[(r0 + 1) * HS + hc]) = make_float4(a[0].y, a[1].y, a[2].y, a[3].y);
@@ -655,11 +216,6 @@ __global__ __launch_bounds__(256) void k_gauss_pk2(
         if (kout >= 0) {   // V pass of output chunk kout (lag 1 chunk: FW - 1 <= SR2)
             const int t0 = kout * SR2 + 4 * vq;
             f2v acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};   // rows t0+j
-            if (g_variant & 128) {   // timing probe only
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    acc[j] = *reinterpret_cast<const f2v*>(&s_h[((t0 + j + HALF) & (RS - 1)) * HS + vc]);
-            } else {
 #pragma unroll
             for (int m = 0; m < FW + 3; m++) {
                 const f2v v = *reinterpret_cast<const f2v*>(&s_h[((t0 + m) & (RS - 1)) * HS + vc]);
@@ -667,16 +223,12 @@ __global__ __launch_bounds__(256) void k_gauss_pk2(
                 for (int j = 0; j < 4; j++)
                     if (m - j >= 0 && m - j < FW) acc[j] = pk_fma(v, taps.k[m - j], acc[j]);
             }
-            }
             if (x < W) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const int y = yb + t0 + j;
                     if (y < ye) {
-                        if (g_variant & 131072)   // test hook: non-temporal stores (no effect)
-                            __builtin_nontemporal_store(acc[j], reinterpret_cast<f2v*>(&d[(long long)y * W + x]));
-                        else
-                            *reinterpret_cast<f2v*>(&d[(long long)y * W + x]) = acc[j];
+                        *reinterpret_cast<f2v*>(&d[(long long)y * W + x]) = acc[j];
                         // DownsampleKernel<1> (ProgramCU.cu:287-298) into the next octave's
                         // level 0: dst(r, c) = src(2r, min(2c, W-1)); x is even, W is even.
                         if (dd && !(y & 1) && (y >> 1) < dsh) {
@@ -704,81 +256,32 @@ hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
                           long long src_img_stride, float* dst, long long dst_img_stride, int w,
                           int h, const Taps& taps, int batch, float* ds, int dsw, int dsh,
                           long long ds_img_stride, hipStream_t stream) {
-    if (!(g_host_variant & 8)) {
-        // strips: enough workgroups for ~8 per CU, strip height a multiple of SR
-        const int strips_x = (w + GT - 1) / GT;
-        const long long per_col = (long long)strips_x * batch;
-        int nsy = (int)std::min<long long>((2048 + per_col - 1) / per_col, (h + SR - 1) / SR);
-        nsy = std::max(nsy, 1);
-        int rows = (h + nsy - 1) / nsy;
-        rows = (rows + SR - 1) / SR * SR;
-        nsy = (h + rows - 1) / rows;
-        dim3 grid((unsigned)(strips_x * nsy * batch));
-        if (!(g_host_variant & (32 | 64))) {
-            // 32-row chunks: bands of at most 17 chunks (544 rows), and at least 1024 workgroups
-            // when the image is short (kernel traces: 2 bands of 540 rows beat 1 band of 1080 on
-            // 1080p, and 1 band beats 2 on the 540- and 270-row octaves).  Test hook: variant 512
-            // restores the former rule (about 2048 workgroups).
-            int nsy2;
-            if (g_host_variant & 512) {
-                nsy2 = (int)std::min<long long>((2048 + per_col - 1) / per_col, (h + SR2 - 1) / SR2);
-            } else {
-                nsy2 = (h + 17 * SR2 - 1) / (17 * SR2);
-                const int need = (int)std::min<long long>((1024 + per_col - 1) / per_col, (h + SR2 - 1) / SR2);
-                nsy2 = std::max(nsy2, need);
-            }
-            nsy2 = std::max(nsy2, 1);
-            int rows2 = (h + nsy2 - 1) / nsy2;
-            rows2 = (rows2 + SR2 - 1) / SR2 * SR2;
-            nsy2 = (h + rows2 - 1) / rows2;
-            dim3 grid2((unsigned)(strips_x * nsy2 * batch));
-            // aligned quads need 4-element row strides and image strides, a 16-B aligned base
-            // and a width that is a multiple of 4 (always true for pyramid levels)
-            const bool vec = !(g_host_variant & 256) && (src_stride % 4) == 0 &&
-                             (src_img_stride % 4) == 0 && (w % 4) == 0 && w >= 4 &&
-                             ((uintptr_t)(src8 ? (const void*)src8 : (const void*)src) % 16) == 0;
+    // bands of at most 17 chunks (544 rows), and at least 1024 workgroups when the image is
+    // short (kernel traces: 2 bands of 540 rows beat 1 band of 1080 on 1080p, and 1 band beats 2
+    // on the 540- and 270-row octaves)
+    const int strips_x = (w + GT - 1) / GT;
+    const long long per_col = (long long)strips_x * batch;
+    int nsy = (h + 17 * SR2 - 1) / (17 * SR2);
+    const int need = (int)std::min<long long>((1024 + per_col - 1) / per_col, (h + SR2 - 1) / SR2);
+    nsy = std::max(std::max(nsy, need), 1);
+    int rows = (h + nsy - 1) / nsy;
+    rows = (rows + SR2 - 1) / SR2 * SR2;
+    nsy = (h + rows - 1) / rows;
+    const dim3 grid((unsigned)(strips_x * nsy * batch));
+    // aligned quads need 4-element row strides and image strides, a 16-B aligned base and a
+    // width that is a multiple of 4 (always true for pyramid levels)
+    const bool vec = (src_stride % 4) == 0 && (src_img_stride % 4) == 0 && (w % 4) == 0 &&
+                     w >= 4 && ((uintptr_t)(src8 ? (const void*)src8 : (const void*)src) % 16) == 0;
 #define SGK_PK2(U8, VEC)                                                                   \
-    hipLaunchKernelGGL((k_gauss_pk2<FW, U8, VEC>), grid2, dim3(256), 0, stream, src, src8,   \
+    hipLaunchKernelGGL((k_gauss_pk2<FW, U8, VEC>), grid, dim3(256), 0, stream, src, src8,    \
                        src_stride, src_img_stride, dst, dst_img_stride, w, h, taps, ds, dsw,  \
-                       dsh, ds_img_stride, rows2)
-            if (src8) {
-                if (vec) SGK_PK2(true, true); else SGK_PK2(true, false);
-            } else {
-                if (vec) SGK_PK2(false, true); else SGK_PK2(false, false);
-            }
-#undef SGK_PK2
-            return hipGetLastError();
-        }
-        if (!(g_host_variant & 32)) {
-            if (src8)
-                hipLaunchKernelGGL((k_gauss_pk<FW, true>), grid, dim3(256), 0, stream, src, src8,
-                                   src_stride, src_img_stride, dst, dst_img_stride, w, h, taps,
-                                   ds, dsw, dsh, ds_img_stride, rows);
-            else
-                hipLaunchKernelGGL((k_gauss_pk<FW, false>), grid, dim3(256), 0, stream, src,
-                                   src8, src_stride, src_img_stride, dst, dst_img_stride, w, h,
-                                   taps, ds, dsw, dsh, ds_img_stride, rows);
-            return hipGetLastError();
-        }
-        if (src8)
-            hipLaunchKernelGGL((k_gauss_strip<FW, true>), grid, dim3(256), 0, stream, src, src8,
-                               src_stride, src_img_stride, dst, dst_img_stride, w, h, taps, ds,
-                               dsw, dsh, ds_img_stride, rows);
-        else
-            hipLaunchKernelGGL((k_gauss_strip<FW, false>), grid, dim3(256), 0, stream, src, src8,
-                               src_stride, src_img_stride, dst, dst_img_stride, w, h, taps, ds,
-                               dsw, dsh, ds_img_stride, rows);
-        return hipGetLastError();
+                       dsh, ds_img_stride, rows)
+    if (src8) {
+        if (vec) SGK_PK2(true, true); else SGK_PK2(true, false);
+    } else {
+        if (vec) SGK_PK2(false, true); else SGK_PK2(false, false);
     }
-    dim3 grid(((w + GT - 1) / GT) * ((h + GT - 1) / GT) * batch);
-    if (src8)
-        hipLaunchKernelGGL((k_gauss<FW, true>), grid, dim3(256), 0, stream, src, src8,
-                           src_stride, src_img_stride, dst, dst_img_stride, w, h, taps, ds, dsw,
-                           dsh, ds_img_stride);
-    else
-        hipLaunchKernelGGL((k_gauss<FW, false>), grid, dim3(256), 0, stream, src, src8,
-                           src_stride, src_img_stride, dst, dst_img_stride, w, h, taps, ds, dsw,
-                           dsh, ds_img_stride);
+#undef SGK_PK2
     return hipGetLastError();
 }
 
@@ -863,245 +366,6 @@ __device__ __forceinline__ KeyOut key_test(Get get, float t0, float t, float edg
     if (ok) o.result = v > nmax ? 1.0f : -1.0f;
     o.dx = dx; o.dy = dy; o.ds = ds;
     return o;
-}
-
-// ------------------------------------------------------------------------------------------
-// Extremum detection for one octave: tile 64 x 16 pixels, all d DoG levels.  The d+2 DoG
-// planes (with a 1-pixel halo) are formed in LDS from the d+3 Gaussian planes: D_m = G_m -
-// G_{m-1} (ComputeDOG_Kernel, ProgramCU.cu:494).  Each wave covers 64 consecutive columns of a
-// row, so a ballot is directly the 64-bit mask of that row segment.
-constexpr int ET_X = 64, ET_Y = 16, ES = ET_X + 3;
-
-template <int ND>   // ND = number of DoG planes = d + 2
-__global__ __launch_bounds__(256) void k_extrema(const float* __restrict__ pyr,
-                                                 uint32_t* __restrict__ mask,
-                                                 uint32_t* __restrict__ row_count,
-                                                 const FeatureParams fp, int o) {
-    __shared__ float s_d[ND * (ET_Y + 2) * ES];
-    const OctaveDesc& od = fp.oct[o];
-    const int W = od.wa, H = od.h;
-    const int tid = threadIdx.x;
-    // XCD-aware tile order (as k_gauss): neighbouring tiles share halo rows in one L2
-    const int tiles_x = (W + ET_X - 1) / ET_X, tiles_y = (H + ET_Y - 1) / ET_Y;
-    int wid = blockIdx.x;
-    if (g_variant & 4) {
-        const int nwg = gridDim.x, id = blockIdx.x, xcd = id & 7, q = nwg >> 3, r = nwg & 7;
-        wid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
-    }
-    const int bx = wid % tiles_x, rest = wid / tiles_x;
-    const int by = rest % tiles_y, b = rest / tiles_y;
-    const int x0 = bx * ET_X, y0 = by * ET_Y;
-    const long long npx = (long long)W * H;
-    const float* g0 = pyr + od.gauss_off + (long long)b * npx;
-    const int lane = tid & 63, wave = tid >> 6;
-    // each wave streams whole halo rows; the ND+1 Gaussian planes are loaded together
-    for (int ty = wave; ty < ET_Y + 2; ty += 4) {
-        const int gy = y0 - 1 + ty;
-        for (int tx = lane; tx < ET_X + 2; tx += 64) {
-            const int gx = x0 - 1 + tx;
-            const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
-            const long long p = (long long)gy * W + gx;
-            float gv[ND + 1];
-#pragma unroll
-            for (int m = 0; m <= ND; m++) gv[m] = in ? g0[p + m * od.level_stride] : 0.f;
-#pragma unroll
-            for (int m = 1; m <= ND; m++)
-                s_d[(m - 1) * (ET_Y + 2) * ES + ty * ES + tx] = gv[m] - gv[m - 1];
-        }
-    }
-    __syncthreads();
-    const int x = x0 + lane;
-    for (int rr = 0; rr < 4; rr++) {
-        const int ly = wave * 4 + rr;
-        const int y = y0 + ly;
-        if (y >= H) break;
-        const bool interior = x > 0 && x < W - 1 && y > 0 && y < H - 1;
-        for (int j = 0; j < ND - 2; j++) {
-            bool flag = false;
-            if (interior) {
-                const float* base = s_d + j * (ET_Y + 2) * ES + (ly + 1) * ES + (lane + 1);
-                auto get = [&](int m, int r, int c) {
-                    return base[m * (ET_Y + 2) * ES + (r - 1) * ES + (c - 1)];
-                };
-                KeyOut k = key_test(get, fp.t0, fp.t, fp.edge, fp.subpixel);
-                flag = k.result != 0.f;
-            }
-            const unsigned long long bal = __ballot(flag);
-            if (lane == 0) {
-                uint32_t* mrow = mask + od.mask_off + j * od.mask_level_stride +
-                                 ((long long)b * H + y) * od.nwords;
-                const int w0 = x0 >> 5;
-                mrow[w0] = (uint32_t)bal;
-                if (w0 + 1 < od.nwords) mrow[w0 + 1] = (uint32_t)(bal >> 32);
-                const int cnt = __popcll(bal);
-                if (cnt)
-                    atomicAdd(&row_count[(long long)b * fp.rows_per_image + fp.row_off[o] +
-                                         j * H + y],
-                              (uint32_t)cnt);
-            }
-        }
-    }
-}
-
-// Extremum detection, strip-pipelined form (the shipped one): a workgroup walks a 64-column
-// strip tile by tile (64 x 16 pixels + 1-pixel halo); the ND+1 Gaussian planes of tile t+1 are
-// loaded into registers while tile t is evaluated from LDS, so HBM loads overlap the tests.
-// Same DoG arithmetic (D_m = G_m - G_{m-1}), same key_test, same mask / count outputs.
-// All octaves in one launch: workgroups [block0[o], block0[o+1]) cover octave o, largest
-// first, so the small octaves fill the tail of the big one instead of paying their own launch
-// ramp-up and tail.
-struct ExtremaGrid {
-    int block0[kMaxOctaves + 1];
-    int rows_per_strip[kMaxOctaves];
-};
-
-template <int ND>   // ND = number of DoG planes = d + 2
-__global__ __launch_bounds__(256) void k_extrema_strip(const float* __restrict__ pyr,
-                                                       uint32_t* __restrict__ mask,
-                                                       uint32_t* __restrict__ row_count,
-                                                       const FeatureParams fp,
-                                                       const ExtremaGrid eg) {
-    int o = 0;
-    while (o + 1 < fp.n_octaves && (int)blockIdx.x >= eg.block0[o + 1]) o++;
-    const int rows_per_strip = eg.rows_per_strip[o];
-    const int bid = blockIdx.x - eg.block0[o];
-    constexpr int PLANE = (ET_Y + 2) * ES;
-    __shared__ float s_d[ND * PLANE];
-    __shared__ uint16_t s_list[4 * 4 * (ND - 2) * 64];   // per-wave candidate lists
-    const OctaveDesc& od = fp.oct[o];
-    const int W = od.wa, H = od.h;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int strips_x = (W + ET_X - 1) / ET_X;
-    const int strips_y = (H + rows_per_strip - 1) / rows_per_strip;
-    const int sx = bid % strips_x, rest = bid / strips_x;
-    const int sy = rest % strips_y, b = rest / strips_y;
-    const int x0 = sx * ET_X, yb = sy * rows_per_strip, ye = min(H, yb + rows_per_strip);
-    const int ntiles = (ye - yb + ET_Y - 1) / ET_Y;
-    const long long npx = (long long)W * H;
-    const long long lstride = od.level_stride;
-    const float* g0 = pyr + od.gauss_off + (long long)b * npx;
-    // Row-aligned loads: each wave instruction reads one aligned 64-float row segment of a plane
-    // (2 cache lines) -- wave w takes tile rows w, w+4, ... -- and 36 lanes fetch the two halo
-    // columns of the 18 rows.  Every thread keeps the same (row, column) slot for all d+3
-    // planes, so it forms the DoG differences itself.  Loads are unconditional (coordinates
-    // clamped into the image): halo positions outside the image are only ever neighbours of
-    // non-interior pixels, whose tests are skipped.
-    constexpr int NR = (ET_Y + 2 + 3) / 4;          // row slots per wave (5 for 18 rows)
-    float stage[NR][ND + 1], stage_h[ND + 1];
-    const bool has_h = tid < 2 * (ET_Y + 2);
-    const int h_ty = tid >> 1, h_tx = (tid & 1) ? ET_X + 1 : 0;
-    auto load_tile = [&](int t) {
-        const int y0 = yb + t * ET_Y;
-        const int gx = min(x0 + lane, W - 1);
-#pragma unroll
-        for (int r = 0; r < NR; r++) {
-            const int ty = min(wave + 4 * r, ET_Y + 1);
-            const int gy = clampi(y0 - 1 + ty, 0, H - 1);
-            const float* q = g0 + (long long)gy * W + gx;
-#pragma unroll
-            for (int mm = 0; mm <= ND; mm++) stage[r][mm] = q[mm * lstride];
-        }
-        const int hy = clampi(y0 - 1 + min(h_ty, ET_Y + 1), 0, H - 1);
-        const int hx = clampi(x0 - 1 + h_tx, 0, W - 1);
-        const float* q = g0 + (long long)hy * W + hx;
-#pragma unroll
-        for (int mm = 0; mm <= ND; mm++) stage_h[mm] = q[mm * lstride];
-    };
-    auto store_tile = [&]() {
-#pragma unroll
-        for (int r = 0; r < NR; r++) {
-            const int ty = wave + 4 * r;
-            if (ty < ET_Y + 2) {
-#pragma unroll
-                for (int mm = 1; mm <= ND; mm++)
-                    s_d[(mm - 1) * PLANE + ty * ES + lane + 1] = stage[r][mm] - stage[r][mm - 1];
-            }
-        }
-        if (has_h) {
-#pragma unroll
-            for (int mm = 1; mm <= ND; mm++)
-                s_d[(mm - 1) * PLANE + h_ty * ES + h_tx] = stage_h[mm] - stage_h[mm - 1];
-        }
-    };
-    load_tile(0);
-    store_tile();
-    __syncthreads();
-    const int x = x0 + lane;
-    constexpr int NJ = ND - 2;
-    uint16_t* list = s_list + wave * (4 * NJ * 64);
-    for (int t = 0; t < ntiles; t++) {
-        const bool has_next = t + 1 < ntiles;
-        if (has_next) load_tile(t + 1);
-        const int y0 = yb + t * ET_Y;
-        // (1) Branch-free pre-filter.  key_test accepts only pixels with |v| > t0 that are >= or
-        // <= all 26 neighbours (its tie rules are stricter), so "v is the max or the min of its
-        // 3x3x3 block" is a superset of its accept set.  Per plane: 3-wide row max/min of the
-        // six LDS rows this wave's four rows touch, then 3-high column max/min.
-        float vmx[ND][4], vmn[ND][4], cv[ND][4];
-#pragma unroll
-        for (int m = 0; m < ND; m++) {
-            float hmx[6], hmn[6];
-#pragma unroll
-            for (int k = 0; k < 6; k++) {
-                const float* p = s_d + m * PLANE + (wave * 4 + k) * ES + lane;
-                const float a = p[0], c = p[1], e = p[2];
-                hmx[k] = fmax_(fmax_(a, c), e);
-                hmn[k] = fmin_(fmin_(a, c), e);
-                if (k >= 1 && k <= 4) cv[m][k - 1] = c;
-            }
-#pragma unroll
-            for (int rr = 0; rr < 4; rr++) {
-                vmx[m][rr] = fmax_(fmax_(hmx[rr], hmx[rr + 1]), hmx[rr + 2]);
-                vmn[m][rr] = fmin_(fmin_(hmn[rr], hmn[rr + 1]), hmn[rr + 2]);
-            }
-        }
-        // (2) compact the candidates of this wave's 4 rows x NJ levels into its LDS list
-        int ncand = 0;
-#pragma unroll
-        for (int rr = 0; rr < 4; rr++) {
-            const int y = y0 + wave * 4 + rr;
-            const bool interior = x > 0 && x < W - 1 && y > 0 && y < H - 1 && y < ye;
-#pragma unroll
-            for (int j = 0; j < NJ; j++) {
-                const float v = cv[j + 1][rr];
-                const float mx = fmax_(fmax_(vmx[j][rr], vmx[j + 1][rr]), vmx[j + 2][rr]);
-                const float mn = fmin_(fmin_(vmn[j][rr], vmn[j + 1][rr]), vmn[j + 2][rr]);
-                const bool cand = interior && fabs_(v) > fp.t0 && (v >= mx || v <= mn);
-                const unsigned long long bal = __ballot(cand);
-                if (cand) {
-                    const int pos = ncand + __builtin_amdgcn_mbcnt_hi(
-                                                (uint32_t)(bal >> 32),
-                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    list[pos] = (uint16_t)((rr << 9) | (j << 6) | lane);
-                }
-                ncand += __popcll(bal);
-            }
-        }
-        // (3) the exact reference test on the compacted candidates, 64 at a time; accepted
-        // ones set their mask bit (mask zeroed beforehand) and count in their row.
-        for (int c0 = 0; c0 < ncand; c0 += 64) {
-            if (c0 + lane < ncand) {
-                const int code = list[c0 + lane];
-                const int rr = code >> 9, j = (code >> 6) & 7, cl = code & 63;
-                const int ly = wave * 4 + rr;
-                const float* base = s_d + j * PLANE + (ly + 1) * ES + (cl + 1);
-                auto get = [&](int m, int r, int c) {
-                    return base[m * PLANE + (r - 1) * ES + (c - 1)];
-                };
-                if (key_test(get, fp.t0, fp.t, fp.edge, fp.subpixel).result != 0.f) {
-                    const int y = y0 + ly, xx = x0 + cl;
-                    uint32_t* mrow = mask + od.mask_off + j * od.mask_level_stride +
-                                     ((long long)b * H + y) * od.nwords;
-                    atomicOr(&mrow[xx >> 5], 1u << (xx & 31));
-                    atomicAdd(&row_count[(long long)b * fp.rows_per_image + fp.row_off[o] +
-                                         j * H + y], 1u);
-                }
-            }
-        }
-        __syncthreads();
-        if (has_next) store_tile();
-        __syncthreads();
-    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1953,6 +1217,100 @@ __global__ __launch_bounds__(256) void k_orient_keys(const float* __restrict__ p
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Feature-count limiting (-tc / -tc2 / -tc3), per image, on the level counts in octave-major
+// order: the level skip of PyramidCU::GenerateFeatureList (PyramidCU.cpp:829-853; levels are
+// visited coarsest first for -tc2, and a level is skipped once the running count exceeds the
+// threshold) when list_stage, then SiftPyramid::LimitFeatureCount (SiftPyramid.cpp:219-260):
+// -tc3 keeps the first levels until the threshold is reached, -tc / -tc2 drop the finest levels
+// while the rest still exceeds it.
+constexpr int kMaxLimitLevels = kMaxOctaves * 8;
+
+__device__ void limit_levels(int* cnt, int nl, int T, int method, bool list_stage) {
+    if (list_stage && method != 0) {
+        int total = 0;
+        for (int q = 0; q < nl; q++) {
+            const int l = method == 1 ? nl - 1 - q : q;
+            if (total > T) cnt[l] = 0;
+            else total += cnt[l];
+        }
+    }
+    int num = 0;
+    for (int l = 0; l < nl; l++) num += cnt[l];
+    if (method == 2) {
+        int i = 0, kept = 0;
+        for (; kept < T && i < nl; ++i) kept += cnt[i];
+        for (; i < nl; ++i) cnt[i] = 0;
+    } else {
+        for (int i = 0; i < nl && num - cnt[i] > T; ++i) {
+            num -= cnt[i];
+            cnt[i] = 0;
+        }
+    }
+}
+
+__device__ __forceinline__ int level_of_row(const FeatureParams& fp, int r) {
+    int o = 0;
+    while (o + 1 < fp.n_octaves && fp.row_off[o + 1] <= r) o++;
+    return o * fp.d + (r - fp.row_off[o]) / fp.oct[o].h;
+}
+
+// Stages 1-2 on the detected keypoints: the row counts of dropped levels are zeroed before the
+// row scan, so their keypoints never enter the list.  One workgroup per image.
+__global__ __launch_bounds__(256) void k_limit_rows(uint32_t* __restrict__ row_count,
+                                                    const FeatureParams fp, int T, int method) {
+    __shared__ int s_cnt[kMaxLimitLevels];
+    const int nl = fp.n_octaves * fp.d;
+    uint32_t* rc = row_count + (size_t)blockIdx.x * fp.rows_per_image;
+    for (int l = threadIdx.x; l < nl; l += 256) s_cnt[l] = 0;
+    __syncthreads();
+    for (int r = threadIdx.x; r < fp.rows_per_image; r += 256) {
+        const uint32_t v = rc[r];
+        if (v) atomicAdd(&s_cnt[level_of_row(fp, r)], (int)v);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) limit_levels(s_cnt, nl, T, method, true);
+    __syncthreads();
+    for (int r = threadIdx.x; r < fp.rows_per_image; r += 256)
+        if (s_cnt[level_of_row(fp, r)] == 0) rc[r] = 0;
+}
+
+// Stage 3 (LimitFeatureCount(1) after ReshapeFeatureListCPU, SiftPyramid.cpp:152-160) on the
+// oriented feature counts: the counts of dropped levels' keypoints are zeroed before the
+// feature scan.  One workgroup per image.
+__global__ __launch_bounds__(256) void k_limit_oriented(uint32_t* __restrict__ ocount,
+                                                        const uint32_t* __restrict__ row_base,
+                                                        const FeatureParams fp, int T, int method,
+                                                        uint32_t cap) {
+    __shared__ int s_cnt[kMaxLimitLevels];
+    const int nl = fp.n_octaves * fp.d;
+    const size_t r0 = (size_t)blockIdx.x * fp.rows_per_image;
+    auto range = [&](int l, uint32_t& lo, uint32_t& hi) {
+        const int o = l / fp.d, j = l - o * fp.d;
+        const size_t first = r0 + fp.row_off[o] + (size_t)j * fp.oct[o].h;
+        lo = min(row_base[first], cap);
+        hi = min(row_base[first + fp.oct[o].h], cap);
+    };
+    for (int l = threadIdx.x; l < nl; l += 256) s_cnt[l] = 0;
+    __syncthreads();
+    for (int l = 0; l < nl; l++) {
+        uint32_t lo, hi;
+        range(l, lo, hi);
+        int sum = 0;
+        for (uint32_t f = lo + threadIdx.x; f < hi; f += 256) sum += (int)ocount[f];
+        if (sum) atomicAdd(&s_cnt[l], sum);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) limit_levels(s_cnt, nl, T, method, false);
+    __syncthreads();
+    for (int l = 0; l < nl; l++) {
+        if (s_cnt[l] != 0) continue;
+        uint32_t lo, hi;
+        range(l, lo, hi);
+        for (uint32_t f = lo + threadIdx.x; f < hi; f += 256) ocount[f] = 0;
+    }
+}
+
 __global__ void k_image_offsets(const uint32_t* __restrict__ row_base,
                                 const uint32_t* __restrict__ eoff, int batch, int rows_per_image,
                                 int total_rows, uint32_t cap, int64_t* __restrict__ off) {
@@ -1977,13 +1335,6 @@ __global__ __launch_bounds__(64) void k_debug_candidates(
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
-int get_variant() { return g_host_variant; }
-
-hipError_t set_variant(int v) {
-    g_host_variant = v;
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_variant), &v, sizeof(int));
-}
-
 hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         long long src_img_stride, float* dst, long long dst_img_stride, int w,
                         int h, int fw, const Taps& taps, int batch, float* ds_dst, int ds_w,
@@ -2048,73 +1399,31 @@ hipError_t launch_first_octave_input(const float* src, const uint8_t* src_u8, in
 
 hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
                           const FeatureParams& fp, hipStream_t stream) {
-    if (!(g_host_variant & (16 | 65536))) {
-        // one wave per (image, 64-column strip, row segment); ~32k waves in all
-        ExtremaWaveGrid eg{};
-        int nw = 0;
-        for (int o = 0; o < fp.n_octaves; o++) {
-            const OctaveDesc& od = fp.oct[o];
-            const int strips_x = (od.wa + 63) / 64;
-            const long long per_col = (long long)strips_x * fp.batch;
-            int nseg = (int)std::min<long long>(std::max<long long>(1, (32768 + per_col - 1) / per_col),
-                                                std::max(1, od.h / 16));
-            const int rows = (od.h + nseg - 1) / nseg;
-            nseg = (od.h + rows - 1) / rows;
-            eg.wave0[o] = nw;
-            eg.seg_rows[o] = rows;
-            eg.nseg[o] = nseg;
-            nw += strips_x * nseg * fp.batch;
-        }
-        eg.wave0[fp.n_octaves] = nw;
-        const unsigned nb = (unsigned)((nw + 3) / 4);
-        switch (fp.d + 2) {
+    // one wave per (image, 64-column strip, row segment); ~32k waves in all
+    ExtremaWaveGrid eg{};
+    int nw = 0;
+    for (int o = 0; o < fp.n_octaves; o++) {
+        const OctaveDesc& od = fp.oct[o];
+        const int strips_x = (od.wa + 63) / 64;
+        const long long per_col = (long long)strips_x * fp.batch;
+        int nseg = (int)std::min<long long>(std::max<long long>(1, (32768 + per_col - 1) / per_col),
+                                            std::max(1, od.h / 16));
+        const int rows = (od.h + nseg - 1) / nseg;
+        nseg = (od.h + rows - 1) / rows;
+        eg.wave0[o] = nw;
+        eg.seg_rows[o] = rows;
+        eg.nseg[o] = nseg;
+        nw += strips_x * nseg * fp.batch;
+    }
+    eg.wave0[fp.n_octaves] = nw;
+    const unsigned nb = (unsigned)((nw + 3) / 4);
+    switch (fp.d + 2) {
 #define SGK_EXTW(ND)     case ND: hipLaunchKernelGGL((k_extrema_wave<ND>), dim3(nb), dim3(256), 0, stream, pyr, mask, row_count, fp, eg); break;
-            SGK_EXTW(3) SGK_EXTW(4) SGK_EXTW(5) SGK_EXTW(6) SGK_EXTW(7) SGK_EXTW(8)
-            default: return hipErrorInvalidValue;
+        SGK_EXTW(3) SGK_EXTW(4) SGK_EXTW(5) SGK_EXTW(6) SGK_EXTW(7) SGK_EXTW(8)
+        default: return hipErrorInvalidValue;
 #undef SGK_EXTW
-        }
-        return hipGetLastError();
     }
-    if (!(g_host_variant & 16)) {
-        ExtremaGrid eg{};
-        int nb = 0;
-        for (int o = 0; o < fp.n_octaves; o++) {
-            const OctaveDesc& od = fp.oct[o];
-            const int strips_x = (od.wa + ET_X - 1) / ET_X;
-            const long long per_col = (long long)strips_x * fp.batch;
-            int nsy = (int)std::min<long long>((2048 + per_col - 1) / per_col, (od.h + ET_Y - 1) / ET_Y);
-            nsy = std::max(nsy, 1);
-            int rows = (od.h + nsy - 1) / nsy;
-            rows = (rows + ET_Y - 1) / ET_Y * ET_Y;
-            nsy = (od.h + rows - 1) / rows;
-            eg.block0[o] = nb;
-            eg.rows_per_strip[o] = rows;
-            nb += strips_x * nsy * fp.batch;
-        }
-        eg.block0[fp.n_octaves] = nb;
-        switch (fp.d + 2) {
-#define SGK_EXTS(ND) \
-    case ND: hipLaunchKernelGGL((k_extrema_strip<ND>), dim3(nb), dim3(256), 0, stream, pyr, mask, row_count, fp, eg); break;
-            SGK_EXTS(3) SGK_EXTS(4) SGK_EXTS(5) SGK_EXTS(6) SGK_EXTS(7) SGK_EXTS(8)
-            default: return hipErrorInvalidValue;
-#undef SGK_EXTS
-        }
-        return hipGetLastError();
-    }
-    for (int octave = 0; octave < fp.n_octaves; octave++) {
-        const OctaveDesc& od = fp.oct[octave];
-        dim3 grid(((od.wa + ET_X - 1) / ET_X) * ((od.h + ET_Y - 1) / ET_Y) * fp.batch);
-        switch (fp.d + 2) {
-#define SGK_EXT(ND) \
-    case ND: hipLaunchKernelGGL((k_extrema<ND>), grid, dim3(256), 0, stream, pyr, mask, row_count, fp, octave); break;
-            SGK_EXT(3) SGK_EXT(4) SGK_EXT(5) SGK_EXT(6) SGK_EXT(7) SGK_EXT(8)
-            default: return hipErrorInvalidValue;
-#undef SGK_EXT
-        }
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
+    return hipGetLastError();
 }
 
 static size_t scan_blocks(size_t n) { return (n + 1023) / 1024; }
@@ -2189,6 +1498,23 @@ hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* f
     else
         hipLaunchKernelGGL(k_descriptor<false>, dim3(grid), dim3(256), 0, stream, pyr, feat,
                            feat_info, n_feat_dev, fp, desc, out_index);
+    return hipGetLastError();
+}
+
+hipError_t launch_limit_rows(uint32_t* row_count, const FeatureParams& fp, int threshold,
+                             int method, hipStream_t stream) {
+    if (fp.n_octaves * fp.d > kMaxLimitLevels) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_limit_rows, dim3(fp.batch), dim3(256), 0, stream, row_count, fp,
+                       threshold, method);
+    return hipGetLastError();
+}
+
+hipError_t launch_limit_oriented(uint32_t* ocount, const uint32_t* row_base,
+                                 const FeatureParams& fp, int threshold, int method,
+                                 uint32_t cand_cap, hipStream_t stream) {
+    if (fp.n_octaves * fp.d > kMaxLimitLevels) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_limit_oriented, dim3(fp.batch), dim3(256), 0, stream, ocount, row_base,
+                       fp, threshold, method, cand_cap);
     return hipGetLastError();
 }
 

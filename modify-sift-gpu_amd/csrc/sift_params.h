@@ -105,7 +105,40 @@ inline int make_filter(float sigma, float factor, float* taps) {
 // every level image is wa x h floats with wa = ((w+3)/4)*4.
 struct Octave { int w, h, wa; };
 
-// Octave geometry for an input of w x h pixels (no -maxd clamping).  The first octave is
+// How the reference turns a w x h input into the first octave (GLTexInput::SetImageData,
+// GLTexImage.cpp:918-1009, then PyramidCU::InitPyramid, PyramidCU.cpp:89-135):
+//   * ds: with -fo > 0 and pre-processing on the CPU (-prep, the default: GlobalUtil.cpp:81) or
+//     an input beyond _texMaxDim, the input is first sampled by 2^fo -- pixel (r << fo, c << fo)
+//     -- and its width truncated to a multiple of 4 (DownSamplePixelDataI2F/F); the pyramid
+//     then starts at octave 0 of that image with _down_sample_factor = fo;
+//   * octave_min: otherwise -fo (>= -3) on the truncated input; in both cases raised by one
+//     while the first octave is wider or taller than _texMaxDim (-maxd, 13200 in this fork,
+//     GlobalUtil.cpp:86).
+// Coordinates and the initial smoothing then use 2^(octave_min + ds)
+// (GetInitialSmoothSigma(_octave_min + _down_sample_factor), PyramidCU.cpp:1009-1019, 463, 542).
+struct InputPlan {
+    int ds;           // CPU-side sampling exponent (0: none)
+    int w, h;         // the image the pyramid starts from (after sampling; w % 4 == 0)
+    int octave_min;   // first octave relative to that image
+};
+
+inline InputPlan plan_input(int w, int h, int fo, int max_dim, int prep_on_cpu) {
+    InputPlan p;
+    p.ds = (fo > 0 && (w > max_dim || h > max_dim || prep_on_cpu)) ? fo : 0;
+    p.w = (w >> p.ds) & ~3;   // TruncateWidthCU (GLTexImage.h:125)
+    p.h = h >> p.ds;
+    p.octave_min = p.ds > 0 ? 0 : (fo < -3 ? -3 : fo);
+    int wp = p.octave_min >= 0 ? p.w >> p.octave_min : p.w << -p.octave_min;
+    int hp = p.octave_min >= 0 ? p.h >> p.octave_min : p.h << -p.octave_min;
+    while (wp > max_dim || hp > max_dim) {
+        p.octave_min++;
+        wp >>= 1;
+        hp >>= 1;
+    }
+    return p;
+}
+
+// Octave geometry for an input of w x h pixels (after plan_input).  The first octave is
 // octave_min (-fo): its size is the truncated input shifted by octave_min, up-sampled for
 // octave_min < 0 (PyramidCU::InitPyramid, PyramidCU.cpp:89-112; SiftGPU::AllocatePyramid,
 // SiftGPU.cpp:1435-1448).  octave_num <= 0 selects floor(log2(min(w,h))) - 3 of that size

@@ -513,7 +513,15 @@ int SiftGPU::RunSIFT(int num, const SiftKeypoint* keys, int keys_have_orientatio
 int SiftGPU::GetImageCount() { return (int)LIST(_list)->size(); }
 void SiftGPU::SetTightPyramid(int) {}
 int SiftGPU::AllocatePyramid(int, int) { return 1; }
-void SiftGPU::SetMaxDimension(int) {}
+// SiftGPU::SetMaxDimension (SiftGPU.cpp:1452-1458): below the GL texture limit (14096,
+// GlobalUtil.cpp:88) it becomes _texMaxDim, which raises the first octave of larger inputs
+// (PyramidCU.cpp:129-135).
+void SiftGPU::SetMaxDimension(int sz) {
+    if (sz >= 14096) return;
+    Runtime* rt = RT(_pyramid);
+    rt->opt.max_dimension = sz;
+    if (rt->ctx) sgpu_ctx_set_options(rt->ctx, &rt->opt);
+}
 
 // ---------------------------------------------------------------------------------- matcher
 namespace {
@@ -606,8 +614,7 @@ void SiftMatchGPU::SetDescriptors(int index, int num, const float* descriptors, 
     if (num > m->max_sift) num = m->max_sift;
     std::vector<uint8_t> q((size_t)num * 128);
     sgpu_quantize_descriptors(descriptors, q.size(), q.data());
-    m->id[index] = -1;   // a float upload always replaces the set
-    SetDescriptors(index, num, q.data(), id);
+    SetDescriptors(index, num, q.data(), id);   // the id cache applies as SiftMatchCU.cpp:100
 }
 
 int SiftMatchGPU::GetSiftMatch(int max_match, int match_buffer[][2], float distmax,

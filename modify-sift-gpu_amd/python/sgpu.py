@@ -25,7 +25,7 @@ C_API = [
     "sgpu_extract_f32", "sgpu_stage_input", "sgpu_feature_count", "sgpu_feature_total", "sgpu_copy_features",
     "sgpu_device_features", "sgpu_match", "sgpu_quantize_descriptors", "sgpu_last_timing",
     "sgpu_debug_geometry", "sgpu_debug_gaussian", "sgpu_debug_candidates",
-    "sgpu_debug_set_variant", "sgpu_comm_unique_id", "sgpu_comm_init", "sgpu_comm_allgather_i32",
+    "sgpu_debug_set_flags", "sgpu_comm_unique_id", "sgpu_comm_init", "sgpu_comm_allgather_i32",
     "sgpu_comm_allreduce_f64", "sgpu_extract_keypoints", "sgpu_match_guided", "sgpu_extract_color",
     "sgpu_match_shard_begin", "sgpu_match_shard_end", "sgpu_match_sharded",
 ]
@@ -68,7 +68,7 @@ def lib():
         L.sgpu_extract_color.argtypes = [vp, vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int]
         L.sgpu_quantize_descriptors.argtypes = [vp, c.c_size_t, vp]
         L.sgpu_last_timing.argtypes = [vp, vp, c.c_int]
-        L.sgpu_debug_set_variant.argtypes = [c.c_int]
+        L.sgpu_debug_set_flags.argtypes = [vp, c.c_int]
         L.sgpu_debug_geometry.argtypes = [vp, P(c.c_int), vp, c.c_int]
         L.sgpu_debug_gaussian.argtypes = [vp, c.c_int, c.c_int, c.c_int, vp]
         L.sgpu_debug_candidates.argtypes = [vp, vp, vp, c.c_int, P(c.c_int)]
@@ -336,6 +336,12 @@ class SiftContext:
         return a
 
     # ---- test hooks
+    DEBUG_PARTS2, DEBUG_PARTS4, DEBUG_TINY_CAP = 1, 2, 4
+
+    def set_debug_flags(self, flags: int):
+        """Per-context debug flags (sgpu_debug_set_flags; 0 = shipped configuration)."""
+        self._check(lib().sgpu_debug_set_flags(self._ctx, flags), "sgpu_debug_set_flags")
+
     def geometry(self):
         n = ctypes.c_int(0)
         dims = np.zeros(48, np.int32)

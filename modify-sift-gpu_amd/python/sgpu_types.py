@@ -25,6 +25,10 @@ class SgpuOptions(ctypes.Structure):
         ("keep_extremum_sign", ctypes.c_int),
         ("circular_window", ctypes.c_int),
         ("verbose", ctypes.c_int),
+        ("max_dimension", ctypes.c_int),
+        ("preprocess_on_cpu", ctypes.c_int),
+        ("feature_count_threshold", ctypes.c_int),
+        ("truncate_method", ctypes.c_int),
     ]
 
 
@@ -34,7 +38,8 @@ def default_options(**kw) -> SgpuOptions:
                     dog_threshold=0.0, edge_threshold=0.0, subpixel=1, max_orientation=2,
                     fixed_orientation=0, octave_min=0, octave_num=-1, dog_level_num=3,
                     lowe_origin=0, normalized=1, descriptors=1, keep_extremum_sign=0,
-                    circular_window=0, verbose=0)
+                    circular_window=0, verbose=0, max_dimension=13200, preprocess_on_cpu=1,
+                    feature_count_threshold=-1, truncate_method=0)
     for k, v in kw.items():
         setattr(o, k, v)
     return o

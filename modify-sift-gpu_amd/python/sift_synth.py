@@ -49,6 +49,40 @@ def synth_image(w: int, h: int, seed: int, n_blobs: int = 400, n_rects: int = 20
     return np.clip(np.rint(img), 0, 255).astype(np.uint8)
 
 
+_SYNTH_LIB = None
+
+
+def _synth_lib():
+    """tests/synth/libsynth.so (built here with gcc when missing)."""
+    global _SYNTH_LIB
+    if _SYNTH_LIB is None:
+        import ctypes
+        import os
+        import subprocess
+        d = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                         "tests", "synth")
+        so = os.path.join(d, "libsynth.so")
+        if not os.path.exists(so):
+            subprocess.check_call(["gcc", "-O3", "-fopenmp", "-shared", "-fPIC", "-o", so,
+                                   os.path.join(d, "synth.c"), "-lm"])
+        L = ctypes.CDLL(so)
+        L.synth_batch_u8.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_uint64, ctypes.c_int]
+        _SYNTH_LIB = L
+    return _SYNTH_LIB
+
+
+def synth_batch_fast(n: int, w: int, h: int, seed0: int, threads: int | None = None) -> np.ndarray:
+    """n distinct images [n, h, w] from seeds seed0 .. seed0 + n - 1, the synth_image recipe in C
+    (tests/synth/synth.c; its own generator, so not the NumPy images), on up to 16 threads."""
+    import os
+    if threads is None:
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    out = np.empty((n, h, w), np.uint8)
+    _synth_lib().synth_batch_u8(out.ctypes.data, n, w, h, seed0, threads)
+    return out
+
+
 def synth_batch(n: int, w: int, h: int, seed0: int, unique: int | None = None) -> np.ndarray:
     """n images [n, h, w]; with `unique` set, only that many distinct images are generated and
     the batch cycles through them (generation cost only; every image is still processed)."""

@@ -15,6 +15,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <fstream>
+#include <iomanip>
 #include <stdexcept>
 
 #include "../modify-sift-gpu_amd/csrc/sift_math.h"
@@ -359,6 +361,10 @@ std::vector<Candidate> histo_list(const std::vector<Key4>& key, int W, int H, in
 }
 
 inline uint32_t f2u(float f) { return as_uint(f); }
+
+// float -> int as the GPU converts (cvt.rzi.s32.f32): NaN gives 0 (C++ leaves it undefined).
+// Only a NaN pyramid (-fo -2, see extract) reaches it with NaN.
+inline int cvt_rz(float f) { return f != f ? 0 : (int)f; }
 inline float u2f(uint32_t u) { return as_float(u); }
 
 // --- ComputeOrientation_Kernel (ProgramCU.cu:813-977) for one list entry.  grad is the
@@ -416,7 +422,7 @@ void orientation_key(Key4 key, const std::vector<float>& grad, int W, int H,
             float gm = grad[t], ga = grad[t + 1];
             float weight = gm * exp_(sq_dist * factor);
             float fidx = floor_(ga * ten_degree_per_radius);
-            int oidx = (int)fidx;
+            int oidx = cvt_rz(fidx);
             if (oidx < 0) oidx += 36;
             vote[oidx] += weight;
         }
@@ -548,7 +554,7 @@ void descriptor(const float* key, const std::vector<float>& grad, int W, int H,
                     float theta = (anglef - ga) * rpi;
                     if (theta < 0) theta += 8.0f;
                     float fo = floor_(theta);
-                    int fidx = (int)fo;
+                    int fidx = cvt_rz(fo);
                     float weight1 = fo + 1.0f - theta;
                     float weight2 = theta - fo;
                     if (fidx >= 0 && fidx < 8) {   // the unrolled k == fidx test drops fidx == 8
@@ -593,7 +599,7 @@ void descriptor_rect(const float* key, const std::vector<float>& grad, int W, in
                     float theta = (-ga) * rpi;
                     if (theta < 0) theta += 8.0f;
                     const float fo = floor_(theta);
-                    const int fidx = (int)fo;
+                    const int fidx = cvt_rz(fo);
                     const float weight1 = fo + 1.0f - theta, weight2 = theta - fo;
                     if (fidx >= 0 && fidx < 8) {
                         des[fidx] = fma_(weight1, weight, des[fidx]);
@@ -607,31 +613,80 @@ void descriptor_rect(const float* key, const std::vector<float>& grad, int W, in
     normalize_descriptor(des128, normalize);
 }
 
+// --- GLTexInput::SetImageData with _down_sampled = ds > 0 (GLTexImage.cpp:928-1009,
+//     DownSamplePixelDataI2F / DownSamplePixelDataF with skip): pixel (r << ds, c << ds) of the
+//     full-width input for r < h >> ds, c < ((w >> ds) & ~3).
+Image ingest_sampled(const uint8_t* img, const float* img_f32, int w, int h, int stride, int ds) {
+    Image o;
+    o.w = (w >> ds) & ~3;
+    o.h = h >> ds;
+    o.px.resize((size_t)o.w * o.h);
+    for (int y = 0; y < o.h; y++)
+        for (int x = 0; x < o.w; x++) {
+            const size_t src = (size_t)(y << ds) * stride + (size_t)(x << ds);
+            o.px[(size_t)y * o.w + x] = img_f32 ? img_f32[src] : img[src] / 255.0f;
+        }
+    return o;
+}
+
+// --- SiftPyramid::LimitFeatureCount (SiftPyramid.cpp:219-260), preceded for the keypoint
+//     list by the level skip of PyramidCU::GenerateFeatureList (PyramidCU.cpp:829-853, with
+//     FOR_EACH_OCTAVE / FOR_EACH_LEVEL reversed for -tc2, SiftPyramid.h:174-184).  A skipped
+//     level has no features (the reference keeps the previous image's stale count there when
+//     the pyramid is reused; a fresh pyramid has 0).
+void limit_feature_count(std::vector<int>& cnt, int T, int method, bool list_stage) {
+    const int nl = (int)cnt.size();
+    if (list_stage && method != 0) {
+        int feature_num = 0;
+        for (int q = 0; q < nl; q++) {
+            const int l = method == 1 ? nl - 1 - q : q;
+            if (feature_num > T) { cnt[l] = 0; continue; }
+            feature_num += cnt[l];
+        }
+    }
+    int feature_num = 0;
+    for (int c : cnt) feature_num += c;
+    if (method == 2) {
+        int i = 0, new_feature_num = 0;
+        for (; new_feature_num < T && i < nl; ++i) new_feature_num += cnt[i];
+        for (; i < nl; ++i) cnt[i] = 0;
+    } else {
+        int i = 0;
+        while (i < nl && feature_num - cnt[i] > T) {
+            feature_num -= cnt[i];
+            cnt[i++] = 0;
+        }
+    }
+}
 
 }  // namespace
 
 Result extract(const uint8_t* img, int w, int h, int stride, const sgpu_options& opt,
                bool keep, const float* img_f32) {
+    // first octave: -fo, -prep and -maxd (sgp::plan_input restates GLTexImage.cpp:928-960 and
+    // PyramidCU.cpp:89-135)
+    const sgp::InputPlan plan = sgp::plan_input(w, h, std::max(-3, opt.octave_min),
+                                                opt.max_dimension, opt.preprocess_on_cpu);
     sgp::Options po;
     po.filter_width_factor = opt.filter_width_factor;
     po.dog_level_num = opt.dog_level_num;
     po.dog_threshold = opt.dog_threshold;
     po.edge_threshold = opt.edge_threshold;
-    po.octave_min = opt.octave_min;
+    po.octave_min = plan.octave_min + plan.ds;   // GetInitialSmoothSigma(_octave_min + ds)
     const sgp::Schedule S = sgp::make_schedule(po);
     const int d = S.dog_level_num, nlev = S.level_num;
-    const int fo = opt.octave_min;
-    if (fo < -1 || !(S.initial_smooth > 0.0f))   // NaN filter taps (see sgpu_ctx_set_options)
-        throw std::invalid_argument("first octave must be >= -1");
+    const int fo = plan.octave_min;
     Result R;
-    R.octaves = sgp::make_octaves(w, h, opt.octave_num, fo);
+    R.octaves = sgp::make_octaves(plan.w, plan.h, opt.octave_num, fo);
     const int noct = (int)R.octaves.size();
 
     // ResizeFeatureStorage (PyramidCU.cpp:341-347): histopyramid depth from the base level
     int whmax = std::max(R.octaves[0].wa, R.octaves[0].h);
     int hp_levels = (int)std::ceil(std::log(double(whmax)) / std::log(4.0));
 
-    Image input = img_f32 ? ingest_f32(img_f32, w, h, stride) : ingest(img, w, h, stride);
+    Image input = plan.ds > 0 ? ingest_sampled(img, img_f32, w, h, stride, plan.ds)
+                  : img_f32   ? ingest_f32(img_f32, w, h, stride)
+                              : ingest(img, w, h, stride);
     float taps[sgp::kMaxFilterWidth];
     std::vector<Image> prev;  // previous octave's Gaussian levels
     const float sigma_step = powf(2.0f, 1.0f / d);  // PyramidCU.cpp:1200
@@ -641,6 +696,9 @@ Result extract(const uint8_t* img, int w, int h, int stride, const sgpu_options&
     const double twopi = 2.0 * 3.14159265358979323846;
     const float offset = opt.lowe_origin ? 0.0f : 0.5f;
 
+    // ---- BuildPyramid + DetectKeypointsEX + GenerateFeatureList, octave by octave
+    std::vector<std::vector<std::vector<float>>> grad(noct);   // [octave][j]: grad of G[1+j]
+    std::vector<std::vector<float>> sign(noct * d);            // extremum sign per candidate
     for (int o = 0; o < noct; o++) {
         const sgp::Octave& oc = R.octaves[o];
         std::vector<Image> g(nlev);
@@ -663,9 +721,9 @@ Result extract(const uint8_t* img, int w, int h, int stride, const sgpu_options&
         }
         // DetectKeypointsEX (PyramidCU.cpp:1046-1114): dog 1..nlev-1, grad for 1..d
         std::vector<Image> dog(nlev);
-        std::vector<std::vector<float>> grad(nlev);
+        std::vector<std::vector<float>> gr(nlev);
         for (int m = 1; m < nlev; m++)
-            compute_dog(g[m], g[m - 1], &dog[m], (m >= 1 && m < 1 + d) ? &grad[m] : nullptr);
+            compute_dog(g[m], g[m - 1], &dog[m], (m >= 1 && m < 1 + d) ? &gr[m] : nullptr);
         for (int j = 0; j < d; j++) {
             std::vector<Key4> key;
             compute_key(dog[1 + j], dog[2 + j], dog[3 + j], tdog1, S.dog_threshold, tedge,
@@ -674,59 +732,97 @@ Result extract(const uint8_t* img, int w, int h, int stride, const sgpu_options&
             L.octave = o;
             L.level = j;
             L.candidates = histo_list(key, oc.wa, oc.h, hp_levels);
-            // GetFeatureOrientations (PyramidCU.cpp:1195-1222): grad of G[1+j], GetLevelSigma(j)
-            float sigma = sgp::level_sigma(S, j + S.level_min + 1);
-            L.oriented.resize(L.candidates.size() * 4);
-            for (size_t f = 0; f < L.candidates.size(); f++) {
-                orientation(L.candidates[f], grad[1 + j], oc.wa, oc.h, sigma, sigma_step,
-                            opt.orientation_gaussian_factor,
-                            opt.orientation_gaussian_factor * opt.orientation_window_factor,
-                            num_orientation, opt.subpixel, opt.keep_extremum_sign,
-                            opt.circular_window, &L.oriented[f * 4]);
-                if (opt.keep_extremum_sign) {  // ProgramCU.cu:849: z *= sign of the extremum
-                    const Key4& kk = key[(size_t)L.candidates[f].row * oc.wa + L.candidates[f].col];
-                    L.oriented[f * 4 + 2] *= kk.x;
-                }
-            }
-            // feature expansion + image coordinates
-            const float oss = ldexpf(1.0f, o + fo);   // os * 2^o, os = 2^octave_min
-            auto emit = [&](const float* src, float ang) {
-                R.feat_oct.insert(R.feat_oct.end(), {src[0], src[1], src[2], ang});
-                R.keys.push_back(oss * (src[0] - 0.5f) + offset);
-                R.keys.push_back(oss * (src[1] - 0.5f) + offset);
-                R.keys.push_back(oss * src[2]);
-                R.keys.push_back((float)std::fmod(twopi - ang, twopi));
-                R.feat_level.push_back(o * d + j);
-            };
-            for (size_t f = 0; f < L.candidates.size(); f++) {
-                const float* src = &L.oriented[f * 4];
-                if (num_orientation >= 2) {
-                    // ReshapeFeatureListCPU (PyramidCU.cpp:521-606)
-                    const double factor = 2.0 * 3.14159265358979323846 / 65535.0;
-                    uint32_t pk = f2u(src[3]);
-                    unsigned short o1 = pk & 0xffff, o2 = pk >> 16;
-                    if (o1 != 65535) {
-                        emit(src, float(factor * o1));
-                        if (o2 != 65535 && o2 != o1) emit(src, float(factor * o2));
-                    }
-                } else {
-                    // DownloadKeypoints (PyramidCU.cpp:701-751)
-                    emit(src, src[3]);
-                }
-            }
-            if (opt.descriptors) {
-                // GetFeatureDescriptors (PyramidCU.cpp:413-452): grad of G[1+j]
-                size_t nf = R.feat_level.size();
-                size_t first = R.desc.size() / 128;
-                R.desc.resize(nf * 128);
-                for (size_t f = first; f < nf; f++)
-                    descriptor(&R.feat_oct[f * 4], grad[1 + j], oc.wa, oc.h,
-                               opt.descriptor_window_factor, opt.normalized, &R.desc[f * 128]);
-            }
+            for (const Candidate& c : L.candidates)
+                sign[o * d + j].push_back(key[(size_t)c.row * oc.wa + c.col].x);
             R.levels.push_back(std::move(L));
         }
+        for (int j = 0; j < d; j++) grad[o].push_back(std::move(gr[1 + j]));
         prev = std::move(g);
         if (keep) R.gauss.push_back(prev);
+    }
+    const int nl = noct * d;
+    const int T = opt.feature_count_threshold;
+    if (T > 0) {   // GenerateFeatureList level skip + LimitFeatureCount(0) (SiftPyramid.cpp:117)
+        std::vector<int> cnt(nl);
+        for (int l = 0; l < nl; l++) cnt[l] = (int)R.levels[l].candidates.size();
+        limit_feature_count(cnt, T, opt.truncate_method, true);
+        for (int l = 0; l < nl; l++)
+            if (cnt[l] == 0) R.levels[l].candidates.clear();
+    }
+
+    // ---- GetFeatureOrientations (PyramidCU.cpp:1195-1222): grad of G[1+j], GetLevelSigma(j)
+    for (int l = 0; l < nl; l++) {
+        LevelResult& L = R.levels[l];
+        const int o = L.octave, j = L.level;
+        const sgp::Octave& oc = R.octaves[o];
+        const float sigma = sgp::level_sigma(S, j + S.level_min + 1);
+        L.oriented.resize(L.candidates.size() * 4);
+        for (size_t f = 0; f < L.candidates.size(); f++) {
+            orientation(L.candidates[f], grad[o][j], oc.wa, oc.h, sigma, sigma_step,
+                        opt.orientation_gaussian_factor,
+                        opt.orientation_gaussian_factor * opt.orientation_window_factor,
+                        num_orientation, opt.subpixel, opt.keep_extremum_sign,
+                        opt.circular_window, &L.oriented[f * 4]);
+            if (opt.keep_extremum_sign)   // ProgramCU.cu:849: z *= sign of the extremum
+                L.oriented[f * 4 + 2] *= sign[l][f];
+        }
+    }
+    // ReshapeFeatureListCPU (PyramidCU.cpp:521-606): a keypoint becomes 0, 1 or 2 features
+    auto n_oriented = [&](const float* src) -> int {
+        if (num_orientation < 2) return 1;
+        const uint32_t pk = f2u(src[3]);
+        const unsigned o1 = pk & 0xffff, o2 = pk >> 16;
+        if (o1 == 65535) return 0;
+        return (o2 != 65535 && o2 != o1) ? 2 : 1;
+    };
+    std::vector<char> level_kept(nl, 1);
+    if (T > 0 && num_orientation >= 2) {   // LimitFeatureCount(1) (SiftPyramid.cpp:152-160)
+        std::vector<int> cnt(nl, 0);
+        for (int l = 0; l < nl; l++)
+            for (size_t f = 0; f < R.levels[l].candidates.size(); f++)
+                cnt[l] += n_oriented(&R.levels[l].oriented[f * 4]);
+        limit_feature_count(cnt, T, opt.truncate_method, false);
+        for (int l = 0; l < nl; l++) level_kept[l] = cnt[l] != 0;
+    }
+
+    // ---- feature expansion, image coordinates (DownloadKeypoints / ReshapeFeatureListCPU)
+    //      and GetFeatureDescriptors (PyramidCU.cpp:413-452)
+    for (int l = 0; l < nl; l++) {
+        if (!level_kept[l]) continue;
+        const LevelResult& L = R.levels[l];
+        const int o = L.octave, j = L.level;
+        const sgp::Octave& oc = R.octaves[o];
+        const float oss = ldexpf(1.0f, o + fo + plan.ds);   // os * 2^o, os = 2^(octave_min + ds)
+        auto emit = [&](const float* src, float ang) {
+            R.feat_oct.insert(R.feat_oct.end(), {src[0], src[1], src[2], ang});
+            R.keys.push_back(oss * (src[0] - 0.5f) + offset);
+            R.keys.push_back(oss * (src[1] - 0.5f) + offset);
+            R.keys.push_back(oss * src[2]);
+            R.keys.push_back((float)std::fmod(twopi - ang, twopi));
+            R.feat_level.push_back(l);
+        };
+        const size_t first = R.feat_level.size();
+        for (size_t f = 0; f < L.candidates.size(); f++) {
+            const float* src = &L.oriented[f * 4];
+            if (num_orientation >= 2) {
+                const double factor = 2.0 * 3.14159265358979323846 / 65535.0;
+                uint32_t pk = f2u(src[3]);
+                unsigned short o1 = pk & 0xffff, o2 = pk >> 16;
+                if (o1 != 65535) {
+                    emit(src, float(factor * o1));
+                    if (o2 != 65535 && o2 != o1) emit(src, float(factor * o2));
+                }
+            } else {
+                emit(src, src[3]);
+            }
+        }
+        if (opt.descriptors) {
+            const size_t nf = R.feat_level.size();
+            R.desc.resize(nf * 128);
+            for (size_t f = first; f < nf; f++)
+                descriptor(&R.feat_oct[f * 4], grad[o][j], oc.wa, oc.h,
+                           opt.descriptor_window_factor, opt.normalized, &R.desc[f * 128]);
+        }
     }
     return R;
 }
@@ -745,13 +841,17 @@ std::vector<float> describe_keys(const uint8_t* img, int w, int h, int stride,
                                  int has_orientation, std::vector<float>* keys_out) {
     sgpu_options o2 = opt;
     o2.descriptors = 0;
+    o2.feature_count_threshold = -1;   // LimitFeatureCount skips existing keypoints
     Result R = extract(img, w, h, stride, o2, true);
+    const sgp::InputPlan plan = sgp::plan_input(w, h, std::max(-3, opt.octave_min),
+                                                opt.max_dimension, opt.preprocess_on_cpu);
+    const int oexp = plan.octave_min + plan.ds;   // coordinates scale by 2^(octave_min + ds)
     sgp::Options po;
     po.filter_width_factor = opt.filter_width_factor;
     po.dog_level_num = opt.dog_level_num;
     po.dog_threshold = opt.dog_threshold;
     po.edge_threshold = opt.edge_threshold;
-    po.octave_min = opt.octave_min;
+    po.octave_min = oexp;
     const sgp::Schedule S = sgp::make_schedule(po);
     const int d = S.dog_level_num, noct = (int)R.octaves.size();
     const double twopi = 2.0 * 3.14159265358979323846;
@@ -759,7 +859,7 @@ std::vector<float> describe_keys(const uint8_t* img, int w, int h, int stride,
     const float offset = opt.lowe_origin ? 0.0f : 0.5f;
     struct Entry { float k[4]; int index, octave, level; };
     std::vector<Entry> list;
-    float octave_sigma = ldexpf(1.0f, opt.octave_min);   // PyramidCU.cpp:461
+    float octave_sigma = ldexpf(1.0f, oexp);   // PyramidCU.cpp:461-463
     for (int i = 0; i < noct; i++, octave_sigma *= 2.0f)
         for (int j = 0; j < d; j++) {
             const float level_sigma = sgp::level_sigma(S, j + S.level_min + 1) * octave_sigma;
@@ -812,7 +912,7 @@ std::vector<float> describe_keys(const uint8_t* img, int w, int h, int stride,
     const int m = std::min<int>(num, (int)list.size());
     for (int i = 0; i < m; i++) {
         const Entry& e = list[i];
-        const float os = ldexpf(1.0f, e.octave + opt.octave_min);
+        const float os = ldexpf(1.0f, e.octave + oexp);
         if (!has_orientation) {
             float* kk = keys_out->data() + 4 * (size_t)e.index;
             kk[0] = os * (e.k[0] - 0.5f) + offset;
@@ -980,6 +1080,66 @@ std::vector<int> match(const uint8_t* d1, int n1, const uint8_t* d2, int n2, flo
 // ---------------------------------------------------------------------------------------------
 // C entry points for ctypes (tests / bench cpu_baseline).
 extern "C" {
+
+// The first-octave plan (sgp::plan_input): out = {ds, w, h, octave_min}.
+void oracle_plan(int w, int h, int fo, int max_dim, int prep, int* out) {
+    const sgp::InputPlan p = sgp::plan_input(w, h, fo < -3 ? -3 : fo, max_dim, prep);
+    out[0] = p.ds;
+    out[1] = p.w;
+    out[2] = p.h;
+    out[3] = p.octave_min;
+}
+
+// SiftPyramid::SaveSIFT (SiftPyramid.cpp:311-387), restated with the same iostream formatting:
+// binary (-b): n, dim, then per feature y, x, s, o (+ 128 floats); ASCII: "n 128" then per
+// feature "y x s o" at fixed precision 2 2 3 3 and the 128 values (floor(0.5 + 512 d) when
+// normalised, setprecision(8) floats with -unn), a newline after every 20; without descriptors
+// (-sd) "n 0" and "y x s o" at the fixed default precision.
+int oracle_save_sift(const char* path, const float* keys, const float* desc, int n, int binary,
+                     int normalized, int has_desc) {
+    if (n <= 0) return 0;
+    const float* pk = keys;
+    if (binary) {
+        std::ofstream out(path, std::ios::binary);
+        out.write((const char*)&n, sizeof(int));
+        const int dim = has_desc ? 128 : 0;
+        out.write((const char*)&dim, sizeof(int));
+        const float* pd = desc;
+        for (int i = 0; i < n; i++, pk += 4) {
+            out.write((const char*)(pk + 1), sizeof(float));
+            out.write((const char*)pk, sizeof(float));
+            out.write((const char*)(pk + 2), 2 * sizeof(float));
+            if (has_desc) {
+                out.write((const char*)pd, 128 * sizeof(float));
+                pd += 128;
+            }
+        }
+        return 0;
+    }
+    std::ofstream out(path);
+    out.flags(std::ios::fixed);
+    if (has_desc) {
+        const float* pd = desc;
+        out << n << " 128" << std::endl;
+        for (int i = 0; i < n; i++) {
+            out << std::setprecision(2) << pk[1] << " " << std::setprecision(2) << pk[0] << " "
+                << std::setprecision(3) << pk[2] << " " << std::setprecision(3) << pk[3]
+                << std::endl;
+            pk += 4;
+            for (int k = 0; k < 128; k++, pd++) {
+                if (normalized) out << ((unsigned int)floor(0.5 + 512.0f * (*pd))) << " ";
+                else out << std::setprecision(8) << pd[0] << " ";
+                if ((k + 1) % 20 == 0) out << std::endl;
+            }
+            out << std::endl;
+        }
+    } else {
+        out << n << " 0" << std::endl;
+        for (int i = 0; i < n; i++, pk += 4)
+            out << pk[1] << " " << pk[0] << " " << pk[2] << " " << pk[3] << std::endl;
+    }
+    return 0;
+}
 
 int oracle_extract(const uint8_t* img, int w, int h, int stride, const sgpu_options* opt,
                    float* keys, float* desc, int cap, int* n_out) {

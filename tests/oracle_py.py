@@ -54,6 +54,9 @@ def lib():
         L.oracle_extract_f32.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_int, ctypes.c_void_p]
+        L.oracle_plan.argtypes = [ctypes.c_int] * 5 + [ctypes.c_void_p]
+        L.oracle_save_sift.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.oracle_match_distance.argtypes = [ctypes.c_int]
         L.oracle_match_distance.restype = ctypes.c_float
         L.oracle_schedule.argtypes = [ctypes.c_int, P(ctypes.c_float), P(ctypes.c_float),
@@ -241,3 +244,12 @@ def bench_extract(images: np.ndarray, opts=None, threads=1):
     secs = lib().oracle_bench_extract(images.ctypes.data, n, w, h, w, ctypes.byref(opts),
                                       threads, ctypes.byref(feats))
     return secs, feats.value
+
+
+def save_sift(path, keys, desc, binary=False, normalized=True):
+    """SiftPyramid::SaveSIFT's output for (keys [n,4], desc [n,128] or None) -- the
+    reference's writer restated in oracle/sift_oracle.cpp (oracle_save_sift)."""
+    k = np.ascontiguousarray(keys, np.float32)
+    d = None if desc is None else np.ascontiguousarray(desc, np.float32)
+    lib().oracle_save_sift(str(path).encode(), k.ctypes.data, None if d is None else d.ctypes.data,
+                           len(k), int(binary), int(normalized), int(d is not None))

@@ -76,6 +76,22 @@ def test_parse_options():
     assert o.fixed_orientation == 0
 
 
+def test_parse_feature_limit_and_first_octave_options():
+    # SiftGPU.cpp:1185-1203: -tc / -tc1 -> method 0, -tc2 -> 1, -tc3 -> 2, count > 0 consumed;
+    # :1213-1222: -maxd > 0; :921-926: -prep / -noprep
+    d = default_options()
+    assert (d.feature_count_threshold, d.truncate_method, d.max_dimension, d.preprocess_on_cpu) == (-1, 0, 13200, 1)
+    for flag, method in [("-tc", 0), ("-tc1", 0), ("-tc2", 1), ("-TC3", 2)]:
+        o, _ = _parse([flag, "500"])
+        assert (o.feature_count_threshold, o.truncate_method) == (500, method), flag
+    o, _ = _parse(["-tc2", "0", "-d", "4"])          # count not > 0: method set, "0" not consumed
+    assert (o.feature_count_threshold, o.truncate_method, o.dog_level_num) == (-1, 1, 4)
+    o, _ = _parse(["-maxd", "2560", "-noprep"])
+    assert (o.max_dimension, o.preprocess_on_cpu) == (2560, 0)
+    o, _ = _parse(["-maxd", "-5", "-noprep", "-prep"])
+    assert (o.max_dimension, o.preprocess_on_cpu) == (13200, 1)
+
+
 def test_quantize_matches_reference_semantics():
     rng = np.random.default_rng(3)
     d = np.concatenate([rng.uniform(0, 0.6, 4000), [0.0, 0.4990234, 0.5, 0.75, 1.0]]).astype(np.float32)

@@ -1,0 +1,118 @@
+"""The drop-in C++ API (include/SiftGPU.h) driven by compiled replicas of the reference's own
+call sequences:
+  * SiftGPU::SaveSIFT, byte for byte against the reference's writer restated on the oracle side
+    (SiftPyramid.cpp:311-387): ASCII and -b binary, normalised and -unn, with and without
+    descriptors (-sd), plus option paths that change the feature list (-fo, -tc2, -maxd through
+    SetMaxDimension);
+  * SiftMatchGPU::SetDescriptors' id cache (SiftMatchCU.cpp:71-101);
+  * TestWin/MultiThreadSIFT.cpp: one SiftGPU per thread on one device, initialisation
+    serialised, the runs concurrent."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from sgpu_types import default_options
+from sift_synth import quantize, synth_descriptors, synth_image
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIBDIR = os.path.join(ROOT, "modify-sift-gpu_amd", "lib")
+
+
+def _compile(tmp_path, name):
+    exe = tmp_path / name
+    r = subprocess.run(["g++", "-std=c++11", "-O1", "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "tests", "abi", name + ".cpp"), "-o", str(exe),
+                        "-L" + LIBDIR, "-lsiftgpu", "-Wl,-rpath," + LIBDIR, "-lpthread"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return str(exe)
+
+
+def _write_pgm(path, img):
+    h, w = img.shape
+    with open(path, "wb") as f:
+        f.write(f"P5\n{w} {h}\n255\n".encode())
+        f.write(np.ascontiguousarray(img, np.uint8).tobytes())
+
+
+# (replica command-line options, oracle options, binary, normalised, descriptors)
+SAVE_CASES = [
+    ([], {}, False, True, True),
+    (["-b"], {}, True, True, True),
+    (["-unn"], {"normalized": 0}, False, False, True),
+    (["-b", "-unn"], {"normalized": 0}, True, False, True),
+    (["-sd"], {"descriptors": 0}, False, True, False),
+    (["-sd", "-b"], {"descriptors": 0}, True, True, False),
+    (["-fo", "1"], {"octave_min": 1}, False, True, True),
+    (["-tc2", "200"], {"feature_count_threshold": 200, "truncate_method": 1}, False, True, True),
+    (["=maxd", "300"], {"max_dimension": 300}, False, True, True),
+    (["-maxd", "200", "-noprep", "-fo", "1"], {"max_dimension": 200, "octave_min": 1,
+                                                "preprocess_on_cpu": 0}, False, True, True),
+]
+
+
+@pytest.mark.parametrize("args,over,binary,normalized,desc", SAVE_CASES,
+                         ids=lambda v: " ".join(v) if isinstance(v, list) else None)
+def test_save_sift_bytes_vs_reference_writer(tmp_path, args, over, binary, normalized, desc):
+    exe = _compile(tmp_path, "save_sift_replica")
+    img = synth_image(480, 352, 91)
+    pgm = tmp_path / "in.pgm"
+    _write_pgm(pgm, img)
+    out = tmp_path / "gpu.sift"
+    r = subprocess.run([exe, str(pgm), str(out)] + args, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    num = int([l for l in r.stdout.split("\n") if l.startswith("NUM ")][0].split()[1])
+    rk, rd = O.extract(img, default_options(**over))
+    assert num == len(rk) > 0
+    ref = tmp_path / "oracle.sift"
+    O.save_sift(ref, rk, rd if desc else None, binary=binary, normalized=normalized)
+    a, b = out.read_bytes(), ref.read_bytes()
+    assert a == b, f"{len(a)} vs {len(b)} bytes; first difference at {next((i for i in range(min(len(a), len(b))) if a[i] != b[i]), None)}"
+
+
+def test_match_id_cache(tmp_path):
+    exe = _compile(tmp_path, "match_id_replica")
+    a = synth_descriptors(900, 11)
+    b = synth_descriptors(1000, 12, base=a, n_dup=600)
+    c = synth_descriptors(800, 13, base=b, n_dup=300)
+    paths = []
+    for name, d in (("a", a), ("b", b), ("c", c)):
+        p = tmp_path / f"{name}.f32"
+        np.ascontiguousarray(d, np.float32).tofile(p)
+        paths += [str(p), str(len(d))]
+    r = subprocess.run([exe] + paths, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = {l.split()[1]: int(l.split()[2]) for l in r.stdout.splitlines() if l.startswith("COUNT")}
+    ab = len(O.match(quantize(a), quantize(b)))
+    cb = len(O.match(quantize(c), quantize(b)))
+    assert ab != cb and ab > 100
+    assert got == {"ab": ab, "cached": ab, "cb": cb, "cb_again": cb}
+
+
+def test_multithread_contexts_one_device(tmp_path):
+    exe = _compile(tmp_path, "multithread_replica")
+    imgs = [synth_image(640, 480, 300 + i) for i in range(2)]
+    args = ["0", "10"]
+    for i, img in enumerate(imgs):
+        _write_pgm(tmp_path / f"{i}.pgm", img)
+        args += [str(tmp_path / f"{i}.pgm"), str(tmp_path / f"{i}.bin")]
+    r = subprocess.run([exe] + args, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [l.split() for l in r.stdout.splitlines() if l.startswith("THREAD")]
+    assert len(lines) == 2
+    opts = default_options(octave_min=-1)   # MultiThreadSIFT.cpp:148: -fo -1
+    for i, (_, _, num, equal) in enumerate(lines):
+        assert int(equal) == 1, f"thread {i}: a repeated run differed"
+        rk, rd = O.extract(imgs[i], opts)
+        assert int(num) == len(rk) > 0
+        raw = np.fromfile(tmp_path / f"{i}.bin", np.float32)
+        k = raw[:4 * len(rk)].reshape(-1, 4)
+        d = raw[4 * len(rk):].reshape(-1, 128)
+        assert np.array_equal(k.view(np.uint32), rk.view(np.uint32))
+        assert np.linalg.norm(d.astype(np.float64) - rd, axis=1).max() < 1e-4

@@ -1,0 +1,82 @@
+"""The BASELINE.json configurations on the HIP path:
+  * C4 -- one 4096 x 4096 tile with 6 octaves, every keypoint and descriptor against the oracle;
+  * C3 -- the per-GPU shard the bench times (128 distinct 1920 x 1080 images, -fo 0 -no 4 -d 3):
+    every image of the batch equals its single-image run, two of them equal the oracle;
+  * the keypoint-capacity overflow path of a batch (grow the buffers, re-run the part)."""
+import numpy as np
+import pytest
+
+import oracle_py as O
+from sgpu_types import default_options
+from sift_synth import synth_batch_fast, synth_image
+
+pytestmark = pytest.mark.gpu
+
+DESC_L2_TOL = 1e-4
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def _equal(a, b):
+    return a[0].shape == b[0].shape and np.array_equal(_bits(a[0]), _bits(b[0])) and \
+        np.array_equal(_bits(a[1]), _bits(b[1]))
+
+
+def test_c4_4096_six_octaves_vs_oracle(gpu_ctx):
+    img = synth_batch_fast(1, 4096, 4096, 4000)[0]
+    opts = default_options(octave_num=6)
+    gpu_ctx.set_options(opts)
+    gpu_ctx.extract(img)
+    assert len(gpu_ctx.geometry()) == 6 and gpu_ctx.geometry()[5][:2] == (128, 128)
+    k, d = gpu_ctx.features(0)
+    rk, rd = O.extract(img, opts)
+    assert k.shape == rk.shape and len(k) > 2000, (k.shape, rk.shape)
+    assert np.array_equal(_bits(k), _bits(rk))
+    assert np.linalg.norm(d.astype(np.float64) - rd, axis=1).max() < DESC_L2_TOL
+    assert np.array_equal(_bits(d), _bits(rd))
+    gpu_ctx.set_options(default_options())
+
+
+def test_c3_shard_128_full_hd(gpu_ctx):
+    n = 128
+    imgs = synth_batch_fast(n, 1920, 1080, 3000)
+    opts = default_options(octave_num=4)
+    gpu_ctx.set_options(opts)
+    gpu_ctx.extract(imgs)
+    batch = [gpu_ctx.features(i) for i in range(n)]
+    total = gpu_ctx.total()
+    assert total == sum(len(b[0]) for b in batch) and total > n * 500
+    for i in range(n):
+        gpu_ctx.extract(imgs[i])
+        assert _equal(gpu_ctx.features(0), batch[i]), f"image {i}: batch != single"
+    for i in (0, n - 1):
+        rk, rd = O.extract(imgs[i], opts)
+        assert np.array_equal(_bits(batch[i][0]), _bits(rk)), i
+        assert np.linalg.norm(batch[i][1].astype(np.float64) - rd, axis=1).max() < DESC_L2_TOL
+    gpu_ctx.set_options(default_options())
+
+
+def test_capacity_overflow_rerun(gpu_ctx):
+    """SGPU_DEBUG_TINY_CAP starts the keypoint capacity at 64: the first pass overflows, the
+    part is re-run with grown buffers and the results equal the normal run's."""
+    import sgpu
+    imgs = np.stack([synth_image(480, 360, 200 + i) for i in range(3)])
+    ctx = sgpu.SiftContext(0)
+    try:
+        ctx.extract(imgs)
+        ref = [ctx.features(i) for i in range(3)]
+        assert ctx.total() > 64
+        ctx2 = sgpu.SiftContext(0)
+        try:
+            ctx2.set_debug_flags(ctx2.DEBUG_TINY_CAP)
+            ctx2.extract(imgs)
+            for i in range(3):
+                assert _equal(ctx2.features(i), ref[i]), i
+            ctx2.extract(imgs[:1])   # grown buffers persist: no overflow the second time
+            assert _equal(ctx2.features(0), ref[0])
+        finally:
+            ctx2.close()
+    finally:
+        ctx.close()

@@ -417,10 +417,13 @@ def test_first_octave_input_vs_numpy(fo):
     np.testing.assert_array_equal(got, want)
 
 
-def test_first_octave_minus_two_is_refused():
-    """-fo -2 makes the reference's initial sigma 0 and CreateFilterKernel's taps NaN."""
-    with pytest.raises(AssertionError):
-        O.extract(synth_image(64, 48, 1), default_options(octave_min=-2))
+def test_first_octave_minus_two_runs_to_zero_features():
+    """-fo -2 makes the reference's initial sigma 0 (SiftGPU.cpp:446-452) and CreateFilterKernel's
+    taps NaN (ProgramCU.cu:391-398).  The NaN pyramid passes every ComputeKEY test (all NaN
+    comparisons are false), so every interior pixel is listed, and no keypoint gets an
+    orientation (no histogram bin exceeds 0.8 * NaN): RunSIFT succeeds with 0 features."""
+    k, d = O.extract(synth_image(64, 48, 1), default_options(octave_min=-2))
+    assert k.shape == (0, 4) and d.shape == (0, 128)
 
 
 def test_float_ingest_equals_u8_ingest():
@@ -440,3 +443,78 @@ def test_color_formula_kat():
     assert g[0, 0] == np.float32(65536 * 255) / np.float32(65535.0 * 255.0) > 1.0
     assert g[0, 1] == np.float32(19595 * 255) / np.float32(65535.0 * 255.0)
     assert O.gray_from_color(px, "bgra")[0, 2] == g[0, 1]
+
+
+# ---- feature-count limiting (-tc / -tc2 / -tc3) and the first-octave plan ----------------------
+
+def _limit_py(cnt, T, method, list_stage):
+    """SiftPyramid::LimitFeatureCount (SiftPyramid.cpp:219-260), with the level skip of
+    PyramidCU::GenerateFeatureList (PyramidCU.cpp:829-853) first when list_stage."""
+    cnt = list(cnt)
+    nl = len(cnt)
+    if list_stage and method != 0:
+        total = 0
+        order = range(nl - 1, -1, -1) if method == 1 else range(nl)
+        for l in order:
+            if total > T:
+                cnt[l] = 0
+            else:
+                total += cnt[l]
+    num = sum(cnt)
+    if method == 2:
+        i, kept = 0, 0
+        while kept < T and i < nl:
+            kept += cnt[i]
+            i += 1
+        for l in range(i, nl):
+            cnt[l] = 0
+    else:
+        i = 0
+        while i < nl and num - cnt[i] > T:
+            num -= cnt[i]
+            cnt[i] = 0
+            i += 1
+    return cnt
+
+
+@pytest.mark.parametrize("method", [0, 1, 2])
+@pytest.mark.parametrize("T", [30, 200, 600])
+def test_feature_limit_keeps_whole_levels(method, T):
+    """-tc only removes whole levels: the limited run equals the full run restricted to the
+    levels the reference's two LimitFeatureCount passes keep (on the keypoint counts, then on
+    the oriented feature counts)."""
+    img = synth_image(320, 240, 21)
+    d = 3
+    full_k, _ = O.extract(img)
+    _, lvl = O.features_oct(img)
+    ci, _ = O.candidates(img)
+    nl = int(max(ci[:, 2].max(), lvl.max())) + 1
+    nl = (nl + d - 1) // d * d
+    cand = np.bincount(ci[:, 2], minlength=nl)
+    feat = np.bincount(lvl, minlength=nl)
+    keep1 = _limit_py(cand, T, method, True)
+    feat1 = [f if k else 0 for f, k in zip(feat, keep1)]
+    keep = _limit_py(feat1, T, method, False)
+    want = full_k[np.isin(lvl, [l for l in range(nl) if keep[l]])]
+    got, _ = O.extract(img, default_options(feature_count_threshold=T, truncate_method=method))
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+    if T < len(full_k):
+        assert len(got) < len(full_k)
+
+
+@pytest.mark.parametrize("w,h,fo,maxd,prep,want", [
+    (1920, 1080, 0, 13200, 1, (0, 1920, 1080, 0)),
+    (1921, 1080, 1, 13200, 1, (1, 960, 540, 0)),       # -prep: sampled, then octave 0
+    (1012, 301, 2, 13200, 1, (2, 252, 75, 0)),         # width truncated after sampling
+    (1012, 301, 2, 13200, 0, (0, 1012, 301, 2)),       # -noprep: SampleImageD from the input
+    (4096, 4096, 0, 2560, 1, (0, 4096, 4096, 1)),      # -maxd raises octave_min
+    (4096, 3000, -1, 4000, 1, (0, 4096, 3000, 1)),     # 8192 > 4000 -> -1 -> 0 -> 1
+    (20000, 100, 1, 13200, 0, (1, 10000, 50, 0)),      # beyond _texMaxDim: sampled even -noprep
+    (640, 480, -5, 13200, 1, (0, 640, 480, -3)),       # clamped to -3 (PyramidCU.cpp:106-107)
+])
+def test_first_octave_plan(w, h, fo, maxd, prep, want):
+    """sgp::plan_input: GLTexInput::SetImageData (GLTexImage.cpp:928-960) + PyramidCU::
+    InitPyramid (PyramidCU.cpp:89-135) as (ds, image w, image h, octave_min)."""
+    out = np.zeros(4, np.int32)
+    O.lib().oracle_plan(w, h, fo, maxd, prep, out.ctypes.data)
+    assert tuple(out) == want
