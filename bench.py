@@ -26,7 +26,7 @@ import numpy as np  # noqa: E402
 
 import sgpu  # noqa: E402  (loads libsiftgpu.so before torch: one HIP runtime, /opt/rocm's)
 from sgpu_types import default_options  # noqa: E402
-from sift_synth import synth_batch, synth_descriptors, synth_guided_scene, quantize  # noqa: E402
+from sift_synth import synth_batch_fast, synth_descriptors, synth_guided_scene, quantize  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters (spec)
 I8_MFMA_PEAK_TOPS = 5000.0     # dense i8 MFMA = 2x the ~2.5 PF bf16 rate (same guide)
@@ -41,6 +41,25 @@ def geometry_sum(w, h, octaves):
     return tot
 
 
+def self_launch(n):
+    """`--gpus N` without a launcher: start N ranks of this script as child processes (one per
+    GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run would) and return
+    the worst exit code.  Runs before anything touches the GPU in this process."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc != 0), 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -50,7 +69,10 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--octaves", type=int, default=4)
-    ap.add_argument("--unique", type=int, default=16, help="distinct synthetic images per GPU")
+    ap.add_argument("--workload", default="c3", choices=["c3", "c4"],
+                    help="c3: 128 x 1920x1080 per GPU (-no 4), the headline; c4: BASELINE "
+                         "configs[3], 4096x4096 tiles with 6 octaves, as the headline line")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 sub-measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-match", action="store_true")
     ap.add_argument("--match-n", type=int, default=50000)
@@ -60,11 +82,18 @@ def main():
                          "share one GPU)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"note: WORLD_SIZE={world} differs from --gpus {args.gpus}", file=sys.stderr)
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    if args.workload == "c4":
+        args.width = args.height = 4096
+        args.octaves = 6
+        if args.batch == 128:
+            args.batch = 16
     sgpu.lib()   # libsiftgpu (and /opt/rocm's HIP runtime) before torch: torch never touches
                  # the GPU here -- torch.distributed (gloo, host) is only the rendezvous
     # Initialise /opt/rocm's HIP runtime now, before `import torch` maps torch's own copy of
@@ -98,8 +127,9 @@ def main():
         uid = [sgpu.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(world, rank, uid[0])
-    # shard of the global batch: images [rank*B, (rank+1)*B), seeds 3000 + global index
-    imgs = synth_batch(B, W, H, seed0=3000 + rank * B, unique=args.unique)
+    # shard of the global batch: images [rank*B, (rank+1)*B), distinct seeds 3000 + global
+    # index (4000 + index for C4), SURVEY.md §8(d)
+    imgs = synth_batch_fast(B, W, H, (4000 if args.workload == "c4" else 3000) + rank * B)
     ctx.stage(imgs)
 
     def step():
@@ -151,8 +181,16 @@ def main():
     achieved = pyr_bytes / (pyr_ms * 1e-3) / 1e9 if pyr_ms > 0 else 0.0
 
     traffic, prof_note = profiled_traffic(B, W, H, args.octaves)
+    if args.workload == "c4":
+        workload = (f"C4: {B} x {W}x{H} u8 gray tiles per GPU per step, -fo 0 -no "
+                    f"{args.octaves} -d 3 (BASELINE.json configs[3], HBM-bound pyramid stress)")
+        metric = "SIFT images/sec on 4096x4096 6-octave tiles (features/sec alongside)"
+    else:
+        workload = (f"C3 per-GPU shard: {B} x {W}x{H} u8 gray per GPU per step, "
+                    f"C2 parameters -fo 0 -no {args.octaves} -d 3 (BASELINE.json configs[1-2])")
+        metric = "SIFT images/sec at 1080p (features/sec alongside), 1/2/4/8 MI355X"
     result = {
-        "metric": "SIFT images/sec at 1080p (features/sec alongside), 1/2/4/8 MI355X",
+        "metric": metric,
         "value": total_images / elapsed,
         "unit": "images/s",
         "n_gpus": world,
@@ -165,8 +203,7 @@ def main():
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": f"C3 per-GPU shard: {B} x {W}x{H} u8 gray per GPU per step, "
-                        f"C2 parameters -fo 0 -no {args.octaves} -d 3 (BASELINE.json configs[1-2])",
+            "workload": workload,
             "images_per_gpu": B, "width": W, "height": H, "octaves": args.octaves,
             "parallelism": f"dp{world}",
         },
@@ -191,6 +228,8 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_match:
         result["match"] = bench_match(ctx, args.match_n)
+    if rank == 0 and world == 1 and args.workload == "c3" and not args.no_c4:
+        result["c4"] = bench_c4(ctx)
     if world > 1 and not args.no_match:
         sm = bench_match_sharded(ctx, args.match_n, rank, world, None if rccl else dist)
         if rank == 0:
@@ -234,7 +273,16 @@ def bench_match(ctx, n):
         m = ctx.match(q1, q2)
         ms += ctx.timing()["match"]
     ms /= reps
-    ops = 2.0 * 128 * n * n * 2      # both directions (rows and columns) are computed
+    ops = 2.0 * 128 * n * n          # F = 2 * 128 * N1 * N2 useful ops
+    # the same call through the one-GEMM mutual kernel (both decisions from one set of dots)
+    ctx.set_debug_flags(ctx.DEBUG_FUSED_MATCH)
+    ctx.match(q1, q2)
+    fms, fm = 0.0, None
+    for _ in range(reps):
+        fm = ctx.match(q1, q2)
+        fms += ctx.timing()["match"]
+    fms /= reps
+    ctx.set_debug_flags(0)
     # guided matching (GetGuidedSiftMatch) on a synthetic two-view scene of the same size
     g1, g2, l1, l2, H, F = synth_guided_scene(n, n, 5002)
     ctx.match_guided(g1, g2, l1, l2, H, F)
@@ -245,9 +293,50 @@ def bench_match(ctx, n):
     gms /= reps
     return {"workload": f"C5 {n}x{n} u8 descriptors, mutual best match",
             "ms": ms, "matches": int(len(m)),
+            "path": "two i8-MFMA GEMMs (row side, then the sets swapped for the column side)",
+            "ops": ops, "ops_note": "F = 2*128*N1*N2 counted once (SURVEY.md 8d)",
             "tops": ops / (ms * 1e-3) / 1e12,
             "mfma_util": ops / (ms * 1e-3) / 1e12 / I8_MFMA_PEAK_TOPS,
+            "fused_ms": fms, "fused_matches": int(len(fm)),
+            "fused_mfma_util": ops / (fms * 1e-3) / 1e12 / I8_MFMA_PEAK_TOPS,
             "guided_ms": gms, "guided_matches": int(len(gm))}
+
+
+def bench_c4(ctx, batch=8, steps=3):
+    """BASELINE configs[3]: 4096x4096 tiles, -no 6 (the HBM-bound pyramid stress), a batch of
+    `batch` distinct tiles (seeds 4000..) staged in HBM, `steps` timed passes after one warm-up.
+    Roofline of the pyramid stage as for the headline: 48 B per octave pixel, sum N = 22,364,160
+    px per tile (1.0735 GB per tile)."""
+    opts = default_options(octave_num=6)
+    c4 = sgpu.SiftContext(ctx.device, opts)
+    try:
+        imgs = synth_batch_fast(batch, 4096, 4096, 4000)
+        c4.stage(imgs)
+        c4.extract_staged()
+        t0 = time.perf_counter()
+        pyr, feats, st = 0.0, 0, {}
+        for _ in range(steps):
+            c4.extract_staged()
+            feats += c4.total()
+            t = c4.timing()
+            pyr += t["pyramid"]
+            for k, v in t.items():
+                st[k] = st.get(k, 0.0) + v
+        el = time.perf_counter() - t0
+        sumN = geometry_sum(4096, 4096, 6)
+        n_gauss = 1 + 6 * 5
+        achieved = 48.0 * sumN * batch * steps / (pyr * 1e-3) / 1e9
+        return {"workload": f"C4: {batch} x 4096x4096 u8 tiles per step, -fo 0 -no 6 -d 3, "
+                            f"staged in HBM", "value": batch * steps / el, "unit": "images/s",
+                "ms_per_step": el / steps * 1e3, "features_per_image": feats / (batch * steps),
+                "stage_ms_per_step": {k: v / steps for k, v in st.items() if k != "match"},
+                "roofline": {"kernel": f"k_gauss_pk2 ({n_gauss} launches per step)",
+                             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                             "algorithmic_bytes_per_launch": 48.0 * sumN * batch / n_gauss,
+                             "avg_launch_ms": pyr / steps / n_gauss}}
+    finally:
+        c4.close()
 
 
 def bench_match_sharded(ctx, n, rank, world, host_dist=None):
@@ -302,8 +391,9 @@ def cpu_baseline(imgs, opts):
     n = threads
     secs, feats = oracle_py.bench_extract(imgs[:n], opts, threads=threads)
     return {"value": n / secs, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} of the staged 1920x1080 images (-fo 0 -no 4 -d 3), one per OpenMP "
-                      f"thread, oracle/liboracle.so (g++ -O3, strict IEEE)",
+            "sample": f"{n} of the staged {imgs.shape[2]}x{imgs.shape[1]} images (-fo 0 -no "
+                      f"{opts.octave_num} -d 3), one per OpenMP thread, oracle/liboracle.so "
+                      f"(g++ -O3, strict IEEE)",
             "features_per_image": feats / n}
 
 

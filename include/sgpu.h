@@ -221,6 +221,8 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
 #define SGPU_DEBUG_PARTS4   2   /* ... into 4 parts                                            */
 #define SGPU_DEBUG_TINY_CAP 4   /* start the keypoint capacity at 64 per part, so that the
                                    capacity-overflow re-run of a part is exercised             */
+#define SGPU_DEBUG_FUSED_MATCH 8 /* plain mutual matching through the fused one-GEMM kernel
+                                   (the guided matcher always uses it)                         */
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);

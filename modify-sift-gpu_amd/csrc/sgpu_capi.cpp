@@ -107,7 +107,7 @@ struct sgpu_ctx {
     hipEvent_t ev[T_N + 1] = {};
     float timing[T_N] = {};
     // matcher
-    DevBuf m_d1, m_d2, m_s1, m_s2, m_part, m_terms, m_match, m_dist, m_mask, m_loc;
+    DevBuf m_d1, m_d2, m_s1, m_s2, m_part, m_terms, m_match, m_dist, m_mask, m_loc, m_colpart;
     std::vector<int> h_match;
     bool dist_ready = false;
     // multi-GPU: RCCL communicator of this context's device (sgpu_comm_*)
@@ -312,6 +312,7 @@ int sgpu_ctx_destroy(sgpu_ctx* ctx) {
     ctx->comm = nullptr;
     DevBuf* bufs[] = {&ctx->input, &ctx->all_keys, &ctx->all_desc, &ctx->gray, &ctx->pre, &ctx->m_d1, &ctx->m_d2, &ctx->m_s1, &ctx->m_s2,
                       &ctx->m_part, &ctx->m_terms, &ctx->m_match, &ctx->m_dist, &ctx->m_mask, &ctx->m_loc,
+                      &ctx->m_colpart,
                       &ctx->c_buf};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i <= T_N; i++)
@@ -795,7 +796,7 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     }
     // guided: locations (float2 per feature) and the two geometric masks
     const size_t rmask_bytes = sgk::guided_mask_bytes(n1, n2);
-    const size_t cmask_bytes = mbm ? sgk::guided_mask_bytes(n2, n1) : 0;
+    const size_t cmask_bytes = 0;   // the fused GEMM derives the column side from the same values
     const float* l1 = loc1;
     const float* l2 = loc2;
     if (guided) {
@@ -811,20 +812,26 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
         }
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], st));
-    const int ca = sgk::match_chunks(n1, n2), cb = mbm ? sgk::match_chunks(n2, n1) : 0;
-    const size_t part_n = std::max((size_t)ca * n1, (size_t)cb * n2);
-    ALLOCCHK(ctx, ctx->m_part.ensure(part_n * sizeof(sgk::Top2)));
+    // Mutual matching: guided (or SGPU_DEBUG_FUSED_MATCH) computes the dots once and derives
+    // both decisions from them (k_match_rows<.., COLS>); plain matching runs the row kernel a
+    // second time with the sets swapped, which measured faster (1.07 vs 1.15 ms at 50k x 50k,
+    // DESIGN.md section 10) because the fused epilogue halves the kernel's occupancy.
+    const bool fused = mbm && (guided || (ctx->debug_flags & SGPU_DEBUG_FUSED_MATCH));
+    const int ca = sgk::match_chunks(n1, n2), panels = sgk::match_panels(n1);
+    const int cb = mbm && !fused ? sgk::match_chunks(n2, n1) : 0;
+    ALLOCCHK(ctx, ctx->m_part.ensure(std::max((size_t)ca * n1, (size_t)cb * n2) * sizeof(sgk::Top2)));
+    if (fused) ALLOCCHK(ctx, ctx->m_colpart.ensure((size_t)panels * n2 * sizeof(sgk::Top2)));
     ALLOCCHK(ctx, ctx->m_terms.ensure((size_t)2 * (n1 + n2) * sizeof(int)));
     ALLOCCHK(ctx, ctx->m_match.ensure((size_t)(n1 + n2) * sizeof(int)));
-    int* row1 = ctx->m_terms.as<int>();          // row terms 128 * sum(d1), 128 * sum(d2); the
-    int* row2 = row1 + n1;                       // column terms are formed in k_match_rows
+    int* row1 = ctx->m_terms.as<int>();          // row terms 128 * sum(d1), column terms
+    int* col2 = row1 + n1;                       // 128 * sum(d2) - 2^21
     int* match1 = ctx->m_match.as<int>();
     int* match2 = match1 + n1;
     sgk::Top2* part = ctx->m_part.as<sgk::Top2>();
+    sgk::Top2* colpart = fused ? ctx->m_colpart.as<sgk::Top2>() : nullptr;
     uint8_t* rmask = guided ? ctx->m_mask.as<uint8_t>() : nullptr;
-    uint8_t* cmask = guided && mbm ? rmask + rmask_bytes : nullptr;
     if (guided)
-        HIPCHK(ctx, sgk::launch_guided_mask(l1, n1, l2, n2, *guided, rmask, cmask, st));
+        HIPCHK(ctx, sgk::launch_guided_mask(l1, n1, l2, n2, *guided, rmask, nullptr, st));
     // s8 forms of both sets: the operands of the i8 MFMA
     ALLOCCHK(ctx, ctx->m_s1.ensure((size_t)n1 * 128));
     ALLOCCHK(ctx, ctx->m_s2.ensure((size_t)n2 * 128));
@@ -833,14 +840,28 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     HIPCHK(ctx, sgk::launch_to_s8(a, n1, ctx->m_s1.as<uint8_t>(), st));
     HIPCHK(ctx, sgk::launch_to_s8(b, n2, ctx->m_s2.as<uint8_t>(), st));
     HIPCHK(ctx, sgk::launch_rowsums(a, n1, row1, 128, 0, st));
-    HIPCHK(ctx, sgk::launch_match_rows(s1, n1, s2, n2, ca, part, st, rmask, true));
-    HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, row1, ctx->m_dist.as<float>(), distmax,
-                                         ratiomax, match1, nullptr, st, true));
-    if (mbm) {
-        HIPCHK(ctx, sgk::launch_rowsums(b, n2, row2, 128, 0, st));
-        HIPCHK(ctx, sgk::launch_match_rows(s2, n2, s1, n1, cb, part, st, cmask, false));
-        HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, row2, ctx->m_dist.as<float>(), distmax,
+    if (mbm && !fused) {
+        HIPCHK(ctx, sgk::launch_match_rows(s1, n1, s2, n2, ca, part, st, nullptr, true));
+        HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, row1, ctx->m_dist.as<float>(), distmax,
+                                             ratiomax, match1, nullptr, st, true));
+        HIPCHK(ctx, sgk::launch_rowsums(b, n2, col2, 128, 0, st));
+        HIPCHK(ctx, sgk::launch_match_rows(s2, n2, s1, n1, cb, part, st, nullptr, false));
+        HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, col2, ctx->m_dist.as<float>(), distmax,
                                              ratiomax, match2, nullptr, st, false));
+    } else if (mbm) {
+        // one GEMM for both decisions (MultiplyDescriptor_Kernel's row results + column
+        // partials, ProgramCU.cu:1466-1564)
+        // guided: the column values already hold the column term (col_term 0)
+        HIPCHK(ctx, sgk::launch_rowsums(b, n2, col2, guided ? 0 : 128, guided ? 0 : -2097152, st));
+        HIPCHK(ctx, sgk::launch_match_rows(s1, n1, s2, n2, ca, part, st, rmask, true, row1, colpart));
+        HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, row1, ctx->m_dist.as<float>(),
+                                             distmax, ratiomax, match1, nullptr, st, true));
+        HIPCHK(ctx, sgk::launch_match_cols(colpart, n2, panels, col2, ctx->m_dist.as<float>(),
+                                           distmax, ratiomax, match2, nullptr, st));
+    } else {
+        HIPCHK(ctx, sgk::launch_match_rows(s1, n1, s2, n2, ca, part, st, rmask, true));
+        HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, row1, ctx->m_dist.as<float>(), distmax,
+                                             ratiomax, match1, nullptr, st, true));
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
     ctx->h_match.resize((size_t)n1 + n2);
@@ -924,17 +945,21 @@ int sgpu_match_shard_begin(sgpu_ctx* ctx, const uint8_t* d1, int ns, int row_beg
         b = ctx->m_d2.as<uint8_t>();
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], st));
-    const int ca = sgk::match_chunks(ns, n2), cb = mbm ? sgk::match_chunks(n2, ns) : 0;
+    const bool fused = mbm && (ctx->debug_flags & SGPU_DEBUG_FUSED_MATCH);   // see match_impl
+    const int ca = sgk::match_chunks(ns, n2), panels = sgk::match_panels(ns);
+    const int cb = mbm && !fused ? sgk::match_chunks(n2, ns) : 0;
     const size_t part_n = std::max((size_t)ca * ns, (size_t)cb * n2);
     ALLOCCHK(ctx, ctx->m_part.ensure(part_n * sizeof(sgk::Top2) + (size_t)n2 * sizeof(sgk::Top2)));
+    if (fused) ALLOCCHK(ctx, ctx->m_colpart.ensure((size_t)panels * n2 * sizeof(sgk::Top2)));
     ALLOCCHK(ctx, ctx->m_terms.ensure((size_t)2 * (ns + n2) * sizeof(int)));
     ALLOCCHK(ctx, ctx->m_match.ensure((size_t)(ns + n2) * sizeof(int)));
     int* row1 = ctx->m_terms.as<int>();
-    int* row2 = row1 + ns;
+    int* col2 = row1 + ns;
     int* match1 = ctx->m_match.as<int>();
     int* match2 = match1 + ns;
     sgk::Top2* part = ctx->m_part.as<sgk::Top2>();
     sgk::Top2* best2 = part + part_n;
+    sgk::Top2* colpart = fused ? ctx->m_colpart.as<sgk::Top2>() : nullptr;
     const float* dist = ctx->m_dist.as<float>();
     ALLOCCHK(ctx, ctx->m_s1.ensure((size_t)ns * 128));
     ALLOCCHK(ctx, ctx->m_s2.ensure((size_t)n2 * 128));
@@ -943,14 +968,25 @@ int sgpu_match_shard_begin(sgpu_ctx* ctx, const uint8_t* d1, int ns, int row_beg
     HIPCHK(ctx, sgk::launch_to_s8(a, ns, ctx->m_s1.as<uint8_t>(), st));
     HIPCHK(ctx, sgk::launch_to_s8(b, n2, ctx->m_s2.as<uint8_t>(), st));
     HIPCHK(ctx, sgk::launch_rowsums(a, ns, row1, 128, 0, st));
-    HIPCHK(ctx, sgk::launch_match_rows(s1, ns, s2, n2, ca, part, st, nullptr, true));
-    HIPCHK(ctx, sgk::launch_match_finish(part, ns, ca, row1, dist, distmax, ratiomax, match1,
-                                         nullptr, st, true));
-    if (mbm) {
-        HIPCHK(ctx, sgk::launch_rowsums(b, n2, row2, 128, 0, st));
+    if (mbm && !fused) {
+        HIPCHK(ctx, sgk::launch_match_rows(s1, ns, s2, n2, ca, part, st, nullptr, true));
+        HIPCHK(ctx, sgk::launch_match_finish(part, ns, ca, row1, dist, distmax, ratiomax, match1,
+                                             nullptr, st, true));
+        HIPCHK(ctx, sgk::launch_rowsums(b, n2, col2, 128, 0, st));
         HIPCHK(ctx, sgk::launch_match_rows(s2, n2, s1, ns, cb, part, st, nullptr, false));
-        HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, row2, dist, distmax, ratiomax, match2,
+        HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, col2, dist, distmax, ratiomax, match2,
                                              best2, st, false));
+    } else if (mbm) {
+        HIPCHK(ctx, sgk::launch_rowsums(b, n2, col2, 128, -2097152, st));
+        HIPCHK(ctx, sgk::launch_match_rows(s1, ns, s2, n2, ca, part, st, nullptr, true, row1, colpart));
+        HIPCHK(ctx, sgk::launch_match_finish(part, ns, ca, row1, dist, distmax, ratiomax,
+                                             match1, nullptr, st, true));
+        HIPCHK(ctx, sgk::launch_match_cols(colpart, n2, panels, col2, dist, distmax, ratiomax,
+                                           match2, best2, st));
+    } else {
+        HIPCHK(ctx, sgk::launch_match_rows(s1, ns, s2, n2, ca, part, st, nullptr, true));
+        HIPCHK(ctx, sgk::launch_match_finish(part, ns, ca, row1, dist, distmax, ratiomax, match1,
+                                             nullptr, st, true));
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
     HIPCHK(ctx, hipMemcpyAsync(row_match, match1, (size_t)ns * sizeof(int), hipMemcpyDeviceToHost, st));

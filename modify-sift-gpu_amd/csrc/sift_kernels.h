@@ -142,9 +142,18 @@ int match_chunks(int nA, int nB);
 // row_side: equal maxima resolve as RowMatch_Kernel does (A = set 1); else in column order.
 // With a mask (launch_guided_mask, this side's lane records): the guided values
 // (k_match_rows<true>).
+// colpart != nullptr (row_side only; row_term = 128 * sum(A rows)): the fused mutual form --
+// colpart[panel][nB] also receives every 128-row panel's column-side (max, row, second) of
+// (dot - column term) (guided: of the guided value), for launch_match_cols.
 hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
                              int chunks, Top2* part, hipStream_t stream,
-                             const uint8_t* mask, bool row_side);
+                             const uint8_t* mask, bool row_side, const int* row_term = nullptr,
+                             Top2* colpart = nullptr);
+int match_panels(int nA);
+// Column decisions from the panels' partials: col_term[j] = 128 * sum(B_j) - 2^21 (guided: 0).
+hipError_t launch_match_cols(const Top2* colpart, int n, int panels, const int* col_term,
+                             const float* dist, float distmax, float ratiomax, int* out,
+                             Top2* best, hipStream_t stream);
 // Guided matching geometry (SiftMatchGPU::GetGuidedSiftMatch): H, F row-major 3x3.
 struct GuidedParams { float H[9]; float F[9]; float hdistmax, fdistmax; };
 // bytes of one side's guided mask records (A rows, B columns)
@@ -154,7 +163,8 @@ size_t guided_mask_bytes(int nA, int nB);
 hipError_t launch_guided_mask(const float* loc1, int n1, const float* loc2, int n2,
                               const GuidedParams& gp, uint8_t* rec1, uint8_t* rec2,
                               hipStream_t stream);
-// merge chunks, add row_term, apply distmax / ratiomax -> out[i] = matched index or -1
+// merge chunks, add row_term (nullptr: none), apply distmax / ratiomax -> out[i] = matched
+// index or -1
 hipError_t launch_match_finish(const Top2* part, int n, int chunks, const int* row_term,
                                const float* dist, float distmax, float ratiomax, int* out,
                                Top2* best, hipStream_t stream, bool row_side);

@@ -223,6 +223,11 @@ __global__ __launch_bounds__(256) void k_gauss_pk2(
                 for (int j = 0; j < 4; j++)
                     if (m - j >= 0 && m - j < FW) acc[j] = pk_fma(v, taps.k[m - j], acc[j]);
             }
+            // the sums are complete here: without this, each row's FMA chain is sunk into its
+            // conditional store below and every ring value of the pass stays live until then
+            // (+2 VGPRs per tap: a wave per SIMD of occupancy, pyramid +9 %)
+#pragma unroll
+            for (int j = 0; j < 4; j++) asm volatile("" : "+v"(acc[j]));
             if (x < W) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {

@@ -95,14 +95,26 @@ __device__ __forceinline__ bool tie_before(int a, int b) {
 // low bits order equal dots that way, so the tile's maximum key is its winner.  Across tiles a
 // later tile may only take over when the key's tie-relevant prefix grows (the dot; TIE32: the dot
 // and col % 32), and the key is recorded with its tile at that moment.
-template <bool GUIDED, bool TIE32>
+//
+// COLS (mutual matching, one GEMM for both decisions): every tile also yields the column side
+// (ColMatch_Kernel's decision over set-1 rows, ProgramCU.cu:1844-1900, fed by
+// MultiplyDescriptor_Kernel's per-block partials, :1540-1552).  A column's value over the rows
+// is acc + row term (= dot - column term; guided: = the guided value, the column term is already
+// in acc); per column the panel's (max, argmax row, second) comes from keys ((acc + rt) << 7) |
+// (127 - row in panel) -- equal values keep the lowest row -- merged over the 16 lanes and 4
+// waves that hold the column and written to colpart[panel][column].  k_match_cols merges the
+// panels in row order.  The row side is the plain kernel's.
+template <bool GUIDED, bool TIE32, bool COLS>
 __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ A, int nA,
                                                     const uint8_t* __restrict__ B, int nB,
                                                     int cols_per_chunk, Top2* __restrict__ part,
                                                     const uint4* __restrict__ mask,
-                                                    int mask_tiles) {
+                                                    int mask_tiles,
+                                                    const int* __restrict__ row_term,
+                                                    Top2* __restrict__ colpart) {
     __shared__ __attribute__((aligned(16))) uint8_t s_b[2][kTile * kLdsRow];
     __shared__ int s_ct[2][kTile];   // column terms of the staged tile (from its bytes)
+    __shared__ int s_cm[COLS ? 4 : 1][COLS ? kTile : 1], s_cs[COLS ? 4 : 1][COLS ? kTile : 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int panel = blockIdx.x, chunk = blockIdx.y;
     const int c_begin = chunk * cols_per_chunk;
@@ -120,6 +132,17 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
             else afrag[rb][kh] = v4i{0, 0, 0, 0};
         }
     }
+    // COLS: per row of this lane, the column keys' addend (row term << 7) | (127 - row in
+    // panel); rows past nA get a row term of -2^22, so their values stay <= 0 and can only win
+    // a column whose result the finish clamps to "no match" anyway
+    int rtlow[2][4];
+#pragma unroll
+    for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int rp = wave * 32 + rb * 16 + quad * 4 + i, row = panel * kPanel + rp;
+            rtlow[rb][i] = COLS ? (((row < nA ? row_term[row] : -(1 << 22)) << 7) | (127 - rp)) : 0;
+        }
     // guided: this lane's mask records (rows past nA read none)
     const bool rec_ok = GUIDED && panel * kPanel + wave * 32 < nA;
     const uint4* rec_p = rec_ok ? mask + (size_t)(panel * 4 + wave) * mask_tiles * 64 + lane : nullptr;
@@ -235,18 +258,61 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         for (int rb = 0; rb < 2; rb++)
 #pragma unroll
             for (int i = 0; i < 4; i++) { mt[rb][i] = M[rb][i]; st[rb][i] = S[rb][i]; }
+        if constexpr (!COLS) {
 #pragma unroll
-        for (int half = 0; half < 2; half++)
+            for (int half = 0; half < 2; half++)
 #pragma unroll
-            for (int rb = 0; rb < 2; rb++)
+                for (int rb = 0; rb < 2; rb++)
 #pragma unroll
-                for (int i = 0; i < 4; i++)
+                    for (int i = 0; i < 4; i++)
 #pragma unroll
-                    for (int cb = 4 * half; cb < 4 * half + 4; cb++) {
-                        const int key = (acc[rb][cb][i] << 7) + ctlow[cb];
+                        for (int cb = 4 * half; cb < 4 * half + 4; cb++) {
+                            const int key = (acc[rb][cb][i] << 7) + ctlow[cb];
+                            st[rb][i] = med3i(st[rb][i], mt[rb][i], key);
+                            mt[rb][i] = max(mt[rb][i], key);
+                        }
+        } else {
+            // both sides per column block, so that each accumulator block dies after its
+            // folds: the row keys into the running row state, the column keys ((acc << 7) |
+            // (127 - row in panel)) over this lane's 8 rows, then over the 4 lanes of the column
+            // in this wave (xor 16, 32); the 4 waves meet in LDS
+#pragma unroll
+            for (int cb = 0; cb < 8; cb++) {
+                int cm = kNeg, cs = kNeg;
+#pragma unroll
+                for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const int a = acc[rb][cb][i];
+                        const int key = (a << 7) + ctlow[cb];
                         st[rb][i] = med3i(st[rb][i], mt[rb][i], key);
                         mt[rb][i] = max(mt[rb][i], key);
+                        const int ck = (a << 7) + rtlow[rb][i];
+                        cs = med3i(cs, cm, ck);
+                        cm = max(cm, ck);
                     }
+                // lanes l, l ^ 16 and l ^ 32 by v_permlane16/32_swap (VALU, no LDS): after a
+                // swap of a value with itself the two results hold the pair's two values
+                {
+                    const auto a = __builtin_amdgcn_permlane16_swap(cm, cm, false, false);
+                    const auto b2 = __builtin_amdgcn_permlane16_swap(cs, cs, false, false);
+                    const int a0 = (int)a[0], a1 = (int)a[1];
+                    cs = max(min(a0, a1), max((int)b2[0], (int)b2[1]));
+                    cm = max(a0, a1);
+                }
+                {
+                    const auto a = __builtin_amdgcn_permlane32_swap(cm, cm, false, false);
+                    const auto b2 = __builtin_amdgcn_permlane32_swap(cs, cs, false, false);
+                    const int a0 = (int)a[0], a1 = (int)a[1];
+                    cs = max(min(a0, a1), max((int)b2[0], (int)b2[1]));
+                    cm = max(a0, a1);
+                }
+                if (quad == 0) {
+                    s_cm[wave][cb * 16 + l16] = cm;
+                    s_cs[wave][cb * 16 + l16] = cs;
+                }
+            }
+        }
 #pragma unroll
         for (int rb = 0; rb < 2; rb++)
 #pragma unroll
@@ -259,6 +325,19 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
                 S[rb][i] = st[rb][i];
             }
         __syncthreads();
+        if constexpr (COLS) {
+            if (tid < kTile && tb + tid < c_end) {
+                int cm = s_cm[0][tid], cs = s_cs[0][tid];
+#pragma unroll
+                for (int w = 1; w < 4; w++) {
+                    const int m2 = s_cm[w][tid], s2 = s_cs[w][tid];
+                    cs = max(min(cm, m2), max(cs, s2));
+                    cm = max(cm, m2);
+                }
+                colpart[(size_t)panel * nB + tb + tid] =
+                    Top2{cm >> 7, panel * kPanel + 127 - (cm & 127), cs >> 7};
+            }
+        }
         if (has_next) {
             buf ^= 1;
             stage_store(buf, stg, tb + kTile);
@@ -327,7 +406,7 @@ __global__ __launch_bounds__(256) void k_match_finish(const Top2* __restrict__ p
                                                      : tie_before<false>(u.idx, t.idx)));
         t = Top2{m, later ? u.idx : t.idx, s};
     }
-    const int rt = row_term[r];
+    const int rt = row_term ? row_term[r] : 0;   // COLS: already in the accumulators
     // the reference's running maxima start at 0 with index -1 (ProgramCU.cu:1803)
     int mx = t.max + rt, sc = t.second + rt;
     int idx = t.idx;
@@ -336,6 +415,46 @@ __global__ __launch_bounds__(256) void k_match_finish(const Top2* __restrict__ p
     if (best) best[r] = Top2{mx, idx, sc};
     const float d1 = dist[min(mx, 262144)], d2 = dist[min(sc, 262144)];
     out[r] = (d1 < distmax) && (d1 < d2 * ratiomax) ? idx : -1;
+}
+
+// Column decision of the fused GEMM (COLS): merge the panels' partials of column j in row
+// order (equal maxima keep the earlier panel: ColMatch_Kernel, ProgramCU.cu:1874-1882), add the
+// column term (acc = dot - column term), clamp as the reference's running state from (0, -1, 0)
+// and apply the distance / ratio test.
+constexpr int kColGroups = 16;   // panel groups per column in k_match_cols
+
+__device__ __forceinline__ void top2_merge(Top2& t, const Top2& u) {
+    // equal maxima keep the lower row: the order of the merges does not matter
+    const int s = max(min(t.max, u.max), max(t.second, u.second));
+    if (u.max > t.max || (u.max == t.max && u.idx < t.idx)) t.idx = u.idx;
+    t.max = max(t.max, u.max);
+    t.second = s;
+}
+
+__global__ __launch_bounds__(256) void k_match_cols(const Top2* __restrict__ colpart, int n,
+                                                    int panels, const int* __restrict__ col_term,
+                                                    const float* __restrict__ dist,
+                                                    float distmax, float ratiomax,
+                                                    int* __restrict__ out,
+                                                    Top2* __restrict__ best) {
+    // 16 columns x 16 panel groups per workgroup: group g merges panels g, g + 16, ...
+    __shared__ Top2 s_t[kColGroups][256 / kColGroups];
+    const int cl = threadIdx.x % (256 / kColGroups), g = threadIdx.x / (256 / kColGroups);
+    const int j = blockIdx.x * (256 / kColGroups) + cl;
+    Top2 t{INT_MIN, INT_MAX, INT_MIN};
+    if (j < n)
+        for (int p = g; p < panels; p += kColGroups) top2_merge(t, colpart[(size_t)p * n + j]);
+    s_t[g][cl] = t;
+    __syncthreads();
+    if (g != 0 || j >= n) return;
+    for (int q = 1; q < kColGroups; q++) top2_merge(t, s_t[q][cl]);
+    const int ct = col_term[j];
+    int mx = t.max + ct, sc = t.second + ct, idx = t.idx;
+    if (mx <= 0) { mx = 0; idx = -1; }
+    if (sc < 0) sc = 0;
+    if (best) best[j] = Top2{mx, idx, sc};
+    const float d1 = dist[min(mx, 262144)], d2 = dist[min(sc, 262144)];
+    out[j] = (d1 < distmax) && (d1 < d2 * ratiomax) ? idx : -1;
 }
 
 // Geometric test of MultiplyDescriptorG_Kernel (ProgramCU.cu:1648-1681), once per pair, in
@@ -518,27 +637,40 @@ int match_chunks(int nA, int nB) {
     return max(1, min(chunks, max_chunks));
 }
 
+int match_panels(int nA) { return (nA + kPanel - 1) / kPanel; }
+
 hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
                              int chunks, Top2* part, hipStream_t stream,
-                             const uint8_t* mask, bool row_side) {
+                             const uint8_t* mask, bool row_side, const int* row_term,
+                             Top2* colpart) {
     if (nA <= 0 || nB <= 0) return hipSuccess;
+    if (colpart && (!row_term || !row_side)) return hipErrorInvalidValue;
     int per = (nB + chunks - 1) / chunks;
     per = (per + kTile - 1) / kTile * kTile;
     dim3 grid((nA + kPanel - 1) / kPanel, chunks);
     const int tiles = (nB + kTile - 1) / kTile;
     const uint4* rec = reinterpret_cast<const uint4*>(mask);
-    if (!mask && row_side)
-        hipLaunchKernelGGL((k_match_rows<false, true>), grid, dim3(256), 0, stream, A, nA, B, nB,
-                           per, part, rec, tiles);
-    else if (!mask)
-        hipLaunchKernelGGL((k_match_rows<false, false>), grid, dim3(256), 0, stream, A, nA, B,
-                           nB, per, part, rec, tiles);
-    else if (row_side)
-        hipLaunchKernelGGL((k_match_rows<true, true>), grid, dim3(256), 0, stream, A, nA, B, nB,
-                           per, part, rec, tiles);
-    else
-        hipLaunchKernelGGL((k_match_rows<true, false>), grid, dim3(256), 0, stream, A, nA, B, nB,
-                           per, part, rec, tiles);
+#define SGK_MR(G, T, C)                                                                       \
+    hipLaunchKernelGGL((k_match_rows<G, T, C>), grid, dim3(256), 0, stream, A, nA, B, nB, per, \
+                       part, rec, tiles, row_term, colpart)
+    if (colpart) {
+        if (mask) SGK_MR(true, true, true); else SGK_MR(false, true, true);
+    } else if (!mask) {
+        if (row_side) SGK_MR(false, true, false); else SGK_MR(false, false, false);
+    } else {
+        if (row_side) SGK_MR(true, true, false); else SGK_MR(true, false, false);
+    }
+#undef SGK_MR
+    return hipGetLastError();
+}
+
+hipError_t launch_match_cols(const Top2* colpart, int n, int panels, const int* col_term,
+                             const float* dist, float distmax, float ratiomax, int* out,
+                             Top2* best, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    const int per = 256 / kColGroups;
+    hipLaunchKernelGGL(k_match_cols, dim3((n + per - 1) / per), dim3(256), 0, stream, colpart, n,
+                       panels, col_term, dist, distmax, ratiomax, out, best);
     return hipGetLastError();
 }
 

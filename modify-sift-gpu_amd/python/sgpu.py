@@ -131,6 +131,7 @@ class SiftContext:
 
     def __init__(self, device: int = 0, opts: SgpuOptions | None = None):
         self.opts = opts or default_options()
+        self.device = device
         self._ctx = ctypes.c_void_p()
         rc = lib().sgpu_ctx_create(device, ctypes.byref(self.opts), ctypes.byref(self._ctx))
         if rc != SGPU_OK:
@@ -336,7 +337,7 @@ class SiftContext:
         return a
 
     # ---- test hooks
-    DEBUG_PARTS2, DEBUG_PARTS4, DEBUG_TINY_CAP = 1, 2, 4
+    DEBUG_PARTS2, DEBUG_PARTS4, DEBUG_TINY_CAP, DEBUG_FUSED_MATCH = 1, 2, 4, 8
 
     def set_debug_flags(self, flags: int):
         """Per-context debug flags (sgpu_debug_set_flags; 0 = shipped configuration)."""

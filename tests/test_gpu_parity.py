@@ -370,6 +370,25 @@ def test_match_exact_ties(gpu_ctx, n1, n2, cols):
     assert [pairs.get(i) for i in rows] == [tie_winner(x, y) for x, y in cols]
 
 
+@pytest.mark.parametrize("n1,n2,dup", [(1, 700, 0), (700, 1, 0), (257, 1000, 100),
+                                       (3000, 2500, 1000), (4096, 4096, 2000), (5000, 129, 50)])
+def test_fused_match_vs_oracle(gpu_ctx, n1, n2, dup):
+    """The one-GEMM mutual matcher (row decisions and per-panel column partials from the same
+    accumulators, SGPU_DEBUG_FUSED_MATCH) gives the oracle's pairs, ties included."""
+    d1 = synth_descriptors(n1, 10 * n1 + n2)
+    d2 = synth_descriptors(n2, 10 * n2 + n1 + 1, base=d1, n_dup=min(dup, n1, n2))
+    q1, q2 = quantize(d1), quantize(d2)
+    try:
+        gpu_ctx.set_debug_flags(gpu_ctx.DEBUG_FUSED_MATCH)
+        assert np.array_equal(gpu_ctx.match(q1, q2), O.match(q1, q2))
+        q1t, q2t, _ = synth_tie_scene(3000, 9000, 17, [(200, 129), (130, 2), (4000, 33), (8999, 1)],
+                                      [(60, 61), (1, 2995)])
+        a = gpu_ctx.match(q1t, q2t, distmax=2.0, ratiomax=1.5, mbm=1)
+        assert np.array_equal(a, O.match(q1t, q2t, distmax=2.0, ratiomax=1.5, mbm=1))
+    finally:
+        gpu_ctx.set_debug_flags(0)
+
+
 def test_match_max_match_truncates(gpu_ctx):
     d1 = synth_descriptors(1000, 81)
     d2 = synth_descriptors(1000, 82, base=d1, n_dup=900)
@@ -666,8 +685,9 @@ def test_guided_api_replica(tmp_path):
         assert np.array_equal(np.array(got, np.int32).reshape(-1, 2), want)
 
 
+@pytest.mark.parametrize("fused", [0, 1])
 @pytest.mark.parametrize("bounds", [[0, 5000], [0, 1234, 1235, 3100, 5000], [0, 0, 2500, 5000]])
-def test_sharded_match_equals_full(gpu_ctx, bounds):
+def test_sharded_match_equals_full(gpu_ctx, bounds, fused):
     """Sharded matcher on the device: sgpu_match_shard_begin per shard, the
     column states merged by sgpu_match_shard_end; the concatenated pairs equal sgpu_match and
     the oracle, ties between rows of different shards included."""
@@ -676,10 +696,12 @@ def test_sharded_match_equals_full(gpu_ctx, bounds):
     q1, q2 = quantize(d1), quantize(d2)
     q1[4000] = q1[17]
     q1[2600] = q1[1300]
+    gpu_ctx.set_debug_flags(gpu_ctx.DEBUG_FUSED_MATCH if fused else 0)
     full = gpu_ctx.match(q1, q2)
     np.testing.assert_array_equal(full, O.match(q1, q2))
     shards = list(zip(bounds[:-1], bounds[1:]))
     begun = [gpu_ctx.match_shard_begin(q1[a:b], a, q2) for a, b in shards]
+    gpu_ctx.set_debug_flags(0)
     allc = np.stack([c for _, c in begun])
     got = np.concatenate([sgpu.match_shard_end(allc, r, a) for (a, _), (r, _) in zip(shards, begun)])
     np.testing.assert_array_equal(got, full)
