@@ -223,6 +223,11 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
                                    capacity-overflow re-run of a part is exercised             */
 #define SGPU_DEBUG_FUSED_MATCH 8 /* plain mutual matching through the fused one-GEMM kernel
                                    (the guided matcher always uses it)                         */
+#define SGPU_DEBUG_EXACT_DESCRIPTOR 16 /* descriptors in the reference's per-bin fma order with the
+                                   oracle's transcendentals: bit-identical to the oracle.  The
+                                   shipped kernel sums in any order with hardware sqrt/rcp/exp
+                                   (descriptor L2 ~1e-6 from the oracle).  Also set at context
+                                   creation by the environment variable SGPU_EXACT_DESCRIPTOR=1 */
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);

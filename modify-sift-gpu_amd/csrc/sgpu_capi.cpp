@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -290,6 +291,9 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
         }
         for (hipEvent_t& e : pt.ev) (void)hipEventCreate(&e);
     }
+    // test mode for the C++ replicas, which only see SiftGPU.h: the bit-exact descriptor
+    if (const char* ev = getenv("SGPU_EXACT_DESCRIPTOR"))
+        if (ev[0] == '1') ctx->debug_flags |= SGPU_DEBUG_EXACT_DESCRIPTOR;
     int rc = sgpu_ctx_set_options(ctx, opt);
     if (rc != SGPU_OK) {
         sgpu_ctx_destroy(ctx);
@@ -508,7 +512,9 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     HIPCHK(ctx, hipEventRecord(pt.ev[4], st));
     if (O.descriptors)
         HIPCHK(ctx, sgk::launch_descriptor(pyr, pt.feat.as<float4>(), pt.feat_info.as<int2>(),
-                                           n_feat_dev, feat_grid, fp, pt.desc.as<float>(), st));
+                                           n_feat_dev, feat_grid, fp, pt.desc.as<float>(), st,
+                                           nullptr, false,
+                                           ctx->debug_flags & SGPU_DEBUG_EXACT_DESCRIPTOR));
     HIPCHK(ctx, hipEventRecord(pt.ev[5], st));
     HIPCHK(ctx, sgk::launch_image_offsets(pt.row_base.as<uint32_t>(), pt.eoff.as<uint32_t>(), n,
                                           fp.rows_per_image, pt.total_rows, (int)nc,
@@ -748,7 +754,8 @@ int sgpu_extract_keypoints(sgpu_ctx* ctx, int image, const float* keys, int num,
         HIPCHK(ctx, hipMemsetAsync(pt.desc.p, 0, (size_t)num * 128 * sizeof(float), st));
         HIPCHK(ctx, sgk::launch_descriptor(pt.pyr.as<float>(), pt.feat.as<float4>(),
                                            pt.feat_info.as<int2>(), d_m, std::max(m, 1), pt.fp,
-                                           pt.desc.as<float>(), st, d_index, rect));
+                                           pt.desc.as<float>(), st, d_index, rect,
+                                           ctx->debug_flags & SGPU_DEBUG_EXACT_DESCRIPTOR));
     }
     HIPCHK(ctx, hipStreamSynchronize(st));
     // the described image now owns the context's feature list

@@ -93,10 +93,12 @@ hipError_t launch_expand(const float4* cand, const int2* info, const uint32_t* e
 // per feature), the kernel grid-strides over *n_feat_dev.  out_index (optional): feature e's
 // descriptor goes to row out_index[e].  rect: the rectangle descriptor of keys given with
 // keys_have_orientation == -1 (feat = (x, y, width, height) in octave coordinates).
+// exact: the reference's per-bin fma order and the oracle's transcendentals (bit-identical to the
+// oracle; the test mode); otherwise the relaxed-order kernel (L2 ~1e-6 from the oracle).
 hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* feat_info,
                              const uint32_t* n_feat_dev, int n_feat_cap, const FeatureParams& fp,
                              float* desc, hipStream_t stream, const int* out_index = nullptr,
-                             bool rect = false);
+                             bool rect = false, bool exact = false);
 
 // Caller-supplied keypoints: strongest orientation into feat[e].w (num_orientation != 0, else
 // 0) and the image-coordinate key at keys_out[index[e]].

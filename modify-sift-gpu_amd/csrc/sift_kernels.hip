@@ -1167,6 +1167,231 @@ __device__ __forceinline__ void descriptor_one(uint32_t e, int lane,
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Relaxed-order descriptor (the shipped default).  Same samples, same weights, same bins as
+// descriptor_one -- the reference's ComputeDescriptor_Kernel / ComputeDescriptorRECT_Kernel
+// (ProgramCU.cu:1013-1171) -- but each sample's contribution is formed and accumulated by ONE
+// lane, in any order:
+//   * each of the quad's 4 lanes walks every 4th sample of its cell and keeps all 8 bins in
+//     registers; the 4 partial histograms are summed by DPP at the end (descriptor_one instead
+//     broadcasts every sample to the 4 lanes so that each bin sees the reference's fma order);
+//   * the linear bin interpolation is the tent max(0, 1 - |theta - k|) per bin (bin 0 also
+//     takes the wrap-around of bin 8, ProgramCU.cu:1094): 2 VALU + 1 fma per bin, no selects;
+//   * gradient magnitude, atan2, the Gaussian window and the normalisation use the hardware
+//     v_sqrt / v_rcp / v_exp (1 ulp) and a short atan2 series (|error| < 1e-6 rad), except
+//     near the one discontinuity of the reference's binning (a sample whose theta rounds to
+//     8.0 is dropped), where the oracle's atan2 decides.
+// Every difference to the reference's arithmetic is continuous in the inputs and of the order of
+// a float ulp, so descriptors agree with the oracle to L2 ~1e-6 (tests: < 1e-4, the north star's
+// bound; descriptor_one stays the bit-exact test mode, SGPU_DEBUG_EXACT_DESCRIPTOR).
+__device__ __forceinline__ float atan2_relaxed(float y, float x) {
+    const float ax = fabs_(x), ay = fabs_(y);
+    const float mx = fmax_(ax, ay), mn = fmin_(ax, ay);
+    const bool red = mn > 0.414213562f * mx;           // reduce to |t| <= tan(pi/8)
+    const float t = (red ? mn - mx : mn) * __builtin_amdgcn_rcpf(red ? mn + mx : mx);
+    const float z = t * t;
+    float p = -0.0909090909f;                           // odd series to t^11: |err| < 1e-6
+    p = fma_(p, z, 0.111111111f);
+    p = fma_(p, z, -0.142857143f);
+    p = fma_(p, z, 0.2f);
+    p = fma_(p, z, -0.333333333f);
+    float r = fma_(p * z, t, t) + (red ? 0.785398163f : 0.0f);
+    r = ay > ax ? 1.57079633f - r : r;
+    r = (as_uint(x) >> 31) ? 3.14159265f - r : r;
+    return (as_uint(y) >> 31) ? -r : r;
+}
+
+// Quad (xor) butterfly sum: every lane of the quad ends with the quad's total.
+__device__ __forceinline__ float quad_sum(float v) {
+    v += as_float((uint32_t)__builtin_amdgcn_mov_dpp((int)as_uint(v), 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+    v += as_float((uint32_t)__builtin_amdgcn_mov_dpp((int)as_uint(v), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+    return v;
+}
+
+template <bool RECT>
+__device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
+                                                const float* __restrict__ pyr,
+                                                const float4* __restrict__ feat,
+                                                const int2* __restrict__ feat_info,
+                                                const FeatureParams& fp,
+                                                float* __restrict__ desc, uint32_t out) {
+    const int cell = lane >> 2, sub = lane & 3;
+    const int ix = cell & 3, iy = cell >> 2;
+    const float4 key = feat[e];
+    const int2 in = feat_info[e];
+    const int o = in.y / fp.d, j = in.y - o * fp.d;
+    const OctaveDesc& od = fp.oct[o];
+    const int W = od.wa, H = od.h;
+    const float* g = pyr + od.gauss_off + (long long)(1 + j) * od.level_stride +
+                     (long long)in.x * W * H;
+    const float rpi = (float)(4.0 / 3.14159265358979323846);
+    // cell geometry exactly as descriptor_one (so both visit the same samples)
+    float spt = 0.f, anglef = 0.f, cspt = 0.f, sspt = 0.f, crspt = 0.f, srspt = 0.f;
+    float ox = 0.f, oy = 0.f, ptx, pty, bszx, bszy;
+    const float sptx = key.z * 0.25f, spty = key.w * 0.25f;
+    if (RECT) {
+        ptx = fma_(sptx, ix + 0.5f, key.x);
+        pty = fma_(spty, iy + 0.5f, key.y);
+        bszx = sptx;
+        bszy = spty;
+    } else {
+        spt = fabs_(key.z * fp.window_factor);
+        float s, c;
+        sincos_(key.w, &s, &c);
+        anglef = (double)key.w > 3.14159265358979323846
+                     ? (float)((double)key.w - (2.0 * 3.14159265358979323846))
+                     : key.w;
+        cspt = c * spt;
+        sspt = s * spt;
+        crspt = c / spt;
+        srspt = s / spt;
+        ox = ix - 1.5f;
+        oy = iy - 1.5f;
+        ptx = fma_(cspt, ox, -(sspt * oy)) + key.x;
+        pty = fma_(cspt, oy, sspt * ox) + key.y;
+        bszx = bszy = fabs_(cspt) + fabs_(sspt);
+    }
+    const float xmin = fmax_(1.5f, floor_(ptx - bszx) + 0.5f);
+    const float ymin = fmax_(1.5f, floor_(pty - bszy) + 0.5f);
+    const float xmax = fmin_(W - 1.5f, floor_(ptx + bszx) + 0.5f);
+    const float ymax = fmin_(H - 1.5f, floor_(pty + bszy) + 0.5f);
+    const int ncols = xmax >= xmin ? (int)(xmax - xmin) + 1 : 0;
+    const int nrows = ymax >= ymin ? (int)(ymax - ymin) + 1 : 0;
+    const bool use_c = !RECT && fabs_(crspt) > 1e-4f / spt;
+    const bool use_s = !RECT && fabs_(srspt) > 1e-4f / spt;
+    const float icr = use_c ? 1.0f / crspt : 0.0f, isr = use_s ? 1.0f / srspt : 0.0f;
+    const float kInf = as_float(0x7f800000u);
+    auto row_span = [&](int r, int& lo, int& len) {
+        const float dy = (ymin + (float)r) - pty;
+        float a = -kInf, bnd = kInf;
+        if (use_c) {
+            const float p = (-1.0f - srspt * dy) * icr, q = (1.0f - srspt * dy) * icr;
+            a = fmax_(a, fmin_(p, q));
+            bnd = fmin_(bnd, fmax_(p, q));
+        }
+        if (use_s) {
+            const float p = (crspt * dy - 1.0f) * isr, q = (crspt * dy + 1.0f) * isr;
+            a = fmax_(a, fmin_(p, q));
+            bnd = fmin_(bnd, fmax_(p, q));
+        }
+        const float cl = fmax_(0.0f, ceilf(ptx + a - xmin - 0.01f));
+        const float ch = fmin_((float)(ncols - 1), floor_(ptx + bnd - xmin + 0.01f));
+        lo = (int)cl;
+        len = ch >= cl ? (int)ch - lo + 1 : 0;
+    };
+    const float irx = RECT ? __builtin_amdgcn_rcpf(sptx) : 0.f;
+    const float iry = RECT ? __builtin_amdgcn_rcpf(spty) : 0.f;
+    const float kexp = -0.125f * 1.44269504f;           // e^(-x/8) = 2^(kexp x)
+    const int ixmin = (int)xmin, iymin = (int)ymin;
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) acc[k] = 0.0f;
+    // lane sub takes samples sub, sub+4, ... of the span sequence
+    int wr = 0, wc = sub, wlo = 0, wlen = 0;
+    if (nrows > 0 && ncols > 0) row_span(0, wlo, wlen);
+    else wr = nrows;
+    auto normalize = [&]() {
+        while (wr < nrows && wc >= wlen) {
+            wc -= wlen;
+            if (++wr < nrows) row_span(wr, wlo, wlen);
+        }
+    };
+    normalize();
+    while (wr < nrows) {
+        const int cx = wlo + wc;
+        const float dx = (xmin + (float)cx) - ptx, dy = (ymin + (float)wr) - pty;
+        float nx, ny;
+        if (RECT) {
+            nx = dx * irx;
+            ny = dy * iry;
+        } else {
+            nx = fma_(crspt, dx, srspt * dy);
+            ny = fma_(crspt, dy, -(srspt * dx));
+        }
+        const float wx = 1.0f - fabs_(nx), wy = 1.0f - fabs_(ny);
+        // the samples' 4 neighbours are inside the level (x in [1, W-2], y in [1, H-2]); a level
+        // image has < 2^31 pixels, so a 32-bit offset from the wave-uniform base addresses it
+        const uint32_t po = 4u * (uint32_t)((iymin + wr) * W + (ixmin + cx));
+        const char* gb = reinterpret_cast<const char*>(g);
+        auto ldb = [&](uint32_t b) { return *reinterpret_cast<const float*>(gb + b); };
+        const float gx = ldb(po + 4u) - ldb(po - 4u);
+        const float gy = ldb(po + 4u * W) - ldb(po - 4u * W);
+        const float m2 = fma_(gx, gx, gy * gy);
+        const float m = 0.5f * __builtin_amdgcn_sqrtf(m2);
+        float rot = atan2_relaxed(gy, gx);   // NaN at (0, 0)
+        // theta = (anglef - rot) * 4/pi, +8 if negative, is dropped when it rounds to 8.0
+        // (ProgramCU.cu:1071-1090): a discontinuity at anglef - rot in (-2^-21, 0] and near +2pi.
+        // Within 1e-5 rad of those points (rare) rot is recomputed with the oracle's atan2, so
+        // the drop decisions are the reference's exactly; elsewhere |error| < 1e-6 cannot reach
+        // them.
+        const float dd = fabs_(anglef - rot);
+        if (dd < 1e-5f || dd > 6.2831753f) rot = atan2_(gy, gx);
+        rot = m2 == 0.0f ? 0.0f : rot;
+        float w = m * wx * wy;
+        float theta;
+        if (RECT) {
+            theta = -rot * rpi;
+        } else {
+            const float dnx = nx + ox, dny = ny + oy;
+            w *= __builtin_amdgcn_exp2f(kexp * fma_(dnx, dnx, dny * dny));
+            theta = (anglef - rot) * rpi;
+        }
+        if (theta < 0) theta += 8.0f;
+        // outside the rotated square (|n| >= 1) or theta == 8 (the reference's fidx == 8 is
+        // dropped) the sample adds nothing
+        w = (wx > 0.0f && wy > 0.0f && theta < 8.0f) ? w : 0.0f;
+        acc[0] = fma_(__builtin_amdgcn_fmed3f(fmax_(1.0f - theta, theta - 7.0f), 0.0f, 1.0f), w,
+                      acc[0]);
+#pragma unroll
+        for (int k = 1; k < 8; k++)
+            acc[k] = fma_(__builtin_amdgcn_fmed3f(1.0f - fabs_(theta - (float)k), 0.0f, 1.0f), w,
+                          acc[k]);
+        wc += 4;
+        normalize();
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) acc[k] = quad_sum(acc[k]);
+    // lane sub owns bins 2 sub, 2 sub + 1 of its cell
+    float b0 = acc[0], b1 = acc[1];
+    b0 = sub == 1 ? acc[2] : b0; b1 = sub == 1 ? acc[3] : b1;
+    b0 = sub == 2 ? acc[4] : b0; b1 = sub == 2 ? acc[5] : b1;
+    b0 = sub == 3 ? acc[6] : b0; b1 = sub == 3 ? acc[7] : b1;
+    if (fp.normalize) {
+        float s = fma_(b0, b0, b1 * b1);
+#pragma unroll
+        for (int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k, 64);
+        const float n1 = __builtin_amdgcn_rsqf(s);
+        b0 = fmin_(0.2f, b0 * n1);
+        b1 = fmin_(0.2f, b1 * n1);
+        s = fma_(b0, b0, b1 * b1);
+#pragma unroll
+        for (int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k, 64);
+        const float n2 = __builtin_amdgcn_rsqf(s);
+        b0 *= n2;
+        b1 *= n2;
+    }
+    *reinterpret_cast<float2*>(desc + (size_t)out * 128 + cell * 8 + sub * 2) = make_float2(b0, b1);
+}
+
+// One wave per feature, grid-stride over the features (count read on the device).
+template <bool RECT>
+__global__ __launch_bounds__(256) void k_descriptor_fast(const float* __restrict__ pyr,
+                                                         const float4* __restrict__ feat,
+                                                         const int2* __restrict__ feat_info,
+                                                         const uint32_t* __restrict__ n_feat_dev,
+                                                         const FeatureParams fp,
+                                                         float* __restrict__ desc,
+                                                         const int* __restrict__ out_index) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t n = *n_feat_dev;
+    // the feature index is wave-uniform: say so, so that the feature's record, level pointer and
+    // geometry live in SGPRs and the gathers use the SGPR-base + 32-bit-offset form
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint32_t e = blockIdx.x * 4 + wave; e < n; e += gridDim.x * 4)
+        descriptor_fast<RECT>(e, lane, pyr, feat, feat_info, fp, desc,
+                              out_index ? (uint32_t)out_index[e] : e);
+}
+
 // One wave per feature, grid-stride over the features (count read on the device).
 template <bool RECT>
 __global__ __launch_bounds__(256) void k_descriptor(const float* __restrict__ pyr,
@@ -1494,9 +1719,18 @@ hipError_t launch_orient_keys(const float* pyr, float4* feat, const int2* feat_i
 hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* feat_info,
                              const uint32_t* n_feat_dev, int n_feat_cap, const FeatureParams& fp,
                              float* desc, hipStream_t stream, const int* out_index,
-                             bool rect) {
+                             bool rect, bool exact) {
     if (n_feat_cap <= 0) return hipSuccess;
     const unsigned grid = (unsigned)std::min(((long long)n_feat_cap + 3) / 4, 65536LL);
+    if (!exact) {
+        if (rect)
+            hipLaunchKernelGGL(k_descriptor_fast<true>, dim3(grid), dim3(256), 0, stream, pyr,
+                               feat, feat_info, n_feat_dev, fp, desc, out_index);
+        else
+            hipLaunchKernelGGL(k_descriptor_fast<false>, dim3(grid), dim3(256), 0, stream, pyr,
+                               feat, feat_info, n_feat_dev, fp, desc, out_index);
+        return hipGetLastError();
+    }
     if (rect)
         hipLaunchKernelGGL(k_descriptor<true>, dim3(grid), dim3(256), 0, stream, pyr, feat,
                            feat_info, n_feat_dev, fp, desc, out_index);

@@ -4,6 +4,7 @@ The binding fails loudly when the library or a usable GPU is missing: there is n
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import subprocess
@@ -338,10 +339,21 @@ class SiftContext:
 
     # ---- test hooks
     DEBUG_PARTS2, DEBUG_PARTS4, DEBUG_TINY_CAP, DEBUG_FUSED_MATCH = 1, 2, 4, 8
+    DEBUG_EXACT_DESCRIPTOR = 16
 
     def set_debug_flags(self, flags: int):
         """Per-context debug flags (sgpu_debug_set_flags; 0 = shipped configuration)."""
         self._check(lib().sgpu_debug_set_flags(self._ctx, flags), "sgpu_debug_set_flags")
+
+    @contextlib.contextmanager
+    def exact_descriptors(self):
+        """Within the block the descriptors come from the bit-exact kernel (the reference's fma
+        order, the oracle's transcendentals) instead of the shipped relaxed-order one."""
+        self.set_debug_flags(self.DEBUG_EXACT_DESCRIPTOR)
+        try:
+            yield self
+        finally:
+            self.set_debug_flags(0)
 
     def geometry(self):
         n = ctypes.c_int(0)

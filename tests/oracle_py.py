@@ -253,3 +253,22 @@ def save_sift(path, keys, desc, binary=False, normalized=True):
     d = None if desc is None else np.ascontiguousarray(desc, np.float32)
     lib().oracle_save_sift(str(path).encode(), k.ctypes.data, None if d is None else d.ctypes.data,
                            len(k), int(binary), int(normalized), int(d is not None))
+
+
+def read_sift(path, binary=False):
+    """Parse a SaveSIFT file (the layout save_sift writes): keys [n, 4] as stored (y, x, scale,
+    orientation) and the descriptors -- ASCII: [n, 128] int64 of floor(0.5 + 512 d) (-unn
+    files are not parsed here); binary: [n, 128] float32."""
+    if binary:
+        raw = np.fromfile(path, np.uint8)
+        n, dim = np.frombuffer(raw[:8].tobytes(), np.int32)
+        rec = np.frombuffer(raw[8:].tobytes(), np.float32).reshape(n, 4 + dim)
+        return rec[:, :4].copy(), rec[:, 4:].copy()
+    with open(path) as f:
+        tok = f.read().split()
+    n, dim = int(tok[0]), int(tok[1])
+    vals = tok[2:]
+    keys = np.array([[float(v) for v in vals[i * (4 + dim):i * (4 + dim) + 4]] for i in range(n)])
+    desc = np.array([[int(v) for v in vals[i * (4 + dim) + 4:(i + 1) * (4 + dim)]]
+                     for i in range(n)], np.int64).reshape(n, dim)
+    return keys, desc

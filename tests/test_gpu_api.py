@@ -59,13 +59,14 @@ SAVE_CASES = [
 @pytest.mark.parametrize("args,over,binary,normalized,desc", SAVE_CASES,
                          ids=lambda v: " ".join(v) if isinstance(v, list) else None)
 def test_save_sift_bytes_vs_reference_writer(tmp_path, args, over, binary, normalized, desc):
+    """Byte for byte, with the bit-exact descriptor kernel (SGPU_EXACT_DESCRIPTOR=1)."""
     exe = _compile(tmp_path, "save_sift_replica")
     img = synth_image(480, 352, 91)
     pgm = tmp_path / "in.pgm"
     _write_pgm(pgm, img)
     out = tmp_path / "gpu.sift"
     r = subprocess.run([exe, str(pgm), str(out)] + args, capture_output=True, text=True,
-                       timeout=120)
+                       timeout=120, env=dict(os.environ, SGPU_EXACT_DESCRIPTOR="1"))
     assert r.returncode == 0, r.stdout + r.stderr
     num = int([l for l in r.stdout.split("\n") if l.startswith("NUM ")][0].split()[1])
     rk, rd = O.extract(img, default_options(**over))
@@ -74,6 +75,32 @@ def test_save_sift_bytes_vs_reference_writer(tmp_path, args, over, binary, norma
     O.save_sift(ref, rk, rd if desc else None, binary=binary, normalized=normalized)
     a, b = out.read_bytes(), ref.read_bytes()
     assert a == b, f"{len(a)} vs {len(b)} bytes; first difference at {next((i for i in range(min(len(a), len(b))) if a[i] != b[i]), None)}"
+
+
+@pytest.mark.parametrize("binary", [False, True])
+def test_save_sift_shipped_descriptors(tmp_path, binary):
+    """The shipped (relaxed-order) descriptors through SaveSIFT: the key columns are the
+    oracle's, and every descriptor entry floor(0.5 + 512 d) is within 1 of the oracle's."""
+    exe = _compile(tmp_path, "save_sift_replica")
+    img = synth_image(480, 352, 91)
+    pgm = tmp_path / "in.pgm"
+    _write_pgm(pgm, img)
+    out = tmp_path / "gpu.sift"
+    env = {k: v for k, v in os.environ.items() if k != "SGPU_EXACT_DESCRIPTOR"}
+    r = subprocess.run([exe, str(pgm), str(out)] + (["-b"] if binary else []),
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rk, rd = O.extract(img, default_options())
+    ref = tmp_path / "oracle.sift"
+    O.save_sift(ref, rk, rd, binary=binary, normalized=True)
+    ka, da = O.read_sift(out, binary=binary)
+    kb, db = O.read_sift(ref, binary=binary)
+    assert np.array_equal(ka, kb)
+    assert da.shape == db.shape and len(da) > 0
+    if binary:
+        assert np.linalg.norm(da.astype(np.float64) - db, axis=1).max() < 1e-4
+    else:
+        assert np.abs(da - db).max() <= 1 and (da != db).mean() < 1e-3
 
 
 def test_match_id_cache(tmp_path):

@@ -27,6 +27,9 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 DESC_L2_TOL = 1e-4   # BASELINE.json north_star: descriptor L2 < 1e-4
+# C++ replicas that compare with the oracle bit for bit (or through matches of quantised
+# descriptors) run the bit-exact descriptor kernel (sgpu.h SGPU_DEBUG_EXACT_DESCRIPTOR)
+EXACT_ENV = dict(os.environ, SGPU_EXACT_DESCRIPTOR="1")
 
 
 def _bits(a):
@@ -56,7 +59,11 @@ def test_golden_extract(gpu_ctx, path):
     gpu_ctx.extract(z["image"])
     k, d = gpu_ctx.features(0)
     _assert_features_equal(k, d, z["keys"], z["desc"], os.path.basename(path))
-    # bitwise, which is what the shared deterministic math gives
+    # the bit-exact descriptor kernel: bitwise, which is what the shared deterministic math gives
+    with gpu_ctx.exact_descriptors():
+        gpu_ctx.extract(z["image"])
+        k, d = gpu_ctx.features(0)
+    assert np.array_equal(_bits(k), _bits(z["keys"]))
     assert np.array_equal(_bits(d), _bits(z["desc"]))
 
 
@@ -167,6 +174,40 @@ def test_options_vs_oracle(gpu_ctx, over):
     k, d = gpu_ctx.features(0)
     rk, rd = O.extract(img, opts)
     _assert_features_equal(k, d, rk, rd, str(over))
+    with gpu_ctx.exact_descriptors():
+        gpu_ctx.extract(img)
+        k, d = gpu_ctx.features(0)
+    assert np.array_equal(_bits(k), _bits(rk)) and np.array_equal(_bits(d), _bits(rd)), over
+
+
+@pytest.mark.parametrize("over", [{}, {"normalized": 0}, {"descriptor_window_factor": 2},
+                                  {"octave_min": -1}, {"dog_level_num": 5}],
+                         ids=lambda o: "-".join(f"{k}{v}" for k, v in o.items()) or "default")
+def test_shipped_descriptor_vs_exact(gpu_ctx, over):
+    """The shipped relaxed-order descriptor kernel against the bit-exact one on 4 HD images
+    (tens of thousands of features): same keypoints bit for bit, descriptors within L2 1e-5
+    (relative to |d| for -unn), i.e. 10x inside the north star's 1e-4."""
+    from sift_synth import synth_batch_fast
+    imgs = synth_batch_fast(4, 1280, 720, 510)
+    opts = default_options(**over)
+    gpu_ctx.set_options(opts)
+    gpu_ctx.extract(imgs)
+    fast = [gpu_ctx.features(i) for i in range(4)]
+    with gpu_ctx.exact_descriptors():
+        gpu_ctx.extract(imgs)
+        exact = [gpu_ctx.features(i) for i in range(4)]
+    kf = np.concatenate([f[0] for f in fast])
+    ke = np.concatenate([e[0] for e in exact])
+    df = np.concatenate([f[1] for f in fast]).astype(np.float64)
+    de = np.concatenate([e[1] for e in exact]).astype(np.float64)
+    assert len(kf) > 4000 and np.array_equal(_bits(kf), _bits(ke))
+    l2 = np.linalg.norm(df - de, axis=1)
+    if not opts.normalized:
+        l2 = l2 / np.maximum(np.linalg.norm(de, axis=1), 1e-30)
+    print(f"descriptor L2 fast vs exact over {len(kf)} features: max {l2.max():.3g}, "
+          f"median {np.median(l2):.3g}")
+    assert l2.max() < 1e-5
+    gpu_ctx.set_options(default_options())
 
 
 def test_no_descriptors_option(gpu_ctx):
@@ -448,7 +489,7 @@ def test_simplesift_replica(tmp_path):
     _write_pgm(p2, img2)
     s1, s2 = tmp_path / "a.sift", tmp_path / "b.sift"
     r = subprocess.run([str(exe), lib, str(p1), str(p2), str(s1), str(s2)], capture_output=True,
-                       text=True, timeout=300)
+                       text=True, timeout=300, env=EXACT_ENV)
     assert r.returncode == 0, r.stdout + r.stderr
     lines = r.stdout.strip().splitlines()
     res = [l for l in lines if l.startswith("RESULT ")]
@@ -526,6 +567,11 @@ def test_keypoints_vs_oracle(gpu_ctx, has_orientation, over):
     assert gpu_ctx.count(0) == len(keys) and gpu_ctx.total() == len(keys)
     k, d = gpu_ctx.features(0)
     rk, rd = O.describe_keys(img, keys, has_orientation, opts)
+    _assert_features_equal(k, d, rk, rd, "keypoints")
+    with gpu_ctx.exact_descriptors():
+        gpu_ctx.extract(img)
+        gpu_ctx.extract_keypoints(keys, has_orientation)
+        k, d = gpu_ctx.features(0)
     assert np.array_equal(_bits(k), _bits(rk))
     assert np.array_equal(_bits(d), _bits(rd))
 
@@ -552,6 +598,11 @@ def test_rect_keypoints_vs_oracle(gpu_ctx, over):
     k, d = gpu_ctx.features(0)
     rk, rd = O.describe_keys(img, keys, -1, opts)
     assert np.array_equal(_bits(k), _bits(keys)) and np.array_equal(_bits(rk), _bits(keys))
+    _assert_features_equal(k, d, rk, rd, "rect")
+    with gpu_ctx.exact_descriptors():
+        gpu_ctx.extract(img)
+        gpu_ctx.extract_keypoints(keys, -1)
+        k, d = gpu_ctx.features(0)
     assert np.array_equal(_bits(d), _bits(rd))
     gpu_ctx.set_options(default_options())
 
@@ -566,6 +617,11 @@ def test_detected_keypoints_fed_back(gpu_ctx):
     k, d = gpu_ctx.features(0)
     rk, rd = O.describe_keys(img, keys, True)
     assert np.array_equal(_bits(k), _bits(keys))
+    _assert_features_equal(k, d, rk, rd, "fed back")
+    with gpu_ctx.exact_descriptors():
+        gpu_ctx.extract(img)
+        gpu_ctx.extract_keypoints(keys, True)
+        k, d = gpu_ctx.features(0)
     assert np.array_equal(_bits(d), _bits(rd))
 
 
@@ -578,6 +634,11 @@ def test_keypoints_on_batch_image(gpu_ctx):
     assert [gpu_ctx.count(i) for i in range(3)] == [0, 0, 50]
     k, d = gpu_ctx.features(2)
     rk, rd = O.describe_keys(imgs[2], keys, False)
+    _assert_features_equal(k, d, rk, rd, "batch image")
+    with gpu_ctx.exact_descriptors():
+        gpu_ctx.extract(imgs)
+        gpu_ctx.extract_keypoints(keys, False, image=2)
+        k, d = gpu_ctx.features(2)
     assert np.array_equal(_bits(k), _bits(rk)) and np.array_equal(_bits(d), _bits(rd))
 
 
@@ -595,7 +656,7 @@ def test_keypoint_api_replica(tmp_path):
     keys.tofile(tmp_path / "keys.f32")
     r = subprocess.run([str(exe), lib, str(tmp_path / "a.pgm"), str(tmp_path / "keys.f32"),
                         str(len(keys)), str(tmp_path / "A.f32"), str(tmp_path / "B.f32")],
-                       capture_output=True, text=True, timeout=300)
+                       capture_output=True, text=True, timeout=300, env=EXACT_ENV)
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
     n = len(keys)
     for name, has_o in (("A.f32", True), ("B.f32", False)):

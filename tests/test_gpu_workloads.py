@@ -35,6 +35,10 @@ def test_c4_4096_six_octaves_vs_oracle(gpu_ctx):
     assert k.shape == rk.shape and len(k) > 2000, (k.shape, rk.shape)
     assert np.array_equal(_bits(k), _bits(rk))
     assert np.linalg.norm(d.astype(np.float64) - rd, axis=1).max() < DESC_L2_TOL
+    with gpu_ctx.exact_descriptors():
+        gpu_ctx.extract(img)
+        k, d = gpu_ctx.features(0)
+    assert np.array_equal(_bits(k), _bits(rk))
     assert np.array_equal(_bits(d), _bits(rd))
     gpu_ctx.set_options(default_options())
 
