@@ -73,6 +73,8 @@ def main():
                     help="c3: 128 x 1920x1080 per GPU (-no 4), the headline; c4: BASELINE "
                          "configs[3], 4096x4096 tiles with 6 octaves, as the headline line")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 sub-measurement")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the host-in / host-out (PCIe-inclusive) sub-measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-match", action="store_true")
     ap.add_argument("--match-n", type=int, default=50000)
@@ -230,6 +232,8 @@ def main():
         result["match"] = bench_match(ctx, args.match_n)
     if rank == 0 and world == 1 and args.workload == "c3" and not args.no_c4:
         result["c4"] = bench_c4(ctx)
+    if rank == 0 and world == 1 and args.workload == "c3" and not args.no_e2e:
+        result["end_to_end"] = bench_end_to_end(ctx, imgs, B, W, H)
     if world > 1 and not args.no_match:
         sm = bench_match_sharded(ctx, args.match_n, rank, world, None if rccl else dist)
         if rank == 0:
@@ -337,6 +341,47 @@ def bench_c4(ctx, batch=8, steps=3):
                              "avg_launch_ms": pyr / steps / n_gauss}}
     finally:
         c4.close()
+
+
+def bench_end_to_end(ctx, imgs, B, W, H, nbatches=16):
+    """Host-in / host-out throughput (sgpu_extract_stream): batches of B images in page-locked
+    host memory go up over PCIe, through the whole path, and every key and descriptor comes
+    back to page-locked host memory -- the work of the reference's RunSIFT + GetFeatureVector per
+    image (PyramidCU.cpp:949-976 upload, :434 descriptor download).  Uploads of batch k+1 and
+    downloads of batch k-1 overlap batch k's kernels.  Two distinct input batches (seeds 3000..,
+    the staged one, and 3000 + B..) alternate over `nbatches` batches; one warm-up call."""
+    pins = []
+    try:
+        ins = []
+        for k, src in enumerate((imgs, synth_batch_fast(B, W, H, 3000 + B))):
+            p = sgpu.PinnedArray(src.shape, np.uint8)
+            p.array[...] = src
+            pins.append(p)
+            ins.append(p.array)
+        cap = nbatches * B * 4000
+        kb = sgpu.PinnedArray((cap, 4), np.float32)
+        db = sgpu.PinnedArray((cap, 128), np.float32)
+        pins += [kb, db]
+        batches = [ins[k % 2] for k in range(nbatches)]
+        ctx.extract_stream(batches[:2], kb.array, db.array)   # warm-up (buffers, capacities)
+        t0 = time.perf_counter()
+        k, d, c = ctx.extract_stream(batches, kb.array, db.array)
+        el = time.perf_counter() - t0
+        in_bytes = float(nbatches) * B * W * H
+        out_bytes = float(len(k)) * (16 + 512)
+        return {"workload": f"{nbatches} batches of {B} x {W}x{H} u8 from page-locked host "
+                            "memory, keys + descriptors back to page-locked host memory "
+                            "(sgpu_extract_stream)",
+                "value": nbatches * B / el, "unit": "images/s",
+                "ms_per_batch": el / nbatches * 1e3,
+                "features_per_image": float(len(k)) / (nbatches * B),
+                "pcie_bytes_per_batch": {"h2d": in_bytes / nbatches, "d2h": out_bytes / nbatches},
+                "pcie_GBps": {"h2d": in_bytes / el / 1e9, "d2h": out_bytes / el / 1e9}}
+    except Exception as ex:   # never costs the main measurement
+        return {"error": str(ex)}
+    finally:
+        for p in pins:
+            p.free()
 
 
 def bench_match_sharded(ctx, n, rank, world, host_dist=None):

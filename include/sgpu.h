@@ -99,6 +99,24 @@ int sgpu_stage_input(sgpu_ctx* ctx, const uint8_t* images, int n, int w, int h, 
 int sgpu_extract(sgpu_ctx* ctx, const uint8_t* images, int n, int w, int h, int stride,
                  int flags);
 
+/* Host-in / host-out extraction of a stream of batches: nbatches batches of `batch` u8 gray
+ * images (batches[k] -> batch images of w x h, rows `stride` bytes apart, in host memory).  The
+ * keys (x, y, scale, orientation) and descriptors of all images go to keys[cap][4] and
+ * desc[cap][128] (either may be NULL) in image order, counts[nbatches * batch] the per-image
+ * feature counts.  Replaces a loop of SiftGPU::RunSIFT(w, h, data, GL_LUMINANCE,
+ * GL_UNSIGNED_BYTE) + GetFeatureVector (SiftGPU.cpp:233-268, SiftPyramid.cpp:287-291) with the
+ * reference's upload (PyramidCU.cpp:949-976) and descriptor download (PyramidCU.cpp:434) in the
+ * pipeline: the upload of batch k+1 and the download of batch k-1 overlap batch k's kernels.
+ * The copies overlap only from page-locked memory (sgpu_host_alloc).  Returns SGPU_ERANGE when
+ * the features exceed cap (counts are complete, the features stop at the last batch that fit).
+ * Afterwards the context holds no "last batch" for the per-image queries. */
+int sgpu_extract_stream(sgpu_ctx* ctx, const uint8_t* const* batches, int nbatches, int batch,
+                        int w, int h, int stride, float* keys, float* desc, int64_t cap,
+                        int32_t* counts);
+/* Page-locked host memory for sgpu_extract_stream's input and output (hipHostMalloc). */
+void* sgpu_host_alloc(size_t bytes);
+void sgpu_host_free(void* p);
+
 /* Same with float luminance input in [0, 1] (stride in floats): the GL_FLOAT / converted-RGB
  * input path of GLTexInput::SetImageData (GLTexImage.cpp:981-1006). */
 int sgpu_extract_f32(sgpu_ctx* ctx, const float* images, int n, int w, int h, int stride,

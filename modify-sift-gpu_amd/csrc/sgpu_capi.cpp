@@ -104,6 +104,10 @@ struct sgpu_ctx {
     Part part[kMaxParts];
     DevBuf input, all_keys, all_desc, gray, pre;  // all_*: lazily gathered multi-part outputs;
                                                   // pre: the 2^ds-sampled input (-fo > 0)
+    // sgpu_extract_stream: second input slot, copy-engine streams, slot events
+    DevBuf input2;
+    hipStream_t h2d = nullptr, d2h = nullptr;
+    hipEvent_t up_ev[2] = {}, down_ev[2] = {};
     bool gathered = false;
     hipEvent_t ev[T_N + 1] = {};
     float timing[T_N] = {};
@@ -314,7 +318,15 @@ int sgpu_ctx_destroy(sgpu_ctx* ctx) {
     }
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     ctx->comm = nullptr;
-    DevBuf* bufs[] = {&ctx->input, &ctx->all_keys, &ctx->all_desc, &ctx->gray, &ctx->pre, &ctx->m_d1, &ctx->m_d2, &ctx->m_s1, &ctx->m_s2,
+    for (hipStream_t st : {ctx->h2d, ctx->d2h})
+        if (st) (void)hipStreamSynchronize(st);
+    for (int i = 0; i < 2; i++) {
+        if (ctx->up_ev[i]) (void)hipEventDestroy(ctx->up_ev[i]);
+        if (ctx->down_ev[i]) (void)hipEventDestroy(ctx->down_ev[i]);
+    }
+    if (ctx->h2d) (void)hipStreamDestroy(ctx->h2d);
+    if (ctx->d2h) (void)hipStreamDestroy(ctx->d2h);
+    DevBuf* bufs[] = {&ctx->input, &ctx->input2, &ctx->all_keys, &ctx->all_desc, &ctx->gray, &ctx->pre, &ctx->m_d1, &ctx->m_d2, &ctx->m_s1, &ctx->m_s2,
                       &ctx->m_part, &ctx->m_terms, &ctx->m_match, &ctx->m_dist, &ctx->m_mask, &ctx->m_loc,
                       &ctx->m_colpart,
                       &ctx->c_buf};
@@ -331,7 +343,7 @@ const char* sgpu_last_error(const sgpu_ctx* ctx) { return ctx ? ctx->err.c_str()
 // Queue the whole pipeline of one part on its stream.  `wait` (may be null) is an event the
 // part's pyramid must wait for.  No host synchronisation.
 static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32, int stride,
-                        hipEvent_t wait) {
+                        hipEvent_t wait, hipEvent_t wait_lo = nullptr) {
     hipStream_t st = pt.stream;   // reassigned per stage below
     const sgpu_options& O = ctx->opt;
     const sgp::Schedule& S = ctx->sched;
@@ -489,6 +501,7 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     // kernels grid-stride over whatever the device count is)
     st = pt.stream_lo;
     HIPCHK(ctx, hipStreamWaitEvent(st, pt.ev[2], 0));
+    if (wait_lo) HIPCHK(ctx, hipStreamWaitEvent(st, wait_lo, 0));   // previous features read out
     const uint32_t* n_cand_dev = pt.row_base.as<uint32_t>() + pt.total_rows;
     HIPCHK(ctx, hipMemsetAsync(pt.ocount.p, 0, nc * sizeof(uint32_t), st));
     const int cand_grid = (int)std::min(nc, pt.cand_hint ? pt.cand_hint : nc);
@@ -534,20 +547,10 @@ static int enqueue_readback(sgpu_ctx* ctx, Part& pt) {
     return SGPU_OK;
 }
 
-static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, int w, int h,
-                        int stride, int flags, int color = 0) {
-    if (!ctx) return SGPU_EINVAL;
-    const bool staged = (flags & SGPU_INPUT_STAGED) != 0;
-    const int channels = color == SGPU_RGB || color == SGPU_BGR ? 3 : color ? 4 : 1;
-    if ((!images && !staged) || n <= 0 || w < 8 || h < 8 || stride < w * channels)
-        return ctx->fail(SGPU_EINVAL, "bad image arguments");
-    if (color && (staged || is_f32 || color > SGPU_BGRA))
-        return ctx->fail(SGPU_EINVAL, "bad color input");
-    if (staged && (is_f32 || ctx->staged_bytes < (size_t)n * h * stride))
-        return ctx->fail(SGPU_EINVAL, "staged input does not match the batch");
-    HIPCHK(ctx, hipSetDevice(ctx->device));
+// Geometry of a batch of n images of w x h (first octave: GLTexInput::SetImageData +
+// PyramidCU::InitPyramid with -fo, -prep, -maxd; octaves; sigma schedule) into the context.
+static int plan_batch(sgpu_ctx* ctx, int n, int w, int h) {
     const sgpu_options& O = ctx->opt;
-    // first octave (GLTexInput::SetImageData + PyramidCU::InitPyramid): -fo, -prep, -maxd
     const sgp::InputPlan plan = sgp::plan_input(w, h, O.octave_min, O.max_dimension, O.preprocess_on_cpu);
     if (plan.w < 8 || plan.h < 8) return ctx->fail(SGPU_EINVAL, "image too small for the first octave");
     {
@@ -569,6 +572,24 @@ static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
     ctx->w = plan.ds ? plan.w : w;
     ctx->h = plan.h;
     ctx->gathered = false;
+    return SGPU_OK;
+}
+
+static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, int w, int h,
+                        int stride, int flags, int color = 0) {
+    if (!ctx) return SGPU_EINVAL;
+    const bool staged = (flags & SGPU_INPUT_STAGED) != 0;
+    const int channels = color == SGPU_RGB || color == SGPU_BGR ? 3 : color ? 4 : 1;
+    if ((!images && !staged) || n <= 0 || w < 8 || h < 8 || stride < w * channels)
+        return ctx->fail(SGPU_EINVAL, "bad image arguments");
+    if (color && (staged || is_f32 || color > SGPU_BGRA))
+        return ctx->fail(SGPU_EINVAL, "bad color input");
+    if (staged && (is_f32 || ctx->staged_bytes < (size_t)n * h * stride))
+        return ctx->fail(SGPU_EINVAL, "staged input does not match the batch");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int rc0 = plan_batch(ctx, n, w, h);
+    if (rc0 != SGPU_OK) return rc0;
+    const sgp::InputPlan plan = ctx->plan;
 
     // parts: one by default.  Measured on MI355X (profiles/): a second
     // part's pyramid starves beside the previous part's descriptor kernel (the dispatcher keeps
@@ -675,6 +696,144 @@ static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
     (void)hipEventElapsedTime(&ctx->timing[T_DOWNLOAD], p0.ev[5], p0.ev[6]);
     (void)hipEventElapsedTime(&ctx->timing[T_TOTAL], ctx->ev[0], ctx->part[np - 1].ev[6]);
     return SGPU_OK;
+}
+
+// Host-in / host-out extraction of a stream of batches: SiftGPU::RunSIFT(w, h, data) per image
+// followed by GetFeatureVector, i.e. with the reference's input upload (PyramidCU.cpp:949-976)
+// and descriptor download (PyramidCU.cpp:434) in the measured work.  Two slots -- parts 0 and 1
+// with their own buffers, two device input buffers -- alternate between batches: the upload of
+// batch k+1 (host-to-device copy engine) and the download of batch k-1's keys and descriptors
+// (device-to-host copy engine) run while batch k computes.  Kernels of consecutive batches stay
+// in order (batch k+1's pyramid waits for batch k's last kernel), so every batch sees the whole
+// GPU as in sgpu_extract.  One host wait per batch: the small count readback of batch k-1, needed
+// to size its download, happens after batch k is queued.
+int sgpu_extract_stream(sgpu_ctx* ctx, const uint8_t* const* batches, int nbatches, int batch,
+                        int w, int h, int stride, float* keys, float* desc, int64_t cap,
+                        int32_t* counts) {
+    if (!ctx) return SGPU_EINVAL;
+    if (!batches || nbatches <= 0 || batch <= 0 || w < 8 || h < 8 || stride < w || !counts ||
+        cap < 0)
+        return ctx->fail(SGPU_EINVAL, "bad stream arguments");
+    for (int k = 0; k < nbatches; k++)
+        if (!batches[k]) return ctx->fail(SGPU_EINVAL, "null batch pointer");
+    if (desc && !ctx->opt.descriptors) return ctx->fail(SGPU_EINVAL, "descriptors disabled (-sd)");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int rc = plan_batch(ctx, batch, w, h);
+    if (rc != SGPU_OK) return rc;
+    int64_t out_base = 0;
+    int result = SGPU_OK;
+    auto emit_counts = [&](int k, const std::vector<int64_t>& off, int n) {
+        for (int i = 0; i < n; i++) counts[(size_t)k * batch + i] = (int32_t)(off[i + 1] - off[i]);
+    };
+    if (ctx->plan.ds > 0) {
+        // -fo > 0 with -prep samples the input on the device first (extract_impl): no overlap,
+        // batch by batch
+        for (int k = 0; k < nbatches; k++) {
+            rc = extract_impl(ctx, batches[k], false, batch, w, h, stride, SGPU_INPUT_HOST);
+            if (rc != SGPU_OK) return rc;
+            emit_counts(k, ctx->img_off, batch);
+            const int64_t nf = ctx->img_off[batch];
+            if (out_base + nf > cap) {
+                result = ctx->fail(SGPU_ERANGE, "features exceed the output capacity");
+            } else if (nf > 0) {
+                const Part& pt = ctx->part[0];
+                if (keys)
+                    HIPCHK(ctx, hipMemcpy(keys + out_base * 4, pt.keys.p, nf * sizeof(float4),
+                                          hipMemcpyDeviceToHost));
+                if (desc)
+                    HIPCHK(ctx, hipMemcpy(desc + out_base * 128, pt.desc.p,
+                                          nf * 128 * sizeof(float), hipMemcpyDeviceToHost));
+            }
+            out_base += nf;
+        }
+        return result;
+    }
+    if (!ctx->h2d) {
+        HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->h2d, hipStreamNonBlocking));
+        HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->d2h, hipStreamNonBlocking));
+        for (int i = 0; i < 2; i++) {
+            HIPCHK(ctx, hipEventCreateWithFlags(&ctx->up_ev[i], hipEventDisableTiming));
+            HIPCHK(ctx, hipEventCreateWithFlags(&ctx->down_ev[i], hipEventDisableTiming));
+        }
+    }
+    const size_t in_bytes = (size_t)batch * h * stride;
+    ctx->staged_bytes = 0;
+    ALLOCCHK(ctx, ctx->input.ensure(in_bytes));
+    ALLOCCHK(ctx, ctx->input2.ensure(in_bytes));
+    void* din[2] = {ctx->input.p, ctx->input2.p};
+    ctx->nparts = 1;
+    // batch k's results: wait for its counts, re-run it on overflow, queue its download
+    auto finish = [&](int k) -> int {
+        Part& pt = ctx->part[k & 1];
+        HIPCHK(ctx, hipEventSynchronize(pt.ev[6]));
+        uint32_t nc = (uint32_t)pt.h_read[0];
+        if (nc > pt.cand_cap) {
+            pt.cand_cap = (size_t)nc + nc / 4 + 1024;
+            int r = enqueue_part(ctx, pt, din[k & 1], false, stride, nullptr, nullptr);
+            if (r == SGPU_OK) r = enqueue_readback(ctx, pt);
+            if (r != SGPU_OK) return r;
+            HIPCHK(ctx, hipStreamSynchronize(pt.stream_lo));
+            nc = (uint32_t)pt.h_read[0];
+            if (nc > pt.cand_cap) return ctx->fail(SGPU_ERANGE, "keypoint capacity overflow");
+        }
+        pt.n_cand = nc;
+        pt.img_off.assign(pt.h_read + 1, pt.h_read + 2 + pt.n);
+        pt.cand_hint = (size_t)nc + nc / 16 + 64;
+        pt.feat_hint = (size_t)pt.img_off[pt.n] + pt.img_off[pt.n] / 16 + 64;
+        emit_counts(k, pt.img_off, pt.n);
+        const int64_t nf = pt.img_off[pt.n];
+        if (out_base + nf > cap) {
+            result = ctx->fail(SGPU_ERANGE, "features exceed the output capacity");
+        } else if (nf > 0) {
+            HIPCHK(ctx, hipStreamWaitEvent(ctx->d2h, pt.ev[6], 0));
+            if (keys)
+                HIPCHK(ctx, hipMemcpyAsync(keys + out_base * 4, pt.keys.p, nf * sizeof(float4),
+                                           hipMemcpyDeviceToHost, ctx->d2h));
+            if (desc)
+                HIPCHK(ctx, hipMemcpyAsync(desc + out_base * 128, pt.desc.p,
+                                           nf * 128 * sizeof(float), hipMemcpyDeviceToHost,
+                                           ctx->d2h));
+        }
+        HIPCHK(ctx, hipEventRecord(ctx->down_ev[k & 1], ctx->d2h));
+        out_base += nf;
+        return SGPU_OK;
+    };
+    for (int k = 0; k < nbatches; k++) {
+        const int slot = k & 1;
+        Part& pt = ctx->part[slot];
+        pt.img0 = 0;
+        pt.n = batch;
+        // upload k into its slot once batch k-2's pyramid (the slot's last reader) is done
+        if (k >= 2) HIPCHK(ctx, hipStreamWaitEvent(ctx->h2d, pt.ev[1], 0));
+        HIPCHK(ctx, hipMemcpyAsync(din[slot], batches[k], in_bytes, hipMemcpyHostToDevice,
+                                   ctx->h2d));
+        HIPCHK(ctx, hipEventRecord(ctx->up_ev[slot], ctx->h2d));
+        // compute k after batch k-1's last kernel; its features overwrite the slot only after
+        // batch k-2's download
+        if (k >= 1) HIPCHK(ctx, hipStreamWaitEvent(pt.stream, ctx->part[slot ^ 1].ev[5], 0));
+        rc = enqueue_part(ctx, pt, din[slot], false, stride, ctx->up_ev[slot],
+                          k >= 2 ? ctx->down_ev[slot] : nullptr);
+        if (rc == SGPU_OK) rc = enqueue_readback(ctx, pt);
+        if (rc == SGPU_OK && k >= 1) rc = finish(k - 1);
+        if (rc != SGPU_OK) return rc;
+    }
+    rc = finish(nbatches - 1);
+    if (rc != SGPU_OK) return rc;
+    HIPCHK(ctx, hipStreamSynchronize(ctx->d2h));
+    // the per-image queries (sgpu_copy_features, ...) have no "last batch" after a stream
+    ctx->batch = 0;
+    ctx->img_off.clear();
+    return result;
+}
+
+void* sgpu_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void sgpu_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 // SiftGPU::RunSIFT(num, keys, keys_have_orientation) on image `image` of the last extract

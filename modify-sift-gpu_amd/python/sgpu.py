@@ -29,6 +29,7 @@ C_API = [
     "sgpu_debug_set_flags", "sgpu_comm_unique_id", "sgpu_comm_init", "sgpu_comm_allgather_i32",
     "sgpu_comm_allreduce_f64", "sgpu_extract_keypoints", "sgpu_match_guided", "sgpu_extract_color",
     "sgpu_match_shard_begin", "sgpu_match_shard_end", "sgpu_match_sharded",
+    "sgpu_extract_stream", "sgpu_host_alloc", "sgpu_host_free",
 ]
 
 _LIB = None
@@ -84,8 +85,36 @@ def lib():
                                            c.c_float, c.c_int, c.c_int, vp]
         L.sgpu_match_sharded.argtypes = [vp, vp, c.c_int, c.c_int, vp, c.c_int, c.c_float,
                                          c.c_float, c.c_int, c.c_int, vp, c.c_int]
+        L.sgpu_extract_stream.argtypes = [vp, P(vp), c.c_int, c.c_int, c.c_int, c.c_int, c.c_int,
+                                          vp, vp, c.c_int64, vp]
+        L.sgpu_host_alloc.argtypes = [c.c_size_t]
+        L.sgpu_host_alloc.restype = vp
+        L.sgpu_host_free.argtypes = [vp]
         _LIB = L
     return _LIB
+
+
+class PinnedArray:
+    """A numpy view of page-locked host memory (sgpu_host_alloc): the form of host buffer whose
+    copies overlap the kernels in sgpu_extract_stream.  Freed with .free() or on collection."""
+
+    def __init__(self, shape, dtype):
+        dt = np.dtype(dtype)
+        n = int(np.prod(shape)) * dt.itemsize
+        self._p = lib().sgpu_host_alloc(max(n, 1))
+        if not self._p:
+            raise MemoryError(f"sgpu_host_alloc({n}) failed")
+        buf = (ctypes.c_uint8 * max(n, 1)).from_address(self._p)
+        self.array = np.frombuffer(buf, dtype=dt, count=int(np.prod(shape))).reshape(shape)
+
+    def free(self):
+        if self._p:
+            self.array = None
+            lib().sgpu_host_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        self.free()
 
 
 def match_shard_end(col_best_all: np.ndarray, row_match: np.ndarray, row_begin: int,
@@ -213,6 +242,30 @@ class SiftContext:
                                              self.COLOR_FORMATS[fmt], SGPU_INPUT_HOST),
                     "extract_color")
         self.batch = n
+
+    def extract_stream(self, batches, keys=None, desc=None, cap=None):
+        """Host-in / host-out extraction of a list of u8 batches [n, h, w] (sgpu_extract_stream:
+        uploads and downloads overlap the kernels).  keys / desc: optional preallocated [cap, 4] /
+        [cap, 128] float32 outputs (PinnedArray(...).array for overlapped copies).  Returns
+        (keys, desc, counts[total images]) trimmed to the features written."""
+        bl = [np.ascontiguousarray(b) for b in batches]
+        n, h, w = bl[0].shape
+        if any(b.shape != (n, h, w) or b.dtype != np.uint8 for b in bl):
+            raise ValueError("batches must be u8 arrays of one shape")
+        if cap is None:
+            cap = len(keys) if keys is not None else (len(desc) if desc is not None else 4096 * n * len(bl))
+        if keys is None:
+            keys = np.zeros((cap, 4), np.float32)
+        if desc is None:
+            desc = np.zeros((cap, 128), np.float32)
+        ptrs = (ctypes.c_void_p * len(bl))(*[b.ctypes.data for b in bl])
+        counts = np.zeros(n * len(bl), np.int32)
+        rc = lib().sgpu_extract_stream(self._ctx, ptrs, len(bl), n, w, h, w, keys.ctypes.data,
+                                       desc.ctypes.data, cap, counts.ctypes.data)
+        self._check(rc, "sgpu_extract_stream")
+        t = int(counts.sum())
+        self.batch = 0
+        return keys[:t], desc[:t], counts
 
     def extract_keypoints(self, keys: np.ndarray, has_orientation=True, image: int = 0):
         """Descriptors of caller-supplied keys [n, 4] (x, y, scale, orientation) on image

@@ -84,3 +84,57 @@ def test_capacity_overflow_rerun(gpu_ctx):
             ctx2.close()
     finally:
         ctx.close()
+
+
+def _stream_reference(ctx, batches):
+    keys, desc, counts = [], [], []
+    for b in batches:
+        ctx.extract(b)
+        for i in range(len(b)):
+            k, d = ctx.features(i)
+            keys.append(k)
+            desc.append(d)
+            counts.append(len(k))
+    return np.concatenate(keys), np.concatenate(desc), np.array(counts, np.int32)
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_extract_stream_equals_batches(gpu_ctx, pinned):
+    """sgpu_extract_stream (two slots, uploads and downloads on the copy engines beside the
+    kernels) gives exactly the batch-by-batch results, for 5 batches (every slot reused twice)."""
+    import sgpu
+    gpu_ctx.set_options(default_options())
+    batches = [synth_batch_fast(6, 480, 360, 700 + 10 * k) for k in range(5)]
+    rk, rd, rc = _stream_reference(gpu_ctx, batches)
+    cap = len(rk) + 100
+    bufs = []
+    if pinned:
+        pin_in = [sgpu.PinnedArray(b.shape, np.uint8) for b in batches]
+        for p, b in zip(pin_in, batches):
+            p.array[...] = b
+        kb, db = sgpu.PinnedArray((cap, 4), np.float32), sgpu.PinnedArray((cap, 128), np.float32)
+        bufs = pin_in + [kb, db]
+        k, d, c = gpu_ctx.extract_stream([p.array for p in pin_in], kb.array, db.array)
+    else:
+        k, d, c = gpu_ctx.extract_stream(batches, cap=cap)
+    assert np.array_equal(c, rc)
+    assert np.array_equal(_bits(k), _bits(rk)) and np.array_equal(_bits(d), _bits(rd))
+    for p in bufs:
+        p.free()
+
+
+def test_extract_stream_capacity_and_first_octave(gpu_ctx):
+    """Output capacity: SGPU_ERANGE with complete counts; -fo 1 (sampled input, the serial
+    path) equals the batch-by-batch results too."""
+    import sgpu
+    batches = [synth_batch_fast(3, 320, 240, 900 + k) for k in range(3)]
+    gpu_ctx.set_options(default_options())
+    rk, rd, rc = _stream_reference(gpu_ctx, batches)
+    with pytest.raises(RuntimeError):
+        gpu_ctx.extract_stream(batches, cap=int(rc[:5].sum()))
+    gpu_ctx.set_options(default_options(octave_min=1))
+    fk, fd, fc = _stream_reference(gpu_ctx, batches)
+    k, d, c = gpu_ctx.extract_stream(batches, cap=len(fk))
+    assert np.array_equal(c, fc) and np.array_equal(_bits(k), _bits(fk))
+    assert np.array_equal(_bits(d), _bits(fd))
+    gpu_ctx.set_options(default_options())
