@@ -14,12 +14,20 @@ sys.path.insert(0, os.path.join(ROOT, "modify-sift-gpu_amd", "python"))
 from sgpu_types import SgpuOptions, default_options  # noqa: E402
 
 _LIB = None
+_PATH = os.path.join(ROOT, "oracle", "liboracle.so")
+
+
+def use_library(path):
+    """Bind a different build of the oracle (e.g. oracle/liboracle_perturb.so, the CUDA-like
+    transcendental errors of tests/parity_trust.py) for the calls that follow."""
+    global _LIB, _PATH
+    _LIB, _PATH = None, path
 
 
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(ROOT, "oracle", "liboracle.so")
+        path = _PATH
         if not os.path.exists(path):
             subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle")])
         L = ctypes.CDLL(path)
