@@ -424,6 +424,9 @@ def bench_match_sharded(ctx, n, rank, world, host_dist=None):
                             f"{'RCCL' if host_dist is None else 'gloo'} all-gather of the column "
                             f"states", "device_ms": v[0], "wall_ms": v[1], "matches": int(v[2])}
     except Exception as ex:   # never costs the main measurement
+        # every rank reaches here together: sgpu_match_sharded agrees on failure (an all-reduce of
+        # a status flag) before its all-gather, and the timing all-reduces above run only after
+        # every rank's match returned
         return {"error": str(ex)}
 
 

@@ -1212,9 +1212,20 @@ int sgpu_match_sharded(sgpu_ctx* ctx, const uint8_t* d1, int ns, int row_begin,
     std::vector<int> rows((size_t)std::max(ns, 1)), mine((size_t)3 * std::max(n2, 1));
     int rc = sgpu_match_shard_begin(ctx, d1, ns, row_begin, d2, n2, distmax, ratiomax, mbm,
                                     rows.data(), mine.data(), flags);
-    if (rc != SGPU_OK) return rc;
+    const bool collective = mbm && ctx->comm && n2 > 0;
+    if (collective) {
+        // every rank learns whether any rank failed locally before the data collective, so a
+        // local failure never leaves the peers waiting inside ncclAllGather
+        double failed = rc != SGPU_OK ? 1.0 : 0.0;
+        const int rs = sgpu_comm_allreduce_f64(ctx, &failed, 1, 1);
+        if (rs != SGPU_OK) return rs;
+        if (failed != 0.0)
+            return rc != SGPU_OK ? rc : ctx->fail(SGPU_ENODEV, "sgpu_match_sharded: a peer rank failed");
+    } else if (rc != SGPU_OK) {
+        return rc;
+    }
     std::vector<int> all;
-    if (mbm && ctx->comm && n2 > 0) {   // RCCL all-gather of the n2 x 3 column states
+    if (collective) {   // RCCL all-gather of the n2 x 3 column states
         all.resize((size_t)3 * n2 * ranks);
         rc = sgpu_comm_allgather_i32(ctx, mine.data(), 3 * n2, all.data());
         if (rc != SGPU_OK) return rc;
