@@ -256,11 +256,292 @@ __global__ __launch_bounds__(256) void k_gauss_pk2(
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Gaussian level, wave-streaming form: the same H-then-V filter as k_gauss_pk2 (same taps, same
+// summation order i = 0..FW-1, so bit-identical outputs), but every WAVE owns a 64-column strip
+// band and walks it on its own with a wave-private LDS row-pair buffer and H ring -- no
+// workgroup barriers, so each wave keeps its row loads in flight independently of the other
+// waves of its workgroup (the extremum kernel gained 3.9 -> 5.9 TB/s from the same change).
+// Per step a wave:
+//   * H-filters input chunk c (8 rows: 4 row pairs x 16 lanes x 4 columns, packed FMAs) from
+//     the row-pair buffer into ring rows 8c .. 8c+7;
+//   * V-filters output chunk c - L (L = ceil((FW-1)/8) chunks of lag: 2 row groups x 32 lanes
+//     x 2 columns x 4 rows) from the ring and stores it (plus the decimated next-octave level);
+//   * moves input chunk c+1 from registers into the row-pair buffer and issues the loads of
+//     chunk c+2.
+// LDS ops of one wave execute in issue order, so a wave needs no barrier between writing a
+// buffer and reading what other lanes wrote; the empty asm statements only stop the compiler
+// from moving LDS accesses across the phase boundaries.
+constexpr int WCH = 8;   // rows per chunk (wave kernel)
+
+struct GaussWaveGrid {
+    int strips_x, nsy, rows_per_band, total_waves;
+};
+
+template <int FW, bool U8, int NW>
+__global__ __launch_bounds__(256) void k_gauss_wave(
+    const float* __restrict__ src, const uint8_t* __restrict__ src8, int src_stride,
+    long long src_img_stride, float* __restrict__ dst, long long dst_img_stride, int W, int H,
+    Taps taps, float* __restrict__ ds, int dsw, int dsh, long long ds_img_stride,
+    GaussWaveGrid gg) {
+    constexpr int HALF = FW >> 1;
+    constexpr int OFF = (-HALF) & 3;                  // LDS column of the strip's first input
+    constexpr int SW = GT * NW;                       // columns loaded per strip
+    constexpr int IN_W = SW + FW - 1 + OFF;           // input columns held per row
+    constexpr int NQ = (IN_W + 3) / 4;                // aligned quads per row
+    constexpr int NRD = (FW + 3) / 2;                 // ds_read_b128 per H-pass lane
+    constexpr int IN_S = (SW + FW + 3 + OFF + 3) & ~3;   // float2 per row pair
+    static_assert(4 * NQ <= IN_S, "quad stores stay inside the row pair");
+    constexpr int LAG = (FW - 1 + WCH - 1) / WCH;     // chunks between H and V of a row
+    constexpr int RS0 = WCH * (LAG + 1);
+    constexpr int RS = RS0 <= 32 ? 32 : 64;           // ring rows (power of two)
+    static_assert(RS0 <= RS, "ring holds the lag");
+    constexpr int HS = GT + 4;                        // ring row stride (floats)
+    constexpr int NPAIR = WCH / 2;
+    constexpr int NLD = (NPAIR * NQ + 64 * NW - 1) / (64 * NW);   // staged quads per lane
+#ifndef SGK_GW_NST
+#define SGK_GW_NST 4
+#endif
+    constexpr int NST = SGK_GW_NST;                   // chunks in registers (loads NST-1 ahead)
+    static_assert(NW == 1 || NW == 4, "one strip per wave, or one per 4-wave workgroup");
+    static_assert(NW == 1 || NST % 2 == 0, "shared input buffers alternate by step parity");
+    // NW == 1: a wave-private row-pair buffer per wave; NW > 1: the NW waves of a workgroup
+    // share one double-buffered buffer of their NW * 64 columns
+    constexpr int NBUF = NW == 1 ? 4 : 2;
+    __shared__ __attribute__((aligned(16))) f2v s_in_all[NBUF][NPAIR * IN_S + 4];   // + pad slot
+    __shared__ __attribute__((aligned(16))) float s_h_all[4][RS * HS];
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int ld = NW == 1 ? lane : threadIdx.x;     // index among the strip's loaders
+    int sx, rest, x0, xs;                            // xs: first column of the loaded strip
+    if (NW == 1) {
+        const int gw = blockIdx.x * 4 + wave;
+        if (gw >= gg.total_waves) return;             // uniform per wave
+        sx = gw % gg.strips_x;
+        rest = gw / gg.strips_x;
+        xs = x0 = sx * GT;
+    } else {
+        sx = blockIdx.x % gg.strips_x;                // strips of NW * 64 columns
+        rest = blockIdx.x / gg.strips_x;
+        xs = sx * SW;
+        x0 = xs + GT * wave;
+    }
+    float* s_h = s_h_all[wave];
+    const int sy = rest % gg.nsy, b = rest / gg.nsy;
+    const int yb = sy * gg.rows_per_band;
+    const int ye = min(H, yb + gg.rows_per_band);
+    const int nchunk_out = (ye - yb + WCH - 1) / WCH;
+
+    const float* sf = U8 ? nullptr : src + (long long)b * src_img_stride;
+    const uint8_t* s8 = U8 ? src8 + (long long)b * src_img_stride : nullptr;
+    const int a0 = xs - HALF - OFF;
+    // a staged element is the raw fetch of one aligned quad of rows 2p, 2p+1; the u8 -> f32
+    // conversion and the clamp-to-edge selects happen when it is written to LDS, so that nothing
+    // consumes the registers right after the loads are issued (the compiler would wait for them
+    // there, one step early, and the prefetch would hide nothing)
+    struct Elem { float4 v0, v1; };
+    Elem st[NST][NLD];
+    auto load_chunk = [&](Elem (&stage)[NLD], int c) {
+#pragma unroll
+        for (int m = 0; m < NLD; m++) {
+            const int e = min(ld + 64 * NW * m, NPAIR * NQ - 1);
+            const int p = e / NQ, j = e - p * NQ;
+            const int gy0 = clampi(yb - HALF + c * WCH + 2 * p, 0, H - 1);
+            const int gy1 = clampi(yb - HALF + c * WCH + 2 * p + 1, 0, H - 1);
+            const int lq = clampi(a0 + 4 * j, 0, W - 4);          // aligned first column
+            if (U8) {
+                stage[m].v0.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(s8 + (long long)gy0 * src_stride + lq));
+                stage[m].v1.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(s8 + (long long)gy1 * src_stride + lq));
+            } else {
+                stage[m].v0 = *reinterpret_cast<const float4*>(sf + (long long)gy0 * src_stride + lq);
+                stage[m].v1 = *reinterpret_cast<const float4*>(sf + (long long)gy1 * src_stride + lq);
+            }
+        }
+    };
+    // every lane writes every staged element (lanes past the chunk's last quad write a pad
+    // slot): a lane-conditional write would leave the registers "maybe pending" on the skip
+    // path, and the next load into them would wait for everything in flight
+    auto store_chunk = [&](const Elem (&stage)[NLD], f2v* s_in) {
+#pragma unroll
+        for (int m = 0; m < NLD; m++) {
+            const int e = ld + 64 * NW * m;
+            {
+                const bool real = e < NPAIR * NQ;
+                const int p = e / NQ, j = e - p * NQ;
+                const int gq = a0 + 4 * j;
+                float r0[4], r1[4];
+                if (U8) {
+                    const uint32_t w0 = __float_as_uint(stage[m].v0.x), w1 = __float_as_uint(stage[m].v1.x);
+#pragma unroll
+                    for (int t = 0; t < 4; t++) {
+                        r0[t] = u8_to_unit((w0 >> (8 * t)) & 255u);
+                        r1[t] = u8_to_unit((w1 >> (8 * t)) & 255u);
+                    }
+                } else {
+                    r0[0] = stage[m].v0.x; r0[1] = stage[m].v0.y; r0[2] = stage[m].v0.z; r0[3] = stage[m].v0.w;
+                    r1[0] = stage[m].v1.x; r1[1] = stage[m].v1.y; r1[2] = stage[m].v1.z; r1[3] = stage[m].v1.w;
+                }
+                // clamp-to-edge: a quad left of column 0 repeats column 0, right of W-1 repeats W-1
+                const bool left = gq < 0, right = gq > W - 4;
+                float u0[4], u1[4];
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    u0[t] = left ? r0[0] : (right ? r0[3] : r0[t]);
+                    u1[t] = left ? r1[0] : (right ? r1[3] : r1[t]);
+                }
+                float4* q = reinterpret_cast<float4*>(&s_in[real ? p * IN_S + 4 * j : NPAIR * IN_S]);
+                q[0] = make_float4(u0[0], u1[0], u0[1], u1[1]);
+                q[1] = make_float4(u0[2], u1[2], u0[3], u1[3]);
+            }
+        }
+    };
+
+#pragma unroll
+    for (int k = 0; k < NST; k++) load_chunk(st[k], k);
+    store_chunk(st[0], s_in_all[NW == 1 ? wave : 0]);
+    if (NW > 1) __syncthreads();
+    float* d = dst + (long long)b * dst_img_stride;
+    float* dd = ds ? ds + (long long)b * ds_img_stride : nullptr;
+    const int hp = lane >> 4, hc = (lane & 15) * 4;    // H pass: rows 2hp, 2hp+1; columns hc..hc+3
+    const int vq = lane >> 5, vc = (lane & 31) * 2;    // V pass: rows 4vq..4vq+3; columns vc, vc+1
+    const int x = x0 + vc;
+    // Loads, the H pass and the LDS store run unconditionally (past the band's last input
+    // chunk they fetch clamped rows and fill ring rows no output reads): with a conditional
+    // load block the compiler's wait counting must assume no loads were issued after `cur`'s
+    // and waits for everything in flight before storing `cur`.
+    // Order inside a step: H pass, V pass + its global stores, THEN the loads of chunk c+2,
+    // then `cur` (chunk c+1, loaded a step ago) into LDS.  The wait before that LDS store then
+    // leaves the 4 loads just issued in flight (only older ops are waited for); loads issued
+    // before the (branchy, variable-count) stores would be waited for too.
+    const bool active = x0 < W;                      // a wave right of the image only loads
+    auto step = [&](int c, Elem (&cur)[NLD], Elem (&nxt)[NLD], int par) {
+        f2v* s_in = s_in_all[NW == 1 ? wave : par];
+        f2v* s_in_next = s_in_all[NW == 1 ? wave : 1 - par];
+        {   // H pass of input chunk c -> ring rows c*WCH .. c*WCH+7
+            const f2v* rowp = &s_in[hp * IN_S + hc + OFF + (NW == 1 ? 0 : GT * wave)];
+            f2v a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};   // columns hc+i
+#pragma unroll
+            for (int q = 0; q < NRD; q++) {
+                f2v e[2];                            // pair columns hc+2q, hc+2q+1
+                if (OFF % 2 == 0) {
+                    const float4 v = reinterpret_cast<const float4*>(rowp)[q];
+                    e[0] = f2v{v.x, v.y};
+                    e[1] = f2v{v.z, v.w};
+                } else {
+                    e[0] = rowp[2 * q];
+                    e[1] = rowp[2 * q + 1];
+                }
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const int m = 2 * q + u;
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        if (m - i >= 0 && m - i < FW) a[i] = pk_fma(e[u], taps.k[m - i], a[i]);
+                }
+            }
+            const int r0 = (c * WCH + 2 * hp) & (RS - 1);
+            *reinterpret_cast<float4*>(&s_h[r0 * HS + hc]) = make_float4(a[0].x, a[1].x, a[2].x, a[3].x);
+            *reinterpret_cast<float4*>(&s_h[(r0 + 1) * HS + hc]) = make_float4(a[0].y, a[1].y, a[2].y, a[3].y);
+        }
+        asm volatile("" ::: "memory");
+        const int kout = c - LAG;
+        if (active && kout >= 0 && kout < nchunk_out) {   // V pass of output chunk kout
+            const int t0 = kout * WCH + 4 * vq;
+            f2v acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};   // rows t0+j
+#pragma unroll
+            for (int m = 0; m < FW + 3; m++) {
+                const f2v v = *reinterpret_cast<const f2v*>(&s_h[((t0 + m) & (RS - 1)) * HS + vc]);
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (m - j >= 0 && m - j < FW) acc[j] = pk_fma(v, taps.k[m - j], acc[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) asm volatile("" : "+v"(acc[j]));
+            if (x < W) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int y = yb + t0 + j;
+                    if (y < ye) {
+                        *reinterpret_cast<f2v*>(&d[(long long)y * W + x]) = acc[j];
+                        // DownsampleKernel<1> (ProgramCU.cu:287-298), as in k_gauss_pk2
+                        if (dd && !(y & 1) && (y >> 1) < dsh) {
+                            float* drow = dd + (long long)(y >> 1) * dsw;
+                            if ((x >> 1) < dsw) drow[x >> 1] = acc[j].x;
+                            if (x + 1 == W - 1)
+                                for (int cc = W >> 1; cc < dsw; cc++) drow[cc] = acc[j].y;
+                        }
+                    }
+                }
+            }
+        }
+        asm volatile("" ::: "memory");
+        load_chunk(nxt, c + NST);
+        store_chunk(cur, s_in_next);
+        if (NW > 1) {
+            // LDS-only barrier: chunk c+1 is in the other buffer for every wave, and every wave
+            // is done reading this step's buffer (no vmcnt wait: the loads stay in flight)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+        asm volatile("" ::: "memory");
+    };
+    // NST register stages, rotated by unrolling: step c stores chunk c+1 from st[(c+1) % NST]
+    // and loads chunk c+NST into st[c % NST].  Every step of the unrolled group runs (a
+    // conditional one would turn the stages into phis, and their copies wait for the loads in
+    // flight).
+    const int nsteps = nchunk_out + LAG;
+    for (int c = 0; c < nsteps; c += NST) {
+#pragma unroll
+        for (int k = 0; k < NST; k++) step(c + k, st[(k + 1) % NST], st[k], k & 1);
+    }
+}
+
+// band height of the wave kernel: rows_hint > 0 forces it (test / tuning hook), else bands of
+// the whole image unless that leaves fewer than ~8 waves per CU, then as many bands as needed
+static GaussWaveGrid gauss_wave_grid(int w, int h, int batch, int rows_hint, int nw) {
+    GaussWaveGrid g{};
+    g.strips_x = (w + GT * nw - 1) / (GT * nw);
+    const long long per_band = (long long)g.strips_x * nw * batch;   // waves per band
+    int rows = h;
+    if (rows_hint > 0) {
+        rows = rows_hint;
+    } else {
+        const long long want = 8 * 256;
+        const int nsy = (int)std::min<long long>((want + per_band - 1) / per_band,
+                                                 std::max(1, h / (4 * WCH)));
+        rows = (h + std::max(nsy, 1) - 1) / std::max(nsy, 1);
+    }
+    rows = std::max(WCH, (rows + WCH - 1) / WCH * WCH);
+    g.rows_per_band = rows;
+    g.nsy = (h + rows - 1) / rows;
+    g.total_waves = (int)(per_band * g.nsy);
+    return g;
+}
+
 template <int FW>
 hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
                           long long src_img_stride, float* dst, long long dst_img_stride, int w,
                           int h, const Taps& taps, int batch, float* ds, int dsw, int dsh,
-                          long long ds_img_stride, hipStream_t stream) {
+                          long long ds_img_stride, hipStream_t stream, int wave_rows) {
+    const bool vec = (src_stride % 4) == 0 && (src_img_stride % 4) == 0 && (w % 4) == 0 &&
+                     w >= 4 && ((uintptr_t)(src8 ? (const void*)src8 : (const void*)src) % 16) == 0;
+    if (vec && wave_rows >= 0) {
+#ifndef SGK_GW_NW
+#define SGK_GW_NW 1
+#endif
+        constexpr int NW = SGK_GW_NW;
+        const GaussWaveGrid gg = gauss_wave_grid(w, h, batch, wave_rows, NW);
+        const dim3 wgrid((unsigned)((gg.total_waves + 3) / 4));
+        if (src8)
+            hipLaunchKernelGGL((k_gauss_wave<FW, true, NW>), wgrid, dim3(256), 0, stream, src,
+                               src8, src_stride, src_img_stride, dst, dst_img_stride, w, h, taps,
+                               ds, dsw, dsh, ds_img_stride, gg);
+        else
+            hipLaunchKernelGGL((k_gauss_wave<FW, false, NW>), wgrid, dim3(256), 0, stream, src,
+                               src8, src_stride, src_img_stride, dst, dst_img_stride, w, h, taps,
+                               ds, dsw, dsh, ds_img_stride, gg);
+        return hipGetLastError();
+    }
     // bands of at most 17 chunks (544 rows), and at least 1024 workgroups when the image is
     // short (kernel traces: 2 bands of 540 rows beat 1 band of 1080 on 1080p, and 1 band beats 2
     // on the 540- and 270-row octaves)
@@ -275,8 +556,6 @@ hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
     const dim3 grid((unsigned)(strips_x * nsy * batch));
     // aligned quads need 4-element row strides and image strides, a 16-B aligned base and a
     // width that is a multiple of 4 (always true for pyramid levels)
-    const bool vec = (src_stride % 4) == 0 && (src_img_stride % 4) == 0 && (w % 4) == 0 &&
-                     w >= 4 && ((uintptr_t)(src8 ? (const void*)src8 : (const void*)src) % 16) == 0;
 #define SGK_PK2(U8, VEC)                                                                   \
     hipLaunchKernelGGL((k_gauss_pk2<FW, U8, VEC>), grid, dim3(256), 0, stream, src, src8,    \
                        src_stride, src_img_stride, dst, dst_img_stride, w, h, taps, ds, dsw,  \
@@ -1589,11 +1868,12 @@ __global__ __launch_bounds__(64) void k_debug_candidates(
 hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         long long src_img_stride, float* dst, long long dst_img_stride, int w,
                         int h, int fw, const Taps& taps, int batch, float* ds_dst, int ds_w,
-                        int ds_h, long long ds_img_stride, hipStream_t stream) {
+                        int ds_h, long long ds_img_stride, hipStream_t stream, int wave_rows) {
 #define SGK_GAUSS(FW)                                                                       \
     case FW:                                                                                  \
         return gauss_dispatch<FW>(src, src_u8, src_stride, src_img_stride, dst, dst_img_stride, \
-                                  w, h, taps, batch, ds_dst, ds_w, ds_h, ds_img_stride, stream);
+                                  w, h, taps, batch, ds_dst, ds_w, ds_h, ds_img_stride, stream, \
+                                  wave_rows);
     switch (fw) {
         SGK_GAUSS(5) SGK_GAUSS(7) SGK_GAUSS(9) SGK_GAUSS(11) SGK_GAUSS(13) SGK_GAUSS(15)
         SGK_GAUSS(17) SGK_GAUSS(19) SGK_GAUSS(21) SGK_GAUSS(23) SGK_GAUSS(25) SGK_GAUSS(27)

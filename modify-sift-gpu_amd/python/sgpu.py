@@ -14,7 +14,9 @@ import numpy as np
 from sgpu_types import SgpuOptions, default_options
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG, "lib", "libsiftgpu.so")
+# SGPU_LIB_PATH: an experiment build of the same library (tests/build_variant.sh); default: the
+# in-tree product build
+LIB_PATH = os.environ.get("SGPU_LIB_PATH") or os.path.join(PKG, "lib", "libsiftgpu.so")
 
 SGPU_OK, SGPU_EINVAL, SGPU_ENODEV, SGPU_ENOMEM, SGPU_ERANGE = 0, -1, -2, -3, -4
 SGPU_INPUT_HOST, SGPU_INPUT_DEVICE, SGPU_INPUT_STAGED = 0, 1, 2
@@ -393,6 +395,7 @@ class SiftContext:
     # ---- test hooks
     DEBUG_PARTS2, DEBUG_PARTS4, DEBUG_TINY_CAP, DEBUG_FUSED_MATCH = 1, 2, 4, 8
     DEBUG_EXACT_DESCRIPTOR = 16
+    DEBUG_GAUSS_WAVE = 32     # wave-streaming Gaussian; band rows in bits 16..
 
     def set_debug_flags(self, flags: int):
         """Per-context debug flags (sgpu_debug_set_flags; 0 = shipped configuration)."""

@@ -1,0 +1,90 @@
+"""Gaussian pyramid kernels on the GPU: the wave-streaming level kernel (k_gauss_wave) against
+the workgroup strip kernel (k_gauss_pk2) and the oracle, bit for bit.
+
+Both kernels restate FilterH / FilterV (ProgramCU.cu:115-222) with the taps summed i = 0..FW-1
+and the 2x decimation of DownsampleKernel<1> (ProgramCU.cu:287-298) fused into the level that
+feeds the next octave; the band walk (rows per wave), the lag between H and V passes and the
+ring wrap must not change a single bit, so every level of every octave is compared."""
+import numpy as np
+import pytest
+
+import oracle_py as O
+import sgpu
+from sgpu_types import default_options
+from sift_synth import synth_batch, synth_image
+
+pytestmark = pytest.mark.gpu
+
+WAVE = sgpu.SiftContext.DEBUG_GAUSS_WAVE
+
+
+def _bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+def _levels(ctx, image, opts):
+    geo = ctx.geometry()
+    return [[ctx.gaussian(image, o, lvl).copy() for lvl in range(opts.dog_level_num + 3)]
+            for o in range(len(geo))]
+
+
+@pytest.mark.parametrize("w,h,seed", [(16, 16, 3), (203, 97, 2), (640, 480, 1000)])
+def test_wave_levels_vs_oracle(gpu_ctx, w, h, seed):
+    img = synth_image(w, h, seed)
+    opts = default_options()
+    gpu_ctx.set_options(opts)
+    gpu_ctx.set_debug_flags(WAVE)
+    try:
+        gpu_ctx.extract(img)
+        for o in range(len(gpu_ctx.geometry())):
+            for lvl in range(opts.dog_level_num + 3):
+                g = gpu_ctx.gaussian(0, o, lvl)
+                r = O.gaussian(img, o, lvl, opts)
+                assert np.array_equal(_bits(g), _bits(r)), (o, lvl)
+    finally:
+        gpu_ctx.set_debug_flags(0)
+
+
+# band heights: auto, one chunk, bands not a multiple of the lag span, a band taller than the
+# image; sizes: tiny, ragged (width not a multiple of 64, odd height), 1080p
+@pytest.mark.parametrize("rows", [0, 8, 24, 40, 4096])
+@pytest.mark.parametrize("n,w,h", [(2, 16, 16), (3, 203, 97), (2, 1920, 1080), (5, 300, 1203)])
+def test_wave_levels_equal_block_kernel(gpu_ctx, rows, n, w, h):
+    imgs = synth_batch(n, w, h, 40 + w % 7)
+    opts = default_options()
+    gpu_ctx.set_options(opts)
+    gpu_ctx.set_debug_flags(0)
+    gpu_ctx.extract(imgs)
+    ref = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
+    k_ref = [gpu_ctx.features(i)[0].copy() for i in range(n)]
+    gpu_ctx.set_debug_flags(WAVE | (rows << 16))
+    try:
+        gpu_ctx.extract(imgs)
+        got = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
+        for a, b in zip(ref, got):
+            for o, (la, lb) in enumerate(zip(a, b)):
+                for lvl, (x, y) in enumerate(zip(la, lb)):
+                    assert np.array_equal(_bits(x), _bits(y)), (o, lvl)
+        for i in range(n):
+            assert np.array_equal(_bits(gpu_ctx.features(i)[0]), _bits(k_ref[i]))
+    finally:
+        gpu_ctx.set_debug_flags(0)
+
+
+@pytest.mark.parametrize("fo", [1, -1])
+def test_wave_first_octave_float_path(gpu_ctx, fo):
+    """-fo != 0 feeds the first level from an f32 buffer (the resampled input)."""
+    img = synth_image(321, 241, 17 + fo)
+    opts = default_options(octave_min=fo)
+    gpu_ctx.set_options(opts)
+    gpu_ctx.set_debug_flags(WAVE)
+    try:
+        gpu_ctx.extract(img)
+        for o in range(min(len(gpu_ctx.geometry()), 2)):
+            for lvl in range(opts.dog_level_num + 3):
+                g = gpu_ctx.gaussian(0, o, lvl)
+                r = O.gaussian(img, o, lvl, opts)
+                assert np.array_equal(_bits(g), _bits(r)), (o, lvl)
+    finally:
+        gpu_ctx.set_debug_flags(0)
+        gpu_ctx.set_options(default_options())
