@@ -653,13 +653,12 @@ __device__ __forceinline__ KeyOut key_test(Get get, float t0, float t, float edg
 }
 
 // ------------------------------------------------------------------------------------------
-// Extremum detection, wave-streaming form (the shipped one).  Each WAVE owns a 64-column strip
-// segment of one image/octave and walks it row by row on its own -- no workgroup barriers, so
-// every wave keeps its loads in flight independently (a workgroup-synchronised tile walk
-// reached ~3.9 TB/s, the same read pattern without barriers ~5.9 TB/s, tests/microbench).
-//   * row y+1 of the d+3 Gaussian planes (64 columns + the two halo columns) is loaded into
-//     registers one step ahead, turned into the d+2 DoG rows (D_m = G_m - G_{m-1}) and written
-//     to a wave-private 4-row LDS ring;
+// Extremum detection, wave-streaming form.  Each WAVE owns a strip segment of one image/octave
+// and walks it row by row on its own -- no workgroup barriers, so every wave keeps its loads in
+// flight independently (a workgroup-synchronised tile walk reached ~3.9 TB/s, the same read
+// pattern without barriers ~5.9 TB/s, tests/microbench).
+//   * the d+3 Gaussian planes' rows are loaded into registers two rows ahead, turned into the
+//     d+2 DoG rows (D_m = G_m - G_{m-1}) and written to a wave-private 4-row LDS ring;
 //   * the 3-wide row max/min of each DoG row is computed once and kept in registers for the
 //     three output rows it borders; a branch-free 3x3x3 max/min pre-filter selects candidates,
 //     which are compacted per wave (ballot + mbcnt) and given the exact ComputeKEY test
@@ -671,60 +670,76 @@ struct ExtremaWaveGrid {
     int nseg[kMaxOctaves];             // segments per strip column
 };
 
+// Layout of the loop (k_extrema_wave2):
+//   * A wave covers 62 output columns with 64 lanes: lane l holds column x0 - 1 + l, lanes 0
+//     and 63 only feed their neighbours, so no lane issues a separate halo load (halo loads
+//     behind a lane branch made the compiler's wait counting assume they were missing and wait
+//     for every load in flight).
+//   * Two register row sets alternate (the loop is unrolled by two and both halves always run;
+//     the second half of the last pair tests no pixel).
+//   * The octave's fields are read as scalars before the loop: read inside the candidate branch
+//     they were vector loads whose vmcnt(0) waited for the rows in flight.
+// Round 2: 1.94 -> 1.72 ms per 128 x 1080p against the one-row form.
+#ifndef SGK_EXT2_WAVES
+#define SGK_EXT2_WAVES 1
+#endif
 template <int ND>   // ND = number of DoG planes = d + 2
-__global__ __launch_bounds__(256) void k_extrema_wave(const float* __restrict__ pyr,
-                                                      uint32_t* __restrict__ mask,
-                                                      uint32_t* __restrict__ row_count,
-                                                      const FeatureParams fp,
-                                                      const ExtremaWaveGrid eg) {
-    constexpr int RW = 68;                          // ring row: columns x0-1 .. x0+64 (+pad)
+__global__ __launch_bounds__(256, SGK_EXT2_WAVES) void k_extrema_wave2(const float* __restrict__ pyr,
+                                                       uint32_t* __restrict__ mask,
+                                                       uint32_t* __restrict__ row_count,
+                                                       const FeatureParams fp,
+                                                       const ExtremaWaveGrid eg) {
+    constexpr int RW = 68;                          // ring row: lane l at column l + 1 (+pad)
     constexpr int NJ = ND - 2;
-    __shared__ float s_ring[4][ND][4][RW];          // [wave][plane][row & 3][column + 1]
+    __shared__ float s_ring[4][ND][4][RW];          // [wave][plane][row & 3][lane + 1]
     __shared__ uint16_t s_list[4][NJ * 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int gw = blockIdx.x * 4 + wave;
     if (gw >= eg.wave0[fp.n_octaves]) return;       // uniform per wave
     int o = 0;
     while (o + 1 < fp.n_octaves && gw >= eg.wave0[o + 1]) o++;
+    // o is wave-uniform: said so, the octave's fields are scalar loads (lgkmcnt) instead of
+    // vector loads from the argument block inside the candidate branch, whose vmcnt(0) would
+    // wait for the rows in flight
+    o = __builtin_amdgcn_readfirstlane(o);
     const OctaveDesc& od = fp.oct[o];
+    const long long mask_off = od.mask_off, mask_lstride = od.mask_level_stride;
+    const int nwords = od.nwords;
+    const long long rc_base = fp.row_off[o];
     const int W = od.wa, H = od.h;
-    const int strips_x = (W + 63) / 64;
+    const int strips_x = (W + 61) / 62;
     const int id = gw - eg.wave0[o];
     const int sx = id % strips_x, rest = id / strips_x;
     const int sg = rest % eg.nseg[o], b = rest / eg.nseg[o];
-    const int x0 = sx * 64;
+    const int x0 = sx * 62;
     const int ys = sg * eg.seg_rows[o], ye = min(H, ys + eg.seg_rows[o]);
     const long long lstride = od.level_stride;
     const float* g0 = pyr + od.gauss_off + (long long)b * W * H;
     float(*ring)[4][RW] = s_ring[wave];
     uint16_t* list = s_list[wave];
 
-    // this lane's columns: main x0 + lane; lanes 0 / 1 also fetch the halo columns x0-1 / x0+64
-    const int gx = min(x0 + lane, W - 1);
-    const bool halo = lane < 2;
-    const int hx = clampi(lane == 0 ? x0 - 1 : x0 + 64, 0, W - 1);
-    const int htx = lane == 0 ? 0 : 65;
-    float gm[ND + 1], gh[ND + 1];
-    auto fetch = [&](int y) {   // G row y (clamped) into registers
-        const float* q = g0 + (long long)clampi(y, 0, H - 1) * W;
+    const int x = x0 - 1 + lane;                    // this lane's column
+    const int gx = clampi(x, 0, W - 1);
+    const bool out_lane = lane >= 1 && lane <= 62 && x > 0 && x < W - 1;
+    struct Row { float m[ND + 1]; };
+    Row rA, rB;
+    auto fetch = [&](Row& r, int y) {   // G row y (clamped) into registers
+        const float* q = g0 + (long long)clampi(y, 0, H - 1) * W + gx;
 #pragma unroll
-        for (int m = 0; m <= ND; m++) gm[m] = q[gx + m * lstride];
-        if (halo) {
-#pragma unroll
-            for (int m = 0; m <= ND; m++) gh[m] = q[hx + m * lstride];
-        }
+        for (int m = 0; m <= ND; m++) r.m[m] = q[m * lstride];
     };
-    auto put = [&](int y) {     // DoG row y into the ring
-        float* r = &ring[0][y & 3][0];
+    // Lanes exchange values through the wave-private ring and list.  LDS accesses of one wave
+    // complete in issue order, but the compiler sees only per-lane addresses (a lane writes
+    // column lane + 1 and reads lane .. lane + 2) and may reorder them: the empty asm
+    // statements keep every write before the reads that follow it.
+    auto put = [&](const Row& r, int y) {   // DoG row y into the ring
+        float* rr = &ring[0][y & 3][lane + 1];
 #pragma unroll
-        for (int m = 0; m < ND; m++) r[m * 4 * RW + lane + 1] = gm[m + 1] - gm[m];
-        if (halo) {
-#pragma unroll
-            for (int m = 0; m < ND; m++) r[m * 4 * RW + htx] = gh[m + 1] - gh[m];
-        }
+        for (int m = 0; m < ND; m++) rr[m * 4 * RW] = r.m[m + 1] - r.m[m];
+        asm volatile("" ::: "memory");
     };
     // rolling 3-wide row max/min of DoG rows y-1 and y (per plane), refreshed per step
-    float hx0[ND], hn0[ND], hx1[ND], hn1[ND];
+    float hx0[ND], hn0[ND], hx1[ND], hn1[ND], cvx[ND];
     auto rowmm = [&](int y, float* mx, float* mn, float* cv) {
 #pragma unroll
         for (int m = 0; m < ND; m++) {
@@ -735,21 +750,10 @@ __global__ __launch_bounds__(256) void k_extrema_wave(const float* __restrict__ 
             if (cv) cv[m] = c;
         }
     };
-    fetch(ys - 1);
-    put(ys - 1);
-    fetch(ys);
-    put(ys);
-    if (ys + 1 < ye + 1) fetch(ys + 1);
-    float cvx[ND];
-    rowmm(ys - 1, hx0, hn0, nullptr);
-    rowmm(ys, hx1, hn1, cvx);
-    const int x = x0 + lane;
-    for (int y = ys; y < ye; y++) {
-        put(y + 1);                                  // row y+1 arrived (fetched one step ago)
-        if (y + 2 < ye + 1) fetch(y + 2);            // next row in flight during this step
+    auto body = [&](int y) {   // test row y: DoG rows y-1, y, y+1 are in the ring
         float hx2[ND], hn2[ND], cnx[ND];
         rowmm(y + 1, hx2, hn2, cnx);
-        const bool interior = x > 0 && x < W - 1 && y > 0 && y < H - 1;
+        const bool interior = out_lane && y < ye && y > 0 && y < H - 1;
         int ncand = 0;
 #pragma unroll
         for (int j = 0; j < NJ; j++) {
@@ -770,18 +774,19 @@ __global__ __launch_bounds__(256) void k_extrema_wave(const float* __restrict__ 
             }
             ncand += __popcll(bal);
         }
+        asm volatile("" ::: "memory");
         for (int c0 = 0; c0 < ncand; c0 += 64) {
             if (c0 + lane < ncand) {
                 const int code = list[c0 + lane];
                 const int j = code >> 6, cl = code & 63;
                 auto get = [&](int m, int r, int c) { return ring[j + m][(y + r - 1) & 3][cl + c]; };
                 if (key_test(get, fp.t0, fp.t, fp.edge, fp.subpixel).result != 0.f) {
-                    const int xx = x0 + cl;
-                    uint32_t* mrow = mask + od.mask_off + j * od.mask_level_stride +
-                                     ((long long)b * H + y) * od.nwords;
+                    const int xx = x0 - 1 + cl;
+                    uint32_t* mrow = mask + mask_off + j * mask_lstride +
+                                     ((long long)b * H + y) * nwords;
                     atomicOr(&mrow[xx >> 5], 1u << (xx & 31));
-                    atomicAdd(&row_count[(long long)b * fp.rows_per_image + fp.row_off[o] +
-                                         j * H + y], 1u);
+                    atomicAdd(&row_count[(long long)b * fp.rows_per_image + rc_base + j * H + y],
+                              1u);
                 }
             }
         }
@@ -791,6 +796,26 @@ __global__ __launch_bounds__(256) void k_extrema_wave(const float* __restrict__ 
             hx1[m] = hx2[m]; hn1[m] = hn2[m];
             cvx[m] = cnx[m];
         }
+        asm volatile("" ::: "memory");   // this row's list and ring reads before the next writes
+    };
+    fetch(rA, ys - 1);
+    put(rA, ys - 1);
+    fetch(rA, ys);
+    put(rA, ys);
+    fetch(rA, ys + 1);
+    fetch(rB, ys + 2);
+    rowmm(ys - 1, hx0, hn0, nullptr);
+    rowmm(ys, hx1, hn1, cvx);
+    // each set is refetched after the row test that follows its put: the test's atomics (a
+    // data-dependent number of them) then come before, not after, the loads that the next wait
+    // must leave in flight
+    for (int y = ys; y < ye; y += 2) {
+        put(rA, y + 1);
+        body(y);
+        fetch(rA, y + 3);
+        put(rB, y + 2);
+        body(y + 1);
+        fetch(rB, y + 4);
     }
 }
 
@@ -1930,12 +1955,12 @@ hipError_t launch_first_octave_input(const float* src, const uint8_t* src_u8, in
 
 hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
                           const FeatureParams& fp, hipStream_t stream) {
-    // one wave per (image, 64-column strip, row segment); ~32k waves in all
+    // one wave per (image, strip of 62 output columns, row segment); ~32k waves in all
     ExtremaWaveGrid eg{};
     int nw = 0;
     for (int o = 0; o < fp.n_octaves; o++) {
         const OctaveDesc& od = fp.oct[o];
-        const int strips_x = (od.wa + 63) / 64;
+        const int strips_x = (od.wa + 61) / 62;
         const long long per_col = (long long)strips_x * fp.batch;
         int nseg = (int)std::min<long long>(std::max<long long>(1, (32768 + per_col - 1) / per_col),
                                             std::max(1, od.h / 16));
@@ -1949,7 +1974,7 @@ hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
     eg.wave0[fp.n_octaves] = nw;
     const unsigned nb = (unsigned)((nw + 3) / 4);
     switch (fp.d + 2) {
-#define SGK_EXTW(ND)     case ND: hipLaunchKernelGGL((k_extrema_wave<ND>), dim3(nb), dim3(256), 0, stream, pyr, mask, row_count, fp, eg); break;
+#define SGK_EXTW(ND)     case ND: hipLaunchKernelGGL((k_extrema_wave2<ND>), dim3(nb), dim3(256), 0, stream, pyr, mask, row_count, fp, eg); break;
         SGK_EXTW(3) SGK_EXTW(4) SGK_EXTW(5) SGK_EXTW(6) SGK_EXTW(7) SGK_EXTW(8)
         default: return hipErrorInvalidValue;
 #undef SGK_EXTW
