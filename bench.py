@@ -213,7 +213,7 @@ def main():
         "features_per_image": local_feats / (B * args.steps),
         "stage_ms_per_step": {k: v / args.steps for k, v in stage_acc.items() if k != "match"},
         "roofline": {
-            "kernel": f"k_gauss_pk2 (separable Gaussian level; all {n_gauss} launches of a step, "
+            "kernel": f"k_gauss_wave (separable Gaussian level; all {n_gauss} launches of a step, "
                       "HIP events around them on the library's stream)",
             "bound": "hbm",
             "achieved": achieved,
@@ -334,7 +334,7 @@ def bench_c4(ctx, batch=8, steps=3):
                             f"staged in HBM", "value": batch * steps / el, "unit": "images/s",
                 "ms_per_step": el / steps * 1e3, "features_per_image": feats / (batch * steps),
                 "stage_ms_per_step": {k: v / steps for k, v in st.items() if k != "match"},
-                "roofline": {"kernel": f"k_gauss_pk2 ({n_gauss} launches per step)",
+                "roofline": {"kernel": f"k_gauss_wave ({n_gauss} launches per step)",
                              "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                              "algorithmic_bytes_per_launch": 48.0 * sumN * batch / n_gauss,

@@ -246,10 +246,11 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
                                    shipped kernel sums in any order with hardware sqrt/rcp/exp
                                    (descriptor L2 ~1e-6 from the oracle).  Also set at context
                                    creation by the environment variable SGPU_EXACT_DESCRIPTOR=1 */
-#define SGPU_DEBUG_GAUSS_WAVE 32 /* Gaussian levels through the wave-streaming kernel
-                                   (k_gauss_wave) instead of the workgroup strip kernel; both
-                                   are bit-identical.  Bits 16.. of the flags, when not 0,
-                                   force its band height in rows (test / tuning hook)     */
+#define SGPU_DEBUG_GAUSS_BLOCK 32 /* Gaussian levels through the workgroup strip kernel
+                                   (k_gauss_pk2) instead of the shipped wave-streaming one
+                                   (k_gauss_wave); both are bit-identical.  Bits 16.. of the
+                                   flags, when not 0, force the wave kernel's band height in
+                                   rows (test / tuning hook)                              */
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);

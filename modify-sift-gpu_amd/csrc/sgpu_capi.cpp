@@ -300,7 +300,7 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
         if (ev[0] == '1') ctx->debug_flags |= SGPU_DEBUG_EXACT_DESCRIPTOR;
     // A/B hook for the Gaussian kernels (bench / probe runs in one process tree)
     if (const char* ev = getenv("SGPU_GAUSS"))
-        if (!strcmp(ev, "wave")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_WAVE;
+        if (!strcmp(ev, "block")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_BLOCK;
     int rc = sgpu_ctx_set_options(ctx, opt);
     if (rc != SGPU_OK) {
         sgpu_ctx_destroy(ctx);
@@ -431,7 +431,7 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     const float* srcf = is_f32 ? (const float*)src_in + (size_t)pt.img0 * img_elems : nullptr;
 
     // ---- Gaussian pyramid (BuildPyramid, PyramidCU.cpp:979-1044): one launch per level
-    // (k_gauss_pk2) for the whole part.  Level kds = level_ds - level_min of octave o also writes
+    // (k_gauss_wave) for the whole part.  Level kds = level_ds - level_min of octave o also writes
     // its 2x decimation as level 0 of octave o+1 (PyramidCU.cpp:1024).
     float* pyr = pt.pyr.as<float>();
     sgk::Taps taps;
@@ -483,8 +483,8 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
                                           k == 0 ? in_img : npx, lvl0 + k * od.level_stride,
                                           npx, od.wa, od.h, fwk, taps, n, dk ? ds : nullptr,
                                           dk ? dsw : 0, dk ? dsh : 0, dk ? ds_stride : 0, st,
-                                          (ctx->debug_flags & SGPU_DEBUG_GAUSS_WAVE)
-                                              ? (ctx->debug_flags >> 16) : -1));
+                                          (ctx->debug_flags & SGPU_DEBUG_GAUSS_BLOCK)
+                                              ? -1 : (ctx->debug_flags >> 16)));
         }
     }
     HIPCHK(ctx, hipEventRecord(pt.ev[1], st));

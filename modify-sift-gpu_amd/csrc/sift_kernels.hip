@@ -290,8 +290,15 @@ __global__ __launch_bounds__(256) void k_gauss_wave(
     constexpr int IN_W = SW + FW - 1 + OFF;           // input columns held per row
     constexpr int NQ = (IN_W + 3) / 4;                // aligned quads per row
     constexpr int NRD = (FW + 3) / 2;                 // ds_read_b128 per H-pass lane
-    constexpr int IN_S = (SW + FW + 3 + OFF + 3) & ~3;   // float2 per row pair
-    static_assert(4 * NQ <= IN_S, "quad stores stay inside the row pair");
+    // LDS layout of a row pair: input column a0 + j at float2 index j + SH, SH = OFF & 1, so
+    // that every H-pass read (index 4 l + OFF + SH + 2 q) is a 16-byte aligned ds_read_b128; the
+    // row-pair stride is = 2 (mod 32) float2, so that the 16 lanes of one row pair and the lanes
+    // of the next one fill disjoint 16-byte bank slots (ds_read_b128 lane groups, LDS table of
+    // MI355X_MICROARCH.md): measured 2-way bank conflicts with the plain stride
+    constexpr int SH = OFF & 1;
+    constexpr int IN_S0 = (4 * NQ + SH + 3) & ~3;
+    constexpr int IN_S = IN_S0 + ((2 - IN_S0) & 31);  // float2 per row pair
+    static_assert(IN_S % 32 == 2 && 4 * NQ + SH <= IN_S, "row-pair stride");
     constexpr int LAG = (FW - 1 + WCH - 1) / WCH;     // chunks between H and V of a row
     constexpr int RS0 = WCH * (LAG + 1);
     constexpr int RS = RS0 <= 32 ? 32 : 64;           // ring rows (power of two)
@@ -389,9 +396,14 @@ __global__ __launch_bounds__(256) void k_gauss_wave(
                     u0[t] = left ? r0[0] : (right ? r0[3] : r0[t]);
                     u1[t] = left ? r1[0] : (right ? r1[3] : r1[t]);
                 }
-                float4* q = reinterpret_cast<float4*>(&s_in[real ? p * IN_S + 4 * j : NPAIR * IN_S]);
-                q[0] = make_float4(u0[0], u1[0], u0[1], u1[1]);
-                q[1] = make_float4(u0[2], u1[2], u0[3], u1[3]);
+                f2v* q = &s_in[real ? p * IN_S + 4 * j + SH : NPAIR * IN_S];
+                if (SH == 0) {
+                    reinterpret_cast<float4*>(q)[0] = make_float4(u0[0], u1[0], u0[1], u1[1]);
+                    reinterpret_cast<float4*>(q)[1] = make_float4(u0[2], u1[2], u0[3], u1[3]);
+                } else {   // 8-byte aligned
+#pragma unroll
+                    for (int t = 0; t < 4; t++) q[t] = f2v{u0[t], u1[t]};
+                }
             }
         }
     };
@@ -418,18 +430,15 @@ __global__ __launch_bounds__(256) void k_gauss_wave(
         f2v* s_in = s_in_all[NW == 1 ? wave : par];
         f2v* s_in_next = s_in_all[NW == 1 ? wave : 1 - par];
         {   // H pass of input chunk c -> ring rows c*WCH .. c*WCH+7
-            const f2v* rowp = &s_in[hp * IN_S + hc + OFF + (NW == 1 ? 0 : GT * wave)];
+            const f2v* rowp = &s_in[hp * IN_S + hc + OFF + SH + (NW == 1 ? 0 : GT * wave)];
             f2v a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};   // columns hc+i
 #pragma unroll
             for (int q = 0; q < NRD; q++) {
                 f2v e[2];                            // pair columns hc+2q, hc+2q+1
-                if (OFF % 2 == 0) {
+                {
                     const float4 v = reinterpret_cast<const float4*>(rowp)[q];
                     e[0] = f2v{v.x, v.y};
                     e[1] = f2v{v.z, v.w};
-                } else {
-                    e[0] = rowp[2 * q];
-                    e[1] = rowp[2 * q + 1];
                 }
 #pragma unroll
                 for (int u = 0; u < 2; u++) {

@@ -15,7 +15,7 @@ from sift_synth import synth_batch, synth_image
 
 pytestmark = pytest.mark.gpu
 
-WAVE = sgpu.SiftContext.DEBUG_GAUSS_WAVE
+BLOCK = sgpu.SiftContext.DEBUG_GAUSS_BLOCK
 
 
 def _bits(a):
@@ -30,10 +30,11 @@ def _levels(ctx, image, opts):
 
 @pytest.mark.parametrize("w,h,seed", [(16, 16, 3), (203, 97, 2), (640, 480, 1000)])
 def test_wave_levels_vs_oracle(gpu_ctx, w, h, seed):
+    """The shipped kernel (k_gauss_wave) against the oracle, every level of every octave."""
     img = synth_image(w, h, seed)
     opts = default_options()
     gpu_ctx.set_options(opts)
-    gpu_ctx.set_debug_flags(WAVE)
+    gpu_ctx.set_debug_flags(0)
     try:
         gpu_ctx.extract(img)
         for o in range(len(gpu_ctx.geometry())):
@@ -53,11 +54,11 @@ def test_wave_levels_equal_block_kernel(gpu_ctx, rows, n, w, h):
     imgs = synth_batch(n, w, h, 40 + w % 7)
     opts = default_options()
     gpu_ctx.set_options(opts)
-    gpu_ctx.set_debug_flags(0)
+    gpu_ctx.set_debug_flags(BLOCK)
     gpu_ctx.extract(imgs)
     ref = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
     k_ref = [gpu_ctx.features(i)[0].copy() for i in range(n)]
-    gpu_ctx.set_debug_flags(WAVE | (rows << 16))
+    gpu_ctx.set_debug_flags(rows << 16)
     try:
         gpu_ctx.extract(imgs)
         got = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
@@ -72,12 +73,13 @@ def test_wave_levels_equal_block_kernel(gpu_ctx, rows, n, w, h):
 
 
 @pytest.mark.parametrize("fo", [1, -1])
-def test_wave_first_octave_float_path(gpu_ctx, fo):
-    """-fo != 0 feeds the first level from an f32 buffer (the resampled input)."""
+def test_block_first_octave_float_path(gpu_ctx, fo):
+    """-fo != 0 feeds the first level from an f32 buffer (the resampled input); the block kernel
+    (the wave kernel runs this case in test_gpu_parity.py::test_first_octave_levels_bitwise)."""
     img = synth_image(321, 241, 17 + fo)
     opts = default_options(octave_min=fo)
     gpu_ctx.set_options(opts)
-    gpu_ctx.set_debug_flags(WAVE)
+    gpu_ctx.set_debug_flags(BLOCK)
     try:
         gpu_ctx.extract(img)
         for o in range(min(len(gpu_ctx.geometry()), 2)):
