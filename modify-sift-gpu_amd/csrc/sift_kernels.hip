@@ -278,8 +278,16 @@ struct GaussWaveGrid {
     int strips_x, nsy, rows_per_band, total_waves;
 };
 
+#ifndef SGK_GW_WPB
+#define SGK_GW_WPB 4
+#endif
+#ifndef SGK_GW_HSPAD
+#define SGK_GW_HSPAD 4
+#endif
+constexpr int kGwWaves = SGK_GW_WPB;   // waves per workgroup of k_gauss_wave
+
 template <int FW, bool U8, int NW>
-__global__ __launch_bounds__(256) void k_gauss_wave(
+__global__ __launch_bounds__(64 * kGwWaves) void k_gauss_wave(
     const float* __restrict__ src, const uint8_t* __restrict__ src8, int src_stride,
     long long src_img_stride, float* __restrict__ dst, long long dst_img_stride, int W, int H,
     Taps taps, float* __restrict__ ds, int dsw, int dsh, long long ds_img_stride,
@@ -303,26 +311,34 @@ __global__ __launch_bounds__(256) void k_gauss_wave(
     constexpr int RS0 = WCH * (LAG + 1);
     constexpr int RS = RS0 <= 32 ? 32 : 64;           // ring rows (power of two)
     static_assert(RS0 <= RS, "ring holds the lag");
-    constexpr int HS = GT + 4;                        // ring row stride (floats)
+    constexpr int HS = GT + SGK_GW_HSPAD;             // ring row stride (floats)
     constexpr int NPAIR = WCH / 2;
     constexpr int NLD = (NPAIR * NQ + 64 * NW - 1) / (64 * NW);   // staged quads per lane
 #ifndef SGK_GW_NST
 #define SGK_GW_NST 4
 #endif
     constexpr int NST = SGK_GW_NST;                   // chunks in registers (loads NST-1 ahead)
-    static_assert(NW == 1 || NW == 4, "one strip per wave, or one per 4-wave workgroup");
+    static_assert(NW == 1 || NW == kGwWaves, "one strip per wave, or one per workgroup");
     static_assert(NW == 1 || NST % 2 == 0, "shared input buffers alternate by step parity");
     // NW == 1: a wave-private row-pair buffer per wave; NW > 1: the NW waves of a workgroup
     // share one double-buffered buffer of their NW * 64 columns
-    constexpr int NBUF = NW == 1 ? 4 : 2;
+    constexpr int NBUF = NW == 1 ? kGwWaves : 2;
     __shared__ __attribute__((aligned(16))) f2v s_in_all[NBUF][NPAIR * IN_S + 4];   // + pad slot
-    __shared__ __attribute__((aligned(16))) float s_h_all[4][RS * HS];
+    __shared__ __attribute__((aligned(16))) float s_h_all[kGwWaves][RS * HS];
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int ld = NW == 1 ? lane : threadIdx.x;     // index among the strip's loaders
     int sx, rest, x0, xs;                            // xs: first column of the loaded strip
     if (NW == 1) {
-        const int gw = blockIdx.x * 4 + wave;
+        // XCD-aware order: blocks are dealt round-robin over the 8 XCDs (observed placement;
+        // speed only), so logical block (xcd, k) -> xcd * q + k keeps neighbouring strips and
+        // their column halos in one L2 (pyramid 3.80-3.84 -> 3.76-3.79 ms)
+        int bid = blockIdx.x;
+        {
+            const int nb = gridDim.x, q = nb / 8, r = nb % 8, xcd = bid % 8, k = bid / 8;
+            bid = xcd < r ? xcd * (q + 1) + k : r * (q + 1) + (xcd - r) * q + k;
+        }
+        const int gw = bid * kGwWaves + wave;
         if (gw >= gg.total_waves) return;             // uniform per wave
         sx = gw % gg.strips_x;
         rest = gw / gg.strips_x;
@@ -540,13 +556,13 @@ hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
 #endif
         constexpr int NW = SGK_GW_NW;
         const GaussWaveGrid gg = gauss_wave_grid(w, h, batch, wave_rows, NW);
-        const dim3 wgrid((unsigned)((gg.total_waves + 3) / 4));
+        const dim3 wgrid((unsigned)((gg.total_waves + kGwWaves - 1) / kGwWaves));
         if (src8)
-            hipLaunchKernelGGL((k_gauss_wave<FW, true, NW>), wgrid, dim3(256), 0, stream, src,
+            hipLaunchKernelGGL((k_gauss_wave<FW, true, NW>), wgrid, dim3(64 * kGwWaves), 0, stream, src,
                                src8, src_stride, src_img_stride, dst, dst_img_stride, w, h, taps,
                                ds, dsw, dsh, ds_img_stride, gg);
         else
-            hipLaunchKernelGGL((k_gauss_wave<FW, false, NW>), wgrid, dim3(256), 0, stream, src,
+            hipLaunchKernelGGL((k_gauss_wave<FW, false, NW>), wgrid, dim3(64 * kGwWaves), 0, stream, src,
                                src8, src_stride, src_img_stride, dst, dst_img_stride, w, h, taps,
                                ds, dsw, dsh, ds_img_stride, gg);
         return hipGetLastError();
