@@ -272,6 +272,14 @@ __global__ __launch_bounds__(256) void k_gauss_pk2(
 // LDS ops of one wave execute in issue order, so a wave needs no barrier between writing a
 // buffer and reading what other lanes wrote; the empty asm statements only stop the compiler
 // from moving LDS accesses across the phase boundaries.
+// XCD-aware block order: blocks are dealt round-robin over the 8 XCDs (observed placement,
+// MI355X_MICROARCH.md; speed only, never correctness), so logical block xcd * q + k runs on XCD
+// xcd and a run of consecutive logical blocks -- neighbouring image regions -- shares one L2.
+__device__ __forceinline__ int xcd_block(int bid, int nb) {
+    const int q = nb / 8, r = nb % 8, xcd = bid % 8, k = bid / 8;
+    return xcd < r ? xcd * (q + 1) + k : r * (q + 1) + (xcd - r) * q + k;
+}
+
 constexpr int WCH = 8;   // rows per chunk (wave kernel)
 
 struct GaussWaveGrid {
@@ -333,12 +341,7 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_wave(
         // XCD-aware order: blocks are dealt round-robin over the 8 XCDs (observed placement;
         // speed only), so logical block (xcd, k) -> xcd * q + k keeps neighbouring strips and
         // their column halos in one L2 (pyramid 3.80-3.84 -> 3.76-3.79 ms)
-        int bid = blockIdx.x;
-        {
-            const int nb = gridDim.x, q = nb / 8, r = nb % 8, xcd = bid % 8, k = bid / 8;
-            bid = xcd < r ? xcd * (q + 1) + k : r * (q + 1) + (xcd - r) * q + k;
-        }
-        const int gw = bid * kGwWaves + wave;
+        const int gw = xcd_block(blockIdx.x, gridDim.x) * kGwWaves + wave;
         if (gw >= gg.total_waves) return;             // uniform per wave
         sx = gw % gg.strips_x;
         rest = gw / gg.strips_x;
