@@ -228,10 +228,25 @@ def main():
         },
     }
 
+    # SURVEY.md §8(d), "full detection (reported separately)": the reference's detection traffic
+    # B_det = 168 B per octave pixel (pyramid 48 + DoG 60 + gradient writes 24 + extremum reads
+    # 36) over this build's pyramid + extremum time.  This build never stores the DoG or gradient
+    # images, so the figure is a reference-equivalent rate, not bytes this build moves.
+    det_ms = stage_acc.get("pyramid", 0.0) + stage_acc.get("detect", 0.0)
+    if det_ms > 0:
+        det_bytes = 168.0 * sumN * B * args.steps
+        result["full_detection"] = {
+            "bytes_per_image": 168.0 * sumN,
+            "ms_per_step": det_ms / args.steps,
+            "reference_equivalent_GBps": det_bytes / (det_ms * 1e-3) / 1e9,
+            # above 1: the reference's intermediate images are neither written nor read here
+            "reference_equivalent_frac": det_bytes / (det_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "note": "168 B x sum(N) per image (SURVEY.md 8d) over pyramid + extremum time; "
+                    "DoG and gradient images are never stored here"}
     if rank == 0 and world == 1 and not args.no_match:
-        result["match"] = bench_match(ctx, args.match_n)
+        result["match"] = bench_match(ctx, args.match_n, cpu=not args.no_cpu_baseline)
     if rank == 0 and world == 1 and args.workload == "c3" and not args.no_c4:
-        result["c4"] = bench_c4(ctx)
+        result["c4"] = bench_c4(ctx, cpu=not args.no_cpu_baseline)
     if rank == 0 and world == 1 and args.workload == "c3" and not args.no_e2e:
         result["end_to_end"] = bench_end_to_end(ctx, imgs, B, W, H)
     if world > 1 and not args.no_match:
@@ -266,7 +281,7 @@ def profiled_traffic(B, W, H, octaves):
     return None, "no profile summary committed"
 
 
-def bench_match(ctx, n):
+def bench_match(ctx, n, cpu=True):
     """Config C5: n x n SiftMatch (u8 dot products on i8 MFMA + fused top-2), mutual best."""
     d1 = synth_descriptors(n, 5000)
     d2 = synth_descriptors(n, 5001, base=d1, n_dup=min(20000, n // 2))
@@ -295,7 +310,7 @@ def bench_match(ctx, n):
         gm = ctx.match_guided(g1, g2, l1, l2, H, F)
         gms += ctx.timing()["match"]
     gms /= reps
-    return {"workload": f"C5 {n}x{n} u8 descriptors, mutual best match",
+    out = {"workload": f"C5 {n}x{n} u8 descriptors, mutual best match",
             "ms": ms, "matches": int(len(m)),
             "path": "two i8-MFMA GEMMs (row side, then the sets swapped for the column side)",
             "ops": ops, "ops_note": "F = 2*128*N1*N2 counted once (SURVEY.md 8d)",
@@ -304,9 +319,25 @@ def bench_match(ctx, n):
             "fused_ms": fms, "fused_matches": int(len(fm)),
             "fused_mfma_util": ops / (fms * 1e-3) / 1e12 / I8_MFMA_PEAK_TOPS,
             "guided_ms": gms, "guided_matches": int(len(gm))}
+    if cpu:
+        # the oracle's row side (exact int32 dots + running top-2),
+        # row-blocked over OpenMP threads; the mutual match needs both sides, so the full-size
+        # time is 2 x the measured row side
+        import oracle_py
+        threads = max(1, min(16, os.cpu_count() or 1))
+        rows = n   # the whole row side (about 1 s on 16 cores); the column side is symmetric
+        secs = oracle_py.bench_match_rows(q1, rows, q2, threads)
+        full_ms = 2.0 * (n / rows) * secs * 1e3
+        out["cpu_baseline"] = {"value": full_ms, "unit": f"ms per {n}x{n} mutual match",
+                               "cores": threads, "kind": "port",
+                               "sample": f"row side of {rows} of the {n} rows against all {n} "
+                                         f"columns (oracle/liboracle.so, g++ -O3), "
+                                         f"{secs:.2f} s, extrapolated to both sides",
+                               "gpu_speedup": full_ms / ms}
+    return out
 
 
-def bench_c4(ctx, batch=8, steps=3):
+def bench_c4(ctx, batch=8, steps=3, cpu=True):
     """BASELINE configs[3]: 4096x4096 tiles, -no 6 (the HBM-bound pyramid stress), a batch of
     `batch` distinct tiles (seeds 4000..) staged in HBM, `steps` timed passes after one warm-up.
     Roofline of the pyramid stage as for the headline: 48 B per octave pixel, sum N = 22,364,160
@@ -330,7 +361,7 @@ def bench_c4(ctx, batch=8, steps=3):
         sumN = geometry_sum(4096, 4096, 6)
         n_gauss = 1 + 6 * 5
         achieved = 48.0 * sumN * batch * steps / (pyr * 1e-3) / 1e9
-        return {"workload": f"C4: {batch} x 4096x4096 u8 tiles per step, -fo 0 -no 6 -d 3, "
+        out = {"workload": f"C4: {batch} x 4096x4096 u8 tiles per step, -fo 0 -no 6 -d 3, "
                             f"staged in HBM", "value": batch * steps / el, "unit": "images/s",
                 "ms_per_step": el / steps * 1e3, "features_per_image": feats / (batch * steps),
                 "stage_ms_per_step": {k: v / steps for k, v in st.items() if k != "match"},
@@ -339,6 +370,17 @@ def bench_c4(ctx, batch=8, steps=3):
                              "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                              "algorithmic_bytes_per_launch": 48.0 * sumN * batch / n_gauss,
                              "avg_launch_ms": pyr / steps / n_gauss}}
+        if cpu:
+            # the oracle on the same tiles, one per OpenMP thread
+            import oracle_py
+            threads = max(1, min(batch, os.cpu_count() or 1))
+            secs, cf = oracle_py.bench_extract(imgs[:threads], opts, threads=threads)
+            out["cpu_baseline"] = {"value": threads / secs, "unit": "images/s", "cores": threads,
+                                   "kind": "port",
+                                   "sample": f"{threads} of the staged 4096x4096 tiles (-no 6), "
+                                             f"one per OpenMP thread, oracle/liboracle.so",
+                                   "features_per_image": cf / threads}
+        return out
     finally:
         c4.close()
 

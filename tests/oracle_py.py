@@ -84,6 +84,10 @@ def lib():
                                            ctypes.c_int, ctypes.c_int, P(SgpuOptions),
                                            ctypes.c_int, P(ctypes.c_longlong)]
         L.oracle_bench_extract.restype = ctypes.c_double
+        L.oracle_bench_match_rows.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.c_int, ctypes.c_int,
+                                              ctypes.POINTER(ctypes.c_longlong)]
+        L.oracle_bench_match_rows.restype = ctypes.c_double
         _LIB = L
     return _LIB
 
@@ -252,6 +256,17 @@ def bench_extract(images: np.ndarray, opts=None, threads=1):
     secs = lib().oracle_bench_extract(images.ctypes.data, n, w, h, w, ctypes.byref(opts),
                                       threads, ctypes.byref(feats))
     return secs, feats.value
+
+
+def bench_match_rows(d1: np.ndarray, rows: int, d2: np.ndarray, threads=1):
+    """Wall seconds of the matcher's row side (exact u8 dots + running top-2) for the first
+    `rows` rows of d1 against all of d2, row-blocked over `threads` OpenMP threads."""
+    d1 = np.ascontiguousarray(d1, np.uint8)
+    d2 = np.ascontiguousarray(d2, np.uint8)
+    cs = ctypes.c_longlong(0)
+    secs = lib().oracle_bench_match_rows(d1.ctypes.data, rows, d2.ctypes.data, d2.shape[0],
+                                         threads, ctypes.byref(cs))
+    return secs
 
 
 def save_sift(path, keys, desc, binary=False, normalized=True):
