@@ -403,7 +403,8 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
                       ? std::max<size_t>(pt.cand_cap, 64)
                       : std::max(pt.cand_cap, std::max<size_t>(1024, sum_px / 256 * n));
     const size_t nc = pt.cand_cap, ne_cap = 2 * nc;
-    ALLOCCHK(ctx, pt.pyr.ensure((size_t)goff * sizeof(float)));
+    // + 256 B: the descriptor's vector loads may read a few floats past a plane's last row
+    ALLOCCHK(ctx, pt.pyr.ensure((size_t)goff * sizeof(float) + 256));
     ALLOCCHK(ctx, pt.mask.ensure((size_t)moff * sizeof(uint32_t)));
     ALLOCCHK(ctx, pt.row_count.ensure((size_t)pt.total_rows * sizeof(uint32_t)));
     ALLOCCHK(ctx, pt.row_base.ensure(((size_t)pt.total_rows + 1) * sizeof(uint32_t)));

@@ -1701,41 +1701,48 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
     const char* gb = reinterpret_cast<const char*>(g);
     typedef float f4v __attribute__((ext_vector_type(4)));
     auto ld4 = [&](uint32_t b) { return *reinterpret_cast<const f4v*>(gb + b); };
-    auto ld1 = [&](uint32_t b) { return *reinterpret_cast<const float*>(gb + b); };
-    if (ncols > 0)
-        for (int r = sub; r < nrows; r += 4) {
-            int lo, len;
+    // The strips are walked as one flat sequence with the next strip's 4 loads issued before the
+    // current strip's samples (software pipelining: a strip's gathers overlap the previous
+    // strip's arithmetic).  The loads are unconditional 16-byte loads: at the right edge a strip
+    // may read up to 4 floats past the row end, which are the next row's (a sample is at most in
+    // column W-2 and row H-2) and feed no valid sample; past the last strip a lane re-reads its
+    // last strip.
+    int r = sub, c = 0, lo = 0, len = 0;
+    auto next_row = [&]() {   // advance r (by 4) to the next row with a non-empty span
+        for (; r < nrows; r += 4) {
             row_span(r, lo, len);
-            const float dy = (ymin + (float)r) - pty;
-            const int y = iymin + r;
-            for (int c = lo; c < lo + len; c += 4) {
-                const int x = ixmin + c;   // first sample's column, in [1, W-2]
-                const uint32_t po = 4u * (uint32_t)(y * W + x);
-                f4v a, b, up, dn;
-                if (x + 4 <= W - 1) {
-                    a = ld4(po - 4u);            // x-1 .. x+2
-                    b = ld4(po + 4u);            // x+1 .. x+4
-                    up = ld4(po - 4u * W);       // row y-1, x .. x+3
-                    dn = ld4(po + 4u * W);       // row y+1, x .. x+3
-                } else {
-                    // the strip reaches the last column: element loads clamped to the row
-                    // (only the samples inside the span are used)
-                    auto cl = [&](int k) { return 4u * (uint32_t)(y * W + min(x + k, W - 1)); };
-                    a = f4v{ld1(cl(-1)), ld1(cl(0)), ld1(cl(1)), ld1(cl(2))};
-                    b = f4v{ld1(cl(1)), ld1(cl(2)), ld1(cl(3)), ld1(cl(4))};
-                    up = f4v{ld1(cl(0) - 4u * W), ld1(cl(1) - 4u * W), ld1(cl(2) - 4u * W),
-                             ld1(cl(3) - 4u * W)};
-                    dn = f4v{ld1(cl(0) + 4u * W), ld1(cl(1) + 4u * W), ld1(cl(2) + 4u * W),
-                             ld1(cl(3) + 4u * W)};
-                }
-                const int nv = lo + len - c;   // samples of this strip inside the span
-                const float dx0 = (xmin + (float)c) - ptx;
-                sample(dx0, dy, b.x - a.x, dn.x - up.x, true);
-                sample(dx0 + 1.0f, dy, b.y - a.y, dn.y - up.y, nv > 1);
-                sample(dx0 + 2.0f, dy, b.z - a.z, dn.z - up.z, nv > 2);
-                sample(dx0 + 3.0f, dy, b.w - a.w, dn.w - up.w, nv > 3);
-            }
+            if (len > 0) break;
         }
+    };
+    if (ncols > 0) next_row(); else r = nrows;
+    c = lo;
+    f4v na, nb, nu, nd;
+    uint32_t npo = 4u * (uint32_t)(iymin * W + ixmin);   // a valid address when nothing is left
+    auto fetch = [&]() {
+        if (r < nrows) npo = 4u * (uint32_t)((iymin + r) * W + ixmin + c);
+        na = ld4(npo - 4u);            // x-1 .. x+2
+        nb = ld4(npo + 4u);            // x+1 .. x+4
+        nu = ld4(npo - 4u * W);        // row y-1, x .. x+3
+        nd = ld4(npo + 4u * W);        // row y+1, x .. x+3
+    };
+    fetch();
+    while (r < nrows) {
+        const f4v a = na, b = nb, up = nu, dn = nd;
+        const float dy = (ymin + (float)r) - pty;
+        const int nv = lo + len - c;   // samples of this strip inside the span
+        const float dx0 = (xmin + (float)c) - ptx;
+        c += 4;
+        if (c >= lo + len) {
+            r += 4;
+            next_row();
+            c = lo;
+        }
+        fetch();
+        sample(dx0, dy, b.x - a.x, dn.x - up.x, true);
+        sample(dx0 + 1.0f, dy, b.y - a.y, dn.y - up.y, nv > 1);
+        sample(dx0 + 2.0f, dy, b.z - a.z, dn.z - up.z, nv > 2);
+        sample(dx0 + 3.0f, dy, b.w - a.w, dn.w - up.w, nv > 3);
+    }
 #pragma unroll
     for (int k = 0; k < 8; k++) acc[k] = quad_sum(acc[k]);
     // lane sub owns bins 2 sub, 2 sub + 1 of its cell
