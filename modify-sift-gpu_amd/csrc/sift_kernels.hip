@@ -760,27 +760,37 @@ __global__ __launch_bounds__(256, SGK_EXT2_WAVES) void k_extrema_wave2(const flo
     // complete in issue order, but the compiler sees only per-lane addresses (a lane writes
     // column lane + 1 and reads lane .. lane + 2) and may reorder them: the empty asm
     // statements keep every write before the reads that follow it.
-    auto put = [&](const Row& r, int y) {   // DoG row y into the ring
+    // DoG row y into the ring (read by key_test for the rare candidates) and into dog[] (the
+    // row max/min below take the neighbours' values by DPP wave shifts, not from LDS)
+    float dog[ND];
+    auto put = [&](const Row& r, int y) {
         float* rr = &ring[0][y & 3][lane + 1];
 #pragma unroll
-        for (int m = 0; m < ND; m++) rr[m * 4 * RW] = r.m[m + 1] - r.m[m];
+        for (int m = 0; m < ND; m++) {
+            dog[m] = r.m[m + 1] - r.m[m];
+            rr[m * 4 * RW] = dog[m];
+        }
         asm volatile("" ::: "memory");
     };
-    // rolling 3-wide row max/min of DoG rows y-1 and y (per plane), refreshed per step
+    // rolling 3-wide row max/min of DoG rows y-1 and y (per plane), refreshed per step; lanes 0
+    // and 63 get a neighbour from outside the wave (0) and are never tested
     float hx0[ND], hn0[ND], hx1[ND], hn1[ND], cvx[ND];
-    auto rowmm = [&](int y, float* mx, float* mn, float* cv) {
+    auto rowmm = [&](float* mx, float* mn, float* cv) {   // of the row in dog[]
 #pragma unroll
         for (int m = 0; m < ND; m++) {
-            const float* p = &ring[m][y & 3][lane];
-            const float a = p[0], c = p[1], e = p[2];
+            const float c = dog[m];
+            const float a = __int_as_float(__builtin_amdgcn_update_dpp(
+                0, __float_as_int(c), 0x138, 0xf, 0xf, false));   // wave_shr:1, lane - 1
+            const float e = __int_as_float(__builtin_amdgcn_update_dpp(
+                0, __float_as_int(c), 0x130, 0xf, 0xf, false));   // wave_shl:1, lane + 1
             mx[m] = fmax_(fmax_(a, c), e);
             mn[m] = fmin_(fmin_(a, c), e);
             if (cv) cv[m] = c;
         }
     };
-    auto body = [&](int y) {   // test row y: DoG rows y-1, y, y+1 are in the ring
+    auto body = [&](int y) {   // test row y: DoG rows y-1, y are rolled, y+1 is in dog[]
         float hx2[ND], hn2[ND], cnx[ND];
-        rowmm(y + 1, hx2, hn2, cnx);
+        rowmm(hx2, hn2, cnx);
         const bool interior = out_lane && y < ye && y > 0 && y < H - 1;
         int ncand = 0;
 #pragma unroll
@@ -828,12 +838,12 @@ __global__ __launch_bounds__(256, SGK_EXT2_WAVES) void k_extrema_wave2(const flo
     };
     fetch(rA, ys - 1);
     put(rA, ys - 1);
+    rowmm(hx0, hn0, nullptr);
     fetch(rA, ys);
     put(rA, ys);
+    rowmm(hx1, hn1, cvx);
     fetch(rA, ys + 1);
     fetch(rB, ys + 2);
-    rowmm(ys - 1, hx0, hn0, nullptr);
-    rowmm(ys, hx1, hn1, cvx);
     // each set is refetched after the row test that follows its put: the test's atomics (a
     // data-dependent number of them) then come before, not after, the loads that the next wait
     // must leave in flight
