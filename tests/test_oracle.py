@@ -518,3 +518,28 @@ def test_first_octave_plan(w, h, fo, maxd, prep, want):
     out = np.zeros(4, np.int32)
     O.lib().oracle_plan(w, h, fo, maxd, prep, out.ctypes.data)
     assert tuple(out) == want
+
+
+def test_cpu_match_baseline_row_side():
+    """bench.py's C5 CPU baseline (oracle_bench_match_rows): exact u8 dots with the reference's
+    running top-2 from (0, -1, 0) (ProgramCU.cu:1785-1841), checked through its checksum."""
+    d1 = quantize(synth_descriptors(300, 77))
+    d2 = quantize(synth_descriptors(500, 78, base=d1, n_dup=100))
+    rows = 200
+    cs = ctypes.c_longlong(0)
+    a = np.ascontiguousarray(d1)
+    b = np.ascontiguousarray(d2)
+    secs = O.lib().oracle_bench_match_rows(a.ctypes.data, rows, b.ctypes.data, b.shape[0], 2,
+                                           ctypes.byref(cs))
+    assert secs >= 0.0
+    dots = a[:rows].astype(np.int64) @ b.astype(np.int64).T
+    want = 0
+    for i in range(rows):
+        best, second, idx = 0, 0, -1
+        for j, v in enumerate(dots[i]):
+            if v > best:
+                second, best, idx = best, v, j
+            elif v > second:
+                second = v
+        want += idx + (int(second) & 1)
+    assert cs.value == want
