@@ -857,156 +857,6 @@ __global__ __launch_bounds__(256, SGK_EXT2_WAVES) void k_extrema_wave2(const flo
     }
 }
 
-// Extremum detection, two columns per lane (k_extrema_wave3): k_extrema_wave2's walk with every
-// lane holding two adjacent columns, fetched as one 8-byte load per plane.  The one-column form
-// is texture-address bound (TA busy ~88 %: a 4-byte load per lane and plane); here a wave covers
-// a 128-column window (124 tested columns, two feed columns each side) with half the load
-// instructions per pixel.  Same decisions as k_extrema_wave2.
-template <int ND>   // ND = number of DoG planes = d + 2
-__global__ __launch_bounds__(256) void k_extrema_wave3(const float* __restrict__ pyr,
-                                                       uint32_t* __restrict__ mask,
-                                                       uint32_t* __restrict__ row_count,
-                                                       const FeatureParams fp,
-                                                       const ExtremaWaveGrid eg) {
-    constexpr int RW = 132;                         // ring row: window column c at c + 2
-    constexpr int NJ = ND - 2;
-    __shared__ __attribute__((aligned(8))) float s_ring[4][ND][4][RW];
-    __shared__ uint16_t s_list[4][NJ * 128];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int gw = blockIdx.x * 4 + wave;
-    if (gw >= eg.wave0[fp.n_octaves]) return;       // uniform per wave
-    int o = 0;
-    while (o + 1 < fp.n_octaves && gw >= eg.wave0[o + 1]) o++;
-    o = __builtin_amdgcn_readfirstlane(o);          // scalar octave fields (k_extrema_wave2)
-    const OctaveDesc& od = fp.oct[o];
-    const long long mask_off = od.mask_off, mask_lstride = od.mask_level_stride;
-    const int nwords = od.nwords;
-    const long long rc_base = fp.row_off[o];
-    const int W = od.wa, H = od.h;
-    const int strips_x = (W + 123) / 124;
-    const int id = gw - eg.wave0[o];
-    const int sx = id % strips_x, rest = id / strips_x;
-    const int sg = rest % eg.nseg[o], b = rest / eg.nseg[o];
-    const int xw = sx * 124 - 2;                    // image column of window column 0
-    const int ys = sg * eg.seg_rows[o], ye = min(H, ys + eg.seg_rows[o]);
-    const long long lstride = od.level_stride;
-    const float* g0 = pyr + od.gauss_off + (long long)b * W * H;
-    float(*ring)[4][RW] = s_ring[wave];
-    uint16_t* list = s_list[wave];
-
-    // this lane's columns: window 2 lane, 2 lane + 1 (image xw + 2 lane + {0, 1}); W is a multiple
-    // of 4, so a pair is entirely inside or entirely right of the image (then it repeats the last
-    // pair: such columns are never tested nor the neighbour of a tested one)
-    const int xa = xw + 2 * lane;
-    const int gx = clampi(xa, 0, W - 2);
-    const bool lane_in = lane >= 1 && lane <= 62;
-    const bool test0 = lane_in && xa > 0 && xa < W - 1;
-    const bool test1 = lane_in && xa + 1 > 0 && xa + 1 < W - 1;
-    struct Row { float2 m[ND + 1]; };
-    Row rA, rB;
-    auto fetch = [&](Row& r, int y) {
-        const float* q = g0 + (long long)clampi(y, 0, H - 1) * W + gx;
-#pragma unroll
-        for (int m = 0; m <= ND; m++) r.m[m] = *reinterpret_cast<const float2*>(q + m * lstride);
-    };
-    float d0[ND], d1[ND];   // DoG of the latest row put, columns 2 lane and 2 lane + 1
-    auto put = [&](const Row& r, int y) {
-        float* rr = &ring[0][y & 3][2 * lane + 2];
-#pragma unroll
-        for (int m = 0; m < ND; m++) {
-            d0[m] = r.m[m + 1].x - r.m[m].x;
-            d1[m] = r.m[m + 1].y - r.m[m].y;
-            *reinterpret_cast<float2*>(&rr[m * 4 * RW]) = make_float2(d0[m], d1[m]);
-        }
-        asm volatile("" ::: "memory");
-    };
-    float hx0[2][ND], hn0[2][ND], hx1[2][ND], hn1[2][ND], cvx[2][ND];
-    auto rowmm = [&](float (*mx)[ND], float (*mn)[ND], float (*cv)[ND]) {
-#pragma unroll
-        for (int m = 0; m < ND; m++) {
-            const float l = __int_as_float(__builtin_amdgcn_update_dpp(
-                0, __float_as_int(d1[m]), 0x138, 0xf, 0xf, false));   // lane - 1's right column
-            const float r = __int_as_float(__builtin_amdgcn_update_dpp(
-                0, __float_as_int(d0[m]), 0x130, 0xf, 0xf, false));   // lane + 1's left column
-            mx[0][m] = fmax_(fmax_(l, d0[m]), d1[m]);
-            mn[0][m] = fmin_(fmin_(l, d0[m]), d1[m]);
-            mx[1][m] = fmax_(fmax_(d0[m], d1[m]), r);
-            mn[1][m] = fmin_(fmin_(d0[m], d1[m]), r);
-            if (cv) { cv[0][m] = d0[m]; cv[1][m] = d1[m]; }
-        }
-    };
-    auto body = [&](int y) {   // test row y: DoG rows y-1, y are rolled, y+1 is in d0/d1
-        float hx2[2][ND], hn2[2][ND], cnx[2][ND];
-        rowmm(hx2, hn2, cnx);
-        const bool row_ok = y < ye && y > 0 && y < H - 1;
-        int ncand = 0;
-#pragma unroll
-        for (int j = 0; j < NJ; j++) {
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const float v = cvx[h][j + 1];
-                float mx = hx0[h][j], mn = hn0[h][j];
-#pragma unroll
-                for (int m = j; m < j + 3; m++) {
-                    mx = fmax_(mx, fmax_(fmax_(hx0[h][m], hx1[h][m]), hx2[h][m]));
-                    mn = fmin_(mn, fmin_(fmin_(hn0[h][m], hn1[h][m]), hn2[h][m]));
-                }
-                const bool cand = row_ok && (h ? test1 : test0) && fabs_(v) > fp.t0 &&
-                                  (v >= mx || v <= mn);
-                const unsigned long long bal = __ballot(cand);
-                if (cand) {
-                    const int pos = ncand + __builtin_amdgcn_mbcnt_hi(
-                                                (uint32_t)(bal >> 32),
-                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    list[pos] = (uint16_t)((j << 7) | (2 * lane + h));
-                }
-                ncand += __popcll(bal);
-            }
-        }
-        asm volatile("" ::: "memory");
-        for (int c0 = 0; c0 < ncand; c0 += 64) {
-            if (c0 + lane < ncand) {
-                const int code = list[c0 + lane];
-                const int j = code >> 7, cl = code & 127;
-                auto get = [&](int m, int r, int c) { return ring[j + m][(y + r - 1) & 3][cl + 1 + c]; };
-                if (key_test(get, fp.t0, fp.t, fp.edge, fp.subpixel).result != 0.f) {
-                    const int xx = xw + cl;
-                    uint32_t* mrow = mask + mask_off + j * mask_lstride +
-                                     ((long long)b * H + y) * nwords;
-                    atomicOr(&mrow[xx >> 5], 1u << (xx & 31));
-                    atomicAdd(&row_count[(long long)b * fp.rows_per_image + rc_base + j * H + y],
-                              1u);
-                }
-            }
-        }
-#pragma unroll
-        for (int h = 0; h < 2; h++)
-#pragma unroll
-            for (int m = 0; m < ND; m++) {
-                hx0[h][m] = hx1[h][m]; hn0[h][m] = hn1[h][m];
-                hx1[h][m] = hx2[h][m]; hn1[h][m] = hn2[h][m];
-                cvx[h][m] = cnx[h][m];
-            }
-        asm volatile("" ::: "memory");
-    };
-    fetch(rA, ys - 1);
-    put(rA, ys - 1);
-    rowmm(hx0, hn0, nullptr);
-    fetch(rA, ys);
-    put(rA, ys);
-    rowmm(hx1, hn1, cvx);
-    fetch(rA, ys + 1);
-    fetch(rB, ys + 2);
-    for (int y = ys; y < ye; y += 2) {
-        put(rA, y + 1);
-        body(y);
-        fetch(rA, y + 3);
-        put(rB, y + 2);
-        body(y + 1);
-        fetch(rB, y + 4);
-    }
-}
-
 // ------------------------------------------------------------------------------------------
 // Exclusive scan (uint32), 1024 elements per block.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
@@ -2185,11 +2035,7 @@ hipError_t launch_first_octave_input(const float* src, const uint8_t* src_u8, in
 hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
                           const FeatureParams& fp, hipStream_t stream) {
     // one wave per (image, strip of tested columns, row segment); ~32k waves in all
-#ifdef SGK_EXT3
-    const int sw = 124;
-#else
     const int sw = 62;
-#endif
     ExtremaWaveGrid eg{};
     int nw = 0;
     for (int o = 0; o < fp.n_octaves; o++) {
@@ -2208,11 +2054,7 @@ hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
     eg.wave0[fp.n_octaves] = nw;
     const unsigned nb = (unsigned)((nw + 3) / 4);
     switch (fp.d + 2) {
-#ifdef SGK_EXT3
-#define SGK_EXTW(ND)     case ND: hipLaunchKernelGGL((k_extrema_wave3<ND>), dim3(nb), dim3(256), 0, stream, pyr, mask, row_count, fp, eg); break;
-#else
 #define SGK_EXTW(ND)     case ND: hipLaunchKernelGGL((k_extrema_wave2<ND>), dim3(nb), dim3(256), 0, stream, pyr, mask, row_count, fp, eg); break;
-#endif
         SGK_EXTW(3) SGK_EXTW(4) SGK_EXTW(5) SGK_EXTW(6) SGK_EXTW(7) SGK_EXTW(8)
         default: return hipErrorInvalidValue;
 #undef SGK_EXTW
