@@ -337,7 +337,7 @@ def bench_match(ctx, n, cpu=True):
     return out
 
 
-def bench_c4(ctx, batch=8, steps=3, cpu=True):
+def bench_c4(ctx, batch=16, steps=3, cpu=True):
     """BASELINE configs[3]: 4096x4096 tiles, -no 6 (the HBM-bound pyramid stress), a batch of
     `batch` distinct tiles (seeds 4000..) staged in HBM, `steps` timed passes after one warm-up.
     Roofline of the pyramid stage as for the headline: 48 B per octave pixel, sum N = 22,364,160
@@ -373,7 +373,7 @@ def bench_c4(ctx, batch=8, steps=3, cpu=True):
         if cpu:
             # the oracle on the same tiles, one per OpenMP thread
             import oracle_py
-            threads = max(1, min(batch, os.cpu_count() or 1))
+            threads = max(1, min(8, batch, os.cpu_count() or 1))   # ~10 s of wall time
             secs, cf = oracle_py.bench_extract(imgs[:threads], opts, threads=threads)
             out["cpu_baseline"] = {"value": threads / secs, "unit": "images/s", "cores": threads,
                                    "kind": "port",
