@@ -1073,15 +1073,25 @@ __device__ __forceinline__ void orientation_hist(const float* __restrict__ g, in
                 if (bin < 0) bin += 36;
             }
         }
-        // apply the 4 votes in sample order (all 4 lanes do the same LDS update)
+        // apply the 4 votes in sample order: lane 0 of the quad issues them as LDS float adds
+        // (ds_add_f32, IEEE round-to-nearest like the VALU add), which the LDS performs in issue
+        // order -- each bin sees the reference's sequence of adds, and no read-modify-write
+        // round trip sits between one group of samples and the next
         const int b0 = qbcast<0>(bin), b1 = qbcast<1>(bin), b2 = qbcast<2>(bin), b3 = qbcast<3>(bin);
         const float w0 = qbcastf<0>(weight), w1 = qbcastf<1>(weight), w2 = qbcastf<2>(weight),
                     w3 = qbcastf<3>(weight);
-        if (b0 >= 0) vote_l[b0] += w0;
-        if (b1 >= 0) vote_l[b1] += w1;
-        if (b2 >= 0) vote_l[b2] += w2;
-        if (b3 >= 0) vote_l[b3] += w3;
+        if (sub == 0) {
+            auto add = [&](int bb, float ww) {
+                __hip_atomic_fetch_add(&vote_l[bb], ww, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            };
+            if (b0 >= 0) add(b0, w0);
+            if (b1 >= 0) add(b1, w1);
+            if (b2 >= 0) add(b2, w2);
+            if (b3 >= 0) add(b3, w3);
+        }
     }
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int i = 0; i < 36; ++i) vote[i] = vote_l[i];
     const float one_third = (float)(1.0 / 3.0);
