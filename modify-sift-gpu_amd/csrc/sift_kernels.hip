@@ -558,22 +558,12 @@ hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
 #define SGK_GW_NW 1
 #endif
         constexpr int NW = SGK_GW_NW;
-#ifndef SGK_U8_NW
-#define SGK_U8_NW SGK_GW_NW
-#endif
-        constexpr int NW8 = SGK_U8_NW;
-        if (src8) {
-            const GaussWaveGrid g8 = gauss_wave_grid(w, h, batch, wave_rows, NW8);
-            const dim3 grid8((unsigned)((g8.total_waves + kGwWaves - 1) / kGwWaves));
-            hipLaunchKernelGGL((k_gauss_wave<FW, true, NW8>), grid8, dim3(64 * kGwWaves), 0,
-                               stream, src, src8, src_stride, src_img_stride, dst, dst_img_stride,
-                               w, h, taps, ds, dsw, dsh, ds_img_stride, g8);
-            return hipGetLastError();
-        }
         const GaussWaveGrid gg = gauss_wave_grid(w, h, batch, wave_rows, NW);
         const dim3 wgrid((unsigned)((gg.total_waves + kGwWaves - 1) / kGwWaves));
-        if (false)
-            ;
+        if (src8)
+            hipLaunchKernelGGL((k_gauss_wave<FW, true, NW>), wgrid, dim3(64 * kGwWaves), 0, stream, src,
+                               src8, src_stride, src_img_stride, dst, dst_img_stride, w, h, taps,
+                               ds, dsw, dsh, ds_img_stride, gg);
         else
             hipLaunchKernelGGL((k_gauss_wave<FW, false, NW>), wgrid, dim3(64 * kGwWaves), 0, stream, src,
                                src8, src_stride, src_img_stride, dst, dst_img_stride, w, h, taps,
