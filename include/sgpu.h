@@ -251,6 +251,9 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
                                    (k_gauss_wave); both are bit-identical.  Bits 16.. of the
                                    flags, when not 0, force the wave kernel's band height in
                                    rows (test / tuning hook)                              */
+#define SGPU_DEBUG_KEYED_MATCH 64 /* plain matching through the keyed epilogue (every value
+                                   folded with its column's tie-order bits) even when
+                                   ratiomax <= 1, where the keyless one is exact and used     */
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);

@@ -1012,14 +1012,22 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     HIPCHK(ctx, sgk::launch_to_s8(a, n1, ctx->m_s1.as<uint8_t>(), st));
     HIPCHK(ctx, sgk::launch_to_s8(b, n2, ctx->m_s2.as<uint8_t>(), st));
     HIPCHK(ctx, sgk::launch_rowsums(a, n1, row1, 128, 0, st));
+    // keyless folding (k_match_rows<..., RAW>): exact whenever a tied maximum cannot pass the
+    // ratio test, i.e. ratiomax <= 1 (the reference's default 0.8); SGPU_DEBUG_KEYED_MATCH keeps
+    // the keyed epilogue
+    const bool raw = !guided && !(ratiomax > 1.0f) && !(ctx->debug_flags & SGPU_DEBUG_KEYED_MATCH);
     if (mbm && !fused) {
-        HIPCHK(ctx, sgk::launch_match_rows(s1, n1, s2, n2, ca, part, st, nullptr, true));
+        HIPCHK(ctx, sgk::launch_match_rows(s1, n1, s2, n2, ca, part, st, nullptr, true, nullptr,
+                                           nullptr, raw));
         HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, row1, ctx->m_dist.as<float>(), distmax,
-                                             ratiomax, match1, nullptr, st, true));
+                                             ratiomax, match1, nullptr, st, true,
+                                             raw ? a : nullptr, raw ? b : nullptr, n2));
         HIPCHK(ctx, sgk::launch_rowsums(b, n2, col2, 128, 0, st));
-        HIPCHK(ctx, sgk::launch_match_rows(s2, n2, s1, n1, cb, part, st, nullptr, false));
+        HIPCHK(ctx, sgk::launch_match_rows(s2, n2, s1, n1, cb, part, st, nullptr, false, nullptr,
+                                           nullptr, raw));
         HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, col2, ctx->m_dist.as<float>(), distmax,
-                                             ratiomax, match2, nullptr, st, false));
+                                             ratiomax, match2, nullptr, st, false,
+                                             raw ? b : nullptr, raw ? a : nullptr, n1));
     } else if (mbm) {
         // one GEMM for both decisions (MultiplyDescriptor_Kernel's row results + column
         // partials, ProgramCU.cu:1466-1564)
@@ -1031,9 +1039,12 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
         HIPCHK(ctx, sgk::launch_match_cols(colpart, n2, panels, col2, ctx->m_dist.as<float>(),
                                            distmax, ratiomax, match2, nullptr, st));
     } else {
-        HIPCHK(ctx, sgk::launch_match_rows(s1, n1, s2, n2, ca, part, st, rmask, true));
+        const bool r1 = raw && !rmask;
+        HIPCHK(ctx, sgk::launch_match_rows(s1, n1, s2, n2, ca, part, st, rmask, true, nullptr,
+                                           nullptr, r1));
         HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, row1, ctx->m_dist.as<float>(), distmax,
-                                             ratiomax, match1, nullptr, st, true));
+                                             ratiomax, match1, nullptr, st, true,
+                                             r1 ? a : nullptr, r1 ? b : nullptr, n2));
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
     ctx->h_match.resize((size_t)n1 + n2);

@@ -150,10 +150,12 @@ int match_chunks(int nA, int nB);
 // colpart != nullptr (row_side only; row_term = 128 * sum(A rows)): the fused mutual form --
 // colpart[panel][nB] also receives every 128-row panel's column-side (max, row, second) of
 // (dot - column term) (guided: of the guided value), for launch_match_cols.
+// raw (plain matching with ratiomax <= 1 only): values folded without keys; part.idx is then
+// (tile + lane) and k_match_finish recovers the column (pass raw_A / raw_B to it).
 hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
                              int chunks, Top2* part, hipStream_t stream,
                              const uint8_t* mask, bool row_side, const int* row_term = nullptr,
-                             Top2* colpart = nullptr);
+                             Top2* colpart = nullptr, bool raw = false);
 int match_panels(int nA);
 // Column decisions from the panels' partials: col_term[j] = 128 * sum(B_j) - 2^21 (guided: 0).
 hipError_t launch_match_cols(const Top2* colpart, int n, int panels, const int* col_term,
@@ -170,8 +172,11 @@ hipError_t launch_guided_mask(const float* loc1, int n1, const float* loc2, int 
                               hipStream_t stream);
 // merge chunks, add row_term (nullptr: none), apply distmax / ratiomax -> out[i] = matched
 // index or -1
+// raw_A / raw_B / nB: the u8 sets of a raw launch_match_rows (A = this side's rows)
 hipError_t launch_match_finish(const Top2* part, int n, int chunks, const int* row_term,
                                const float* dist, float distmax, float ratiomax, int* out,
-                               Top2* best, hipStream_t stream, bool row_side);
+                               Top2* best, hipStream_t stream, bool row_side,
+                               const uint8_t* raw_A = nullptr, const uint8_t* raw_B = nullptr,
+                               int nB = 0);
 
 }  // namespace sgk

@@ -41,6 +41,14 @@ __device__ __forceinline__ int med3i(int a, int b, int c) {
     asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
+// The same, ordered after `after` (an unused operand): the hazard recognizer does not look
+// into inline asm, so an asm that reads an MFMA result must come after a compiler-visible
+// instruction that read it first (that one gets the required wait states).
+__device__ __forceinline__ int med3i_after(int a, int b, int c, int after) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c), "v"(after));
+    return r;
+}
 
 __global__ __launch_bounds__(256) void k_rowsum(const uint8_t* __restrict__ d, int n,
                                                 int* __restrict__ s, int scale, int bias) {
@@ -104,7 +112,14 @@ __device__ __forceinline__ bool tie_before(int a, int b) {
 // (127 - row in panel) -- equal values keep the lowest row -- merged over the 16 lanes and 4
 // waves that hold the column and written to colpart[panel][column].  k_match_cols merges the
 // panels in row order.  The row side is the plain kernel's.
-template <bool GUIDED, bool TIE32, bool COLS>
+// RAW (plain matching with ratiomax <= 1): the values are folded as they are, no key -- the
+// accumulators start at the column term, each value costs one v_med3 and one v_max, and a lane
+// records only the tile in which its maximum last grew.  Which of the lane's 8 columns of that
+// tile holds the maximum is recovered in k_match_finish by recomputing those 8 dot products,
+// and only for rows that pass the ratio test: those have second < max, so the maximum is unique
+// and no tie order is needed (an equal second maximum fails the test for ratiomax <= 1,
+// whichever column the reference would have named).
+template <bool GUIDED, bool TIE32, bool COLS, bool RAW = false>
 __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ A, int nA,
                                                     const uint8_t* __restrict__ B, int nB,
                                                     int cols_per_chunk, Top2* __restrict__ part,
@@ -218,7 +233,11 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
 #pragma unroll
         for (int cb = 0; cb < 8; cb++) {
             const int ct = s_ct[buf][cb * 16 + l16];
-            if constexpr (!GUIDED) {
+            if constexpr (RAW) {
+                ctlow[cb] = 0;
+                acc[0][cb] = v4i{ct, ct, ct, ct};
+                acc[1][cb] = acc[0][cb];
+            } else if constexpr (!GUIDED) {
                 ctlow[cb] = (ct << 7) | low[cb];
                 acc[0][cb] = v4i{0, 0, 0, 0};
                 acc[1][cb] = acc[0][cb];
@@ -258,7 +277,21 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         for (int rb = 0; rb < 2; rb++)
 #pragma unroll
             for (int i = 0; i < 4; i++) { mt[rb][i] = M[rb][i]; st[rb][i] = S[rb][i]; }
-        if constexpr (!COLS) {
+        if constexpr (RAW) {
+#pragma unroll
+            for (int half = 0; half < 2; half++)
+#pragma unroll
+                for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+#pragma unroll
+                        for (int cb = 4 * half; cb < 4 * half + 4; cb++) {
+                            const int v = acc[rb][cb][i];
+                            const int mo = mt[rb][i];
+                            mt[rb][i] = max(mo, v);   // the first read of v: compiler-visible
+                            st[rb][i] = med3i_after(st[rb][i], mo, v, mt[rb][i]);
+                        }
+        } else if constexpr (!COLS) {
 #ifdef SGK_MATCH_EXP_RAW
             // timing experiment only (wrong indices): raw values, med3 + max per value
 #pragma unroll
@@ -336,9 +369,13 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 const int m = mt[rb][i];
-                const bool took = (uint32_t)(m ^ M[rb][i]) >= kPrefix;
-                I[rb][i] = took ? tb : I[rb][i];
-                W[rb][i] = took ? m : W[rb][i];
+                if constexpr (RAW) {
+                    I[rb][i] = m > M[rb][i] ? tb : I[rb][i];
+                } else {
+                    const bool took = (uint32_t)(m ^ M[rb][i]) >= kPrefix;
+                    I[rb][i] = took ? tb : I[rb][i];
+                    W[rb][i] = took ? m : W[rb][i];
+                }
                 M[rb][i] = m;
                 S[rb][i] = st[rb][i];
             }
@@ -363,16 +400,20 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         rec = rec_next;
         __syncthreads();
     }
-    // keys -> (acc, column)
+    // keys -> (acc, column); RAW: (tile, lane) -> tile + l16, the lane's columns in the tile
 #pragma unroll
     for (int rb = 0; rb < 2; rb++)
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            const int k = W[rb][i] & 127;
-            const int in_tile = TIE32 ? (3 - (k & 3)) * 32 + (31 - (k >> 2)) : 127 - k;
-            I[rb][i] = I[rb][i] < 0 ? -1 : I[rb][i] + in_tile;
-            M[rb][i] >>= 7;
-            S[rb][i] >>= 7;
+            if constexpr (RAW) {
+                I[rb][i] = I[rb][i] < 0 ? -1 : I[rb][i] + l16;
+            } else {
+                const int k = W[rb][i] & 127;
+                const int in_tile = TIE32 ? (3 - (k & 3)) * 32 + (31 - (k >> 2)) : 127 - k;
+                I[rb][i] = I[rb][i] < 0 ? -1 : I[rb][i] + in_tile;
+                M[rb][i] >>= 7;
+                S[rb][i] >>= 7;
+            }
         }
     // merge the 16 lanes that share a row (same quad): xor 1, 2, 4, 8; equal dots resolve in the
     // side's tie order
@@ -388,7 +429,7 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
                 const int m1 = M[rb][i], s1 = S[rb][i], i1 = I[rb][i];
                 M[rb][i] = max(m1, m2);
                 S[rb][i] = max(min(m1, m2), max(s1, s2));
-                I[rb][i] = (m2 > m1 || (m2 == m1 && tie_before<TIE32>(i2, i1))) ? i2 : i1;
+                I[rb][i] = (m2 > m1 || (!RAW && m2 == m1 && tie_before<TIE32>(i2, i1))) ? i2 : i1;
             }
     }
     if (l16 == 0) {
@@ -406,12 +447,18 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
 // (RowMatch_Kernel / ColMatch_Kernel decision, ProgramCU.cu:1838-1841, 1884-1887).
 // Equal maxima of two chunks resolve in the side's tie order (tie32: RowMatch_Kernel's, see
 // k_match_rows).
+// raw_A / raw_B (u8, 128 bytes per descriptor; RAW partials): part.idx is (tile + lane) of the
+// maximum; a row that passes the ratio test has a unique maximum, found by recomputing the dot
+// products of the lane's 8 columns of that tile.
 __global__ __launch_bounds__(256) void k_match_finish(const Top2* __restrict__ part, int n,
                                                       int chunks, const int* __restrict__ row_term,
                                                       const float* __restrict__ dist,
                                                       float distmax, float ratiomax,
                                                       int* __restrict__ out,
-                                                      Top2* __restrict__ best, int tie32) {
+                                                      Top2* __restrict__ best, int tie32,
+                                                      const uint8_t* __restrict__ raw_A,
+                                                      const uint8_t* __restrict__ raw_B,
+                                                      int nB) {
     const int r = blockIdx.x * 256 + threadIdx.x;
     if (r >= n) return;
     Top2 t = part[r];
@@ -432,7 +479,33 @@ __global__ __launch_bounds__(256) void k_match_finish(const Top2* __restrict__ p
     if (sc < 0) sc = 0;
     if (best) best[r] = Top2{mx, idx, sc};
     const float d1 = dist[min(mx, 262144)], d2 = dist[min(sc, 262144)];
-    out[r] = (d1 < distmax) && (d1 < d2 * ratiomax) ? idx : -1;
+    const bool ok = (d1 < distmax) && (d1 < d2 * ratiomax);
+    if (raw_A && ok) {
+        const uint4* a = reinterpret_cast<const uint4*>(raw_A + (size_t)r * 128);
+        uint4 av[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) av[q] = a[q];
+        const int base = idx & ~127, lane = idx & 15;
+        int found = -1;
+        for (int k = 0; k < 8; k++) {
+            const int c = base + 16 * k + lane;
+            if (c >= nB) break;
+            const uint4* b = reinterpret_cast<const uint4*>(raw_B + (size_t)c * 128);
+            int d = 0;
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const uint4 bv = b[q];
+                d = __builtin_amdgcn_udot4(av[q].x, bv.x, d, false);
+                d = __builtin_amdgcn_udot4(av[q].y, bv.y, d, false);
+                d = __builtin_amdgcn_udot4(av[q].z, bv.z, d, false);
+                d = __builtin_amdgcn_udot4(av[q].w, bv.w, d, false);
+            }
+            if (d == mx && found < 0) found = c;
+        }
+        idx = found;
+        if (best) best[r].idx = found;
+    }
+    out[r] = ok ? idx : -1;
 }
 
 // Column decision of the fused GEMM (COLS): merge the panels' partials of column j in row
@@ -660,7 +733,8 @@ int match_panels(int nA) { return (nA + kPanel - 1) / kPanel; }
 hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
                              int chunks, Top2* part, hipStream_t stream,
                              const uint8_t* mask, bool row_side, const int* row_term,
-                             Top2* colpart) {
+                             Top2* colpart, bool raw) {
+    if (raw && (mask || colpart)) return hipErrorInvalidValue;
     if (nA <= 0 || nB <= 0) return hipSuccess;
     if (colpart && (!row_term || !row_side)) return hipErrorInvalidValue;
     int per = (nB + chunks - 1) / chunks;
@@ -671,7 +745,12 @@ hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
 #define SGK_MR(G, T, C)                                                                       \
     hipLaunchKernelGGL((k_match_rows<G, T, C>), grid, dim3(256), 0, stream, A, nA, B, nB, per, \
                        part, rec, tiles, row_term, colpart)
-    if (colpart) {
+#define SGK_MRR(T)                                                                            \
+    hipLaunchKernelGGL((k_match_rows<false, T, false, true>), grid, dim3(256), 0, stream, A, nA, \
+                       B, nB, per, part, rec, tiles, row_term, colpart)
+    if (raw) {
+        if (row_side) SGK_MRR(true); else SGK_MRR(false);
+    } else if (colpart) {
         if (mask) SGK_MR(true, true, true); else SGK_MR(false, true, true);
     } else if (!mask) {
         if (row_side) SGK_MR(false, true, false); else SGK_MR(false, false, false);
@@ -679,6 +758,7 @@ hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
         if (row_side) SGK_MR(true, true, false); else SGK_MR(true, false, false);
     }
 #undef SGK_MR
+#undef SGK_MRR
     return hipGetLastError();
 }
 
@@ -694,10 +774,12 @@ hipError_t launch_match_cols(const Top2* colpart, int n, int panels, const int* 
 
 hipError_t launch_match_finish(const Top2* part, int n, int chunks, const int* row_term,
                                const float* dist, float distmax, float ratiomax, int* out,
-                               Top2* best, hipStream_t stream, bool row_side) {
+                               Top2* best, hipStream_t stream, bool row_side,
+                               const uint8_t* raw_A, const uint8_t* raw_B, int nB) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_match_finish, dim3((n + 255) / 256), dim3(256), 0, stream, part, n,
-                       chunks, row_term, dist, distmax, ratiomax, out, best, row_side ? 1 : 0);
+                       chunks, row_term, dist, distmax, ratiomax, out, best, row_side ? 1 : 0,
+                       raw_A, raw_B, nB);
     return hipGetLastError();
 }
 

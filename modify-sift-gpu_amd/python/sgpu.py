@@ -396,6 +396,7 @@ class SiftContext:
     DEBUG_PARTS2, DEBUG_PARTS4, DEBUG_TINY_CAP, DEBUG_FUSED_MATCH = 1, 2, 4, 8
     DEBUG_EXACT_DESCRIPTOR = 16
     DEBUG_GAUSS_BLOCK = 32    # workgroup strip Gaussian (k_gauss_pk2); wave band rows in bits 16..
+    DEBUG_KEYED_MATCH = 64    # keyed matcher epilogue even when ratiomax <= 1
 
     def set_debug_flags(self, flags: int):
         """Per-context debug flags (sgpu_debug_set_flags; 0 = shipped configuration)."""

@@ -411,6 +411,31 @@ def test_match_exact_ties(gpu_ctx, n1, n2, cols):
     assert [pairs.get(i) for i in rows] == [tie_winner(x, y) for x, y in cols]
 
 
+@pytest.mark.parametrize("ratiomax", [0.8, 1.0])
+def test_keyless_match_equals_keyed(gpu_ctx, ratiomax):
+    """With ratiomax <= 1 plain matching folds raw values (no tie-order keys) and recovers the
+    winning column afterwards; pairs must equal the keyed epilogue's (SGPU_DEBUG_KEYED_MATCH),
+    on a large planted-duplicate set and on exact-tie scenes (a tied maximum is rejected)."""
+    d1 = synth_descriptors(20000, 5000)
+    d2 = synth_descriptors(20000, 5001, base=d1, n_dup=8000)
+    q1, q2 = quantize(d1), quantize(d2)
+    q1t, q2t, _ = synth_tie_scene(3000, 9000, 23, [(200, 129), (130, 2), (4000, 33), (8999, 1)],
+                                  [(60, 61), (1, 2995)])
+    base = quantize(synth_descriptors(400, 5))
+    dup2 = np.concatenate([base, base[:200]])
+    cases = [(q1, q2), (q1t, q2t), (base, dup2)]
+    for mbm in (0, 1):
+        raw = [gpu_ctx.match(a, b, 0.9, ratiomax, mbm) for a, b in cases]
+        try:
+            gpu_ctx.set_debug_flags(gpu_ctx.DEBUG_KEYED_MATCH)
+            keyed = [gpu_ctx.match(a, b, 0.9, ratiomax, mbm) for a, b in cases]
+        finally:
+            gpu_ctx.set_debug_flags(0)
+        for r, k in zip(raw, keyed):
+            assert np.array_equal(r, k), mbm
+    assert len(raw[0]) > 5000
+
+
 @pytest.mark.parametrize("n1,n2,dup", [(1, 700, 0), (700, 1, 0), (257, 1000, 100),
                                        (3000, 2500, 1000), (4096, 4096, 2000), (5000, 129, 50)])
 def test_fused_match_vs_oracle(gpu_ctx, n1, n2, dup):
