@@ -112,7 +112,7 @@ struct sgpu_ctx {
     hipEvent_t ev[T_N + 1] = {};
     float timing[T_N] = {};
     // matcher
-    DevBuf m_d1, m_d2, m_s1, m_s2, m_part, m_terms, m_match, m_dist, m_mask, m_loc, m_colpart;
+    DevBuf m_d1, m_d2, m_s1, m_s2, m_part, m_terms, m_match, m_dist, m_mask, m_loc, m_colpart, m_cols;
     std::vector<int> h_match;
     bool dist_ready = false;
     // multi-GPU: RCCL communicator of this context's device (sgpu_comm_*)
@@ -331,7 +331,7 @@ int sgpu_ctx_destroy(sgpu_ctx* ctx) {
     if (ctx->d2h) (void)hipStreamDestroy(ctx->d2h);
     DevBuf* bufs[] = {&ctx->input, &ctx->input2, &ctx->all_keys, &ctx->all_desc, &ctx->gray, &ctx->pre, &ctx->m_d1, &ctx->m_d2, &ctx->m_s1, &ctx->m_s2,
                       &ctx->m_part, &ctx->m_terms, &ctx->m_match, &ctx->m_dist, &ctx->m_mask, &ctx->m_loc,
-                      &ctx->m_colpart,
+                      &ctx->m_colpart, &ctx->m_cols,
                       &ctx->c_buf};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i <= T_N; i++)
@@ -991,8 +991,13 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     const bool fused = mbm && (guided || (ctx->debug_flags & SGPU_DEBUG_FUSED_MATCH));
     const int ca = sgk::match_chunks(n1, n2), panels = sgk::match_panels(n1);
     const int cb = mbm && !fused ? sgk::match_chunks(n2, n1) : 0;
-    ALLOCCHK(ctx, ctx->m_part.ensure(std::max((size_t)ca * n1, (size_t)cb * n2) * sizeof(sgk::Top2)));
+    // plain mutual matching decides only the columns some row matched (see below); their
+    // count is known on the device only, so the partials are sized for any count
+    const bool compact = mbm && !fused && !(ctx->debug_flags & SGPU_DEBUG_FULL_COLUMNS);
+    const size_t part_b = compact ? sgk::match_part_bound(n2, n1) : (size_t)cb * n2;
+    ALLOCCHK(ctx, ctx->m_part.ensure(std::max((size_t)ca * n1, part_b) * sizeof(sgk::Top2)));
     if (fused) ALLOCCHK(ctx, ctx->m_colpart.ensure((size_t)panels * n2 * sizeof(sgk::Top2)));
+    if (compact) ALLOCCHK(ctx, ctx->m_cols.ensure((size_t)(2 * n2 + 1) * sizeof(int)));
     ALLOCCHK(ctx, ctx->m_terms.ensure((size_t)2 * (n1 + n2) * sizeof(int)));
     ALLOCCHK(ctx, ctx->m_match.ensure((size_t)(n1 + n2) * sizeof(int)));
     int* row1 = ctx->m_terms.as<int>();          // row terms 128 * sum(d1), column terms
@@ -1009,30 +1014,52 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     ALLOCCHK(ctx, ctx->m_s2.ensure((size_t)n2 * 128));
     const uint8_t* s1 = ctx->m_s1.as<uint8_t>();
     const uint8_t* s2 = ctx->m_s2.as<uint8_t>();
-    HIPCHK(ctx, sgk::launch_to_s8(a, n1, ctx->m_s1.as<uint8_t>(), st));
-    HIPCHK(ctx, sgk::launch_to_s8(b, n2, ctx->m_s2.as<uint8_t>(), st));
-    HIPCHK(ctx, sgk::launch_rowsums(a, n1, row1, 128, 0, st));
+    // ... with the row terms 128 * sum(d1) and, for mutual matching, the column side's terms
+    // (two GEMMs: 128 * sum(d2), the row terms of the swapped launch; fused: the column terms
+    // 128 * sum(d2) - 2^21, guided: 0) and the matched-column flags cleared
+    int* cw = compact ? ctx->m_cols.as<int>() : nullptr;   // [flag n2][count][list n2]
+    HIPCHK(ctx, sgk::launch_prep_set(a, n1, ctx->m_s1.as<uint8_t>(), row1, 128, 0, nullptr, 0, st));
+    if (mbm)
+        HIPCHK(ctx, sgk::launch_prep_set(b, n2, ctx->m_s2.as<uint8_t>(), col2,
+                                         guided && fused ? 0 : 128,
+                                         fused && !guided ? -2097152 : 0,
+                                         cw, compact ? n2 + 1 : 0, st));
+    else
+        HIPCHK(ctx, sgk::launch_to_s8(b, n2, ctx->m_s2.as<uint8_t>(), st));
     // keyless folding (k_match_rows<..., RAW>): exact whenever a tied maximum cannot pass the
     // ratio test, i.e. ratiomax <= 1 (the reference's default 0.8); SGPU_DEBUG_KEYED_MATCH keeps
     // the keyed epilogue
     const bool raw = !guided && !(ratiomax > 1.0f) && !(ctx->debug_flags & SGPU_DEBUG_KEYED_MATCH);
     if (mbm && !fused) {
+        // The mutual check below reads the column decision match2[j] only for j = match1[i] >=
+        // 0, so the column GEMM runs over those columns alone: the row finish appends each
+        // matched column once to a list (flags and count zeroed here), and the column launches
+        // take their rows from it, their count from the device.  Every listed column still
+        // scans all of set 1, so its decision is the reference's (SGPU_DEBUG_FULL_COLUMNS:
+        // every column, as ColMatch_Kernel does).  The flags and the count were cleared with
+        // the s8 conversion.
+        sgk::ColumnList claim, cols;
+        if (compact) {
+            claim.flag = cw;
+            claim.count = cw + n2;
+            claim.list = cw + n2 + 1;
+            cols.count = claim.count;
+            cols.map = claim.list;
+        }
         HIPCHK(ctx, sgk::launch_match_rows(s1, n1, s2, n2, ca, part, st, nullptr, true, nullptr,
                                            nullptr, raw));
         HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, row1, ctx->m_dist.as<float>(), distmax,
                                              ratiomax, match1, nullptr, st, true,
-                                             raw ? a : nullptr, raw ? b : nullptr, n2));
-        HIPCHK(ctx, sgk::launch_rowsums(b, n2, col2, 128, 0, st));
+                                             raw ? a : nullptr, raw ? b : nullptr, n2, claim));
         HIPCHK(ctx, sgk::launch_match_rows(s2, n2, s1, n1, cb, part, st, nullptr, false, nullptr,
-                                           nullptr, raw));
+                                           nullptr, raw, cols.map, cols.count));
         HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, col2, ctx->m_dist.as<float>(), distmax,
                                              ratiomax, match2, nullptr, st, false,
-                                             raw ? b : nullptr, raw ? a : nullptr, n1));
+                                             raw ? b : nullptr, raw ? a : nullptr, n1, cols));
     } else if (mbm) {
         // one GEMM for both decisions (MultiplyDescriptor_Kernel's row results + column
         // partials, ProgramCU.cu:1466-1564)
         // guided: the column values already hold the column term (col_term 0)
-        HIPCHK(ctx, sgk::launch_rowsums(b, n2, col2, guided ? 0 : 128, guided ? 0 : -2097152, st));
         HIPCHK(ctx, sgk::launch_match_rows(s1, n1, s2, n2, ca, part, st, rmask, true, row1, colpart));
         HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, row1, ctx->m_dist.as<float>(),
                                              distmax, ratiomax, match1, nullptr, st, true));

@@ -140,6 +140,10 @@ struct Top2 { int max, idx, second; };
 hipError_t launch_to_s8(const uint8_t* src, int n, uint8_t* dst, hipStream_t stream);
 // s[i] = scale * sum_k d[i][k] + bias
 hipError_t launch_rowsums(const uint8_t* d, int n, int* s, int scale, int bias, hipStream_t stream);
+// both at once, for one set: dst = s8 form, sums[i] = scale * sum_k src[i][k] + bias, and
+// zero[0 .. nzero) = 0
+hipError_t launch_prep_set(const uint8_t* src, int n, uint8_t* dst, int* sums, int scale,
+                           int bias, int* zero, int nzero, hipStream_t stream);
 int match_chunks(int nA, int nB);
 // part[chunk][nA]: per-row top-2 of (A_i . B_j + col_term[j]) over each column chunk, with
 // col_term[j] = 128 * sum(B_j) - 2^21 formed in the kernel from the staged bytes.  A and B are
@@ -152,10 +156,16 @@ int match_chunks(int nA, int nB);
 // (dot - column term) (guided: of the guided value), for launch_match_cols.
 // raw (plain matching with ratiomax <= 1 only): values folded without keys; part.idx is then
 // (tile + lane) and k_match_finish recovers the column (pass raw_A / raw_B to it).
+// amap / an (plain matching only): the rows are A[amap[r]] for r < *an (a count on the device,
+// at most nA); the launch covers every count and the split is chunks_for(*an, nB), which
+// launch_match_finish with ColumnList{map, count} derives again.  part needs
+// match_part_bound(nA, nB) entries.
 hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
                              int chunks, Top2* part, hipStream_t stream,
                              const uint8_t* mask, bool row_side, const int* row_term = nullptr,
-                             Top2* colpart = nullptr, bool raw = false);
+                             Top2* colpart = nullptr, bool raw = false,
+                             const int* amap = nullptr, const int* an = nullptr);
+size_t match_part_bound(int nA, int nB);
 int match_panels(int nA);
 // Column decisions from the panels' partials: col_term[j] = 128 * sum(B_j) - 2^21 (guided: 0).
 hipError_t launch_match_cols(const Top2* colpart, int n, int panels, const int* col_term,
@@ -172,11 +182,22 @@ hipError_t launch_guided_mask(const float* loc1, int n1, const float* loc2, int 
                               hipStream_t stream);
 // merge chunks, add row_term (nullptr: none), apply distmax / ratiomax -> out[i] = matched
 // index or -1
-// raw_A / raw_B / nB: the u8 sets of a raw launch_match_rows (A = this side's rows)
+// raw_A / raw_B / nB: the u8 sets of a raw launch_match_rows (A = this side's rows; nB = the
+// other side's count, also needed with cl.map)
+// The column side of a mutual match only needs the columns some row matched (the host's check
+// reads match2[j] only for j = match1[i] >= 0).  ColumnList, row side: flag (nB ints, zeroed)
+// and count (zeroed) set -> each matched column is appended once to list.  Column side: map =
+// that list and count -> the launch covers rows map[0 .. *count) (n = the upper bound).
+struct ColumnList {
+    int* flag = nullptr;
+    int* list = nullptr;
+    int* count = nullptr;
+    const int* map = nullptr;
+};
 hipError_t launch_match_finish(const Top2* part, int n, int chunks, const int* row_term,
                                const float* dist, float distmax, float ratiomax, int* out,
                                Top2* best, hipStream_t stream, bool row_side,
                                const uint8_t* raw_A = nullptr, const uint8_t* raw_B = nullptr,
-                               int nB = 0);
+                               int nB = 0, ColumnList cl = ColumnList{});
 
 }  // namespace sgk

@@ -33,6 +33,12 @@ constexpr int kNeg = INT_MIN;
 // so with the row term >= 0 added in the finish it can neither win nor raise a second maximum,
 // and (acc << 7) does not overflow.
 constexpr int kNegCol = -(1 << 22);
+#ifdef SGK_MATCH_SPLIT
+constexpr int kMatchSplit = SGK_MATCH_SPLIT;   // column groups per tile of the keyless kernel
+#else
+constexpr int kMatchSplit = 2;   // 126 VGPRs: 4 waves per SIMD (one group of 8: 160, 3 waves)
+#endif
+static_assert(kMatchSplit == 1 || kMatchSplit == 2, "1 or 2 column groups");
 
 // v_med3_i32: the median of three.  With s <= m, med3(s, m, v) is the new second maximum after
 // seeing v (v > m -> m; s < v <= m -> v; v <= s -> s).
@@ -62,6 +68,16 @@ __global__ __launch_bounds__(256) void k_rowsum(const uint8_t* __restrict__ d, i
     if (lane == 0) s[i] = scale * t + bias;
 }
 
+// Column chunks of one launch: ~4096 workgroups (about 5 per resident slot at 3 per CU) so
+// that the last wave of workgroups is a small tail; each chunk at least two tiles wide.  Also
+// evaluated on the device for a row count that only the device knows (compacted rows).
+__host__ __device__ inline int chunks_for(int nA, int nB) {
+    const int panels = (nA + kPanel - 1) / kPanel;
+    const int chunks = (4096 + panels - 1) / panels;
+    const int max_chunks = max(1, (nB + 2 * kTile - 1) / (2 * kTile));
+    return max(1, min(chunks, max_chunks));
+}
+
 // u8 descriptors -> s8 (s = u - 128, xor 0x80), once per match call for both sets
 __global__ __launch_bounds__(256) void k_to_s8(const uint4* __restrict__ src, size_t n16,
                                                uint4* __restrict__ dst) {
@@ -70,6 +86,30 @@ __global__ __launch_bounds__(256) void k_to_s8(const uint4* __restrict__ src, si
         v.x ^= 0x80808080u; v.y ^= 0x80808080u; v.z ^= 0x80808080u; v.w ^= 0x80808080u;
         dst[i] = v;
     }
+}
+
+// One pass over a descriptor set: the s8 form (xor 0x80), the row sums scale * sum(u8) + bias,
+// and `nzero` ints of `zero` cleared (the matched-column flags).  A thread per 16 bytes, a
+// descriptor per 8 consecutive lanes (the grid stride keeps the groups whole).
+__global__ __launch_bounds__(256) void k_prep_set(const uint4* __restrict__ src, size_t n16,
+                                                  uint4* __restrict__ dst, int* __restrict__ sums,
+                                                  int scale, int bias, int* __restrict__ zero,
+                                                  int nzero) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) {
+        uint4 v = src[i];
+        int t = __builtin_amdgcn_udot4(v.x, 0x01010101u, 0, false);
+        t = __builtin_amdgcn_udot4(v.y, 0x01010101u, t, false);
+        t = __builtin_amdgcn_udot4(v.z, 0x01010101u, t, false);
+        t = __builtin_amdgcn_udot4(v.w, 0x01010101u, t, false);
+        v.x ^= 0x80808080u; v.y ^= 0x80808080u; v.z ^= 0x80808080u; v.w ^= 0x80808080u;
+        dst[i] = v;
+        t += __shfl_xor(t, 1, 64);
+        t += __shfl_xor(t, 2, 64);
+        t += __shfl_xor(t, 4, 64);
+        if ((i & 7) == 0) sums[i >> 3] = scale * t + bias;
+    }
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < (size_t)nzero; i += stride) zero[i] = 0;
 }
 
 // Equal-dot order of the two decisions: does column a come before column b (-1 = none)?
@@ -119,6 +159,9 @@ __device__ __forceinline__ bool tie_before(int a, int b) {
 // and only for rows that pass the ratio test: those have second < max, so the maximum is unique
 // and no tie order is needed (an equal second maximum fails the test for ratiomax <= 1,
 // whichever column the reference would have named).
+// amap / an (compacted rows): row r of A is A[amap[r]], and the row count is *an, known only on
+// the device; the grid is then 1-D and each workgroup derives its (panel, chunk) from the count,
+// with the split chunks_for(*an, nB) (k_match_finish derives the same one).
 template <bool GUIDED, bool TIE32, bool COLS, bool RAW = false>
 __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ A, int nA,
                                                     const uint8_t* __restrict__ B, int nB,
@@ -126,12 +169,23 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
                                                     const uint4* __restrict__ mask,
                                                     int mask_tiles,
                                                     const int* __restrict__ row_term,
-                                                    Top2* __restrict__ colpart) {
+                                                    Top2* __restrict__ colpart,
+                                                    const int* __restrict__ amap,
+                                                    const int* __restrict__ an) {
     __shared__ __attribute__((aligned(16))) uint8_t s_b[2][kTile * kLdsRow];
     __shared__ int s_ct[2][kTile];   // column terms of the staged tile (from its bytes)
     __shared__ int s_cm[COLS ? 4 : 1][COLS ? kTile : 1], s_cs[COLS ? 4 : 1][COLS ? kTile : 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int panel = blockIdx.x, chunk = blockIdx.y;
+    int panel = blockIdx.x, chunk = blockIdx.y;
+    if (an) {
+        nA = *an;
+        if (nA <= 0) return;
+        const int panels = (nA + kPanel - 1) / kPanel, chunks = chunks_for(nA, nB);
+        if ((int)blockIdx.x >= panels * chunks) return;
+        panel = blockIdx.x % panels;
+        chunk = blockIdx.x / panels;
+        cols_per_chunk = ((nB + chunks - 1) / chunks + kTile - 1) / kTile * kTile;
+    }
     const int c_begin = chunk * cols_per_chunk;
     const int c_end = min(nB, c_begin + cols_per_chunk);
     const int quad = lane >> 4, l16 = lane & 15;
@@ -143,7 +197,10 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         const int row = panel * kPanel + wave * 32 + rb * 16 + l16;
 #pragma unroll
         for (int kh = 0; kh < 2; kh++) {
-            if (row < nA) afrag[rb][kh] = *reinterpret_cast<const v4i*>(A + (size_t)row * 128 + kh * 64 + quad * 16);
+            if (row < nA) {
+                const int src = amap ? amap[row] : row;
+                afrag[rb][kh] = *reinterpret_cast<const v4i*>(A + (size_t)src * 128 + kh * 64 + quad * 16);
+            }
             else afrag[rb][kh] = v4i{0, 0, 0, 0};
         }
     }
@@ -225,6 +282,51 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         if (has_next) stage_load(tb + kTile, stg);
         uint4 rec_next = rec;
         if (rec_ok && has_next) rec_next = rec_p[(tb / kTile + 1) * 64];
+        int mt[2][4], st[2][4];
+#pragma unroll
+        for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) { mt[rb][i] = M[rb][i]; st[rb][i] = S[rb][i]; }
+        if constexpr (RAW) {
+            // the tile in kMatchSplit column groups (accumulators start at the column term;
+            // MFMAs, then the folds, per group), each row folding its values in column order
+            constexpr int CB = 8 / kMatchSplit;
+#pragma unroll
+            for (int h = 0; h < kMatchSplit; h++) {
+                v4i acc[2][CB];
+#pragma unroll
+                for (int c = 0; c < CB; c++) {
+                    const int ct = s_ct[buf][(h * CB + c) * 16 + l16];
+                    acc[0][c] = v4i{ct, ct, ct, ct};
+                    acc[1][c] = acc[0][c];
+                }
+#pragma unroll
+                for (int c = 0; c < CB; c++) {
+#pragma unroll
+                    for (int kh = 0; kh < 2; kh++) {
+                        const v4i bfrag = *reinterpret_cast<const v4i*>(
+                            s_b[buf] + ((h * CB + c) * 16 + l16) * kLdsRow + kh * 64 + quad * 16);
+                        acc[0][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[0][kh], bfrag, acc[0][c], 0, 0, 0);
+                        acc[1][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[1][kh], bfrag, acc[1][c], 0, 0, 0);
+                    }
+                }
+                // column blocks in groups of 4 for every row: the first group's reads do not
+                // wait on the group's last MFMAs
+#pragma unroll
+                for (int g = 0; g < CB / 4; g++)
+#pragma unroll
+                    for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+#pragma unroll
+                            for (int c = 4 * g; c < 4 * g + 4; c++) {
+                                const int v = acc[rb][c][i];
+                                const int mo = mt[rb][i];
+                                mt[rb][i] = max(mo, v);   // the first read of v: compiler-visible
+                                st[rb][i] = med3i_after(st[rb][i], mo, v, mt[rb][i]);
+                            }
+            }
+        } else {
         // plain: the accumulators start at 0 and the column term enters the key,
         // key = (acc << 7) + ((ct << 7) | low) = ((acc + ct) << 7) | low;
         // guided: they start at the column term minus the geometric bias (invalid columns: -inf)
@@ -233,11 +335,7 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
 #pragma unroll
         for (int cb = 0; cb < 8; cb++) {
             const int ct = s_ct[buf][cb * 16 + l16];
-            if constexpr (RAW) {
-                ctlow[cb] = 0;
-                acc[0][cb] = v4i{ct, ct, ct, ct};
-                acc[1][cb] = acc[0][cb];
-            } else if constexpr (!GUIDED) {
+            if constexpr (!GUIDED) {
                 ctlow[cb] = (ct << 7) | low[cb];
                 acc[0][cb] = v4i{0, 0, 0, 0};
                 acc[1][cb] = acc[0][cb];
@@ -272,26 +370,7 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         // Column blocks 0..3 of every row first (their MFMAs finished earliest), then 4..7:
         // each row still folds its keys in column order, and the first half's reads do not
         // wait on the last MFMAs.
-        int mt[2][4], st[2][4];
-#pragma unroll
-        for (int rb = 0; rb < 2; rb++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) { mt[rb][i] = M[rb][i]; st[rb][i] = S[rb][i]; }
-        if constexpr (RAW) {
-#pragma unroll
-            for (int half = 0; half < 2; half++)
-#pragma unroll
-                for (int rb = 0; rb < 2; rb++)
-#pragma unroll
-                    for (int i = 0; i < 4; i++)
-#pragma unroll
-                        for (int cb = 4 * half; cb < 4 * half + 4; cb++) {
-                            const int v = acc[rb][cb][i];
-                            const int mo = mt[rb][i];
-                            mt[rb][i] = max(mo, v);   // the first read of v: compiler-visible
-                            st[rb][i] = med3i_after(st[rb][i], mo, v, mt[rb][i]);
-                        }
-        } else if constexpr (!COLS) {
+        if constexpr (!COLS) {
 #ifdef SGK_MATCH_EXP_RAW
             // timing experiment only (wrong indices): raw values, med3 + max per value
 #pragma unroll
@@ -364,6 +443,7 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
                 }
             }
         }
+        }   // !RAW
 #pragma unroll
         for (int rb = 0; rb < 2; rb++)
 #pragma unroll
@@ -446,11 +526,22 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
 // Merge the column chunks of one side, add the row term, apply the distance/ratio test
 // (RowMatch_Kernel / ColMatch_Kernel decision, ProgramCU.cu:1838-1841, 1884-1887).
 // Equal maxima of two chunks resolve in the side's tie order (tie32: RowMatch_Kernel's, see
-// k_match_rows).
+// k_match_rows); that choice is associative, so the chunks are merged in any grouping.
 // raw_A / raw_B (u8, 128 bytes per descriptor; RAW partials): part.idx is (tile + lane) of the
 // maximum; a row that passes the ratio test has a unique maximum, found by recomputing the dot
 // products of the lane's 8 columns of that tile.
-__global__ __launch_bounds__(256) void k_match_finish(const Top2* __restrict__ part, int n,
+// cl.map / cl.count (a launch over compacted rows): row r is row cl.map[r] of this side (its row
+// term, u8 descriptor and output slot), n = *cl.count and the chunks are chunks_for(n, nB).
+// cl.flag (row side of a mutual match): every column that a row matched is appended once to
+// cl.list (count in *cl.count; the order is not deterministic and does not need to be).
+// 8 lanes per row (a chain of dependent loads per row otherwise: partials, distance table,
+// candidate descriptors): lane k merges chunks k, k + 8, ... and recomputes candidate k.
+// The list slots are taken with one atomic add per workgroup: same-address atomics serialise,
+// and one per wave cost ~25 us at 50k rows.
+constexpr int kFinishThreads = 1024;
+constexpr int kFinishRows = kFinishThreads / 8;
+
+__global__ __launch_bounds__(kFinishThreads) void k_match_finish(const Top2* __restrict__ part, int n,
                                                       int chunks, const int* __restrict__ row_term,
                                                       const float* __restrict__ dist,
                                                       float distmax, float ratiomax,
@@ -458,54 +549,84 @@ __global__ __launch_bounds__(256) void k_match_finish(const Top2* __restrict__ p
                                                       Top2* __restrict__ best, int tie32,
                                                       const uint8_t* __restrict__ raw_A,
                                                       const uint8_t* __restrict__ raw_B,
-                                                      int nB) {
-    const int r = blockIdx.x * 256 + threadIdx.x;
-    if (r >= n) return;
-    Top2 t = part[r];
-    for (int c = 1; c < chunks; c++) {
-        const Top2 u = part[(size_t)c * n + r];
-        const int m = max(t.max, u.max);
+                                                      int nB, ColumnList cl) {
+    if (cl.map) {
+        n = *cl.count;
+        chunks = chunks_for(n, nB);
+    }
+    __shared__ int s_cnt[kFinishThreads / 64], s_base;
+    if ((int)blockIdx.x * kFinishRows >= n) return;   // whole workgroups only (barriers below)
+    const int sub = threadIdx.x & 7, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r0 = blockIdx.x * kFinishRows + (threadIdx.x >> 3);
+    const bool valid = r0 < n;   // whole 8-lane groups
+    const int r = valid ? r0 : n - 1;
+    const int g = cl.map ? cl.map[r] : r;
+    auto merge = [&](Top2& t, const Top2& u) {
         const int s = max(min(t.max, u.max), max(t.second, u.second));
         const bool later = u.max > t.max ||
                            (u.max == t.max && (tie32 ? tie_before<true>(u.idx, t.idx)
                                                      : tie_before<false>(u.idx, t.idx)));
-        t = Top2{m, later ? u.idx : t.idx, s};
-    }
-    const int rt = row_term ? row_term[r] : 0;   // COLS: already in the accumulators
+        t = Top2{max(t.max, u.max), later ? u.idx : t.idx, s};
+    };
+    Top2 t{INT_MIN, -1, INT_MIN};
+    for (int c = sub; c < chunks; c += 8) merge(t, part[(size_t)c * n + r]);
+#pragma unroll
+    for (int off = 1; off < 8; off <<= 1)
+        merge(t, Top2{__shfl_xor(t.max, off, 64), __shfl_xor(t.idx, off, 64),
+                      __shfl_xor(t.second, off, 64)});
+    const int rt = row_term ? row_term[g] : 0;   // COLS: already in the accumulators
     // the reference's running maxima start at 0 with index -1 (ProgramCU.cu:1803)
     int mx = t.max + rt, sc = t.second + rt;
     int idx = t.idx;
     if (mx <= 0) { mx = 0; idx = -1; }
     if (sc < 0) sc = 0;
-    if (best) best[r] = Top2{mx, idx, sc};
     const float d1 = dist[min(mx, 262144)], d2 = dist[min(sc, 262144)];
     const bool ok = (d1 < distmax) && (d1 < d2 * ratiomax);
     if (raw_A && ok) {
-        const uint4* a = reinterpret_cast<const uint4*>(raw_A + (size_t)r * 128);
-        uint4 av[8];
+        // lane k: candidate column (tile) + 16 k + (lane in tile); the lowest equal one wins
+        // (there is one: a passing maximum is unique)
+        const int c = (idx & ~127) + 16 * sub + (idx & 15);
+        const uint4* a = reinterpret_cast<const uint4*>(raw_A + (size_t)g * 128);
+        const uint4* b = reinterpret_cast<const uint4*>(raw_B + (size_t)min(c, nB - 1) * 128);
+        uint4 av[8], bv[8];
 #pragma unroll
-        for (int q = 0; q < 8; q++) av[q] = a[q];
-        const int base = idx & ~127, lane = idx & 15;
-        int found = -1;
-        for (int k = 0; k < 8; k++) {
-            const int c = base + 16 * k + lane;
-            if (c >= nB) break;
-            const uint4* b = reinterpret_cast<const uint4*>(raw_B + (size_t)c * 128);
-            int d = 0;
+        for (int q = 0; q < 8; q++) { av[q] = a[q]; bv[q] = b[q]; }
+        int d = 0;
 #pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const uint4 bv = b[q];
-                d = __builtin_amdgcn_udot4(av[q].x, bv.x, d, false);
-                d = __builtin_amdgcn_udot4(av[q].y, bv.y, d, false);
-                d = __builtin_amdgcn_udot4(av[q].z, bv.z, d, false);
-                d = __builtin_amdgcn_udot4(av[q].w, bv.w, d, false);
-            }
-            if (d == mx && found < 0) found = c;
+        for (int q = 0; q < 8; q++) {
+            d = __builtin_amdgcn_udot4(av[q].x, bv[q].x, d, false);
+            d = __builtin_amdgcn_udot4(av[q].y, bv[q].y, d, false);
+            d = __builtin_amdgcn_udot4(av[q].z, bv[q].z, d, false);
+            d = __builtin_amdgcn_udot4(av[q].w, bv[q].w, d, false);
         }
-        idx = found;
-        if (best) best[r].idx = found;
+        const unsigned long long bal = __ballot(c < nB && d == mx);
+        const uint32_t mine = (uint32_t)(bal >> (lane & ~7)) & 0xffu;
+        idx = mine ? (idx & ~127) + 16 * (__ffs(mine) - 1) + (idx & 15) : -1;
     }
-    out[r] = ok ? idx : -1;
+    const int res = ok ? idx : -1;
+    if (valid && sub == 0) {
+        out[g] = res;
+        if (best) best[g] = Top2{mx, idx, sc};
+    }
+    if (cl.flag) {
+        // the first claim of a column appends it: slots per wave (ballot), per workgroup
+        // (LDS prefix), one atomic add
+        const bool first = valid && sub == 0 && res >= 0 && atomicExch(&cl.flag[res], 1) == 0;
+        const unsigned long long bal = __ballot(first);
+        if (lane == 0) s_cnt[wave] = __popcll(bal);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int tot = 0;
+            for (int w = 0; w < kFinishThreads / 64; w++) {
+                const int c = s_cnt[w];
+                s_cnt[w] = tot;
+                tot += c;
+            }
+            s_base = tot ? atomicAdd(cl.count, tot) : 0;
+        }
+        __syncthreads();
+        if (first) cl.list[s_base + s_cnt[wave] + __popcll(bal & ((1ull << lane) - 1))] = res;
+    }
 }
 
 // Column decision of the fused GEMM (COLS): merge the panels' partials of column j in row
@@ -712,6 +833,18 @@ hipError_t launch_to_s8(const uint8_t* src, int n, uint8_t* dst, hipStream_t str
     return hipGetLastError();
 }
 
+hipError_t launch_prep_set(const uint8_t* src, int n, uint8_t* dst, int* sums, int scale,
+                           int bias, int* zero, int nzero, hipStream_t stream) {
+    if (n <= 0 && nzero <= 0) return hipSuccess;
+    const size_t n16 = (size_t)std::max(n, 0) * 8;
+    const size_t work = std::max(n16, (size_t)std::max(nzero, 0));
+    const unsigned grid = (unsigned)std::min<size_t>((work + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_prep_set, dim3(grid), dim3(256), 0, stream,
+                       reinterpret_cast<const uint4*>(src), n16, reinterpret_cast<uint4*>(dst),
+                       sums, scale, bias, zero, nzero);
+    return hipGetLastError();
+}
+
 hipError_t launch_rowsums(const uint8_t* d, int n, int* out, int scale, int bias,
                           hipStream_t stream) {
     if (n <= 0) return hipSuccess;
@@ -719,13 +852,20 @@ hipError_t launch_rowsums(const uint8_t* d, int n, int* out, int scale, int bias
     return hipGetLastError();
 }
 
-int match_chunks(int nA, int nB) {
-    // ~4096 workgroups (about 5 per resident slot at 3 per CU) so that the last wave of
-    // workgroups is a small tail; each chunk at least two tiles wide
-    const int panels = (nA + kPanel - 1) / kPanel;
-    int chunks = (4096 + panels - 1) / panels;
-    const int max_chunks = max(1, (nB + 2 * kTile - 1) / (2 * kTile));
-    return max(1, min(chunks, max_chunks));
+int match_chunks(int nA, int nB) { return chunks_for(nA, nB); }
+
+// bounds over every row count m <= nA of chunks_for(m, nB) * m (partials) and of
+// panels(m) * chunks_for(m, nB) (workgroups): chunks <= max_chunks, and chunks * panels <
+// 4096 + panels
+size_t match_part_bound(int nA, int nB) {
+    const size_t panels = (nA + kPanel - 1) / kPanel;
+    const size_t max_chunks = std::max(1, (nB + 2 * kTile - 1) / (2 * kTile));
+    return std::min((4096 + panels) * kPanel, max_chunks * (size_t)nA);
+}
+static unsigned match_grid_bound(int nA, int nB) {
+    const size_t panels = (nA + kPanel - 1) / kPanel;
+    const size_t max_chunks = std::max(1, (nB + 2 * kTile - 1) / (2 * kTile));
+    return (unsigned)std::min(4096 + panels, max_chunks * panels);
 }
 
 int match_panels(int nA) { return (nA + kPanel - 1) / kPanel; }
@@ -733,23 +873,28 @@ int match_panels(int nA) { return (nA + kPanel - 1) / kPanel; }
 hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
                              int chunks, Top2* part, hipStream_t stream,
                              const uint8_t* mask, bool row_side, const int* row_term,
-                             Top2* colpart, bool raw) {
+                             Top2* colpart, bool raw, const int* amap, const int* an) {
     if (raw && (mask || colpart)) return hipErrorInvalidValue;
     if (nA <= 0 || nB <= 0) return hipSuccess;
     if (colpart && (!row_term || !row_side)) return hipErrorInvalidValue;
+    if ((amap != nullptr) != (an != nullptr) || (an && (mask || colpart))) return hipErrorInvalidValue;
     int per = (nB + chunks - 1) / chunks;
     per = (per + kTile - 1) / kTile * kTile;
-    dim3 grid((nA + kPanel - 1) / kPanel, chunks);
+    // compacted rows (at most nA of them): a 1-D grid large enough for any count
+    const dim3 grid = an ? dim3(match_grid_bound(nA, nB))
+                         : dim3((nA + kPanel - 1) / kPanel, chunks);
     const int tiles = (nB + kTile - 1) / kTile;
     const uint4* rec = reinterpret_cast<const uint4*>(mask);
 #define SGK_MR(G, T, C)                                                                       \
     hipLaunchKernelGGL((k_match_rows<G, T, C>), grid, dim3(256), 0, stream, A, nA, B, nB, per, \
-                       part, rec, tiles, row_term, colpart)
+                       part, rec, tiles, row_term, colpart, amap, an)
 #define SGK_MRR(T)                                                                            \
     hipLaunchKernelGGL((k_match_rows<false, T, false, true>), grid, dim3(256), 0, stream, A, nA, \
-                       B, nB, per, part, rec, tiles, row_term, colpart)
+                       B, nB, per, part, rec, tiles, row_term, colpart, amap, an)
     if (raw) {
         if (row_side) SGK_MRR(true); else SGK_MRR(false);
+    } else if (an) {
+        if (row_side) SGK_MR(false, true, false); else SGK_MR(false, false, false);
     } else if (colpart) {
         if (mask) SGK_MR(true, true, true); else SGK_MR(false, true, true);
     } else if (!mask) {
@@ -775,11 +920,14 @@ hipError_t launch_match_cols(const Top2* colpart, int n, int panels, const int* 
 hipError_t launch_match_finish(const Top2* part, int n, int chunks, const int* row_term,
                                const float* dist, float distmax, float ratiomax, int* out,
                                Top2* best, hipStream_t stream, bool row_side,
-                               const uint8_t* raw_A, const uint8_t* raw_B, int nB) {
+                               const uint8_t* raw_A, const uint8_t* raw_B, int nB,
+                               ColumnList cl) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_match_finish, dim3((n + 255) / 256), dim3(256), 0, stream, part, n,
+    if ((cl.map && !cl.count) || (cl.flag && (!cl.list || !cl.count || cl.map))) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_match_finish, dim3((n + kFinishRows - 1) / kFinishRows), dim3(kFinishThreads), 0,
+                       stream, part, n,
                        chunks, row_term, dist, distmax, ratiomax, out, best, row_side ? 1 : 0,
-                       raw_A, raw_B, nB);
+                       raw_A, raw_B, nB, cl);
     return hipGetLastError();
 }
 

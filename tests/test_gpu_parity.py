@@ -436,6 +436,34 @@ def test_keyless_match_equals_keyed(gpu_ctx, ratiomax):
     assert len(raw[0]) > 5000
 
 
+def test_matched_columns_equal_full_columns(gpu_ctx):
+    """Mutual matching decides only the columns some row matched (a device-side list; the
+    column GEMM takes its rows and their count from it).  Pairs must equal deciding every column
+    (SGPU_DEBUG_FULL_COLUMNS), keyed and keyless, with ratiomax above 1, and where no row or
+    every row matches."""
+    d1 = synth_descriptors(20000, 5000)
+    d2 = synth_descriptors(20000, 5001, base=d1, n_dup=8000)
+    q1t, q2t, _ = synth_tie_scene(3000, 9000, 23, [(200, 129), (130, 2), (4000, 33), (8999, 1)],
+                                  [(60, 61), (1, 2995)])
+    base = quantize(synth_descriptors(400, 5))
+    cases = [(quantize(d1), quantize(d2)), (q1t, q2t),
+             (base, np.concatenate([base, base[:200]])),            # many rows -> one column
+             (base[:130], base[:130].copy()),                       # every row matches
+             (quantize(synth_descriptors(700, 8)), quantize(synth_descriptors(129, 9))),
+             (base[:1], base.copy()), (base.copy(), base[:1])]
+    for flags, ratiomax in ((0, 0.8), (0, 1.0), (gpu_ctx.DEBUG_KEYED_MATCH, 0.8), (0, 1.5)):
+        try:
+            gpu_ctx.set_debug_flags(flags)
+            got = [gpu_ctx.match(a, b, 0.9, ratiomax, 1) for a, b in cases]
+            gpu_ctx.set_debug_flags(flags | gpu_ctx.DEBUG_FULL_COLUMNS)
+            full = [gpu_ctx.match(a, b, 0.9, ratiomax, 1) for a, b in cases]
+        finally:
+            gpu_ctx.set_debug_flags(0)
+        for i, (g, f) in enumerate(zip(got, full)):
+            assert np.array_equal(g, f), (flags, ratiomax, i)
+        assert len(got[0]) > 5000 and len(got[3]) == 130, (flags, ratiomax)
+
+
 @pytest.mark.parametrize("n1,n2,dup", [(1, 700, 0), (700, 1, 0), (257, 1000, 100),
                                        (3000, 2500, 1000), (4096, 4096, 2000), (5000, 129, 50)])
 def test_fused_match_vs_oracle(gpu_ctx, n1, n2, dup):
