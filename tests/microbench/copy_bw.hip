@@ -44,6 +44,40 @@ __global__ void strip_copy2(const float* __restrict__ a, float* __restrict__ b, 
     }
 }
 
+// wave-owned strips (the k_gauss_wave pattern): each wave walks one strip of SW columns over a
+// band of BR rows, float4 per lane (SW / 4 lanes per row, 256 / SW rows per load), 8-row chunks
+// with the next chunk's loads issued before the current chunk's stores
+template <int SW>
+__global__ __launch_bounds__(256) void wave_strip(const float* __restrict__ a, float* __restrict__ b,
+                                                  int W, int H, int BR) {
+    constexpr int LPR = SW / 4;          // lanes per row
+    constexpr int RPL = 64 / LPR;        // rows per load instruction
+    constexpr int LD = 8 / RPL > 0 ? 8 / RPL : 1;   // loads per 8-row chunk
+    const int lane = threadIdx.x & 63;
+    const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int strips = W / SW, bands = (H + BR - 1) / BR;
+    const int sx = gw % strips, rest = gw / strips, band = rest % bands, img = rest / bands;
+    if (img >= 128) return;
+    const float4* s = reinterpret_cast<const float4*>(a + (size_t)img * W * H + sx * SW);
+    float4* d = reinterpret_cast<float4*>(b + (size_t)img * W * H + sx * SW);
+    const int W4 = W / 4, c = lane % LPR, rr = lane / LPR;
+    const int y0 = band * BR, y1 = min(H, y0 + BR);
+    float4 cur[LD], nxt[LD];
+#pragma unroll
+    for (int k = 0; k < LD; k++) cur[k] = s[(size_t)min(y0 + k * RPL + rr, H - 1) * W4 + c];
+    for (int y = y0; y < y1; y += LD * RPL) {
+#pragma unroll
+        for (int k = 0; k < LD; k++) nxt[k] = s[(size_t)min(y + LD * RPL + k * RPL + rr, H - 1) * W4 + c];
+#pragma unroll
+        for (int k = 0; k < LD; k++) {
+            const int yy = y + k * RPL + rr;
+            if (yy < y1) d[(size_t)yy * W4 + c] = cur[k];
+        }
+#pragma unroll
+        for (int k = 0; k < LD; k++) cur[k] = nxt[k];
+    }
+}
+
 int main() {
     const int W = 1920, H = 1080, N = 128;
     const size_t n = (size_t)W * H * N;
@@ -73,5 +107,15 @@ int main() {
     run("copy float grid-stride", [&] { copy1<<<8192, 256>>>(a, b, n); });
     run("strip copy 64 cols f32", [&] { strip_copy<<<N * (W / 64), 256>>>(a, b, W, H); });
     run("strip copy 128 cols f2", [&] { strip_copy2<<<N * (W / 128), 256>>>(a, b, W, H); });
+    for (int br : {270, 540, 1080}) {
+        char nm[64];
+        auto waves = [&](int sw) { return (size_t)N * (W / sw) * ((H + br - 1) / br); };
+        snprintf(nm, sizeof nm, "wave strip 64 cols, %d rows", br);
+        run(nm, [&] { wave_strip<64><<<(waves(64) + 3) / 4, 256>>>(a, b, W, H, br); });
+        snprintf(nm, sizeof nm, "wave strip 128 cols, %d rows", br);
+        run(nm, [&] { wave_strip<128><<<(waves(128) + 3) / 4, 256>>>(a, b, W, H, br); });
+        snprintf(nm, sizeof nm, "wave strip 256 cols, %d rows", br);
+        run(nm, [&] { wave_strip<256><<<(waves(256) + 3) / 4, 256>>>(a, b, W, H, br); });
+    }
     return 0;
 }
