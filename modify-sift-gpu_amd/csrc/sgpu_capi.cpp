@@ -1175,14 +1175,21 @@ int sgpu_match_shard_begin(sgpu_ctx* ctx, const uint8_t* d1, int ns, int row_beg
     ALLOCCHK(ctx, ctx->m_s2.ensure((size_t)n2 * 128));
     const uint8_t* s1 = ctx->m_s1.as<uint8_t>();
     const uint8_t* s2 = ctx->m_s2.as<uint8_t>();
-    HIPCHK(ctx, sgk::launch_to_s8(a, ns, ctx->m_s1.as<uint8_t>(), st));
-    HIPCHK(ctx, sgk::launch_to_s8(b, n2, ctx->m_s2.as<uint8_t>(), st));
-    HIPCHK(ctx, sgk::launch_rowsums(a, ns, row1, 128, 0, st));
+    HIPCHK(ctx, sgk::launch_prep_set(a, ns, ctx->m_s1.as<uint8_t>(), row1, 128, 0, nullptr, 0, st));
+    if (mbm && !fused)
+        HIPCHK(ctx, sgk::launch_prep_set(b, n2, ctx->m_s2.as<uint8_t>(), col2, 128, 0, nullptr, 0, st));
+    else
+        HIPCHK(ctx, sgk::launch_to_s8(b, n2, ctx->m_s2.as<uint8_t>(), st));
+    // the shard's row decisions through the keyless fold as in match_impl; the column side's
+    // per-column (max, row, second) is merged over the ranks, so it needs every column's row
+    // index and stays keyed
+    const bool raw = !(ratiomax > 1.0f) && !(ctx->debug_flags & SGPU_DEBUG_KEYED_MATCH);
     if (mbm && !fused) {
-        HIPCHK(ctx, sgk::launch_match_rows(s1, ns, s2, n2, ca, part, st, nullptr, true));
+        HIPCHK(ctx, sgk::launch_match_rows(s1, ns, s2, n2, ca, part, st, nullptr, true, nullptr,
+                                           nullptr, raw));
         HIPCHK(ctx, sgk::launch_match_finish(part, ns, ca, row1, dist, distmax, ratiomax, match1,
-                                             nullptr, st, true));
-        HIPCHK(ctx, sgk::launch_rowsums(b, n2, col2, 128, 0, st));
+                                             nullptr, st, true, raw ? a : nullptr,
+                                             raw ? b : nullptr, n2));
         HIPCHK(ctx, sgk::launch_match_rows(s2, n2, s1, ns, cb, part, st, nullptr, false));
         HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, col2, dist, distmax, ratiomax, match2,
                                              best2, st, false));
@@ -1194,9 +1201,11 @@ int sgpu_match_shard_begin(sgpu_ctx* ctx, const uint8_t* d1, int ns, int row_beg
         HIPCHK(ctx, sgk::launch_match_cols(colpart, n2, panels, col2, dist, distmax, ratiomax,
                                            match2, best2, st));
     } else {
-        HIPCHK(ctx, sgk::launch_match_rows(s1, ns, s2, n2, ca, part, st, nullptr, true));
+        HIPCHK(ctx, sgk::launch_match_rows(s1, ns, s2, n2, ca, part, st, nullptr, true, nullptr,
+                                           nullptr, raw));
         HIPCHK(ctx, sgk::launch_match_finish(part, ns, ca, row1, dist, distmax, ratiomax, match1,
-                                             nullptr, st, true));
+                                             nullptr, st, true, raw ? a : nullptr,
+                                             raw ? b : nullptr, n2));
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], st));
     HIPCHK(ctx, hipMemcpyAsync(row_match, match1, (size_t)ns * sizeof(int), hipMemcpyDeviceToHost, st));
