@@ -371,24 +371,6 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         // each row still folds its keys in column order, and the first half's reads do not
         // wait on the last MFMAs.
         if constexpr (!COLS) {
-#ifdef SGK_MATCH_EXP_RAW
-            // timing experiment only (wrong indices): raw values, med3 + max per value
-#pragma unroll
-            for (int half = 0; half < 2; half++)
-#pragma unroll
-                for (int rb = 0; rb < 2; rb++)
-#pragma unroll
-                    for (int i = 0; i < 4; i++)
-#pragma unroll
-                        for (int cb = 4 * half; cb < 4 * half + 4; cb++) {
-                            const int key = acc[rb][cb][i];
-#ifndef SGK_MATCH_EXP_MAXONLY
-                            st[rb][i] = med3i(st[rb][i], mt[rb][i], key);
-#endif
-                            mt[rb][i] = max(mt[rb][i], key);
-                        }
-            if (false)
-#endif
 #pragma unroll
             for (int half = 0; half < 2; half++)
 #pragma unroll
