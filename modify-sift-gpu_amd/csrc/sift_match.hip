@@ -441,7 +441,10 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
                 M[rb][i] = m;
                 S[rb][i] = st[rb][i];
             }
-        __syncthreads();
+        // One barrier per tile suffices without COLS: the stores below go to the buffer of tile
+        // t - 1, which every wave finished reading before the barrier that ended iteration t - 1
+        // (COLS: the panel merge reads the other waves' s_cm / s_cs first).
+        if constexpr (COLS) __syncthreads();
         if constexpr (COLS) {
             if (tid < kTile && tb + tid < c_end) {
                 int cm = s_cm[0][tid], cs = s_cs[0][tid];
