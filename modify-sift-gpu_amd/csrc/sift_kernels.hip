@@ -711,16 +711,22 @@ struct ExtremaWaveGrid {
 #ifndef SGK_EXT2_WAVES
 #define SGK_EXT2_WAVES 1
 #endif
-template <int ND>   // ND = number of DoG planes = d + 2
+// CPL = columns per lane.  CPL = 2: lane l holds the column pair x0 - 1 + 2l, x0 + 2l (one 8-byte
+// load per plane and row instead of two 4-byte ones: the texture-address unit, ~88 % busy with
+// 4-byte loads, handles a load per lane whatever its width), 126 tested columns per wave;
+// x0 = 126 sx + 1 keeps the pairs 8-byte aligned.
+template <int ND, int CPL>   // ND = number of DoG planes = d + 2
 __global__ __launch_bounds__(256, SGK_EXT2_WAVES) void k_extrema_wave2(const float* __restrict__ pyr,
                                                        uint32_t* __restrict__ mask,
                                                        uint32_t* __restrict__ row_count,
                                                        const FeatureParams fp,
                                                        const ExtremaWaveGrid eg) {
-    constexpr int RW = 68;                          // ring row: lane l at column l + 1 (+pad)
+    static_assert(CPL == 1 || CPL == 2, "one or two columns per lane");
+    constexpr int TW = 64 * CPL - 2;                // tested columns per wave
+    constexpr int RW = 64 * CPL + 2 * CPL + 2;      // ring row: column index i at i + CPL (+pad)
     constexpr int NJ = ND - 2;
-    __shared__ float s_ring[4][ND][4][RW];          // [wave][plane][row & 3][lane + 1]
-    __shared__ uint16_t s_list[4][NJ * 64];
+    __shared__ __attribute__((aligned(8))) float s_ring[4][ND][4][RW];   // [wave][plane][row & 3][col]
+    __shared__ uint16_t s_list[4][NJ * 64 * CPL];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int gw = blockIdx.x * 4 + wave;
     if (gw >= eg.wave0[fp.n_octaves]) return;       // uniform per wave
@@ -735,89 +741,119 @@ __global__ __launch_bounds__(256, SGK_EXT2_WAVES) void k_extrema_wave2(const flo
     const int nwords = od.nwords;
     const long long rc_base = fp.row_off[o];
     const int W = od.wa, H = od.h;
-    const int strips_x = (W + 61) / 62;
+    const int strips_x = (W + TW - 1) / TW;
     const int id = gw - eg.wave0[o];
     const int sx = id % strips_x, rest = id / strips_x;
     const int sg = rest % eg.nseg[o], b = rest / eg.nseg[o];
-    const int x0 = sx * 62;
+    const int x0 = sx * TW + (CPL - 1);
     const int ys = sg * eg.seg_rows[o], ye = min(H, ys + eg.seg_rows[o]);
     const long long lstride = od.level_stride;
     const float* g0 = pyr + od.gauss_off + (long long)b * W * H;
     float(*ring)[4][RW] = s_ring[wave];
     uint16_t* list = s_list[wave];
 
-    const int x = x0 - 1 + lane;                    // this lane's column
-    const int gx = clampi(x, 0, W - 1);
-    const bool out_lane = lane >= 1 && lane <= 62 && x > 0 && x < W - 1;
-    struct Row { float m[ND + 1]; };
+    // this lane's columns x0 - 1 + CPL * lane + k; CPL = 2 loads the pair from column gx
+    // (even; clamped to W - 2, W is even)
+    const int xl = x0 - 1 + CPL * lane;
+    const int gx = CPL == 1 ? clampi(xl, 0, W - 1) : min(xl, W - 2);
+    bool out_col[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; k++) {
+        const int i = CPL * lane + k, x = xl + k;
+        out_col[k] = i >= 1 && i <= TW && x > 0 && x < W - 1;
+    }
+    struct Row { float m[ND + 1][CPL]; };
     Row rA, rB;
     auto fetch = [&](Row& r, int y) {   // G row y (clamped) into registers
         const float* q = g0 + (long long)clampi(y, 0, H - 1) * W + gx;
 #pragma unroll
-        for (int m = 0; m <= ND; m++) r.m[m] = q[m * lstride];
+        for (int m = 0; m <= ND; m++) {
+            if constexpr (CPL == 1) {
+                r.m[m][0] = q[m * lstride];
+            } else {
+                const float2 v = *reinterpret_cast<const float2*>(q + m * lstride);
+                r.m[m][0] = v.x;
+                r.m[m][1] = v.y;
+            }
+        }
     };
     // Lanes exchange values through the wave-private ring and list.  LDS accesses of one wave
     // complete in issue order, but the compiler sees only per-lane addresses (a lane writes
-    // column lane + 1 and reads lane .. lane + 2) and may reorder them: the empty asm
-    // statements keep every write before the reads that follow it.
+    // its columns and reads its neighbours') and may reorder them: the empty asm statements keep
+    // every write before the reads that follow it.
     // DoG row y into the ring (read by key_test for the rare candidates) and into dog[] (the
     // row max/min below take the neighbours' values by DPP wave shifts, not from LDS)
-    float dog[ND];
+    float dog[ND][CPL];
     auto put = [&](const Row& r, int y) {
-        float* rr = &ring[0][y & 3][lane + 1];
+        float* rr = &ring[0][y & 3][CPL * lane + CPL];
 #pragma unroll
         for (int m = 0; m < ND; m++) {
-            dog[m] = r.m[m + 1] - r.m[m];
-            rr[m * 4 * RW] = dog[m];
+#pragma unroll
+            for (int k = 0; k < CPL; k++) dog[m][k] = r.m[m + 1][k] - r.m[m][k];
+            if constexpr (CPL == 1)
+                rr[m * 4 * RW] = dog[m][0];
+            else
+                *reinterpret_cast<float2*>(&rr[m * 4 * RW]) = make_float2(dog[m][0], dog[m][1]);
         }
         asm volatile("" ::: "memory");
     };
-    // rolling 3-wide row max/min of DoG rows y-1 and y (per plane), refreshed per step; lanes 0
-    // and 63 get a neighbour from outside the wave (0) and are never tested
-    float hx0[ND], hn0[ND], hx1[ND], hn1[ND], cvx[ND];
-    auto rowmm = [&](float* mx, float* mn, float* cv) {   // of the row in dog[]
+    // rolling 3-wide row max/min of DoG rows y-1 and y (per plane), refreshed per step; the
+    // wave's first and last columns get a neighbour from outside the wave (0) and are never
+    // tested
+    float hx0[ND][CPL], hn0[ND][CPL], hx1[ND][CPL], hn1[ND][CPL], cvx[ND][CPL];
+    auto rowmm = [&](float (*mx)[CPL], float (*mn)[CPL], float (*cv)[CPL]) {   // of dog[]
 #pragma unroll
         for (int m = 0; m < ND; m++) {
-            const float c = dog[m];
-            const float a = __int_as_float(__builtin_amdgcn_update_dpp(
-                0, __float_as_int(c), 0x138, 0xf, 0xf, false));   // wave_shr:1, lane - 1
-            const float e = __int_as_float(__builtin_amdgcn_update_dpp(
-                0, __float_as_int(c), 0x130, 0xf, 0xf, false));   // wave_shl:1, lane + 1
-            mx[m] = fmax_(fmax_(a, c), e);
-            mn[m] = fmin_(fmin_(a, c), e);
-            if (cv) cv[m] = c;
+            float v[CPL + 2];   // columns left of, in and right of this lane's
+#pragma unroll
+            for (int k = 0; k < CPL; k++) v[k + 1] = dog[m][k];
+            v[0] = __int_as_float(__builtin_amdgcn_update_dpp(
+                0, __float_as_int(dog[m][CPL - 1]), 0x138, 0xf, 0xf, false));   // wave_shr:1
+            v[CPL + 1] = __int_as_float(__builtin_amdgcn_update_dpp(
+                0, __float_as_int(dog[m][0]), 0x130, 0xf, 0xf, false));         // wave_shl:1
+#pragma unroll
+            for (int k = 0; k < CPL; k++) {
+                mx[m][k] = fmax_(fmax_(v[k], v[k + 1]), v[k + 2]);
+                mn[m][k] = fmin_(fmin_(v[k], v[k + 1]), v[k + 2]);
+                if (cv) cv[m][k] = v[k + 1];
+            }
         }
     };
     auto body = [&](int y) {   // test row y: DoG rows y-1, y are rolled, y+1 is in dog[]
-        float hx2[ND], hn2[ND], cnx[ND];
+        float hx2[ND][CPL], hn2[ND][CPL], cnx[ND][CPL];
         rowmm(hx2, hn2, cnx);
-        const bool interior = out_lane && y < ye && y > 0 && y < H - 1;
+        const bool row_ok = y < ye && y > 0 && y < H - 1;
         int ncand = 0;
 #pragma unroll
         for (int j = 0; j < NJ; j++) {
-            const float v = cvx[j + 1];
-            float mx = hx0[j], mn = hn0[j];
 #pragma unroll
-            for (int m = j; m < j + 3; m++) {
-                mx = fmax_(mx, fmax_(fmax_(hx0[m], hx1[m]), hx2[m]));
-                mn = fmin_(mn, fmin_(fmin_(hn0[m], hn1[m]), hn2[m]));
+            for (int k = 0; k < CPL; k++) {
+                const float v = cvx[j + 1][k];
+                float mx = hx0[j][k], mn = hn0[j][k];
+#pragma unroll
+                for (int m = j; m < j + 3; m++) {
+                    mx = fmax_(mx, fmax_(fmax_(hx0[m][k], hx1[m][k]), hx2[m][k]));
+                    mn = fmin_(mn, fmin_(fmin_(hn0[m][k], hn1[m][k]), hn2[m][k]));
+                }
+                const bool cand = row_ok && out_col[k] && fabs_(v) > fp.t0 && (v >= mx || v <= mn);
+                const unsigned long long bal = __ballot(cand);
+                if (cand) {
+                    const int pos = ncand + __builtin_amdgcn_mbcnt_hi(
+                                                (uint32_t)(bal >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                    list[pos] = (uint16_t)((j << 7) | (CPL * lane + k));
+                }
+                ncand += __popcll(bal);
             }
-            const bool cand = interior && fabs_(v) > fp.t0 && (v >= mx || v <= mn);
-            const unsigned long long bal = __ballot(cand);
-            if (cand) {
-                const int pos = ncand + __builtin_amdgcn_mbcnt_hi(
-                                            (uint32_t)(bal >> 32),
-                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                list[pos] = (uint16_t)((j << 6) | lane);
-            }
-            ncand += __popcll(bal);
         }
         asm volatile("" ::: "memory");
         for (int c0 = 0; c0 < ncand; c0 += 64) {
             if (c0 + lane < ncand) {
                 const int code = list[c0 + lane];
-                const int j = code >> 6, cl = code & 63;
-                auto get = [&](int m, int r, int c) { return ring[j + m][(y + r - 1) & 3][cl + c]; };
+                const int j = code >> 7, cl = code & 127;
+                auto get = [&](int m, int r, int c) {
+                    return ring[j + m][(y + r - 1) & 3][cl + c - 1 + CPL];
+                };
                 if (key_test(get, fp.t0, fp.t, fp.edge, fp.subpixel).result != 0.f) {
                     const int xx = x0 - 1 + cl;
                     uint32_t* mrow = mask + mask_off + j * mask_lstride +
@@ -829,11 +865,13 @@ __global__ __launch_bounds__(256, SGK_EXT2_WAVES) void k_extrema_wave2(const flo
             }
         }
 #pragma unroll
-        for (int m = 0; m < ND; m++) {
-            hx0[m] = hx1[m]; hn0[m] = hn1[m];
-            hx1[m] = hx2[m]; hn1[m] = hn2[m];
-            cvx[m] = cnx[m];
-        }
+        for (int m = 0; m < ND; m++)
+#pragma unroll
+            for (int k = 0; k < CPL; k++) {
+                hx0[m][k] = hx1[m][k]; hn0[m][k] = hn1[m][k];
+                hx1[m][k] = hx2[m][k]; hn1[m][k] = hn2[m][k];
+                cvx[m][k] = cnx[m][k];
+            }
         asm volatile("" ::: "memory");   // this row's list and ring reads before the next writes
     };
     fetch(rA, ys - 1);
@@ -2044,8 +2082,17 @@ hipError_t launch_first_octave_input(const float* src, const uint8_t* src_u8, in
 
 hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
                           const FeatureParams& fp, hipStream_t stream) {
-    // one wave per (image, strip of tested columns, row segment); ~32k waves in all
-    const int sw = 62;
+    // one wave per (image, strip of tested columns, row segment); ~32k waves in all.  Two
+    // columns per lane when every plane is 8-byte aligned (always, for pyramid levels: widths
+    // are multiples of 4)
+#ifndef SGK_EXT_CPL
+#define SGK_EXT_CPL 2
+#endif
+    bool pairs = SGK_EXT_CPL == 2 && ((uintptr_t)pyr % 8) == 0;
+    for (int o = 0; o < fp.n_octaves; o++)
+        pairs = pairs && fp.oct[o].wa % 2 == 0 && fp.oct[o].gauss_off % 2 == 0 &&
+                fp.oct[o].level_stride % 2 == 0 && ((long long)fp.oct[o].wa * fp.oct[o].h) % 2 == 0;
+    const int sw = pairs ? 126 : 62;
     ExtremaWaveGrid eg{};
     int nw = 0;
     for (int o = 0; o < fp.n_octaves; o++) {
@@ -2063,8 +2110,12 @@ hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
     }
     eg.wave0[fp.n_octaves] = nw;
     const unsigned nb = (unsigned)((nw + 3) / 4);
-    switch (fp.d + 2) {
-#define SGK_EXTW(ND)     case ND: hipLaunchKernelGGL((k_extrema_wave2<ND>), dim3(nb), dim3(256), 0, stream, pyr, mask, row_count, fp, eg); break;
+    switch ((fp.d + 2) * 2 + (pairs ? 1 : 0)) {
+#define SGK_EXTW(ND)                                                                             \
+    case 2 * ND: hipLaunchKernelGGL((k_extrema_wave2<ND, 1>), dim3(nb), dim3(256), 0, stream, pyr, \
+                                    mask, row_count, fp, eg); break;                             \
+    case 2 * ND + 1: hipLaunchKernelGGL((k_extrema_wave2<ND, 2>), dim3(nb), dim3(256), 0, stream,  \
+                                        pyr, mask, row_count, fp, eg); break;
         SGK_EXTW(3) SGK_EXTW(4) SGK_EXTW(5) SGK_EXTW(6) SGK_EXTW(7) SGK_EXTW(8)
         default: return hipErrorInvalidValue;
 #undef SGK_EXTW
