@@ -71,9 +71,13 @@ __global__ __launch_bounds__(256) void k_rowsum(const uint8_t* __restrict__ d, i
 // Column chunks of one launch: ~4096 workgroups (about 5 per resident slot at 3 per CU) so
 // that the last wave of workgroups is a small tail; each chunk at least two tiles wide.  Also
 // evaluated on the device for a row count that only the device knows (compacted rows).
+#ifndef SGK_MATCH_WG
+#define SGK_MATCH_WG 4096
+#endif
+constexpr int kMatchWg = SGK_MATCH_WG;   // workgroups aimed at per launch (tuning knob)
 __host__ __device__ inline int chunks_for(int nA, int nB) {
     const int panels = (nA + kPanel - 1) / kPanel;
-    const int chunks = (4096 + panels - 1) / panels;
+    const int chunks = (kMatchWg + panels - 1) / panels;
     const int max_chunks = max(1, (nB + 2 * kTile - 1) / (2 * kTile));
     return max(1, min(chunks, max_chunks));
 }
@@ -845,12 +849,12 @@ int match_chunks(int nA, int nB) { return chunks_for(nA, nB); }
 size_t match_part_bound(int nA, int nB) {
     const size_t panels = (nA + kPanel - 1) / kPanel;
     const size_t max_chunks = std::max(1, (nB + 2 * kTile - 1) / (2 * kTile));
-    return std::min((4096 + panels) * kPanel, max_chunks * (size_t)nA);
+    return std::min((kMatchWg + panels) * kPanel, max_chunks * (size_t)nA);
 }
 static unsigned match_grid_bound(int nA, int nB) {
     const size_t panels = (nA + kPanel - 1) / kPanel;
     const size_t max_chunks = std::max(1, (nB + 2 * kTile - 1) / (2 * kTile));
-    return (unsigned)std::min(4096 + panels, max_chunks * panels);
+    return (unsigned)std::min(kMatchWg + panels, max_chunks * panels);
 }
 
 int match_panels(int nA) { return (nA + kPanel - 1) / kPanel; }
