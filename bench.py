@@ -76,6 +76,8 @@ def main():
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the host-in / host-out (PCIe-inclusive) sub-measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c2", action="store_true",
+                    help="skip the single-image drop-in API measurement (speed.cpp protocol)")
     ap.add_argument("--no-match", action="store_true")
     ap.add_argument("--match-n", type=int, default=50000)
     ap.add_argument("--dist-backend", default="rccl", choices=["rccl", "gloo"],
@@ -104,6 +106,11 @@ def main():
     n_dev = sgpu.device_count()
     dist = None
     device = local
+    if args.dist_backend == "rccl" and (n_dev < world or local >= n_dev):
+        # one GPU per rank (MultiThreadSIFT.cpp:141-155 binds one device per worker): fail here,
+        # before any rendezvous, instead of leaving the peers waiting in the RCCL init
+        sys.exit(f"bench.py: rank {rank}: {n_dev} GPU(s) visible, {world} ranks need one each "
+                 f"(--dist-backend gloo rehearses several ranks on one GPU)")
     if world > 1:
         import torch.distributed as dist  # noqa: F811
         # gloo announces its peers on stdout; keep stdout for the one JSON line
@@ -221,7 +228,8 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE + WRITE_SIZE)",
+            "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x the calibrated "
+                            "read factor + WRITE_SIZE x the write factor)",
             "traffic_source": prof_note,
             "algorithmic_bytes_per_launch": 48.0 * sumN * B / n_gauss,
             "avg_launch_ms": pyr_ms / args.steps / n_gauss,
@@ -253,7 +261,10 @@ def main():
         sm = bench_match_sharded(ctx, args.match_n, rank, world, None if rccl else dist)
         if rank == 0:
             result["match_sharded"] = sm
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and args.workload == "c3" and not args.no_c2:
+        result["c2"] = bench_c2(cpu=not args.no_cpu_baseline)
+    if rank == 0 and not args.no_cpu_baseline:
+        # rank 0 on the host cores beside its GPU work, for every N (the line is self-contained)
         result["cpu_baseline"] = cpu_baseline(imgs, opts)
     if rank == 0:
         print(json.dumps(result))
@@ -264,7 +275,10 @@ def main():
 
 def profiled_traffic(B, W, H, octaves):
     """HBM bytes per Gaussian launch from the committed rocprofv3 summary of this workload
-    (tests/profile_kernels.sh + tests/pmc_summary.py), or None when no summary matches."""
+    (tests/profile_kernels.sh + tests/pmc_summary.py), or None when no summary matches.  The
+    summary's FETCH_SIZE / WRITE_SIZE are corrected per access width with the committed
+    calibration (tests/pmc_calib.sh; MI355X_MICROARCH.md: FETCH_SIZE counts 1/2 of a 16-B-per-lane
+    streaming read): "hbm_bytes_per_extract" when the summary carries it."""
     import glob
     if (B, W, H, octaves) != (128, 1920, 1080, 4):
         return None, "no profile for this workload"
@@ -272,13 +286,15 @@ def profiled_traffic(B, W, H, octaves):
     for path in reversed(files):
         try:
             s = json.load(open(path))
+            if "hbm_bytes_per_extract" not in s:
+                continue
             fams = [f for f in s["launches_per_extract"] if f.startswith("k_gauss")]
             n = sum(s["launches_per_extract"][f] for f in fams)
-            b = sum(s["fetch_bytes_per_extract"][f] + s["write_bytes_per_extract"][f] for f in fams)
+            b = sum(s["hbm_bytes_per_extract"][f] for f in fams)
             return b / n, os.path.relpath(path, ROOT)
         except (KeyError, ValueError, OSError):
             continue
-    return None, "no profile summary committed"
+    return None, "no calibrated profile summary committed"
 
 
 def bench_match(ctx, n, cpu=True):
@@ -381,6 +397,9 @@ def bench_c4(ctx, batch=16, steps=3, cpu=True):
                                    "sample": f"{threads} of the staged 4096x4096 tiles (-no 6), "
                                              f"one per OpenMP thread, oracle/liboracle.so",
                                    "features_per_image": cf / threads}
+            s1, _ = oracle_py.bench_extract(imgs[:1], opts, threads=1)
+            out["cpu_baseline"]["one_thread"] = {"value": 1.0 / s1, "unit": "images/s",
+                                                 "cores": 1, "sample": "tile 0, one thread"}
         return out
     finally:
         c4.close()
@@ -471,6 +490,45 @@ def bench_match_sharded(ctx, n, rank, world, host_dist=None):
         # a status flag) before its all-gather, and the timing all-reduces above run only after
         # every rank's match returned
         return {"error": str(ex)}
+
+
+def bench_c2(repeat=30, cpu=True):
+    """BASELINE configs[1]: one 1920x1080 image through the drop-in C++ API, TestWin/speed.cpp's
+    protocol (speed.cpp:60-155): bin/speed_replica (SiftGPU.h, directly linked) loads the PGM
+    once, warms up, then times `repeat` x RunSIFT() -- host image in, keys and descriptors back in
+    the object's host buffers, as the reference's RunSIFT -- and `repeat` more for the per-stage
+    _timing slots.  The child process shares the GPU with this (idle) one."""
+    import subprocess
+    import tempfile
+    from sift_synth import synth_image
+    exe = os.path.join(ROOT, "modify-sift-gpu_amd", "bin", "speed_replica")
+    img = synth_image(1920, 1080, 2000)       # SURVEY.md 8(d): C2 seed 2000
+    try:
+        with tempfile.TemporaryDirectory() as td:
+            pgm = os.path.join(td, "c2.pgm")
+            with open(pgm, "wb") as f:
+                f.write(b"P5\n1920 1080\n255\n" + img.tobytes())
+            r = subprocess.run([exe, str(repeat), "--", "-i", pgm, "-fo", "0", "-no", "4", "-d", "3"],
+                               capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            return {"error": f"speed_replica exit {r.returncode}: {r.stderr[-300:]}"}
+        sp = json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as ex:   # never costs the main measurement
+        return {"error": str(ex)}
+    out = {"workload": "C2: one 1920x1080 u8 PGM, -fo 0 -no 4 -d 3, SiftGPU::RunSIFT() through "
+                       "include/SiftGPU.h (TestWin/speed.cpp protocol, bin/speed_replica)",
+           "value": 1e3 / sp["avg_ms"], "unit": "images/s", "ms_per_image": sp["avg_ms"],
+           "features": sp["features"], "repeat": sp["repeat"], "stable": sp["stable"],
+           "timing_ms": sp["timing_ms"],
+           "note": "host image in, features in the object's host buffers; _timing slots as "
+                   "SiftGPU.cpp:368 / speed.cpp:147-153"}
+    if cpu:
+        import oracle_py
+        secs, feats = oracle_py.bench_extract(img[None], default_options(octave_num=4), threads=1)
+        out["cpu_baseline"] = {"value": 1.0 / secs, "unit": "images/s", "cores": 1, "kind": "port",
+                               "sample": "the same image, one thread, oracle/liboracle.so",
+                               "ms_per_image": secs * 1e3, "features": int(feats)}
+    return out
 
 
 def cpu_baseline(imgs, opts):

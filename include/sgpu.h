@@ -215,7 +215,8 @@ void sgpu_quantize_descriptors(const float* d, size_t count, uint8_t* out);
 /* Timing of the last call: stage times in milliseconds measured with HIP events
  * (SiftGPU::_timing, SiftPyramid.cpp:48-56).  times[0..7] =
  * {upload, pyramid, detect, orientation, expand, descriptor, download, total} of the last
- * extract; times[8] = the last sgpu_match call. */
+ * extract; times[8] = the last sgpu_match call; times[9] = the feature-list (row scan) part of
+ * detect.  SiftGPU::_timing[2..8] map them to the reference's slots (siftgpu_api.cpp). */
 int sgpu_last_timing(const sgpu_ctx* ctx, float* times, int n);
 
 /* ---- multi-GPU batch driver (no reference counterpart: the reference

@@ -48,7 +48,11 @@ struct DevBuf {
     template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-enum { T_UPLOAD, T_PYRAMID, T_DETECT, T_ORIENT, T_EXPAND, T_DESC, T_DOWNLOAD, T_TOTAL, T_MATCH, T_N };
+// stage timings (sgpu_last_timing): T_DETECT spans the extremum kernel and the row scan (the
+// reference's "Detection" and "Feature List" stages, SiftPyramid.cpp:107,123); T_LIST is the
+// row-scan part of it
+enum { T_UPLOAD, T_PYRAMID, T_DETECT, T_ORIENT, T_EXPAND, T_DESC, T_DOWNLOAD, T_TOTAL, T_MATCH,
+       T_LIST, T_N };
 
 // One part of a batch: consecutive images [img0, img0 + n) with their own stream and buffers.
 struct Part {
@@ -56,7 +60,7 @@ struct Part {
     hipStream_t stream_lo = nullptr;   // low priority: orientation, descriptors, readback
     size_t cand_hint = 0, feat_hint = 0;   // counts of the previous call (launch-grid sizing)
     hipEvent_t ev[10] = {};  // start, pyramid, detect, orientation, expand, descriptor, end,
-                             // octave-1 base ready, octaves >= 1 done, (spare)
+                             // extrema done (before the row scan), (spare), (spare)
     int img0 = 0, n = 0;
     sgk::FeatureParams fp{};
     int total_rows = 0;
@@ -403,7 +407,11 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
                       ? std::max<size_t>(pt.cand_cap, 64)
                       : std::max(pt.cand_cap, std::max<size_t>(1024, sum_px / 256 * n));
     const size_t nc = pt.cand_cap, ne_cap = 2 * nc;
-    // + 256 B: the descriptor's vector loads may read a few floats past a plane's last row
+    // + 256 B: the descriptor's 16-byte strip loads may read up to 4 floats past the end of a
+    // row (k_descriptor_fast).  Invariant: every strip it loads starts at a sample of the
+    // feature's box, which is clamped to columns 1 .. W-2 and rows 1 .. H-2 of the plane for any
+    // keypoint (detected or caller-supplied), and an empty box loads at row 1, column 1; so the
+    // overshoot past the last plane is at most 5 floats, whatever the keypoint.
     ALLOCCHK(ctx, pt.pyr.ensure((size_t)goff * sizeof(float) + 256));
     ALLOCCHK(ctx, pt.mask.ensure((size_t)moff * sizeof(uint32_t)));
     ALLOCCHK(ctx, pt.row_count.ensure((size_t)pt.total_rows * sizeof(uint32_t)));
@@ -498,6 +506,7 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     if (O.feature_count_threshold > 0)   // -tc: GenerateFeatureList skip + LimitFeatureCount(0)
         HIPCHK(ctx, sgk::launch_limit_rows(pt.row_count.as<uint32_t>(), fp,
                                            O.feature_count_threshold, O.truncate_method, st));
+    HIPCHK(ctx, hipEventRecord(pt.ev[7], st));
     HIPCHK(ctx, sgk::launch_scan(pt.row_count.as<uint32_t>(), pt.row_base.as<uint32_t>(),
                                  pt.total_rows, pt.scan_tmp.as<uint32_t>(), st));
     HIPCHK(ctx, hipEventRecord(pt.ev[2], st));
@@ -581,9 +590,26 @@ static int plan_batch(sgpu_ctx* ctx, int n, int w, int h) {
     return SGPU_OK;
 }
 
-static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, int w, int h,
-                        int stride, int flags, int color = 0) {
-    if (!ctx) return SGPU_EINVAL;
+// After a failed extract nothing may still be queued that reads the caller's input or writes
+// the caller's outputs, and no per-image query may read the previous extract's offsets (the
+// batch geometry was already replaced): wait for every stream of the context, then forget the
+// batch.
+static int abandon_batch(sgpu_ctx* ctx, int rc) {
+    for (hipStream_t st : {ctx->stream, ctx->h2d, ctx->d2h})
+        if (st) (void)hipStreamSynchronize(st);
+    for (Part& pt : ctx->part) {
+        if (pt.stream) (void)hipStreamSynchronize(pt.stream);
+        if (pt.stream_lo) (void)hipStreamSynchronize(pt.stream_lo);
+        pt.img_off.clear();
+    }
+    ctx->batch = 0;
+    ctx->img_off.clear();
+    ctx->gathered = false;
+    return rc;
+}
+
+static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, int w, int h,
+                        int stride, int flags, int color) {
     const bool staged = (flags & SGPU_INPUT_STAGED) != 0;
     const int channels = color == SGPU_RGB || color == SGPU_BGR ? 3 : color ? 4 : 1;
     if ((!images && !staged) || n <= 0 || w < 8 || h < 8 || stride < w * channels)
@@ -696,12 +722,20 @@ static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
     (void)hipEventElapsedTime(&ctx->timing[T_UPLOAD], ctx->ev[0], ctx->ev[1]);
     (void)hipEventElapsedTime(&ctx->timing[T_PYRAMID], p0.ev[0], p0.ev[1]);
     (void)hipEventElapsedTime(&ctx->timing[T_DETECT], p0.ev[1], p0.ev[2]);
+    (void)hipEventElapsedTime(&ctx->timing[T_LIST], p0.ev[7], p0.ev[2]);
     (void)hipEventElapsedTime(&ctx->timing[T_ORIENT], p0.ev[2], p0.ev[3]);
     (void)hipEventElapsedTime(&ctx->timing[T_EXPAND], p0.ev[3], p0.ev[4]);
     (void)hipEventElapsedTime(&ctx->timing[T_DESC], p0.ev[4], p0.ev[5]);
     (void)hipEventElapsedTime(&ctx->timing[T_DOWNLOAD], p0.ev[5], p0.ev[6]);
     (void)hipEventElapsedTime(&ctx->timing[T_TOTAL], ctx->ev[0], ctx->part[np - 1].ev[6]);
     return SGPU_OK;
+}
+
+static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, int w, int h,
+                        int stride, int flags, int color = 0) {
+    if (!ctx) return SGPU_EINVAL;
+    const int rc = extract_body(ctx, images, is_f32, n, w, h, stride, flags, color);
+    return rc == SGPU_OK ? rc : abandon_batch(ctx, rc);
 }
 
 // Host-in / host-out extraction of a stream of batches: SiftGPU::RunSIFT(w, h, data) per image
@@ -713,10 +747,9 @@ static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
 // in order (batch k+1's pyramid waits for batch k's last kernel), so every batch sees the whole
 // GPU as in sgpu_extract.  One host wait per batch: the small count readback of batch k-1, needed
 // to size its download, happens after batch k is queued.
-int sgpu_extract_stream(sgpu_ctx* ctx, const uint8_t* const* batches, int nbatches, int batch,
-                        int w, int h, int stride, float* keys, float* desc, int64_t cap,
-                        int32_t* counts) {
-    if (!ctx) return SGPU_EINVAL;
+static int extract_stream_body(sgpu_ctx* ctx, const uint8_t* const* batches, int nbatches,
+                               int batch, int w, int h, int stride, float* keys, float* desc,
+                               int64_t cap, int32_t* counts) {
     if (!batches || nbatches <= 0 || batch <= 0 || w < 8 || h < 8 || stride < w || !counts ||
         cap < 0)
         return ctx->fail(SGPU_EINVAL, "bad stream arguments");
@@ -826,10 +859,19 @@ int sgpu_extract_stream(sgpu_ctx* ctx, const uint8_t* const* batches, int nbatch
     rc = finish(nbatches - 1);
     if (rc != SGPU_OK) return rc;
     HIPCHK(ctx, hipStreamSynchronize(ctx->d2h));
-    // the per-image queries (sgpu_copy_features, ...) have no "last batch" after a stream
-    ctx->batch = 0;
-    ctx->img_off.clear();
     return result;
+}
+
+int sgpu_extract_stream(sgpu_ctx* ctx, const uint8_t* const* batches, int nbatches, int batch,
+                        int w, int h, int stride, float* keys, float* desc, int64_t cap,
+                        int32_t* counts) {
+    if (!ctx) return SGPU_EINVAL;
+    const int rc = extract_stream_body(ctx, batches, nbatches, batch, w, h, stride, keys, desc,
+                                       cap, counts);
+    // on success as on failure: every copy from the caller's batches and into the caller's
+    // outputs has completed, and the per-image queries (sgpu_copy_features, ...) have no "last
+    // batch" after a stream
+    return abandon_batch(ctx, rc);
 }
 
 void* sgpu_host_alloc(size_t bytes) {

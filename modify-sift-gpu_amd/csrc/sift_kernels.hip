@@ -1775,7 +1775,10 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
     if (ncols > 0) next_row(); else r = nrows;
     c = lo;
     f4v na, nb, nu, nd;
-    uint32_t npo = 4u * (uint32_t)(iymin * W + ixmin);   // a valid address when nothing is left
+    // the address loaded when no sample is left: row 1, column 1 of the plane, whose 4 loads
+    // (columns 0 .. 5 of row 1, columns 1 .. 4 of rows 0 and 2) stay inside it for any feature --
+    // a caller keypoint far outside the image has an empty box and unbounded ixmin / iymin
+    uint32_t npo = 4u * (uint32_t)(W + 1);
     auto fetch = [&]() {
         if (r < nrows) npo = 4u * (uint32_t)((iymin + r) * W + ixmin + c);
         na = ld4(npo - 4u);            // x-1 .. x+2

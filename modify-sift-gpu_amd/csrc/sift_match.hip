@@ -41,19 +41,12 @@ constexpr int kMatchSplit = 2;   // 126 VGPRs: 4 waves per SIMD (one group of 8:
 static_assert(kMatchSplit == 1 || kMatchSplit == 2, "1 or 2 column groups");
 
 // v_med3_i32: the median of three.  With s <= m, med3(s, m, v) is the new second maximum after
-// seeing v (v > m -> m; s < v <= m -> v; v <= s -> s).
+// seeing v (v > m -> m; s < v <= m -> v; v <= s -> s).  Written as min / max, which LLVM selects
+// as one v_med3_i32 -- compiler-visible, so the hazard recognizer inserts the wait states an
+// MFMA result needs before it is read (an inline-asm v_med3 hid that read from it and lost
+// matches in rows 4q+1, 4q+2; round 2).
 __device__ __forceinline__ int med3i(int a, int b, int c) {
-    int r;
-    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-// The same, ordered after `after` (an unused operand): the hazard recognizer does not look
-// into inline asm, so an asm that reads an MFMA result must come after a compiler-visible
-// instruction that read it first (that one gets the required wait states).
-__device__ __forceinline__ int med3i_after(int a, int b, int c, int after) {
-    int r;
-    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c), "v"(after));
-    return r;
+    return max(min(a, b), min(max(a, b), c));
 }
 
 __global__ __launch_bounds__(256) void k_rowsum(const uint8_t* __restrict__ d, int n,
@@ -326,8 +319,8 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
                             for (int c = 4 * g; c < 4 * g + 4; c++) {
                                 const int v = acc[rb][c][i];
                                 const int mo = mt[rb][i];
-                                mt[rb][i] = max(mo, v);   // the first read of v: compiler-visible
-                                st[rb][i] = med3i_after(st[rb][i], mo, v, mt[rb][i]);
+                                mt[rb][i] = max(mo, v);
+                                st[rb][i] = med3i(st[rb][i], mo, v);
                             }
             }
         } else {

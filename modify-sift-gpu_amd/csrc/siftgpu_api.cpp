@@ -10,6 +10,7 @@
 //   * image files: PGM/PPM (P2/P3/P5/P6) as the reference's SIFTGPU_NO_DEVIL loader
 //     (GLTexImage.cpp:1128-1189); DevIL formats are not available.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -54,6 +55,9 @@ struct Runtime {
     std::vector<float> pending;
     int pending_orientation = 1;
     bool have_image = false;    // a pyramid of the current image exists on the device
+    // host seconds of the last image load / conversion (SiftGPU::_timing[0], SiftGPU.cpp:249,328)
+    // and of the last feature downloads (keys: _timing[7], descriptors: part of _timing[8])
+    float t_load = 0.f, t_keys = 0.f, t_desc = 0.f;
     Runtime() { sgpu_default_options(&opt); }
 };
 
@@ -64,6 +68,10 @@ HostImage* IMG(GLTexInput* p) { return reinterpret_cast<HostImage*>(p); }
 ImageListImpl* LIST(ImageList* p) { return reinterpret_cast<ImageListImpl*>(p); }
 
 constexpr int kMaxPath = 4096;
+
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 // GLTexInput::LoadImageFile, SIFTGPU_NO_DEVIL branch (GLTexImage.cpp:1128-1189).
 bool load_pnm(const char* path, HostImage* img) {
@@ -352,13 +360,21 @@ void SiftGPU::SetKeypointList(int num, const SiftKeypoint* keys, int keys_have_o
     rt->pending_orientation = keys_have_orientation;
 }
 
-// Copy the context's current features (image 0) into the object's host buffers.
+// Copy the context's current features (image 0) into the object's host buffers: the keys
+// (the reference's DownloadKeypoints stage) and then the descriptors (downloaded inside its
+// GetFeatureDescriptors stage, PyramidCU.cpp:434), each timed on the host.
 static int fetch_features(Runtime* rt) {
     rt->feature_num = sgpu_feature_count(rt->ctx, 0);
     rt->keys.resize((size_t)rt->feature_num * 4);
     rt->desc.resize(rt->opt.descriptors ? (size_t)rt->feature_num * 128 : 0);
-    return sgpu_copy_features(rt->ctx, 0, rt->keys.data(),
-                              rt->opt.descriptors ? rt->desc.data() : nullptr);
+    const double t0 = now_s();
+    int rc = sgpu_copy_features(rt->ctx, 0, rt->keys.data(), nullptr);
+    const double t1 = now_s();
+    if (rc == SGPU_OK && rt->opt.descriptors)
+        rc = sgpu_copy_features(rt->ctx, 0, nullptr, rt->desc.data());
+    rt->t_keys = (float)(t1 - t0);
+    rt->t_desc = (float)(now_s() - t1);
+    return rc;
 }
 
 // Descriptors of a keypoint list on the current image (SiftGPU::RunSIFT(num, keys, ...)).
@@ -445,7 +461,9 @@ int SiftGPU::RunSIFT(int width, int height, const void* data, unsigned int gl_fo
     if (!_initialized) return 0;
     if (width <= 0 || height <= 0 || !data) return 0;
     _imgpath[0] = 0;
+    const double t0 = now_s();
     if (!set_image(IMG(_texImage), width, height, data, gl_format, gl_type)) return 0;
+    RT(_pyramid)->t_load = (float)(now_s() - t0);
     _image_loaded = 2;
     return RunSIFT();
 }
@@ -457,11 +475,15 @@ int SiftGPU::RunSIFT() {
     Runtime* rt = RT(_pyramid);
     HostImage* img = IMG(_texImage);
     if (_image_loaded == 0) {
+        const double t0 = now_s();
         if (!load_pnm(_imgpath, img)) {
             std::cerr << "Unable to open image " << _imgpath << "\n";
             return 0;
         }
+        rt->t_load = (float)(now_s() - t0);
         _image_loaded = 1;
+    } else if (_image_loaded == 1) {
+        rt->t_load = 0.f;   // the file is already loaded (SiftGPU.cpp:348-351)
     }
     const int ch = img->color == SGPU_RGB || img->color == SGPU_BGR ? 3 : 4;
     int rc = img->is_float
@@ -487,13 +509,25 @@ int SiftGPU::RunSIFT() {
     } else if (fetch_features(rt) != SGPU_OK) {
         return 0;
     }
-    float t[9] = {0};
-    sgpu_last_timing(rt->ctx, t, 9);
+    // SiftGPU::_timing in the reference's slots, seconds (SiftGPU.cpp:249-255,328-351,368 ->
+    // SiftPyramid::_timing[0..7], SiftPyramid.cpp:107,123,145,155,180,200,212; printed by
+    // TestWin/speed.cpp:147-153): [0] load/convert the image on the host, [1] initialise the
+    // pyramid (planned inside the extract here: 0), [2] build pyramid (with its input upload,
+    // as ConvertInputToCU in BuildPyramid), [3] detection, [4] feature list, [5] orientation,
+    // [6] multi-orientation feature list, [7] download keys, [8] descriptors (kernel + their
+    // download), [9] display VBO (none: 0).  GPU stages from HIP events, downloads host-timed.
+    float t[10] = {0};
+    sgpu_last_timing(rt->ctx, t, 10);
     for (int i = 0; i < 10; i++) _timing[i] = 0;
-    _timing[0] = t[0] * 1e-3f;                 // upload
-    for (int i = 0; i < 5; i++) _timing[2 + i] = t[1 + i] * 1e-3f;   // stages
-    _timing[7] = t[6] * 1e-3f;
-    if (rt->verbose) std::cout << "[SiftGPU MI355X]: " << rt->feature_num << " features, " << t[7] << " ms\n";
+    _timing[0] = rt->t_load;
+    _timing[2] = (t[0] + t[1]) * 1e-3f;
+    _timing[3] = (t[2] - t[9]) * 1e-3f;
+    _timing[4] = t[9] * 1e-3f;
+    _timing[5] = t[3] * 1e-3f;
+    _timing[6] = t[4] * 1e-3f;
+    _timing[7] = rt->t_keys;
+    _timing[8] = t[5] * 1e-3f + rt->t_desc;
+    if (rt->verbose > 0) std::cout << "[SiftGPU MI355X]: " << rt->feature_num << " features, " << t[7] << " ms\n";
     if (_outpath[0]) {
         SaveSIFT(_outpath);
         _outpath[0] = 0;

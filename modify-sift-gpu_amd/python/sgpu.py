@@ -251,23 +251,43 @@ class SiftContext:
         [cap, 128] float32 outputs (PinnedArray(...).array for overlapped copies).  Returns
         (keys, desc, counts[total images]) trimmed to the features written."""
         bl = [np.ascontiguousarray(b) for b in batches]
+        if not bl:
+            raise ValueError("no batches")
         n, h, w = bl[0].shape
         if any(b.shape != (n, h, w) or b.dtype != np.uint8 for b in bl):
             raise ValueError("batches must be u8 arrays of one shape")
+        want_desc = bool(self.opts.descriptors)
+
+        def check_out(a, width, name):
+            # the library's copies write cap rows: the array must hold them as C-ordered f32
+            if (not isinstance(a, np.ndarray) or a.dtype != np.float32 or a.ndim != 2 or
+                    a.shape[1] != width or not a.flags.c_contiguous or not a.flags.writeable):
+                raise ValueError(f"{name} must be a writable C-contiguous float32 [cap, {width}]")
+        if keys is not None:
+            check_out(keys, 4, "keys")
+        if desc is not None:
+            if not want_desc:
+                raise ValueError("descriptors are disabled (-sd): pass desc=None")
+            check_out(desc, 128, "desc")
+        given = [len(a) for a in (keys, desc) if a is not None]
         if cap is None:
-            cap = len(keys) if keys is not None else (len(desc) if desc is not None else 4096 * n * len(bl))
+            cap = min(given) if given else 4096 * n * len(bl)
+        cap = int(cap)
+        if cap < 0 or any(cap > g for g in given):
+            raise ValueError(f"cap {cap} exceeds an output array ({given})")
         if keys is None:
             keys = np.zeros((cap, 4), np.float32)
-        if desc is None:
+        if desc is None and want_desc:
             desc = np.zeros((cap, 128), np.float32)
         ptrs = (ctypes.c_void_p * len(bl))(*[b.ctypes.data for b in bl])
         counts = np.zeros(n * len(bl), np.int32)
         rc = lib().sgpu_extract_stream(self._ctx, ptrs, len(bl), n, w, h, w, keys.ctypes.data,
-                                       desc.ctypes.data, cap, counts.ctypes.data)
+                                       desc.ctypes.data if desc is not None else None, cap,
+                                       counts.ctypes.data)
         self._check(rc, "sgpu_extract_stream")
         t = int(counts.sum())
         self.batch = 0
-        return keys[:t], desc[:t], counts
+        return keys[:t], (desc[:t] if desc is not None else None), counts
 
     def extract_keypoints(self, keys: np.ndarray, has_orientation=True, image: int = 0):
         """Descriptors of caller-supplied keys [n, 4] (x, y, scale, orientation) on image
@@ -295,10 +315,10 @@ class SiftContext:
         return keys, desc
 
     def timing(self):
-        t = np.zeros(9, np.float32)
-        lib().sgpu_last_timing(self._ctx, t.ctypes.data, 9)
+        t = np.zeros(10, np.float32)
+        lib().sgpu_last_timing(self._ctx, t.ctypes.data, 10)
         return dict(zip(["upload", "pyramid", "detect", "orientation", "expand", "descriptor",
-                         "download", "total", "match"], t.tolist()))
+                         "download", "total", "match", "list"], t.tolist()))
 
     def match_shard_begin(self, d1_shard: np.ndarray, row_begin: int, d2: np.ndarray,
                           distmax=0.7, ratiomax=0.8, mbm=1):

@@ -1042,6 +1042,43 @@ std::vector<int> match_guided(const uint8_t* d1, int n1, const uint8_t* d2, int 
     return out;
 }
 
+// The same decisions as match() with the dot products computed by `threads` OpenMP threads:
+// every row folds its columns in ascending order (row_fold) and every column its rows in
+// ascending order (col_fold), exactly the sequences match() applies -- only the work is split
+// (rows over threads, then columns over threads, each dot computed once per side).  Used at the
+// benched C5 size (50k x 50k), where the single loop would take minutes.
+std::vector<int> match_mt(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float distmax,
+                          float ratiomax, int mbm, int max_match, int threads) {
+    std::vector<Top2> rows(n1), cols(n2);
+    auto dot = [](const uint8_t* a, const uint8_t* b) {
+        int s = 0;
+        for (int k = 0; k < 128; k++) s += (int)a[k] * (int)b[k];
+        return s;
+    };
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 64)
+    for (int i = 0; i < n1; i++)
+        for (int j = 0; j < n2; j++) row_fold(rows[i], dot(d1 + (size_t)i * 128, d2 + (size_t)j * 128), j);
+    if (mbm) {
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 64)
+        for (int j = 0; j < n2; j++)
+            for (int i = 0; i < n1; i++) col_fold(cols[j], dot(d1 + (size_t)i * 128, d2 + (size_t)j * 128), i);
+    }
+    auto accept = [&](const Top2& t) {
+        float dist = match_distance(std::min(t.max, 262144));
+        float distn = match_distance(std::min(t.second, 262144));
+        return (dist < distmax) && (dist < distn * ratiomax) ? t.idx : -1;
+    };
+    std::vector<int> out;
+    for (int i = 0; i < n1 && (int)out.size() / 2 < max_match; ++i) {
+        int j = accept(rows[i]);
+        if (j >= 0 && (!mbm || accept(cols[j]) == i)) {
+            out.push_back(i);
+            out.push_back(j);
+        }
+    }
+    return out;
+}
+
 float match_distance(int dot) {
     // RowMatch_Kernel / ColMatch_Kernel (ProgramCU.cu:1838-1839, 1884-1885):
     // float product, min with 1.0 in double, acos in double, stored as float.
@@ -1253,6 +1290,14 @@ int oracle_describe_keys(const uint8_t* img, int w, int h, int stride, const sgp
 int oracle_match(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float distmax,
                  float ratiomax, int mbm, int max_match, int* out_pairs) {
     std::vector<int> m = oracle::match(d1, n1, d2, n2, distmax, ratiomax, mbm, max_match);
+    memcpy(out_pairs, m.data(), m.size() * sizeof(int));
+    return (int)m.size() / 2;
+}
+
+int oracle_match_mt(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float distmax,
+                    float ratiomax, int mbm, int max_match, int* out_pairs, int threads) {
+    std::vector<int> m = oracle::match_mt(d1, n1, d2, n2, distmax, ratiomax, mbm, max_match,
+                                          threads);
     memcpy(out_pairs, m.data(), m.size() * sizeof(int));
     return (int)m.size() / 2;
 }

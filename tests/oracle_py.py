@@ -51,6 +51,9 @@ def lib():
         L.oracle_match.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                    ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_void_p]
+        L.oracle_match_mt.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                      ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
         L.oracle_match_guided.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                           ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
@@ -199,6 +202,21 @@ def match(d1: np.ndarray, d2: np.ndarray, distmax=0.7, ratiomax=0.8, mbm=1, max_
     out = np.zeros((max(max_match, 1), 2), np.int32)
     m = lib().oracle_match(d1.ctypes.data, n1, d2.ctypes.data, n2, distmax, ratiomax, mbm,
                            max_match, out.ctypes.data)
+    return out[:m]
+
+
+def match_mt(d1: np.ndarray, d2: np.ndarray, distmax=0.7, ratiomax=0.8, mbm=1, max_match=None,
+             threads=None):
+    """match() with the dot products split over OpenMP threads (the same folds in the same
+    order per row and per column): for the benched C5 size."""
+    d1 = np.ascontiguousarray(d1, np.uint8)
+    d2 = np.ascontiguousarray(d2, np.uint8)
+    n1, n2 = d1.shape[0], d2.shape[0]
+    max_match = n1 if max_match is None else max_match
+    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    out = np.zeros((max(max_match, 1), 2), np.int32)
+    m = lib().oracle_match_mt(d1.ctypes.data, n1, d2.ctypes.data, n2, distmax, ratiomax, mbm,
+                              max_match, out.ctypes.data, threads)
     return out[:m]
 
 

@@ -4,15 +4,18 @@ rocprofv3 kernel stats) -- the kernel-level evidence behind bench.py's roofline.
   python tests/pmc_summary.py <prof dir, e.g. gpurun_out/prof_r01> <tag>
 
 Per bench step (one extract of the batch): the Gaussian family's kernel time from the trace,
-and its HBM bytes from FETCH_SIZE + WRITE_SIZE (kB units -> bytes).  The guide's gfx950 note
-(FETCH_SIZE = half the bytes of 16-B-per-lane streaming reads) does not apply to these kernels'
-4-B-per-lane loads: undoubled FETCH_SIZE already equals the bytes the Gaussian kernels must read
-(each input row once plus the strip halo), so no factor is applied.
+and its HBM bytes from FETCH_SIZE + WRITE_SIZE (kB units -> bytes), raw and corrected.  The
+correction (MI355X_MICROARCH.md, HBM section: FETCH_SIZE counts 1/2 of the bytes of a 16-B-per-lane
+streaming read) uses the factors measured by tests/pmc_calib.sh on a known byte count at each
+access width (profiles/*_pmc_calibration.json): the f32 Gaussian levels load 16 B per lane
+(read16), the u8 level 0 4 B per lane (read4), and both store 8 B per lane (write8).  Kernels of
+other access patterns keep their raw counters ("hbm_bytes_per_extract" is then the raw sum).
 """
 import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 from collections import defaultdict
@@ -32,8 +35,24 @@ def family(name):
     return base.split("(")[0].split("<")[0]
 
 
+def calibration():
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_calibration.json")))
+    if not files:
+        return None, None
+    return json.load(open(files[-1]))["factor"], os.path.basename(files[-1])
+
+
+def factors(name, cal):
+    """(read factor, write factor) for a kernel's access widths, (1, 1) when uncalibrated."""
+    if cal is None or "k_gauss_wave" not in name:
+        return 1.0, 1.0
+    u8 = re.search(r"k_gauss_wave<\s*\d+\s*,\s*true", name) is not None
+    return cal.get("read4" if u8 else "read16") or 1.0, cal.get("write8") or 1.0
+
+
 def main():
     src, tag = sys.argv[1], sys.argv[2]
+    cal, cal_src = calibration()
     trace = _one(os.path.join(src, "trace", "**", "*kernel_trace.csv"))
     stats = _one(os.path.join(src, "trace", "**", "*kernel_stats.csv"))
     rows = list(csv.DictReader(open(trace)))
@@ -53,20 +72,30 @@ def main():
         "ms_per_extract": {f: v[0] / n_steps for f, v in per_family.items() if v[1] >= n_steps},
         "launches_per_extract": {f: v[1] / n_steps for f, v in per_family.items() if v[1] >= n_steps},
     }
+    hbm = defaultdict(float)
     for kind, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         pat = os.path.join(src, kind, "**", "*counter_collection.csv")
         files = sorted(glob.glob(pat, recursive=True))
         if not files:
             continue
         acc = defaultdict(float)
+        cor = defaultdict(float)
         calls = 0
         for r in csv.DictReader(open(files[0])):
             if r["Counter_Name"] != counter:
                 continue
-            acc[family(r["Kernel_Name"])] += float(r["Counter_Value"]) * 1024.0   # kB -> B
+            b = float(r["Counter_Value"]) * 1024.0   # kB -> B
+            fr, fw = factors(r["Kernel_Name"], cal)
+            acc[family(r["Kernel_Name"])] += b
+            cor[family(r["Kernel_Name"])] += b * (fr if kind == "fetch" else fw)
             if "k_image_offsets" in r["Kernel_Name"]:
                 calls += 1
         out[f"{kind}_bytes_per_extract"] = {f: v / max(calls, 1) for f, v in acc.items()}
+        for f, v in cor.items():
+            hbm[f] += v / max(calls, 1)
+    if cal is not None:
+        out["hbm_bytes_per_extract"] = dict(hbm)
+        out["calibration"] = cal_src
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))

@@ -660,6 +660,34 @@ def test_rect_keypoints_vs_oracle(gpu_ctx, over):
     gpu_ctx.set_options(default_options())
 
 
+def test_keypoints_outside_the_image(gpu_ctx):
+    """Caller keys far outside the image, with huge, tiny and negative scales: every sample box
+    is clamped to the plane (the relaxed descriptor's loads stay inside it too), the results are
+    the oracle's, and the context keeps working."""
+    img = synth_image(320, 240, 75)
+    keys = np.array([[1e6, 100, 3, 0.5], [100, -1e6, 3, 1.0], [-5e4, -5e4, 2, 2.0],
+                     [3e9, 3e9, 40, 0.1], [160, 120, 1e6, 0.3], [160, 120, 1e20, 4.0],
+                     [160, 120, 1e-8, 1.0], [160, 120, -3, 1.0], [319.9, 239.9, 900, 6.0],
+                     [-1, -1, 0.7, 3.0], [2e9, 120, 1e7, 2.5]], np.float32)
+    keys = np.concatenate([keys, _synth_keys(320, 240, 20, 76)])
+    gpu_ctx.set_options(default_options())
+    for ho in (True, False, -1):
+        gpu_ctx.extract(img)
+        gpu_ctx.extract_keypoints(keys, ho)
+        k, d = gpu_ctx.features(0)
+        rk, rd = O.describe_keys(img, keys, ho)
+        # an empty orientation window gives NaN (0/0 in the peak interpolation) on both sides;
+        # NaN payloads are not compared
+        same = (_bits(k) == _bits(rk)) | (np.isnan(k) & np.isnan(rk))
+        assert same.all(), ho
+        ok = np.isfinite(rd).all(1)
+        assert np.array_equal(np.isfinite(d).all(1), ok), ho
+        assert np.linalg.norm(d[ok].astype(np.float64) - rd[ok], axis=1).max() < DESC_L2_TOL, ho
+    gpu_ctx.extract(img)
+    k, _ = gpu_ctx.features(0)
+    assert np.array_equal(_bits(k), _bits(O.extract(img)[0]))
+
+
 def test_detected_keypoints_fed_back(gpu_ctx):
     """Keys from the detector itself, described again as a caller-supplied list."""
     img = synth_image(400, 300, 73)

@@ -2,13 +2,16 @@
   * C4 -- one 4096 x 4096 tile with 6 octaves, every keypoint and descriptor against the oracle;
   * C3 -- the per-GPU shard the bench times (128 distinct 1920 x 1080 images, -fo 0 -no 4 -d 3):
     every image of the batch equals its single-image run, two of them equal the oracle;
+  * C5 -- the benched 50,000 x 50,000 mutual match (seeds 5000/5001, 20,000 planted
+    near-duplicates, bench.py bench_match) against the oracle's pairs, plus the keyed path
+    (ratiomax 1.5) and the one-sided match (mbm 0) at 20,000 x 20,000;
   * the keypoint-capacity overflow path of a batch (grow the buffers, re-run the part)."""
 import numpy as np
 import pytest
 
 import oracle_py as O
 from sgpu_types import default_options
-from sift_synth import synth_batch_fast, synth_image
+from sift_synth import quantize, synth_batch_fast, synth_descriptors, synth_image
 
 pytestmark = pytest.mark.gpu
 
@@ -41,6 +44,35 @@ def test_c4_4096_six_octaves_vs_oracle(gpu_ctx):
     assert np.array_equal(_bits(k), _bits(rk))
     assert np.array_equal(_bits(d), _bits(rd))
     gpu_ctx.set_options(default_options())
+
+
+def _c5_sets(n, n_dup):
+    # bench.py bench_match: the same seeds and planted duplicates
+    d1 = synth_descriptors(n, 5000)
+    d2 = synth_descriptors(n, 5001, base=d1, n_dup=n_dup)
+    return quantize(d1), quantize(d2)
+
+
+def test_c5_50k_mutual_match_vs_oracle(gpu_ctx):
+    """BASELINE configs[4] at its benched size: the shipped path (keyless fold, matched-columns
+    list, device-sized grids; ProgramCU.cu:1466-1564, 1785-1900, SiftMatchCU.cpp:149-179) gives
+    exactly the oracle's pairs."""
+    q1, q2 = _c5_sets(50000, 20000)
+    got = gpu_ctx.match(q1, q2)
+    ref = O.match_mt(q1, q2)
+    assert len(ref) >= 20000
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("ratiomax,mbm", [(1.5, 1), (1.5, 0), (0.8, 0)])
+def test_c5_20k_keyed_and_one_sided_vs_oracle(gpu_ctx, ratiomax, mbm):
+    """ratiomax > 1 runs the keyed epilogue (exact ties are accepted, so the tie order shows);
+    mbm = 0 skips the column side."""
+    q1, q2 = _c5_sets(20000, 8000)
+    got = gpu_ctx.match(q1, q2, 0.7, ratiomax, mbm)
+    ref = O.match_mt(q1, q2, 0.7, ratiomax, mbm)
+    assert len(ref) >= 8000
+    assert np.array_equal(got, ref)
 
 
 def test_c3_shard_128_full_hd(gpu_ctx):
@@ -138,3 +170,35 @@ def test_extract_stream_capacity_and_first_octave(gpu_ctx):
     assert np.array_equal(c, fc) and np.array_equal(_bits(k), _bits(fk))
     assert np.array_equal(_bits(d), _bits(fd))
     gpu_ctx.set_options(default_options())
+
+
+def test_failed_stream_leaves_no_batch(gpu_ctx):
+    """After a failed extract the per-image queries see no batch (not the previous batch's
+    offsets under the new geometry), and the context keeps working."""
+    gpu_ctx.set_options(default_options())
+    batches = [synth_batch_fast(2, 320, 240, 950 + k) for k in range(2)]
+    gpu_ctx.extract(batches[0])
+    assert gpu_ctx.count(0) > 0
+    with pytest.raises(RuntimeError):
+        gpu_ctx.extract_stream(batches, cap=1)
+    assert gpu_ctx.count(0) == 0 and gpu_ctx.total() == 0
+    gpu_ctx.extract(batches[0])
+    assert gpu_ctx.count(0) > 0
+
+
+def test_extract_stream_without_descriptors(gpu_ctx):
+    """-sd: the stream returns keys only (no descriptor buffer is passed)."""
+    batches = [synth_batch_fast(2, 320, 240, 960 + k) for k in range(3)]
+    gpu_ctx.set_options(default_options(descriptors=0))
+    try:
+        keys = []
+        for b in batches:
+            gpu_ctx.extract(b)
+            keys += [gpu_ctx.features(i, descriptors=False)[0] for i in range(len(b))]
+        rk = np.concatenate(keys)
+        k, d, c = gpu_ctx.extract_stream(batches, cap=len(rk) + 10)
+        assert d is None and np.array_equal(_bits(k), _bits(rk))
+        with pytest.raises(ValueError):
+            gpu_ctx.extract_stream(batches, desc=np.zeros((10, 128), np.float32))
+    finally:
+        gpu_ctx.set_options(default_options())

@@ -543,3 +543,18 @@ def test_cpu_match_baseline_row_side():
                 second = v
         want += idx + (int(second) & 1)
     assert cs.value == want
+
+
+@pytest.mark.parametrize("n1,n2,dup", [(1, 300, 0), (300, 1, 0), (700, 900, 300), (2000, 1500, 800)])
+def test_match_mt_equals_match(n1, n2, dup):
+    """The threaded oracle matcher (C5-size tests) makes the single loop's decisions: same folds
+    per row and per column, in the same order."""
+    d1 = synth_descriptors(n1, 3 * n1 + n2)
+    d2 = synth_descriptors(n2, 3 * n2 + n1, base=d1, n_dup=min(dup, n1, n2))
+    q1, q2 = quantize(d1), quantize(d2)
+    for args in ((0.7, 0.8, 1), (0.7, 0.8, 0), (2.0, 1.5, 1), (2.0, 1.5, 0)):
+        assert np.array_equal(O.match_mt(q1, q2, *args, threads=4), O.match(q1, q2, *args))
+    q1t, q2t, _ = synth_tie_scene(300, 900, 5, [(200, 129), (130, 2), (40, 33)], [(60, 61)])
+    for mbm in (0, 1):
+        assert np.array_equal(O.match_mt(q1t, q2t, 2.0, 1.5, mbm, threads=3),
+                              O.match(q1t, q2t, 2.0, 1.5, mbm))
