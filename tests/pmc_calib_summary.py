@@ -17,8 +17,9 @@ KNOWN = float(1 << 30)
 def width(name):
     if "k_read" in name or "k_write" in name:
         kind = "read" if "k_read" in name else "write"
-        w = 16 if "float __attribute__((ext_vector_type(4)))" in name or "f4" in name else \
-            8 if "ext_vector_type(2)" in name or "f2" in name else 4
+        head = name.split("(")[0] if "<" not in name else name.split(">")[0]
+        w = 16 if "(4)" in head or "vector(4" in name.split(">")[0] else \
+            8 if "(2)" in head or "vector(2" in name.split(">")[0] else 4
         return f"{kind}{w}"
     return None
 
