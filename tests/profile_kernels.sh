@@ -14,7 +14,7 @@ TAG=${1:-r01}
 OUT=gpurun_out/prof_${TAG}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-H="--no-c4 --no-e2e --no-match --no-cpu-baseline"
+H="--no-c4 --no-e2e --no-match --no-cpu-baseline --no-c2"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
     -- python3 bench.py $H > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run \
