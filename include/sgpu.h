@@ -257,6 +257,8 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
                                    ratiomax <= 1, where the keyless one is exact and used     */
 #define SGPU_DEBUG_FULL_COLUMNS 128 /* plain mutual matching decides every column of set 2, not
                                    only the columns some row of set 1 matched                 */
+#define SGPU_DEBUG_GAUSS_WAVE1 256 /* Gaussian levels through k_gauss_wave (round 2's wave-streaming
+                                     kernel) instead of k_gauss_lean: same levels, bit for bit */
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);

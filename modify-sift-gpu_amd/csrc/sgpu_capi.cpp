@@ -303,8 +303,10 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     if (const char* ev = getenv("SGPU_EXACT_DESCRIPTOR"))
         if (ev[0] == '1') ctx->debug_flags |= SGPU_DEBUG_EXACT_DESCRIPTOR;
     // A/B hook for the Gaussian kernels (bench / probe runs in one process tree)
-    if (const char* ev = getenv("SGPU_GAUSS"))
+    if (const char* ev = getenv("SGPU_GAUSS")) {
         if (!strcmp(ev, "block")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_BLOCK;
+        else if (!strcmp(ev, "wave")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_WAVE1;
+    }
     int rc = sgpu_ctx_set_options(ctx, opt);
     if (rc != SGPU_OK) {
         sgpu_ctx_destroy(ctx);
@@ -493,7 +495,8 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
                                           npx, od.wa, od.h, fwk, taps, n, dk ? ds : nullptr,
                                           dk ? dsw : 0, dk ? dsh : 0, dk ? ds_stride : 0, st,
                                           (ctx->debug_flags & SGPU_DEBUG_GAUSS_BLOCK)
-                                              ? -1 : (ctx->debug_flags >> 16)));
+                                              ? -1 : (ctx->debug_flags >> 16),
+                                          !(ctx->debug_flags & SGPU_DEBUG_GAUSS_WAVE1)));
         }
     }
     HIPCHK(ctx, hipEventRecord(pt.ev[1], st));

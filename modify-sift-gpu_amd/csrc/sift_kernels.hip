@@ -546,13 +546,272 @@ static GaussWaveGrid gauss_wave_grid(int w, int h, int batch, int rows_hint, int
     return g;
 }
 
+// ------------------------------------------------------------------------------------------
+// Gaussian level, lean form (the shipped kernel for FW <= 25): k_gauss_wave's filter -- same
+// strips, bands, chunks, row-pair buffer, H ring and lag, the same taps in the same order, so the
+// levels are bit-identical -- with the per-step work that is not filtering taken off the vector
+// ALU.  The kernel traces showed k_gauss_wave issuing ~150 non-FMA VALU instructions per 8-row
+// step against 88 packed FMAs (FW 11): 64-bit load and store addresses, per-lane row clamps,
+// clamp-to-edge selects, ring-row wrap arithmetic.  Here:
+//   * the wave's geometry is uniform (readfirstlane of the wave index), so image, band and row
+//     bases live in SGPRs and every global load / store is a uniform row pointer plus a lane
+//     constant 32-bit offset (the saddr form);
+//   * the loaders are laid out lane = 32 g + j: half-wave g loads the quads j of row pair 2m + g,
+//     so a lane's column (and its clamp) is fixed for the whole kernel, and a chunk's rows are
+//     uniform; only chunks that reach above row 0 or below row H-1 clamp per lane;
+//   * clamp-to-edge column selects only in the strips at the image's left / right edge;
+//   * the ring holds 4 chunk slots (RS = 32, LAG <= 3) and the step's slot is compile-time (the
+//     main loop is unrolled by 4), so ring reads and writes are lane-constant base + immediate
+//     offset; the half-wave whose rows wrap first (vq = 1, 4 rows ahead) reads through a second
+//     base for the 4 rows where only it has wrapped;
+//   * u8 -> f32 (the ingest level) on row pairs with packed multiply / fma;
+//   * the decimation into the next octave's level 0 is a template parameter.
+template <int FW, bool U8, bool DS>
+__global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
+    const float* __restrict__ src, const uint8_t* __restrict__ src8, int src_stride,
+    long long src_img_stride, float* __restrict__ dst, long long dst_img_stride, int W, int H,
+    Taps taps, float* __restrict__ ds, int dsw, int dsh, long long ds_img_stride,
+    GaussWaveGrid gg) {
+    constexpr int HALF = FW >> 1;
+    constexpr int OFF = (-HALF) & 3;                  // LDS column of the strip's first input
+    constexpr int IN_W = GT + FW - 1 + OFF;           // input columns held per row
+    constexpr int NQ = (IN_W + 3) / 4;                // aligned quads per row
+    static_assert(NQ <= 32, "a row's quads fit half a wave");
+    constexpr int NRD = (FW + 3) / 2;                 // ds_read_b128 per H-pass lane
+    constexpr int SH = OFF & 1;
+    constexpr int IN_S0 = (4 * NQ + SH + 3) & ~3;
+    constexpr int IN_S = IN_S0 + ((2 - IN_S0) & 31);  // float2 per row pair (= 2 mod 32)
+    static_assert(IN_S % 32 == 2 && 4 * NQ + SH <= IN_S, "row-pair stride");
+    constexpr int LAG = (FW - 1 + WCH - 1) / WCH;     // chunks between H and V of a row
+    static_assert(WCH * (LAG + 1) <= 32, "the ring's 4 chunk slots hold the lag");
+    constexpr int RS = 32;                            // ring rows: 4 slots of WCH
+    constexpr int HS = GT + SGK_GW_HSPAD;             // ring row stride (floats)
+    constexpr int NPAIR = WCH / 2;
+    constexpr int NST = 4;                            // chunks in registers = ring slots
+    __shared__ __attribute__((aligned(16))) f2v s_in_all[kGwWaves][NPAIR * IN_S + 4];   // + pad slot
+    __shared__ __attribute__((aligned(16))) float s_h_all[kGwWaves][RS * HS];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // XCD-aware order as in k_gauss_wave
+    const int gw = xcd_block(blockIdx.x, gridDim.x) * kGwWaves + wave;
+    if (gw >= gg.total_waves) return;                 // uniform per wave
+    const int sx = gw % gg.strips_x, rest = gw / gg.strips_x;
+    const int x0 = sx * GT;
+    const int sy = rest % gg.nsy, b = rest / gg.nsy;
+    const int yb = sy * gg.rows_per_band;
+    const int ye = min(H, yb + gg.rows_per_band);
+    const int nchunk_out = (ye - yb + WCH - 1) / WCH;
+    f2v* s_in = s_in_all[wave];
+    float* s_h = s_h_all[wave];
+
+    const float* sf = U8 ? nullptr : src + (long long)b * src_img_stride;
+    const uint8_t* s8 = U8 ? src8 + (long long)b * src_img_stride : nullptr;
+    const int a0 = x0 - HALF - OFF;
+    // loader lane: half-wave g, quad j (lanes past the row's last quad re-load the last quad and
+    // store into a pad slot)
+    const int lg = lane >> 5, lj = min(lane & 31, NQ - 1);
+    const bool lreal = (lane & 31) < NQ;
+    const int gq = a0 + 4 * lj;
+    const int lq = clampi(gq, 0, W - 4);
+    const bool left = gq < 0, right = gq > W - 4;
+    const bool edge = a0 < 0 || a0 + 4 * NQ > W;      // uniform: this strip clamps columns
+    // element offsets of the lane's quad in rows 2 g and 2 g + 1 of a row group
+    const uint32_t loff0 = (uint32_t)(2 * lg * src_stride + lq), loff1 = loff0 + (uint32_t)src_stride;
+    const int s_off = lreal ? lg * IN_S + 4 * lj + SH : NPAIR * IN_S;   // LDS float2 index
+
+    struct Elem { float4 v0, v1; };   // the raw fetch of rows 2p, 2p+1 (u8: .x as the u32)
+    Elem st[NST][2];
+    auto load_chunk = [&](Elem (&stage)[2], int c) {
+        const int rb = yb - HALF + WCH * c;           // first input row of chunk c (uniform)
+        if (rb >= 0 && rb + WCH <= H) {
+#pragma unroll
+            for (int m = 0; m < 2; m++) {
+                const long long ro = (long long)(rb + 4 * m) * src_stride;   // uniform
+                if (U8) {
+                    const uint8_t* r = s8 + ro;
+                    stage[m].v0.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(r + loff0));
+                    stage[m].v1.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(r + loff1));
+                } else {
+                    const float* r = sf + ro;
+                    stage[m].v0 = *reinterpret_cast<const float4*>(r + loff0);
+                    stage[m].v1 = *reinterpret_cast<const float4*>(r + loff1);
+                }
+            }
+        } else {   // the band reaches above row 0 or below row H-1: rows clamp per lane
+#pragma unroll
+            for (int m = 0; m < 2; m++) {
+                const int y0 = clampi(rb + 4 * m + 2 * lg, 0, H - 1);
+                const int y1 = clampi(rb + 4 * m + 2 * lg + 1, 0, H - 1);
+                if (U8) {
+                    stage[m].v0.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(s8 + (long long)y0 * src_stride + lq));
+                    stage[m].v1.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(s8 + (long long)y1 * src_stride + lq));
+                } else {
+                    stage[m].v0 = *reinterpret_cast<const float4*>(sf + (long long)y0 * src_stride + lq);
+                    stage[m].v1 = *reinterpret_cast<const float4*>(sf + (long long)y1 * src_stride + lq);
+                }
+            }
+        }
+    };
+    auto store_chunk = [&](const Elem (&stage)[2]) {
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            f2v pr[4];   // column t of the quad: (row 2p, row 2p+1)
+            if (U8) {
+                const uint32_t w0 = __float_as_uint(stage[m].v0.x), w1 = __float_as_uint(stage[m].v1.x);
+                const float c = 1.0f / 255.0f;
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    // u8_to_unit on the pair: q = x / 255 rounded, then one fma correction
+                    const f2v x{(float)((w0 >> (8 * t)) & 255u), (float)((w1 >> (8 * t)) & 255u)};
+                    const f2v q = x * f2v{c, c};
+                    const f2v r = __builtin_elementwise_fma(-q, f2v{255.0f, 255.0f}, x);
+                    pr[t] = __builtin_elementwise_fma(r, f2v{c, c}, q);
+                }
+            } else {
+                pr[0] = f2v{stage[m].v0.x, stage[m].v1.x};
+                pr[1] = f2v{stage[m].v0.y, stage[m].v1.y};
+                pr[2] = f2v{stage[m].v0.z, stage[m].v1.z};
+                pr[3] = f2v{stage[m].v0.w, stage[m].v1.w};
+            }
+            if (edge) {   // clamp-to-edge: a quad left of column 0 repeats column 0, right of W-1 W-1
+                const f2v e0 = pr[0], e3 = pr[3];
+#pragma unroll
+                for (int t = 0; t < 4; t++) pr[t] = left ? e0 : (right ? e3 : pr[t]);
+            }
+            f2v* q = s_in + s_off + 2 * m * IN_S;
+            if (SH == 0) {
+                reinterpret_cast<float4*>(q)[0] = make_float4(pr[0].x, pr[0].y, pr[1].x, pr[1].y);
+                reinterpret_cast<float4*>(q)[1] = make_float4(pr[2].x, pr[2].y, pr[3].x, pr[3].y);
+            } else {   // 8-byte aligned
+#pragma unroll
+                for (int t = 0; t < 4; t++) q[t] = pr[t];
+            }
+        }
+    };
+
+#pragma unroll
+    for (int k = 0; k < NST; k++) load_chunk(st[k], k);
+    store_chunk(st[0]);
+    float* d = dst + (long long)b * dst_img_stride;
+    float* dd = DS ? ds + (long long)b * ds_img_stride : nullptr;
+    const int hp = lane >> 4, hc = (lane & 15) * 4;    // H pass: rows 2hp, 2hp+1; columns hc..hc+3
+    const int vq = lane >> 5, vc = (lane & 31) * 2;    // V pass: rows 4vq..4vq+3; columns vc, vc+1
+    const int x = x0 + vc;
+    const bool active = x0 < W;                      // uniform
+    const bool full_cols = x0 + GT <= W;             // uniform: every lane's columns exist
+    const f2v* h_rd = s_in + hp * IN_S + hc + OFF + SH;
+    float* h_wr = s_h + 2 * hp * HS + hc;
+    const float* v_rd = s_h + 4 * vq * HS + vc;              // rows before the wrap
+    const float* v_rd_amb = v_rd - (vq ? RS * HS : 0);       // rows where only vq = 1 wrapped
+    const uint32_t st_off = (uint32_t)(4 * vq * W + vc);     // lane offset of the V-pass stores
+    const uint32_t ds_off = (uint32_t)(2 * vq * dsw + (x >> 1));
+    // step c (ring slot K = c mod 4): H pass of input chunk c, V pass of output chunk c - LAG,
+    // loads of chunk c + NST into `nxt`, chunk c + 1 (`cur`) into the row-pair buffer
+    auto step = [&](int c, auto KC, Elem (&cur)[2], Elem (&nxt)[2]) {
+        constexpr int K = decltype(KC)::value;
+        {   // H pass -> ring rows 8K .. 8K+7
+            f2v a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};   // columns hc+i
+#pragma unroll
+            for (int q = 0; q < NRD; q++) {
+                const float4 v = reinterpret_cast<const float4*>(h_rd)[q];
+                const f2v e[2] = {f2v{v.x, v.y}, f2v{v.z, v.w}};
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const int m = 2 * q + u;
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        if (m - i >= 0 && m - i < FW) a[i] = pk_fma(e[u], taps.k[m - i], a[i]);
+                }
+            }
+            *reinterpret_cast<float4*>(h_wr + WCH * K * HS) = make_float4(a[0].x, a[1].x, a[2].x, a[3].x);
+            *reinterpret_cast<float4*>(h_wr + (WCH * K + 1) * HS) = make_float4(a[0].y, a[1].y, a[2].y, a[3].y);
+        }
+        asm volatile("" ::: "memory");
+        const int kout = c - LAG;
+        if (active && kout >= 0 && kout < nchunk_out) {   // V pass of output chunk kout (uniform)
+            constexpr int KV = (K - LAG) & 3;                // its ring slot
+            f2v acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};   // rows t0+j
+#pragma unroll
+            for (int m = 0; m < FW + 3; m++) {
+                const int rc = WCH * KV + m;                 // ring row of half-wave 0
+                const float* p = rc < RS - 4 ? v_rd + rc * HS
+                               : rc >= RS ? v_rd + (rc - RS) * HS : v_rd_amb + rc * HS;
+                const f2v v = *reinterpret_cast<const f2v*>(p);
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (m - j >= 0 && m - j < FW) acc[j] = pk_fma(v, taps.k[m - j], acc[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) asm volatile("" : "+v"(acc[j]));
+            const int yu = yb + WCH * kout;                  // first row of the chunk (uniform)
+            if (full_cols && yu + WCH <= ye && (!DS || (yu + WCH) / 2 <= dsh)) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    float* row = d + (long long)(yu + j) * W;             // uniform
+                    *reinterpret_cast<f2v*>(row + st_off) = acc[j];
+                    if (DS && !(j & 1)) {
+                        // DownsampleKernel<1> (ProgramCU.cu:287-298): dst(r, c) = src(2r, min(2c, W-1))
+                        float* drow = dd + (long long)((yu + j) >> 1) * dsw;   // uniform
+                        if ((x >> 1) < dsw) drow[ds_off] = acc[j].x;
+                        if (x + 1 == W - 1)
+                            for (int cc = W >> 1; cc < dsw; cc++) drow[2 * vq * dsw + cc] = acc[j].y;
+                    }
+                }
+            } else if (x < W) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int y = yu + 4 * vq + j;
+                    if (y < ye) {
+                        *reinterpret_cast<f2v*>(&d[(long long)y * W + x]) = acc[j];
+                        if (DS && !(y & 1) && (y >> 1) < dsh) {
+                            float* drow = dd + (long long)(y >> 1) * dsw;
+                            if ((x >> 1) < dsw) drow[x >> 1] = acc[j].x;
+                            if (x + 1 == W - 1)
+                                for (int cc = W >> 1; cc < dsw; cc++) drow[cc] = acc[j].y;
+                        }
+                    }
+                }
+            }
+        }
+        asm volatile("" ::: "memory");
+        load_chunk(nxt, c + NST);
+        store_chunk(cur);
+        asm volatile("" ::: "memory");
+    };
+    const int nsteps = nchunk_out + LAG;
+    for (int c = 0; c < nsteps; c += NST) {
+        step(c + 0, std::integral_constant<int, 0>{}, st[1], st[0]);
+        step(c + 1, std::integral_constant<int, 1>{}, st[2], st[1]);
+        step(c + 2, std::integral_constant<int, 2>{}, st[3], st[2]);
+        step(c + 3, std::integral_constant<int, 3>{}, st[0], st[3]);
+    }
+}
+
 template <int FW>
 hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
                           long long src_img_stride, float* dst, long long dst_img_stride, int w,
                           int h, const Taps& taps, int batch, float* ds, int dsw, int dsh,
-                          long long ds_img_stride, hipStream_t stream, int wave_rows) {
+                          long long ds_img_stride, hipStream_t stream, int wave_rows,
+                          bool lean) {
     const bool vec = (src_stride % 4) == 0 && (src_img_stride % 4) == 0 && (w % 4) == 0 &&
                      w >= 4 && ((uintptr_t)(src8 ? (const void*)src8 : (const void*)src) % 16) == 0;
+    constexpr int LAG_W = (FW - 1 + WCH - 1) / WCH;
+    if constexpr (WCH * (LAG_W + 1) <= 32) if (vec && wave_rows >= 0 && lean) {
+        const GaussWaveGrid gg = gauss_wave_grid(w, h, batch, wave_rows, 1);
+        const dim3 wgrid((unsigned)((gg.total_waves + kGwWaves - 1) / kGwWaves));
+#define SGK_LEAN(U8, DS)                                                                      \
+        hipLaunchKernelGGL((k_gauss_lean<FW, U8, DS>), wgrid, dim3(64 * kGwWaves), 0, stream, src, \
+                           src8, src_stride, src_img_stride, dst, dst_img_stride, w, h, taps, ds, \
+                           dsw, dsh, ds_img_stride, gg)
+        if (src8) {
+            if (ds) SGK_LEAN(true, true); else SGK_LEAN(true, false);
+        } else {
+            if (ds) SGK_LEAN(false, true); else SGK_LEAN(false, false);
+        }
+#undef SGK_LEAN
+        return hipGetLastError();
+    }
     if (vec && wave_rows >= 0) {
 #ifndef SGK_GW_NW
 #define SGK_GW_NW 1
@@ -2023,12 +2282,13 @@ __global__ __launch_bounds__(64) void k_debug_candidates(
 hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         long long src_img_stride, float* dst, long long dst_img_stride, int w,
                         int h, int fw, const Taps& taps, int batch, float* ds_dst, int ds_w,
-                        int ds_h, long long ds_img_stride, hipStream_t stream, int wave_rows) {
+                        int ds_h, long long ds_img_stride, hipStream_t stream, int wave_rows,
+                        bool lean) {
 #define SGK_GAUSS(FW)                                                                       \
     case FW:                                                                                  \
         return gauss_dispatch<FW>(src, src_u8, src_stride, src_img_stride, dst, dst_img_stride, \
                                   w, h, taps, batch, ds_dst, ds_w, ds_h, ds_img_stride, stream, \
-                                  wave_rows);
+                                  wave_rows, lean);
     switch (fw) {
         SGK_GAUSS(5) SGK_GAUSS(7) SGK_GAUSS(9) SGK_GAUSS(11) SGK_GAUSS(13) SGK_GAUSS(15)
         SGK_GAUSS(17) SGK_GAUSS(19) SGK_GAUSS(21) SGK_GAUSS(23) SGK_GAUSS(25) SGK_GAUSS(27)

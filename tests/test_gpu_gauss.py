@@ -1,5 +1,6 @@
-"""Gaussian pyramid kernels on the GPU: the wave-streaming level kernel (k_gauss_wave) against
-the workgroup strip kernel (k_gauss_pk2) and the oracle, bit for bit.
+"""Gaussian pyramid kernels on the GPU: the shipped lean level kernel (k_gauss_lean), round 2's
+wave-streaming kernel (k_gauss_wave) and the workgroup strip kernel (k_gauss_pk2) against each
+other and the oracle, bit for bit.
 
 Both kernels restate FilterH / FilterV (ProgramCU.cu:115-222) with the taps summed i = 0..FW-1
 and the 2x decimation of DownsampleKernel<1> (ProgramCU.cu:287-298) fused into the level that
@@ -16,6 +17,7 @@ from sift_synth import synth_batch, synth_image
 pytestmark = pytest.mark.gpu
 
 BLOCK = sgpu.SiftContext.DEBUG_GAUSS_BLOCK
+WAVE1 = sgpu.SiftContext.DEBUG_GAUSS_WAVE1
 
 
 def _bits(a):
@@ -30,7 +32,7 @@ def _levels(ctx, image, opts):
 
 @pytest.mark.parametrize("w,h,seed", [(16, 16, 3), (203, 97, 2), (640, 480, 1000)])
 def test_wave_levels_vs_oracle(gpu_ctx, w, h, seed):
-    """The shipped kernel (k_gauss_wave) against the oracle, every level of every octave."""
+    """The shipped kernel (k_gauss_lean) against the oracle, every level of every octave."""
     img = synth_image(w, h, seed)
     opts = default_options()
     gpu_ctx.set_options(opts)
@@ -58,18 +60,48 @@ def test_wave_levels_equal_block_kernel(gpu_ctx, rows, n, w, h):
     gpu_ctx.extract(imgs)
     ref = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
     k_ref = [gpu_ctx.features(i)[0].copy() for i in range(n)]
-    gpu_ctx.set_debug_flags(rows << 16)
     try:
+        for kernel in (WAVE1, 0):   # k_gauss_wave, then the shipped k_gauss_lean
+            gpu_ctx.set_debug_flags((rows << 16) | kernel)
+            gpu_ctx.extract(imgs)
+            got = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
+            for a, b in zip(ref, got):
+                for o, (la, lb) in enumerate(zip(a, b)):
+                    for lvl, (x, y) in enumerate(zip(la, lb)):
+                        assert np.array_equal(_bits(x), _bits(y)), (kernel, o, lvl)
+            for i in range(n):
+                assert np.array_equal(_bits(gpu_ctx.features(i)[0]), _bits(k_ref[i])), kernel
+    finally:
+        gpu_ctx.set_debug_flags(0)
+
+
+# every filter width of the lean kernel and the wave kernel's widths past it: -d changes the
+# level sigmas (FW 5 .. 25 at the default -f 4), -f 5.5 reaches FW 27 .. 33 (k_gauss_wave's
+# 64-row ring); first octaves -1 / 0 / 1 (float and u8 first levels)
+@pytest.mark.parametrize("over", [dict(dog_level_num=1), dict(dog_level_num=2),
+                                  dict(dog_level_num=5), dict(filter_width_factor=5.5),
+                                  dict(filter_width_factor=2.0), dict(octave_min=-1),
+                                  dict(octave_min=1)])
+def test_lean_levels_all_widths(gpu_ctx, over):
+    imgs = synth_batch(2, 517, 389, 77)
+    opts = default_options(**over)
+    gpu_ctx.set_options(opts)
+    try:
+        gpu_ctx.set_debug_flags(BLOCK)
         gpu_ctx.extract(imgs)
-        got = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
+        ref = [_levels(gpu_ctx, i, opts) for i in (0, 1)]
+        gpu_ctx.set_debug_flags(0)
+        gpu_ctx.extract(imgs)
+        got = [_levels(gpu_ctx, i, opts) for i in (0, 1)]
         for a, b in zip(ref, got):
             for o, (la, lb) in enumerate(zip(a, b)):
                 for lvl, (x, y) in enumerate(zip(la, lb)):
                     assert np.array_equal(_bits(x), _bits(y)), (o, lvl)
-        for i in range(n):
-            assert np.array_equal(_bits(gpu_ctx.features(i)[0]), _bits(k_ref[i]))
+        r = O.gaussian(imgs[1], len(got[1]) - 1, opts.dog_level_num + 2, opts)
+        assert np.array_equal(_bits(got[1][-1][-1]), _bits(r))
     finally:
         gpu_ctx.set_debug_flags(0)
+        gpu_ctx.set_options(default_options())
 
 
 @pytest.mark.parametrize("fo", [1, -1])
