@@ -89,6 +89,8 @@ struct Part {
 };
 
 constexpr int kMaxParts = 4;
+// candidate counts (of the previous call) up to which orientation runs one wave per candidate
+constexpr size_t kWaveOrientationMax = 16384;
 
 }  // namespace
 
@@ -523,11 +525,15 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     const uint32_t* n_cand_dev = pt.row_base.as<uint32_t>() + pt.total_rows;
     HIPCHK(ctx, hipMemsetAsync(pt.ocount.p, 0, nc * sizeof(uint32_t), st));
     const int cand_grid = (int)std::min(nc, pt.cand_hint ? pt.cand_hint : nc);
+    // few candidates (a single image): one wave per candidate instead of a quad, so that the
+    // SIMDs are filled and each window is walked 64 samples at a time (same bits)
+    const bool ori_wave = (ctx->debug_flags & SGPU_DEBUG_ORIENT_WAVE) ||
+                          (pt.cand_hint > 0 && pt.cand_hint <= kWaveOrientationMax);
     const int feat_grid = (int)std::min(ne_cap, pt.feat_hint ? pt.feat_hint : ne_cap);
     HIPCHK(ctx, sgk::launch_orientation(pyr, pt.mask.as<uint32_t>(), pt.row_base.as<uint32_t>(),
                                         pt.total_rows, n_cand_dev, (int)nc, cand_grid, fp,
                                         pt.cand.as<float4>(), pt.info.as<int2>(),
-                                        pt.ocount.as<uint32_t>(), st));
+                                        pt.ocount.as<uint32_t>(), st, ori_wave));
     if (O.feature_count_threshold > 0 && fp.num_orientation >= 2)   // LimitFeatureCount(1)
         HIPCHK(ctx, sgk::launch_limit_oriented(pt.ocount.as<uint32_t>(), pt.row_base.as<uint32_t>(),
                                                fp, O.feature_count_threshold, O.truncate_method,

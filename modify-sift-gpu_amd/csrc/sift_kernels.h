@@ -78,14 +78,16 @@ size_t scan_tmp_words(size_t n);
 hipError_t launch_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
                        hipStream_t stream);
 
-// Keypoint materialisation + orientation: a quad per detected keypoint, grid-stride over
-// min(*n_cand_dev, n_cand_cap) keypoints (the grid is sized from the capacity).
+// Keypoint materialisation + orientation: a quad per detected keypoint (wave_per_candidate: a
+// wave, for few candidates), grid-stride over min(*n_cand_dev, n_cand_cap) keypoints (the grid
+// is sized from grid_hint).  Both forms give the same bits.
 // out4: (x, y, s, packed orientations) in octave coordinates; info: (image, level id);
 // ocount: number of oriented features the keypoint expands to.
 hipError_t launch_orientation(const float* pyr, const uint32_t* mask, const uint32_t* row_base,
                               int total_rows, const uint32_t* n_cand_dev, int n_cand_cap,
                               int grid_hint, const FeatureParams& fp, float4* out4, int2* info,
-                              uint32_t* ocount, hipStream_t stream);
+                              uint32_t* ocount, hipStream_t stream,
+                              bool wave_per_candidate = false);
 
 // Expansion into oriented features (+ image-coordinate keypoints).
 hipError_t launch_expand(const float4* cand, const int2* info, const uint32_t* eoff,

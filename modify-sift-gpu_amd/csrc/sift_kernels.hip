@@ -1425,14 +1425,18 @@ __device__ __forceinline__ float strongest_orientation(const float (&vote)[37]) 
     return radius_per_ten_degrees * (index_max + 0.5f + off);
 }
 
-__device__ __forceinline__ void orientation_one(uint32_t f, int sub, float* vote_l,
+// Keypoint of candidate f in octave coordinates (ComputeOrientation_Kernel's key, ProgramCU.cu:
+// 838-851) and its info record; false when no orientation is computed (num_orientation == 0:
+// the keypoint is written with orientation 0 here).
+struct OriKey { float kx, ky, kz; const float* g; int W, H; };
+__device__ __forceinline__ bool orientation_key(uint32_t f, bool writer,
                                                 const float* __restrict__ pyr,
                                                 const uint32_t* __restrict__ mask,
                                                 const uint32_t* __restrict__ row_base,
                                                 int total_rows, const FeatureParams& fp,
                                                 float4* __restrict__ out4,
                                                 int2* __restrict__ info,
-                                                uint32_t* __restrict__ ocount) {
+                                                uint32_t* __restrict__ ocount, OriKey& K) {
     const KeyLoc L = locate(f, row_base, total_rows, mask, fp);
     const KeyOut kv = key_at(pyr, fp, L);
     const OctaveDesc& od = fp.oct[L.o];
@@ -1444,22 +1448,33 @@ __device__ __forceinline__ void orientation_one(uint32_t f, int sub, float* vote
         kz *= pow_(fp.sigma_step, kv.ds);
     }
     if (fp.keep_sign) kz *= kv.result;
-    if (sub == 0) info[f] = make_int2(L.b, L.o * fp.d + L.j);
+    if (writer) info[f] = make_int2(L.b, L.o * fp.d + L.j);
     if (fp.num_orientation == 0) {
-        if (sub == 0) {
+        if (writer) {
             out4[f] = make_float4(kx, ky, kz, 0.0f);
             ocount[f] = 1;
         }
-        return;
+        return false;
     }
     // gradient of Gaussian level 1 + j (PyramidCU.cpp:1204)
-    const float* g = pyr + od.gauss_off + (long long)(1 + L.j) * od.level_stride +
-                     (long long)L.b * od.wa * od.h;
-    float vote[37];
-    orientation_hist(g, od.wa, od.h, kx, ky, kz, fp, sub, vote_l, vote);
-    if (sub != 0) return;
+    K.g = pyr + od.gauss_off + (long long)(1 + L.j) * od.level_stride + (long long)L.b * od.wa * od.h;
+    K.W = od.wa;
+    K.H = od.h;
+    K.kx = kx;
+    K.ky = ky;
+    K.kz = kz;
+    return true;
+}
+
+// Peaks of the smoothed histogram (ProgramCU.cu:904-977) -> the keypoint with its one or two
+// orientations packed as u16 fractions of 2 pi, and the feature count it expands to
+// (ReshapeFeatureListCPU, PyramidCU.cpp:560-578: drop "no orientation", keep a distinct second).
+__device__ __forceinline__ void orientation_finish(uint32_t f, const float (&vote)[37],
+                                                   const OriKey& K, const FeatureParams& fp,
+                                                   float4* __restrict__ out4,
+                                                   uint32_t* __restrict__ ocount) {
     if (fp.num_orientation == 1) {
-        out4[f] = make_float4(kx, ky, kz, strongest_orientation(vote));
+        out4[f] = make_float4(K.kx, K.ky, K.kz, strongest_orientation(vote));
         ocount[f] = 1;
         return;
     }
@@ -1494,10 +1509,118 @@ __device__ __forceinline__ void orientation_one(uint32_t f, int sub, float* vote
         if (fr2 < 0) fr2 += 1.0f;
         us2 = (uint32_t)(unsigned short)floor_(fr2 * 65535.0f);
     }
-    out4[f] = make_float4(kx, ky, kz, as_float((us2 << 16) | us1));
-    // ReshapeFeatureListCPU (PyramidCU.cpp:560-578): drop "no orientation", keep a distinct
-    // second orientation
+    out4[f] = make_float4(K.kx, K.ky, K.kz, as_float((us2 << 16) | us1));
     ocount[f] = us1 == 65535u ? 0u : (1u + ((us2 != 65535u && us2 != us1) ? 1u : 0u));
+}
+
+__device__ __forceinline__ void orientation_one(uint32_t f, int sub, float* vote_l,
+                                                const float* __restrict__ pyr,
+                                                const uint32_t* __restrict__ mask,
+                                                const uint32_t* __restrict__ row_base,
+                                                int total_rows, const FeatureParams& fp,
+                                                float4* __restrict__ out4,
+                                                int2* __restrict__ info,
+                                                uint32_t* __restrict__ ocount) {
+    OriKey K;
+    if (!orientation_key(f, sub == 0, pyr, mask, row_base, total_rows, fp, out4, info, ocount, K))
+        return;
+    float vote[37];
+    orientation_hist(K.g, K.W, K.H, K.kx, K.ky, K.kz, fp, sub, vote_l, vote);
+    if (sub != 0) return;
+    orientation_finish(f, vote, K, fp, out4, ocount);
+}
+
+// The histogram of orientation_hist evaluated by a whole wave, for few candidates (a single
+// image: ~1,500 candidates leave most SIMDs idle under the quad form, and each quad walks its
+// window serially): 64 window samples at a time are evaluated in parallel, then lane b < 36
+// adds the batch's votes for bin b in sample order.  Each bin sees the reference's sequence of
+// float adds (the other samples add nothing: acc + 0.0f = acc, acc >= +0), so the histogram is
+// orientation_hist's bit for bit.  Same window, sample arithmetic and smoothing.
+__device__ __forceinline__ void orientation_hist_wave(const OriKey& K, const FeatureParams& fp,
+                                                      int lane, float* s_v, float (&vote)[37]) {
+    const float ten_degree_per_radius = (float)5.7295779513082320876798154814105;
+    const float gsigma = K.kz * fp.gaussian_factor;
+    const float win = fabs_(K.kz) * fp.sample_factor;
+    const float dist_threshold = (float)((double)(win * win) + 0.5);
+    const float factor = -0.5f / (gsigma * gsigma);
+    const float xmin = fmax_(1.5f, floor_(K.kx - win) + 0.5f);
+    const float ymin = fmax_(1.5f, floor_(K.ky - win) + 0.5f);
+    const float xmax = fmin_(K.W - 1.5f, floor_(K.kx + win) + 0.5f);
+    const float ymax = fmin_(K.H - 1.5f, floor_(K.ky + win) + 0.5f);
+    const int ncols = xmax >= xmin ? (int)(xmax - xmin) + 1 : 0;
+    const int nrows = ymax >= ymin ? (int)(ymax - ymin) + 1 : 0;
+    const int total = ncols * nrows;
+    float acc = 0.0f;   // bin `lane`
+    for (int base = 0; base < total; base += 64) {
+        const int sidx = base + lane;
+        int bin = -1;
+        float weight = 0.0f;
+        if (sidx < total) {
+            const int r = sidx / ncols, c = sidx - r * ncols;
+            const float x = xmin + (float)c, y = ymin + (float)r;
+            const float dx = x - K.kx, dy = y - K.ky;
+            const float sq = fma_(dx, dx, dy * dy);
+            if (!(fp.circular && sq >= dist_threshold)) {
+                const float* p = K.g + (long long)(int)y * K.W + (int)x;
+                const float gdx = p[1] - p[-1], gdy = p[K.W] - p[-K.W];   // grad_at
+                const float grd = 0.5f * sqrt_(fma_(gdx, gdx, gdy * gdy));
+                const float rot = grd == 0.0f ? 0.0f : atan2_(gdy, gdx);
+                weight = grd * exp_(sq * factor);
+                bin = (int)floor_(rot * ten_degree_per_radius);
+                if (bin < 0) bin += 36;
+            }
+        }
+        const int nb = min(64, total - base);   // uniform
+        for (int k = 0; k < nb; k++) {
+            const int bk = __builtin_amdgcn_readlane(bin, k);
+            const float wk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(weight), k));
+            acc += bk == lane ? wk : 0.0f;
+        }
+    }
+    if (lane < 36) s_v[lane] = acc;
+    asm volatile("" ::: "memory");   // one wave: its LDS writes complete before its reads
+#pragma unroll
+    for (int i = 0; i < 36; ++i) vote[i] = s_v[i];
+    asm volatile("" ::: "memory");
+    const float one_third = (float)(1.0 / 3.0);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        vote[36] = vote[0];
+        float pre = vote[35];
+#pragma unroll
+        for (int j = 0; j < 36; ++j) {
+            const float temp = one_third * (pre + vote[j] + vote[j + 1]);
+            pre = vote[j];
+            vote[j] = temp;
+        }
+    }
+    vote[36] = vote[0];
+}
+
+// One wave per candidate, grid-stride (the few-candidates form of k_orientation; same outputs).
+__global__ __launch_bounds__(256) void k_orientation_wave(const float* __restrict__ pyr,
+                                                          const uint32_t* __restrict__ mask,
+                                                          const uint32_t* __restrict__ row_base,
+                                                          int total_rows,
+                                                          const uint32_t* __restrict__ n_cand_dev,
+                                                          uint32_t cap, const FeatureParams fp,
+                                                          float4* __restrict__ out4,
+                                                          int2* __restrict__ info,
+                                                          uint32_t* __restrict__ ocount) {
+    __shared__ float s_vote[4][64];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t n = min(*n_cand_dev, cap);
+    for (uint32_t f = blockIdx.x * 4 + wave; f < n; f += gridDim.x * 4) {   // uniform per wave
+        OriKey K;
+        if (!orientation_key(f, lane == 0, pyr, mask, row_base, total_rows, fp, out4, info,
+                             ocount, K))
+            continue;
+        float vote[37];
+        orientation_hist_wave(K, fp, lane, s_vote[wave], vote);
+        if (lane == 0) orientation_finish(f, vote, K, fp, out4, ocount);
+        asm volatile("" ::: "memory");   // the next candidate's votes overwrite s_vote after
+    }
 }
 
 // Grid-stride over the candidates (the grid is sized from the buffer capacity, the count is
@@ -2418,8 +2541,15 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tm
 hipError_t launch_orientation(const float* pyr, const uint32_t* mask, const uint32_t* row_base,
                               int total_rows, const uint32_t* n_cand_dev, int n_cand_cap,
                               int grid_hint, const FeatureParams& fp, float4* out4, int2* info,
-                              uint32_t* ocount, hipStream_t stream) {
+                              uint32_t* ocount, hipStream_t stream, bool wave_per_candidate) {
     if (n_cand_cap <= 0) return hipSuccess;
+    if (wave_per_candidate) {
+        const unsigned grid = (unsigned)std::max(1LL, std::min(((long long)grid_hint + 3) / 4, 8192LL));
+        hipLaunchKernelGGL(k_orientation_wave, dim3(grid), dim3(256), 0, stream, pyr, mask,
+                           row_base, total_rows, n_cand_dev, (uint32_t)n_cand_cap, fp, out4, info,
+                           ocount);
+        return hipGetLastError();
+    }
     const unsigned grid = (unsigned)std::max(1LL, std::min(((long long)grid_hint + 63) / 64, 4096LL));
     hipLaunchKernelGGL(k_orientation, dim3(grid), dim3(256), 0, stream, pyr, mask, row_base,
                        total_rows, n_cand_dev, (uint32_t)n_cand_cap, fp, out4, info, ocount);

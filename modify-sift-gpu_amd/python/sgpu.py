@@ -419,6 +419,7 @@ class SiftContext:
     DEBUG_KEYED_MATCH = 64    # keyed matcher epilogue even when ratiomax <= 1
     DEBUG_FULL_COLUMNS = 128  # mutual matching decides every column, not only the matched ones
     DEBUG_GAUSS_WAVE1 = 256   # round 2's k_gauss_wave instead of the lean level kernel
+    DEBUG_ORIENT_WAVE = 512   # orientation one wave per candidate for any candidate count
 
     def set_debug_flags(self, flags: int):
         """Per-context debug flags (sgpu_debug_set_flags; 0 = shipped configuration)."""

@@ -660,6 +660,35 @@ def test_rect_keypoints_vs_oracle(gpu_ctx, over):
     gpu_ctx.set_options(default_options())
 
 
+@pytest.mark.parametrize("over", [{}, {"max_orientation": 1}, {"fixed_orientation": 1},
+                                  {"circular_window": 1}, {"keep_extremum_sign": 1},
+                                  {"subpixel": 0}, {"octave_min": -1}])
+def test_orientation_wave_equals_quad(gpu_ctx, over):
+    """Orientation one wave per candidate (the few-candidates form, SGPU_DEBUG_ORIENT_WAVE)
+    against the quad form on a batch with more candidates than the wave form's automatic limit
+    (so the unflagged run takes the quad form): every key bit for bit, and the oracle on one
+    image."""
+    imgs = synth_batch(20, 1280, 720, 610)
+    opts = default_options(**over)
+    gpu_ctx.set_options(opts)
+    try:
+        gpu_ctx.set_debug_flags(0)
+        gpu_ctx.extract(imgs)
+        gpu_ctx.extract(imgs)   # the candidate-count hint of this batch: above the wave limit
+        assert len(gpu_ctx.candidates()[0]) > 16384
+        quad = [gpu_ctx.features(i, descriptors=False)[0] for i in range(len(imgs))]
+        gpu_ctx.set_debug_flags(gpu_ctx.DEBUG_ORIENT_WAVE)
+        gpu_ctx.extract(imgs)
+        wave = [gpu_ctx.features(i, descriptors=False)[0] for i in range(len(imgs))]
+        for i, (a, b) in enumerate(zip(quad, wave)):
+            assert a.shape == b.shape and np.array_equal(_bits(a), _bits(b)), i
+        rk, _ = O.extract(imgs[3], opts)
+        assert np.array_equal(_bits(wave[3]), _bits(rk))
+    finally:
+        gpu_ctx.set_debug_flags(0)
+        gpu_ctx.set_options(default_options())
+
+
 def test_keypoints_outside_the_image(gpu_ctx):
     """Caller keys far outside the image, with huge, tiny and negative scales: every sample box
     is clamped to the plane (the relaxed descriptor's loads stay inside it too), the results are
