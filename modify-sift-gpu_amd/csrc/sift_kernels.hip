@@ -704,7 +704,7 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
     float* h_wr = s_h + 2 * hp * HS + hc;
     const float* v_rd = s_h + 4 * vq * HS + vc;              // rows before the wrap
     const float* v_rd_amb = v_rd - (vq ? RS * HS : 0);       // rows where only vq = 1 wrapped
-    const uint32_t st_off = (uint32_t)(4 * vq * W + vc);     // lane offset of the V-pass stores
+    const uint32_t st_off = (uint32_t)(4 * vq * W + x);      // lane offset of the V-pass stores
     const uint32_t ds_off = (uint32_t)(2 * vq * dsw + (x >> 1));
     // step c (ring slot K = c mod 4): H pass of input chunk c, V pass of output chunk c - LAG,
     // loads of chunk c + NST into `nxt`, chunk c + 1 (`cur`) into the row-pair buffer
