@@ -152,7 +152,23 @@ void to_float_f(const float* p, unsigned fmt, int w, int h, std::vector<float>* 
     }
 }
 
-bool set_image(HostImage* img, int w, int h, const void* data, unsigned fmt, unsigned type) {
+// The CUDA path's float luminance input without down-sampling is used in place, and with a
+// width that is not a multiple of 4 the reference compacts its rows to the truncated width IN
+// THE CALLER'S BUFFER (GLTexImage.cpp:994-1006, through the const pointer of RunSIFT): row i
+// (i >= 1) moves from i * w to i * (w & ~3).  Reproduced, because a caller can observe it.
+void compact_caller_rows(const void* data, int w, int h) {
+    const int tw = w & ~3;
+    if (tw == w) return;
+    float* p = const_cast<float*>(static_cast<const float*>(data));
+    for (int i = 1; i < h; ++i) {
+        float* dst = p + (size_t)i * tw;
+        const float* src = p + (size_t)i * w;
+        for (int j = 0; j < tw; ++j) *dst++ = *src++;
+    }
+}
+
+bool set_image(HostImage* img, int w, int h, const void* data, unsigned fmt, unsigned type,
+               int down_sampled) {
     const bool fmt_ok = fmt == kGL_LUMINANCE || fmt == kGL_LUMINANCE_ALPHA || fmt == kGL_RGB ||
                         fmt == kGL_RGBA || fmt == kGL_BGR || fmt == kGL_BGRA;
     const bool type_ok = type == kGL_UNSIGNED_BYTE || type == kGL_UNSIGNED_SHORT || type == kGL_FLOAT;
@@ -181,6 +197,11 @@ bool set_image(HostImage* img, int w, int h, const void* data, unsigned fmt, uns
     if (type == kGL_UNSIGNED_BYTE) to_float((const uint8_t*)data, fmt, w, h, 255.0f, &img->f32);
     else if (type == kGL_UNSIGNED_SHORT) to_float((const uint16_t*)data, fmt, w, h, 65535.0f, &img->f32);
     else to_float_f((const float*)data, fmt, w, h, &img->f32);
+    if (type == kGL_FLOAT && fmt == kGL_LUMINANCE && down_sampled == 0) {
+        // the host copy keeps the caller's full rows (the pipeline truncates on the device);
+        // the caller's buffer is compacted as the reference leaves it
+        compact_caller_rows(data, w, h);
+    }
     return true;
 }
 
@@ -462,7 +483,11 @@ int SiftGPU::RunSIFT(int width, int height, const void* data, unsigned int gl_fo
     if (width <= 0 || height <= 0 || !data) return 0;
     _imgpath[0] = 0;
     const double t0 = now_s();
-    if (!set_image(IMG(_texImage), width, height, data, gl_format, gl_type)) return 0;
+    const sgpu_options& o = RT(_pyramid)->opt;
+    const int down_sampled = sgp::plan_input(width, height, o.octave_min, o.max_dimension,
+                                             o.preprocess_on_cpu).ds;
+    if (!set_image(IMG(_texImage), width, height, data, gl_format, gl_type, down_sampled))
+        return 0;
     RT(_pyramid)->t_load = (float)(now_s() - t0);
     _image_loaded = 2;
     return RunSIFT();

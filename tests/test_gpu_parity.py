@@ -879,3 +879,32 @@ def test_sharded_match_equals_full(gpu_ctx, bounds, fused):
     # the convenience call: column states all-gathered by RCCL (one rank on this box)
     gpu_ctx.comm_init(1, 0, sgpu.comm_unique_id())
     np.testing.assert_array_equal(gpu_ctx.match_sharded(q1, 0, q2), full)
+
+
+def test_float_input_compacts_caller_rows(tmp_path):
+    """RunSIFT(w, h, float*, GL_LUMINANCE, GL_FLOAT) with w % 4 != 0 leaves the caller's buffer
+    with its rows compacted to the truncated width (GLTexImage.cpp:994-1006), and the features
+    are the oracle's for the float input."""
+    lib = os.path.join(ROOT, "modify-sift-gpu_amd", "lib", "libsiftgpu.so")
+    exe = tmp_path / "float_input"
+    r = subprocess.run(["g++", "-std=c++11", "-O1", "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "tests", "abi", "float_input_replica.cpp"),
+                        "-o", str(exe), "-ldl"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    w, h = 331, 251
+    img = (synth_image(w, h, 81).astype(np.float32) / 255.0).astype(np.float32)
+    src = tmp_path / "img.f32"
+    img.tofile(src)
+    after, keys = tmp_path / "after.f32", tmp_path / "keys.f32"
+    r = subprocess.run([str(exe), lib, str(src), str(w), str(h), str(after), str(keys)],
+                       capture_output=True, text=True, timeout=120, env=EXACT_ENV)
+    assert r.returncode == 0, r.stdout + r.stderr
+    num = int([l for l in r.stdout.splitlines() if l.startswith("RESULT ")][0].split()[1])
+    tw = w & ~3
+    want = img.reshape(-1).copy()
+    for i in range(1, h):
+        want[i * tw:(i + 1) * tw] = img[i, :tw]
+    assert np.array_equal(np.fromfile(after, np.float32), want)
+    k = np.fromfile(keys, np.float32).reshape(-1, 4)
+    rk, _ = O.extract_f32(img)
+    assert num == len(rk) and np.array_equal(_bits(k), _bits(rk))
