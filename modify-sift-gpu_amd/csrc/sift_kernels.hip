@@ -2014,6 +2014,11 @@ __device__ __forceinline__ float quad_sum(float v) {
     return v;
 }
 
+#ifndef SGK_DESC_RSTEP
+#define SGK_DESC_RSTEP 4
+#endif
+static_assert(SGK_DESC_RSTEP == 1 || SGK_DESC_RSTEP == 2 || SGK_DESC_RSTEP == 4, "rows per quad step");
+
 template <bool RECT>
 __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
                                                 const float* __restrict__ pyr,
@@ -2147,15 +2152,21 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
     // may read up to 4 floats past the row end, which are the next row's (a sample is at most in
     // column W-2 and row H-2) and feed no valid sample; past the last strip a lane re-reads its
     // last strip.
-    int r = sub, c = 0, lo = 0, len = 0;
-    auto next_row = [&]() {   // advance r (by 4) to the next row with a non-empty span
-        for (; r < nrows; r += 4) {
+    // DESC_RSTEP rows walked by the quad side by side: lanes per row LPR = 4 / RSTEP, lane
+    // (rsub, csub) walks rows rsub, rsub + RSTEP, ... in strips starting 4 csub columns into the
+    // span, 4 LPR apart (RSTEP 4: every lane its own rows; 2: two lanes on adjacent strips of one
+    // row, so a load instruction touches half the cache lines)
+    constexpr int RSTEP = SGK_DESC_RSTEP, LPR = 4 / RSTEP;
+    const int rsub = sub / LPR, c4 = 4 * (sub % LPR);
+    int r = rsub, c = 0, lo = 0, len = 0;
+    auto next_row = [&]() {   // advance r (by RSTEP) to the next row with samples for this lane
+        for (; r < nrows; r += RSTEP) {
             row_span(r, lo, len);
-            if (len > 0) break;
+            if (len > c4) break;
         }
     };
     if (ncols > 0) next_row(); else r = nrows;
-    c = lo;
+    c = lo + c4;
     f4v na, nb, nu, nd;
     // the address loaded when no sample is left: row 1, column 1 of the plane, whose 4 loads
     // (columns 0 .. 5 of row 1, columns 1 .. 4 of rows 0 and 2) stay inside it for any feature --
@@ -2174,11 +2185,11 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
         const float dy = (ymin + (float)r) - pty;
         const int nv = lo + len - c;   // samples of this strip inside the span
         const float dx0 = (xmin + (float)c) - ptx;
-        c += 4;
+        c += 4 * LPR;
         if (c >= lo + len) {
-            r += 4;
+            r += RSTEP;
             next_row();
-            c = lo;
+            c = lo + c4;
         }
         fetch();
         sample(dx0, dy, b.x - a.x, dn.x - up.x, true);
