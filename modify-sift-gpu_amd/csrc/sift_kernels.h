@@ -51,6 +51,18 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         float* ds_dst, int ds_w, int ds_h, long long ds_img_stride,
                         hipStream_t stream, int wave_rows = -1, bool lean = true);
 
+// Two levels per launch (k_gauss_pair): dst_a = V(H(src)) with taps_a, dst_b = V(H(dst_a))
+// with taps_b (+ the 2x decimation of dst_b into ds_dst when given), bit-identical to two
+// launch_gauss calls; level a is written once and never read back.  Compiled for the width pairs
+// of the default schedule: gauss_pair_supported() says whether a call can take it.
+bool gauss_pair_supported(int fw_a, int fw_b, int src_stride, long long src_img_stride, int w,
+                          const void* src);
+hipError_t launch_gauss_pair(const float* src, const uint8_t* src_u8, int src_stride,
+                             long long src_img_stride, float* dst_a, float* dst_b,
+                             long long dst_img_stride, int w, int h, int fw_a, const Taps& taps_a,
+                             int fw_b, const Taps& taps_b, int batch, float* ds_dst, int ds_w,
+                             int ds_h, long long ds_img_stride, hipStream_t stream);
+
 // First octave of -fo != 0 (BuildPyramid, PyramidCU.cpp:1011-1016): the batch's input
 // (u8 p/255 or f32; tw = w & ~3 columns used, rows `stride` apart) resampled into dst
 // (dw x dh per image, dst_img_stride apart): SampleImageD by 2^fo for fo > 0, UpsampleKernel

@@ -788,6 +788,400 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Two Gaussian levels per launch (level k -> k+1 -> k+2), wave-streaming: moves fewer bytes than
+// two level launches -- level k+1 is written once and never read back (the second filter takes
+// it from LDS): 12 B per pixel for two f32 levels instead of 16, 9 instead of 13 for the u8 ingest
+// pair (input -> level 0 -> level 1).  Each wave owns a 64-column strip band as in k_gauss_lean:
+//   stage A (level k+1): the H pass on the input chunk into ring A and the V pass from it, over
+//     the strip plus the second filter's halo (MW = 64 + 2 A2 columns, A2 = HALF_B rounded up to
+//     4); its own 64 columns go to HBM, all MW columns to the mid row-pair buffer (which aliases
+//     the input row-pair buffer: the input chunk has been read, the next one is stored after the
+//     second H pass), mid columns left of 0 / right of W-1 replaced by columns 0 / W-1
+//     (FilterH's clamp-to-edge on level k+1);
+//   stage B (level k+2): k_gauss_lean's H pass on the mid rows into ring B, and its V pass, which
+//     reads the mid rows clamped to 0 .. H-1 (FilterV's clamp on level k+1) -- the mid stream has
+//     a row per stream position, the rows outside the image are never read.
+// Same taps in the same order as the level kernels: bit-identical levels.
+#ifndef SGK_GP_WAVES
+#define SGK_GP_WAVES 2
+#endif
+constexpr int kGpWaves = SGK_GP_WAVES;   // waves per workgroup of k_gauss_pair
+
+template <int FWA, int FWB, bool U8, bool DSB>
+__global__ __launch_bounds__(64 * kGpWaves) void k_gauss_pair(
+    const float* __restrict__ src, const uint8_t* __restrict__ src8, int src_stride,
+    long long src_img_stride, float* __restrict__ dstA, float* __restrict__ dstB,
+    long long dst_img_stride, int W, int H, Taps tapsA, Taps tapsB, float* __restrict__ ds,
+    int dsw, int dsh, long long ds_img_stride, GaussWaveGrid gg) {
+    constexpr int HA = FWA >> 1, HB = FWB >> 1;
+    constexpr int OFFB = (-HB) & 3;
+    constexpr int A2 = HB + OFFB;                     // mid halo per side (multiple of 4)
+    constexpr int MW = GT + 2 * A2;                   // mid columns per strip
+    constexpr int OFFA = (-HA) & 3;
+    constexpr int IN_WA = MW + FWA - 1 + OFFA;        // input columns per row
+    constexpr int NQA = (IN_WA + 3) / 4;
+    static_assert(NQA <= 32, "a row's quads fit half a wave");
+    constexpr int SHA = OFFA & 1;
+    constexpr int IN_SA0 = (4 * NQA + SHA + 3) & ~3;
+    constexpr int IN_SA = IN_SA0 + ((2 - IN_SA0) & 31);
+    constexpr int SHB = OFFB & 1;                     // mid LDS index j + SHB <-> mid column m0 + j
+    constexpr int IN_SB0 = (MW + SHB + 3) & ~3;
+    constexpr int IN_SB = IN_SB0 + ((2 - IN_SB0) & 31);
+    constexpr int NRDA = (FWA + 3) / 2, NRDB = (FWB + 3) / 2;
+    constexpr int LAGA = (FWA - 1 + WCH - 1) / WCH, LAGB = (FWB - 1 + WCH - 1) / WCH;
+    static_assert(WCH * (LAGA + 1) <= 32 && WCH * (LAGB + 1) <= 32, "4 ring slots");
+    constexpr int RS = 32;
+    constexpr int HSA = MW + 4, HSB = GT + SGK_GW_HSPAD;
+    constexpr int NPAIR = WCH / 2;
+    constexpr int NGA = MW / 4, NTA = NPAIR * NGA;    // stage-A H tasks (2 rows x 4 columns)
+    constexpr int NVA = MW / 2, NTV = 2 * NVA;        // stage-A V tasks (4 rows x 2 columns)
+    static_assert(NTA <= 128 && NTV <= 128, "two rounds of 64 lanes");
+    constexpr int NST = 4;
+    constexpr int SIN = (NPAIR * IN_SA > NPAIR * IN_SB ? NPAIR * IN_SA : NPAIR * IN_SB) + 4;
+    __shared__ __attribute__((aligned(16))) f2v s_in_all[kGpWaves][SIN];
+    __shared__ __attribute__((aligned(16))) float s_ha_all[kGpWaves][RS * HSA];
+    __shared__ __attribute__((aligned(16))) float s_hb_all[kGpWaves][RS * HSB];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int gw = xcd_block(blockIdx.x, gridDim.x) * kGpWaves + wave;
+    if (gw >= gg.total_waves) return;
+    const int sx = gw % gg.strips_x, rest = gw / gg.strips_x;
+    const int x0 = sx * GT, m0 = x0 - A2;
+    const int sy = rest % gg.nsy, b = rest / gg.nsy;
+    const int yb = sy * gg.rows_per_band;
+    const int ye = min(H, yb + gg.rows_per_band);
+    const int nchunk_out = (ye - yb + WCH - 1) / WCH;
+    f2v* s_in = s_in_all[wave];
+    f2v* s_mid = s_in_all[wave];                     // aliases s_in (see above)
+    float* s_ha = s_ha_all[wave];
+    float* s_hb = s_hb_all[wave];
+
+    const float* sf = U8 ? nullptr : src + (long long)b * src_img_stride;
+    const uint8_t* s8 = U8 ? src8 + (long long)b * src_img_stride : nullptr;
+    const int a0 = m0 - HA - OFFA;                    // first input column (4-aligned)
+    const int ys0 = yb - HB - HA;                     // input row of stream position 0
+    // loaders: as k_gauss_lean
+    const int lg = lane >> 5, lj = min(lane & 31, NQA - 1);
+    const bool lreal = (lane & 31) < NQA;
+    const int gq = a0 + 4 * lj;
+    const int lq = clampi(gq, 0, W - 4);
+    const bool left = gq < 0, right = gq > W - 4;
+    const bool edge_in = a0 < 0 || a0 + 4 * NQA > W;
+    const uint32_t loff0 = (uint32_t)(2 * lg * src_stride + lq), loff1 = loff0 + (uint32_t)src_stride;
+    const int s_off = lreal ? lg * IN_SA + 4 * lj + SHA : NPAIR * IN_SA;
+
+    struct Elem { float4 v0, v1; };
+    Elem st[NST][2];
+    auto load_chunk = [&](Elem (&stage)[2], int c) {
+        const int rb = ys0 + WCH * c;
+        if (rb >= 0 && rb + WCH <= H) {
+#pragma unroll
+            for (int m = 0; m < 2; m++) {
+                const long long ro = (long long)(rb + 4 * m) * src_stride;
+                if (U8) {
+                    const uint8_t* r = s8 + ro;
+                    stage[m].v0.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(r + loff0));
+                    stage[m].v1.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(r + loff1));
+                } else {
+                    const float* r = sf + ro;
+                    stage[m].v0 = *reinterpret_cast<const float4*>(r + loff0);
+                    stage[m].v1 = *reinterpret_cast<const float4*>(r + loff1);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < 2; m++) {
+                const int y0 = clampi(rb + 4 * m + 2 * lg, 0, H - 1);
+                const int y1 = clampi(rb + 4 * m + 2 * lg + 1, 0, H - 1);
+                if (U8) {
+                    stage[m].v0.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(s8 + (long long)y0 * src_stride + lq));
+                    stage[m].v1.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(s8 + (long long)y1 * src_stride + lq));
+                } else {
+                    stage[m].v0 = *reinterpret_cast<const float4*>(sf + (long long)y0 * src_stride + lq);
+                    stage[m].v1 = *reinterpret_cast<const float4*>(sf + (long long)y1 * src_stride + lq);
+                }
+            }
+        }
+    };
+    auto store_chunk = [&](const Elem (&stage)[2]) {
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            f2v pr[4];
+            if (U8) {
+                const uint32_t w0 = __float_as_uint(stage[m].v0.x), w1 = __float_as_uint(stage[m].v1.x);
+                const float c = 1.0f / 255.0f;
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const f2v x{(float)((w0 >> (8 * t)) & 255u), (float)((w1 >> (8 * t)) & 255u)};
+                    const f2v q = x * f2v{c, c};
+                    const f2v r = __builtin_elementwise_fma(-q, f2v{255.0f, 255.0f}, x);
+                    pr[t] = __builtin_elementwise_fma(r, f2v{c, c}, q);
+                }
+            } else {
+                pr[0] = f2v{stage[m].v0.x, stage[m].v1.x};
+                pr[1] = f2v{stage[m].v0.y, stage[m].v1.y};
+                pr[2] = f2v{stage[m].v0.z, stage[m].v1.z};
+                pr[3] = f2v{stage[m].v0.w, stage[m].v1.w};
+            }
+            if (edge_in) {
+                const f2v e0 = pr[0], e3 = pr[3];
+#pragma unroll
+                for (int t = 0; t < 4; t++) pr[t] = left ? e0 : (right ? e3 : pr[t]);
+            }
+            f2v* q = s_in + s_off + 2 * m * IN_SA;
+            if (SHA == 0) {
+                reinterpret_cast<float4*>(q)[0] = make_float4(pr[0].x, pr[0].y, pr[1].x, pr[1].y);
+                reinterpret_cast<float4*>(q)[1] = make_float4(pr[2].x, pr[2].y, pr[3].x, pr[3].y);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 4; t++) q[t] = pr[t];
+            }
+        }
+    };
+
+#pragma unroll
+    for (int k = 0; k < NST; k++) load_chunk(st[k], k);
+    store_chunk(st[0]);
+    float* dA = dstA + (long long)b * dst_img_stride;
+    float* dB = dstB + (long long)b * dst_img_stride;
+    float* dd = DSB ? ds + (long long)b * ds_img_stride : nullptr;
+    // stage-A lane tasks, two rounds (round 1: lanes past the last task repeat it and store nothing)
+    int haR[2], haW[2], vaR[2], vaRa[2], vaM[2], vaC[2], vaQ[2];
+    bool vaOut[2], vaAny[2];
+#pragma unroll
+    for (int rd = 0; rd < 2; rd++) {
+        const int t = min(lane + 64 * rd, NTA - 1);
+        const int hp = t / NGA, hc = (t - hp * NGA) * 4;
+        haR[rd] = hp * IN_SA + hc + OFFA + SHA;       // f2v index of the first H_A read
+        haW[rd] = 2 * hp * HSA + hc;                  // ring A float index of row 2hp, column hc
+        const int tv = lane + 64 * rd;
+        vaAny[rd] = tv < NTV;
+        const int tvc = min(tv, NTV - 1);
+        const int vq = tvc / NVA, vc = (tvc - vq * NVA) * 2;   // mid column m0 + vc
+        vaQ[rd] = vq;
+        vaC[rd] = vc;
+        vaR[rd] = 4 * vq * HSA + vc;
+        vaRa[rd] = vaR[rd] - (vq ? RS * HSA : 0);
+        vaM[rd] = (2 * vq) * IN_SB + vc + SHB;        // f2v index of the mid pair (rows 4vq, 4vq+1)
+        const int xo = x0 + vc - A2;                  // own output column
+        vaOut[rd] = tv < NTV && vc >= A2 && vc < A2 + GT && xo < W;
+    }
+    const bool edge_mid = m0 < 0 || m0 + MW > W;      // uniform
+    // stage B lanes: as k_gauss_lean
+    const int hp = lane >> 4, hc = (lane & 15) * 4;
+    const int vq = lane >> 5, vc = (lane & 31) * 2;
+    const int x = x0 + vc;
+    const bool full_cols = x0 + GT <= W;
+    const f2v* hb_rd = s_mid + hp * IN_SB + hc + OFFB + SHB;
+    float* hb_wr = s_hb + 2 * hp * HSB + hc;
+    const float* vb_rd = s_hb + 4 * vq * HSB + vc;
+    const float* vb_rd_amb = vb_rd - (vq ? RS * HSB : 0);
+    const uint32_t st_off = (uint32_t)(4 * vq * W + x);
+    const uint32_t ds_off = (uint32_t)(2 * vq * dsw + (x >> 1));
+    const int ym0 = yb - HB;                          // mid row of mid stream position 0
+
+    auto step = [&](int c, auto KC, Elem (&cur)[2], Elem (&nxt)[2]) {
+        constexpr int K = decltype(KC)::value;
+        constexpr int KA = (K - LAGA) & 3;            // ring slot of the V_A chunk / H_B chunk
+        constexpr int KB = (K - LAGA - LAGB) & 3;     // ring-B slot of the V_B chunk
+        // ---- H_A: input chunk c -> ring A slot K
+#pragma unroll
+        for (int rd = 0; rd < 2; rd++) {
+            if (rd == 1 && NTA <= 64) break;
+            const f2v* rp = s_in + haR[rd];
+            f2v a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+            for (int q = 0; q < NRDA; q++) {
+                const float4 v = reinterpret_cast<const float4*>(rp)[q];
+                const f2v e[2] = {f2v{v.x, v.y}, f2v{v.z, v.w}};
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const int m = 2 * q + u;
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        if (m - i >= 0 && m - i < FWA) a[i] = pk_fma(e[u], tapsA.k[m - i], a[i]);
+                }
+            }
+            float* w = s_ha + haW[rd] + WCH * K * HSA;
+            *reinterpret_cast<float4*>(w) = make_float4(a[0].x, a[1].x, a[2].x, a[3].x);
+            *reinterpret_cast<float4*>(w + HSA) = make_float4(a[0].y, a[1].y, a[2].y, a[3].y);
+        }
+        asm volatile("" ::: "memory");
+        const int kA = c - LAGA;                      // mid chunk (uniform)
+        if (kA >= 0) {
+            // ---- V_A: mid chunk kA (stream positions 8 kA ..) from ring A slot KA
+#pragma unroll
+            for (int rd = 0; rd < 2; rd++) {
+                if (rd == 1 && NTV <= 64) break;
+                const float* vr = s_ha + vaR[rd];
+                const float* vra = s_ha + vaRa[rd];
+                f2v acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+                for (int m = 0; m < FWA + 3; m++) {
+                    const int rc = WCH * KA + m;
+                    const float* pp = rc < RS - 4 ? vr + rc * HSA
+                                    : rc >= RS ? vr + (rc - RS) * HSA : vra + rc * HSA;
+                    const f2v v = *reinterpret_cast<const f2v*>(pp);
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        if (m - j >= 0 && m - j < FWA) acc[j] = pk_fma(v, tapsA.k[m - j], acc[j]);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++) asm volatile("" : "+v"(acc[j]));
+                // mid rows -> the row-pair buffer (pairs 2vq, 2vq+1), all MW columns
+                f2v* mp = s_mid + vaM[rd];
+                if (SHB == 0) {
+                    reinterpret_cast<float4*>(mp)[0] = make_float4(acc[0].x, acc[1].x, acc[0].y, acc[1].y);
+                    reinterpret_cast<float4*>(mp + IN_SB)[0] = make_float4(acc[2].x, acc[3].x, acc[2].y, acc[3].y);
+                } else {
+                    mp[0] = f2v{acc[0].x, acc[1].x};
+                    mp[1] = f2v{acc[0].y, acc[1].y};
+                    mp[IN_SB] = f2v{acc[2].x, acc[3].x};
+                    mp[IN_SB + 1] = f2v{acc[2].y, acc[3].y};
+                }
+                // level k+1: the strip's own columns, rows [yb, ye)
+                if (vaOut[rd]) {
+                    const int xo = x0 + vaC[rd] - A2;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int y = ym0 + WCH * kA + 4 * vaQ[rd] + j;
+                        if (y >= yb && y < ye)
+                            *reinterpret_cast<f2v*>(&dA[(long long)y * W + xo]) = acc[j];
+                    }
+                }
+            }
+            asm volatile("" ::: "memory");
+            if (edge_mid) {
+                // FilterH's clamp-to-edge on level k+1: every mid column left of 0 takes column
+                // 0, every one right of W-1 takes column W-1 (the copies never read a position
+                // that is written here)
+                const int j_lo = max(0, -m0), j_hi = min(MW, W - m0);   // in-image mid indices
+                for (int e = lane; e < NPAIR * MW; e += 64) {
+                    const int p = e / MW, j = e - p * MW;
+                    const int js = j < j_lo ? j_lo : (j >= j_hi ? j_hi - 1 : j);
+                    if (js != j) s_mid[p * IN_SB + j + SHB] = s_mid[p * IN_SB + js + SHB];
+                }
+            }
+            asm volatile("" ::: "memory");
+            // ---- H_B: mid chunk kA -> ring B slot KA
+            {
+                f2v a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+                for (int q = 0; q < NRDB; q++) {
+                    const float4 v = reinterpret_cast<const float4*>(hb_rd)[q];
+                    const f2v e[2] = {f2v{v.x, v.y}, f2v{v.z, v.w}};
+#pragma unroll
+                    for (int u = 0; u < 2; u++) {
+                        const int m = 2 * q + u;
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+                            if (m - i >= 0 && m - i < FWB) a[i] = pk_fma(e[u], tapsB.k[m - i], a[i]);
+                    }
+                }
+                float* w = hb_wr + WCH * KA * HSB;
+                *reinterpret_cast<float4*>(w) = make_float4(a[0].x, a[1].x, a[2].x, a[3].x);
+                *reinterpret_cast<float4*>(w + HSB) = make_float4(a[0].y, a[1].y, a[2].y, a[3].y);
+            }
+            asm volatile("" ::: "memory");
+            const int kB = kA - LAGB;                 // output chunk (uniform)
+            if (kB >= 0 && kB < nchunk_out) {
+                // ---- V_B: output chunk kB; mid rows clamped to 0 .. H-1 near the image's top /
+                // bottom (FilterV's clamp on level k+1)
+                const int yu = yb + WCH * kB;
+                f2v acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+                if (yu - HB >= 0 && yu + WCH - 1 + HB <= H - 1) {
+#pragma unroll
+                    for (int m = 0; m < FWB + 3; m++) {
+                        const int rc = WCH * KB + m;
+                        const float* pp = rc < RS - 4 ? vb_rd + rc * HSB
+                                        : rc >= RS ? vb_rd + (rc - RS) * HSB : vb_rd_amb + rc * HSB;
+                        const f2v v = *reinterpret_cast<const f2v*>(pp);
+#pragma unroll
+                        for (int j = 0; j < 4; j++)
+                            if (m - j >= 0 && m - j < FWB) acc[j] = pk_fma(v, tapsB.k[m - j], acc[j]);
+                    }
+                } else {
+                    // row of output row yu + 4vq + j, tap i: mid row clamp(yu + 4vq + j - HB + i),
+                    // stream position (that row - ym0), ring row (position & 31)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+#pragma unroll
+                        for (int i = 0; i < FWB; i++) {
+                            const int mr = clampi(yu + 4 * vq + j - HB + i, 0, H - 1);
+                            const int pos = mr - ym0;
+                            const f2v v = *reinterpret_cast<const f2v*>(s_hb + (pos & (RS - 1)) * HSB + vc);
+                            acc[j] = pk_fma(v, tapsB.k[i], acc[j]);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++) asm volatile("" : "+v"(acc[j]));
+                if (full_cols && yu + WCH <= ye && (!DSB || (yu + WCH) / 2 <= dsh)) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        float* row = dB + (long long)(yu + j) * W;
+                        *reinterpret_cast<f2v*>(row + st_off) = acc[j];
+                        if (DSB && !(j & 1)) {
+                            float* drow = dd + (long long)((yu + j) >> 1) * dsw;
+                            if ((x >> 1) < dsw) drow[ds_off] = acc[j].x;
+                            if (x + 1 == W - 1)
+                                for (int cc = W >> 1; cc < dsw; cc++) drow[2 * vq * dsw + cc] = acc[j].y;
+                        }
+                    }
+                } else if (x < W) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int y = yu + 4 * vq + j;
+                        if (y < ye) {
+                            *reinterpret_cast<f2v*>(&dB[(long long)y * W + x]) = acc[j];
+                            if (DSB && !(y & 1) && (y >> 1) < dsh) {
+                                float* drow = dd + (long long)(y >> 1) * dsw;
+                                if ((x >> 1) < dsw) drow[x >> 1] = acc[j].x;
+                                if (x + 1 == W - 1)
+                                    for (int cc = W >> 1; cc < dsw; cc++) drow[cc] = acc[j].y;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        asm volatile("" ::: "memory");
+        load_chunk(nxt, c + NST);
+        store_chunk(cur);
+        asm volatile("" ::: "memory");
+    };
+    const int nsteps = nchunk_out + LAGA + LAGB;
+    for (int c = 0; c < nsteps; c += NST) {
+        step(c + 0, std::integral_constant<int, 0>{}, st[1], st[0]);
+        step(c + 1, std::integral_constant<int, 1>{}, st[2], st[1]);
+        step(c + 2, std::integral_constant<int, 2>{}, st[3], st[2]);
+        step(c + 3, std::integral_constant<int, 3>{}, st[0], st[3]);
+    }
+}
+
+template <int FWA, int FWB>
+hipError_t gauss_pair_dispatch(const float* src, const uint8_t* src8, int src_stride,
+                               long long src_img_stride, float* dstA, float* dstB,
+                               long long dst_img_stride, int w, int h, const Taps& tapsA,
+                               const Taps& tapsB, int batch, float* ds, int dsw, int dsh,
+                               long long ds_img_stride, hipStream_t stream) {
+    const GaussWaveGrid gg = gauss_wave_grid(w, h, batch, 0, 1);
+    const dim3 grid((unsigned)((gg.total_waves + kGpWaves - 1) / kGpWaves));
+#define SGK_PAIR(U8, DS)                                                                      \
+    hipLaunchKernelGGL((k_gauss_pair<FWA, FWB, U8, DS>), grid, dim3(64 * kGpWaves), 0, stream, \
+                       src, src8, src_stride, src_img_stride, dstA, dstB, dst_img_stride, w, h, \
+                       tapsA, tapsB, ds, dsw, dsh, ds_img_stride, gg)
+    if (src8) {
+        if (ds) SGK_PAIR(true, true); else SGK_PAIR(true, false);
+    } else {
+        if (ds) SGK_PAIR(false, true); else SGK_PAIR(false, false);
+    }
+#undef SGK_PAIR
+    return hipGetLastError();
+}
+
 template <int FW>
 hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
                           long long src_img_stride, float* dst, long long dst_img_stride, int w,
@@ -2430,6 +2824,34 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
         default: return hipErrorInvalidValue;
     }
 #undef SGK_GAUSS
+}
+
+hipError_t launch_gauss_pair(const float* src, const uint8_t* src_u8, int src_stride,
+                             long long src_img_stride, float* dst_a, float* dst_b,
+                             long long dst_img_stride, int w, int h, int fw_a, const Taps& taps_a,
+                             int fw_b, const Taps& taps_b, int batch, float* ds_dst, int ds_w,
+                             int ds_h, long long ds_img_stride, hipStream_t stream) {
+    if (!gauss_pair_supported(fw_a, fw_b, src_stride, src_img_stride, w,
+                              src_u8 ? (const void*)src_u8 : (const void*)src))
+        return hipErrorInvalidValue;
+#define SGK_P(A, B)                                                                           \
+    if (fw_a == A && fw_b == B)                                                               \
+        return gauss_pair_dispatch<A, B>(src, src_u8, src_stride, src_img_stride, dst_a, dst_b, \
+                                         dst_img_stride, w, h, taps_a, taps_b, batch, ds_dst,  \
+                                         ds_w, ds_h, ds_img_stride, stream);
+    // the default schedule's pairs (-f 4, -d 3): input -> levels 0, 1 of octave 0 with the
+    // initial smoothing of -fo 0 (13) or -fo -1 (11); levels 2, 3 and 4, 5 of every octave
+    SGK_P(13, 11) SGK_P(11, 11) SGK_P(13, 17) SGK_P(21, 25)
+#undef SGK_P
+    return hipErrorInvalidValue;
+}
+
+bool gauss_pair_supported(int fw_a, int fw_b, int src_stride, long long src_img_stride, int w,
+                          const void* src) {
+    const bool widths = (fw_a == 13 && fw_b == 11) || (fw_a == 11 && fw_b == 11) ||
+                        (fw_a == 13 && fw_b == 17) || (fw_a == 21 && fw_b == 25);
+    return widths && (src_stride % 4) == 0 && (src_img_stride % 4) == 0 && (w % 4) == 0 &&
+           w >= 4 && ((uintptr_t)src % 16) == 0;
 }
 
 hipError_t launch_color_to_gray(const uint8_t* src, int n, int w, int h, int stride,

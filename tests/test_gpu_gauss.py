@@ -1,6 +1,6 @@
-"""Gaussian pyramid kernels on the GPU: the shipped lean level kernel (k_gauss_lean), round 2's
-wave-streaming kernel (k_gauss_wave) and the workgroup strip kernel (k_gauss_pk2) against each
-other and the oracle, bit for bit.
+"""Gaussian pyramid kernels on the GPU: the shipped two-level kernel (k_gauss_pair) and lean level
+kernel (k_gauss_lean), round 2's wave-streaming kernel (k_gauss_wave) and the workgroup strip
+kernel (k_gauss_pk2) against each other and the oracle, bit for bit.
 
 Both kernels restate FilterH / FilterV (ProgramCU.cu:115-222) with the taps summed i = 0..FW-1
 and the 2x decimation of DownsampleKernel<1> (ProgramCU.cu:287-298) fused into the level that
@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
 
 BLOCK = sgpu.SiftContext.DEBUG_GAUSS_BLOCK
 WAVE1 = sgpu.SiftContext.DEBUG_GAUSS_WAVE1
+SINGLE = sgpu.SiftContext.DEBUG_GAUSS_SINGLE
 
 
 def _bits(a):
@@ -61,7 +62,9 @@ def test_wave_levels_equal_block_kernel(gpu_ctx, rows, n, w, h):
     ref = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
     k_ref = [gpu_ctx.features(i)[0].copy() for i in range(n)]
     try:
-        for kernel in (WAVE1, 0):   # k_gauss_wave, then the shipped k_gauss_lean
+        # k_gauss_wave, k_gauss_lean one level per launch, then the shipped mix of two-level
+        # k_gauss_pair launches and k_gauss_lean
+        for kernel in (WAVE1 | SINGLE, SINGLE, 0):
             gpu_ctx.set_debug_flags((rows << 16) | kernel)
             gpu_ctx.extract(imgs)
             got = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
