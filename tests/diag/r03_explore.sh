@@ -8,3 +8,7 @@ echo "== gauss A/B (single levels vs pairs)"
 timeout -k 10 600 bash tests/diag/ab_env.sh "SGPU_GAUSS=single" "SGPU_GAUSS=pair" 3 || exit 1
 echo "== c2"
 timeout -k 10 100 python -c "import bench, json; print(json.dumps(bench.bench_c2(cpu=False)))"
+echo "== kernel trace (pairs)"
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_pair -o run -- python3 bench.py --no-c4 --no-e2e --no-match --no-cpu-baseline --no-c2 > gpurun_out/prof_pair.log 2>&1 || exit 1
+python3 tests/kt_levels.py gpurun_out/prof_pair/run_kernel_trace.csv 12
