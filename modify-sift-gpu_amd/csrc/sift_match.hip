@@ -150,17 +150,24 @@ __device__ __forceinline__ bool tie_before(int a, int b) {
 // waves that hold the column and written to colpart[panel][column].  k_match_cols merges the
 // panels in row order.  The row side is the plain kernel's.
 // RAW (plain matching with ratiomax <= 1): the values are folded as they are, no key -- the
-// accumulators start at the column term, each value costs one v_med3 and one v_max, and a lane
-// records only the tile in which its maximum last grew.  Which of the lane's 8 columns of that
-// tile holds the maximum is recovered in k_match_finish by recomputing those 8 dot products,
-// and only for rows that pass the ratio test: those have second < max, so the maximum is unique
-// and no tie order is needed (an equal second maximum fails the test for ratiomax <= 1,
-// whichever column the reference would have named).
+// accumulators start at the column term, a lane takes each row's maximum over its 8 columns of
+// the tile (v_max3 chains, half a VALU per value) and folds only that into its running (max,
+// second), recording the tile in which the maximum last grew.  The second is then the second
+// largest (tile, lane) maximum -- a lower bound of the row's second, exact unless the row's two
+// largest values share the winning lane's tile.  k_match_finish recomputes the dot products of
+// those 8 columns for every row that passes the ratio test with the lower bound (a row that
+// fails it fails with the exact second too): they give the column of the maximum and the
+// second within them, and the test is repeated with the larger second.  A row that passes has
+// second < max, so its maximum is unique and no tie order is needed (an equal second maximum
+// fails the test for ratiomax <= 1, whichever column the reference would have named).
 // amap / an (compacted rows): row r of A is A[amap[r]], and the row count is *an, known only on
 // the device; the grid is then 1-D and each workgroup derives its (panel, chunk) from the count,
 // with the split chunks_for(*an, nB) (k_match_finish derives the same one).
+#ifndef SGK_MATCH_RAW_WPE
+#define SGK_MATCH_RAW_WPE 1   // minimum waves per SIMD asked of the RAW kernel (1: no cap)
+#endif
 template <bool GUIDED, bool TIE32, bool COLS, bool RAW = false>
-__global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ A, int nA,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAW ? SGK_MATCH_RAW_WPE : 1))) void k_match_rows(const uint8_t* __restrict__ A, int nA,
                                                     const uint8_t* __restrict__ B, int nB,
                                                     int cols_per_chunk, Top2* __restrict__ part,
                                                     const uint4* __restrict__ mask,
@@ -280,14 +287,17 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
         uint4 rec_next = rec;
         if (rec_ok && has_next) rec_next = rec_p[(tb / kTile + 1) * 64];
         int mt[2][4], st[2][4];
+        if constexpr (!RAW) {
 #pragma unroll
-        for (int rb = 0; rb < 2; rb++)
+            for (int rb = 0; rb < 2; rb++)
 #pragma unroll
-            for (int i = 0; i < 4; i++) { mt[rb][i] = M[rb][i]; st[rb][i] = S[rb][i]; }
+                for (int i = 0; i < 4; i++) { mt[rb][i] = M[rb][i]; st[rb][i] = S[rb][i]; }
+        }
         if constexpr (RAW) {
             // the tile in kMatchSplit column groups (accumulators start at the column term;
-            // MFMAs, then the folds, per group), each row folding its values in column order
+            // MFMAs, then the tile maxima, per group)
             constexpr int CB = 8 / kMatchSplit;
+            int tmx[2][4];
 #pragma unroll
             for (int h = 0; h < kMatchSplit; h++) {
                 v4i acc[2][CB];
@@ -307,22 +317,31 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
                         acc[1][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[1][kh], bfrag, acc[1][c], 0, 0, 0);
                     }
                 }
-                // column blocks in groups of 4 for every row: the first group's reads do not
-                // wait on the group's last MFMAs
+                // the tile's maximum per row over this lane's 8 columns (v_max3 chains: half a
+                // VALU per value); folded into the running top-2 once per tile below
 #pragma unroll
-                for (int g = 0; g < CB / 4; g++)
+                for (int rb = 0; rb < 2; rb++)
 #pragma unroll
-                    for (int rb = 0; rb < 2; rb++)
+                    for (int i = 0; i < 4; i++)
 #pragma unroll
-                        for (int i = 0; i < 4; i++)
-#pragma unroll
-                            for (int c = 4 * g; c < 4 * g + 4; c++) {
-                                const int v = acc[rb][c][i];
-                                const int mo = mt[rb][i];
-                                mt[rb][i] = max(mo, v);
-                                st[rb][i] = med3i(st[rb][i], mo, v);
-                            }
+                        for (int c = 0; c < CB; c += 2) {
+                            const int a = acc[rb][c][i], b2 = acc[rb][c + 1][i];
+                            tmx[rb][i] = (h == 0 && c == 0) ? max(a, b2) : max(max(tmx[rb][i], a), b2);
+                        }
             }
+            // one fold per row and tile: the running (max, second) over the lane's tile maxima,
+            // and the tile where the maximum last grew.  The exact second of the row is the
+            // larger of that second and the second within the winning (tile, lane) set of 8
+            // columns, which k_match_finish recomputes for every row that can still pass.
+#pragma unroll
+            for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int v = tmx[rb][i], mo = M[rb][i];
+                    S[rb][i] = med3i(S[rb][i], mo, v);
+                    I[rb][i] = v > mo ? tb : I[rb][i];
+                    M[rb][i] = max(mo, v);
+                }
         } else {
         // plain: the accumulators start at 0 and the column term enters the key,
         // key = (acc << 7) + ((ct << 7) | low) = ((acc + ct) << 7) | low;
@@ -423,21 +442,19 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
             }
         }
         }   // !RAW
+        if constexpr (!RAW) {
 #pragma unroll
-        for (int rb = 0; rb < 2; rb++)
+            for (int rb = 0; rb < 2; rb++)
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int m = mt[rb][i];
-                if constexpr (RAW) {
-                    I[rb][i] = m > M[rb][i] ? tb : I[rb][i];
-                } else {
+                for (int i = 0; i < 4; i++) {
+                    const int m = mt[rb][i];
                     const bool took = (uint32_t)(m ^ M[rb][i]) >= kPrefix;
                     I[rb][i] = took ? tb : I[rb][i];
                     W[rb][i] = took ? m : W[rb][i];
+                    M[rb][i] = m;
+                    S[rb][i] = st[rb][i];
                 }
-                M[rb][i] = m;
-                S[rb][i] = st[rb][i];
-            }
+        }
         // One barrier per tile suffices without COLS: the stores below go to the buffer of tile
         // t - 1, which every wave finished reading before the barrier that ended iteration t - 1
         // (COLS: the panel merge reads the other waves' s_cm / s_cs first).
@@ -510,8 +527,10 @@ __global__ __launch_bounds__(256) void k_match_rows(const uint8_t* __restrict__ 
 // Equal maxima of two chunks resolve in the side's tie order (tie32: RowMatch_Kernel's, see
 // k_match_rows); that choice is associative, so the chunks are merged in any grouping.
 // raw_A / raw_B (u8, 128 bytes per descriptor; RAW partials): part.idx is (tile + lane) of the
-// maximum; a row that passes the ratio test has a unique maximum, found by recomputing the dot
-// products of the lane's 8 columns of that tile.
+// maximum and part.second the second largest (tile, lane) maximum; for a row that passes the
+// ratio test with it, the dot products of the lane's 8 columns of that tile are recomputed: they
+// give the column of the maximum and the second within those 8 columns, and the test is repeated
+// with the larger second.  (best then holds the exact state only for the rows recomputed.)
 // cl.map / cl.count (a launch over compacted rows): row r is row cl.map[r] of this side (its row
 // term, u8 descriptor and output slot), n = *cl.count and the chunks are chunks_for(n, nB).
 // cl.flag (row side of a mutual match): every column that a row matched is appended once to
@@ -563,7 +582,9 @@ __global__ __launch_bounds__(kFinishThreads) void k_match_finish(const Top2* __r
     if (mx <= 0) { mx = 0; idx = -1; }
     if (sc < 0) sc = 0;
     const float d1 = dist[min(mx, 262144)], d2 = dist[min(sc, 262144)];
-    const bool ok = (d1 < distmax) && (d1 < d2 * ratiomax);
+    // raw partials: sc is a lower bound of the second (see below), so a row that fails here
+    // fails with the exact second too
+    bool ok = (d1 < distmax) && (d1 < d2 * ratiomax);
     if (raw_A && ok) {
         // lane k: candidate column (tile) + 16 k + (lane in tile); the lowest equal one wins
         // (there is one: a passing maximum is unique)
@@ -584,6 +605,17 @@ __global__ __launch_bounds__(kFinishThreads) void k_match_finish(const Top2* __r
         const unsigned long long bal = __ballot(c < nB && d == mx);
         const uint32_t mine = (uint32_t)(bal >> (lane & ~7)) & 0xffu;
         idx = mine ? (idx & ~127) + 16 * (__ffs(mine) - 1) + (idx & 15) : -1;
+        // the partials carry the second largest tile maximum; the row's second is the larger of
+        // that and the second within the winning lane's 8 columns (an equal pair counts twice)
+        int m8 = c < nB ? d : INT_MIN, s8 = INT_MIN;
+#pragma unroll
+        for (int off = 1; off < 8; off <<= 1) {
+            const int m2 = __shfl_xor(m8, off, 64), s2 = __shfl_xor(s8, off, 64);
+            s8 = max(min(m8, m2), max(s8, s2));
+            m8 = max(m8, m2);
+        }
+        sc = max(sc, s8);
+        ok = ok && d1 < dist[min(sc, 262144)] * ratiomax;
     }
     const int res = ok ? idx : -1;
     if (valid && sub == 0) {
