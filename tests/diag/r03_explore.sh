@@ -12,3 +12,11 @@ echo "== kernel trace (pairs)"
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_pair -o run -- python3 bench.py --no-c4 --no-e2e --no-match --no-cpu-baseline --no-c2 > gpurun_out/prof_pair.log 2>&1 || exit 1
 python3 tests/kt_levels.py gpurun_out/prof_pair/run_kernel_trace.csv 12
+echo "== matcher parity"
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_workloads.py -k "match or c5" -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_match.log 2>&1; rc=$?
+tail -2 gpurun_out/pytest_match.log
+[ $rc -eq 0 ] || exit $rc
+echo "== matcher A/B: A = tile-max fold (152 VGPR), B = round 2"
+timeout -k 10 400 bash tests/diag/ab_match.sh build_exp/match_r2/libsiftgpu.so 2 || exit 1
+echo "== matcher A/B: A = tile-max fold, B = capped at 4 waves/SIMD"
+timeout -k 10 400 bash tests/diag/ab_match.sh build_exp/match_wpe4/libsiftgpu.so 2 || exit 1
