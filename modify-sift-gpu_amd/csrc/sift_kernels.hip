@@ -49,6 +49,14 @@ __device__ __forceinline__ f2v pk_fma(f2v a, float b, f2v c) {
     return __builtin_elementwise_fma(a, f2v{b, b}, c);
 }
 
+// Tap t of a width-FW filter.  make_filter's taps are symmetric bit for bit (tap i is
+// exp(-i^2 / 2 sigma^2) / sum for i = t - FW/2), so the kernels holding two filters read only
+// the first half: half the scalar registers (two full tap sets spilled SGPRs to VGPR lanes).
+template <int FW>
+__device__ __forceinline__ float tap(const Taps& taps, int t) {
+    return taps.k[t < FW - 1 - t ? t : FW - 1 - t];
+}
+
 // p / 255.0f for an integer p in [0, 255] (GLTexImage.cpp:818: the reference's u8 -> float),
 // correctly rounded without a division: q = p * (1/255) then one fma residual correction.  Exact
 // for all 256 inputs (tests/test_oracle.py::test_u8_scale_is_exact_division).
@@ -721,7 +729,7 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
                     const int m = 2 * q + u;
 #pragma unroll
                     for (int i = 0; i < 4; i++)
-                        if (m - i >= 0 && m - i < FW) a[i] = pk_fma(e[u], taps.k[m - i], a[i]);
+                        if (m - i >= 0 && m - i < FW) a[i] = pk_fma(e[u], tap<FW>(taps, m - i), a[i]);
                 }
             }
             *reinterpret_cast<float4*>(h_wr + WCH * K * HS) = make_float4(a[0].x, a[1].x, a[2].x, a[3].x);
@@ -740,7 +748,7 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
                 const f2v v = *reinterpret_cast<const f2v*>(p);
 #pragma unroll
                 for (int j = 0; j < 4; j++)
-                    if (m - j >= 0 && m - j < FW) acc[j] = pk_fma(v, taps.k[m - j], acc[j]);
+                    if (m - j >= 0 && m - j < FW) acc[j] = pk_fma(v, tap<FW>(taps, m - j), acc[j]);
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) asm volatile("" : "+v"(acc[j]));
@@ -1001,7 +1009,7 @@ __global__ __launch_bounds__(64 * kGpWaves) void k_gauss_pair(
                     const int m = 2 * q + u;
 #pragma unroll
                     for (int i = 0; i < 4; i++)
-                        if (m - i >= 0 && m - i < FWA) a[i] = pk_fma(e[u], tapsA.k[m - i], a[i]);
+                        if (m - i >= 0 && m - i < FWA) a[i] = pk_fma(e[u], tap<FWA>(tapsA, m - i), a[i]);
                 }
             }
             float* w = s_ha + haW[rd] + WCH * K * HSA;
@@ -1026,7 +1034,7 @@ __global__ __launch_bounds__(64 * kGpWaves) void k_gauss_pair(
                     const f2v v = *reinterpret_cast<const f2v*>(pp);
 #pragma unroll
                     for (int j = 0; j < 4; j++)
-                        if (m - j >= 0 && m - j < FWA) acc[j] = pk_fma(v, tapsA.k[m - j], acc[j]);
+                        if (m - j >= 0 && m - j < FWA) acc[j] = pk_fma(v, tap<FWA>(tapsA, m - j), acc[j]);
                 }
 #pragma unroll
                 for (int j = 0; j < 4; j++) asm volatile("" : "+v"(acc[j]));
@@ -1077,7 +1085,7 @@ __global__ __launch_bounds__(64 * kGpWaves) void k_gauss_pair(
                         const int m = 2 * q + u;
 #pragma unroll
                         for (int i = 0; i < 4; i++)
-                            if (m - i >= 0 && m - i < FWB) a[i] = pk_fma(e[u], tapsB.k[m - i], a[i]);
+                            if (m - i >= 0 && m - i < FWB) a[i] = pk_fma(e[u], tap<FWB>(tapsB, m - i), a[i]);
                     }
                 }
                 float* w = hb_wr + WCH * KA * HSB;
@@ -1100,7 +1108,7 @@ __global__ __launch_bounds__(64 * kGpWaves) void k_gauss_pair(
                         const f2v v = *reinterpret_cast<const f2v*>(pp);
 #pragma unroll
                         for (int j = 0; j < 4; j++)
-                            if (m - j >= 0 && m - j < FWB) acc[j] = pk_fma(v, tapsB.k[m - j], acc[j]);
+                            if (m - j >= 0 && m - j < FWB) acc[j] = pk_fma(v, tap<FWB>(tapsB, m - j), acc[j]);
                     }
                 } else {
                     // row of output row yu + 4vq + j, tap i: mid row clamp(yu + 4vq + j - HB + i),
@@ -1112,7 +1120,7 @@ __global__ __launch_bounds__(64 * kGpWaves) void k_gauss_pair(
                             const int mr = clampi(yu + 4 * vq + j - HB + i, 0, H - 1);
                             const int pos = mr - ym0;
                             const f2v v = *reinterpret_cast<const f2v*>(s_hb + (pos & (RS - 1)) * HSB + vc);
-                            acc[j] = pk_fma(v, tapsB.k[i], acc[j]);
+                            acc[j] = pk_fma(v, tap<FWB>(tapsB, i), acc[j]);
                         }
                     }
                 }
