@@ -261,8 +261,9 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
                                      kernel) instead of k_gauss_lean: same levels, bit for bit */
 #define SGPU_DEBUG_ORIENT_WAVE 512 /* orientation one wave per candidate for any count (the shipped
                                      path picks it for few candidates only): same bits */
-#define SGPU_DEBUG_GAUSS_SINGLE 1024 /* one Gaussian level per launch: no two-level k_gauss_pair
-                                        launches (same levels, bit for bit) */
+#define SGPU_DEBUG_GAUSS_PAIR 1024 /* two Gaussian levels per launch (k_gauss_pair) where the
+                                      widths have a compiled pair: same levels, bit for bit;
+                                      measured slower than one level per launch */
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);

@@ -307,8 +307,8 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     // A/B hook for the Gaussian kernels (bench / probe runs in one process tree)
     if (const char* ev = getenv("SGPU_GAUSS")) {
         if (!strcmp(ev, "block")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_BLOCK;
-        else if (!strcmp(ev, "wave")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_WAVE1 | SGPU_DEBUG_GAUSS_SINGLE;
-        else if (!strcmp(ev, "single")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_SINGLE;
+        else if (!strcmp(ev, "wave")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_WAVE1;
+        else if (!strcmp(ev, "pair")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_PAIR;
     }
     int rc = sgpu_ctx_set_options(ctx, opt);
     if (rc != SGPU_OK) {
@@ -492,7 +492,8 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
             const float* tk = k == 0 ? taps0.k : ltaps[k].k;
             for (int i = 0; i < fwk; i++) taps.k[i] = tk[i];
             const bool dk = ds && kds == k;
-            // ops k and k+1 in one launch (k_gauss_pair) when their widths have a compiled pair,
+            // test hook SGPU_DEBUG_GAUSS_PAIR: ops k and k+1 in one launch (k_gauss_pair) when
+            // their widths have a compiled pair,
             // op k does not feed the next octave (only the second level of a pair decimates),
             // and op k does not read the buffer op k+1 writes (-fo != 0 stages its resampled
             // input in level 1's storage)
@@ -500,8 +501,8 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
             const uint8_t* src8_k = k == 0 ? in_8 : nullptr;
             const int stride_k = k == 0 ? in_stride : od.wa;
             const long long img_k = k == 0 ? in_img : npx;
-            if (k + 1 < nlev && kds != k && !(ctx->debug_flags & (SGPU_DEBUG_GAUSS_SINGLE |
-                                                                  SGPU_DEBUG_GAUSS_BLOCK)) &&
+            if (k + 1 < nlev && kds != k && (ctx->debug_flags & SGPU_DEBUG_GAUSS_PAIR) &&
+                !(ctx->debug_flags & (SGPU_DEBUG_GAUSS_BLOCK | SGPU_DEBUG_GAUSS_WAVE1)) &&
                 !(o == 0 && k == 0 && ctx->plan.octave_min != 0) &&
                 sgk::gauss_pair_supported(fwk, lfw[k + 1], stride_k, img_k, od.wa,
                                           src8_k ? (const void*)src8_k : (const void*)src_k)) {

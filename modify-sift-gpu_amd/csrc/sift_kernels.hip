@@ -803,9 +803,9 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
 // pair (input -> level 0 -> level 1).  Each wave owns a 64-column strip band as in k_gauss_lean:
 //   stage A (level k+1): the H pass on the input chunk into ring A and the V pass from it, over
 //     the strip plus the second filter's halo (MW = 64 + 2 A2 columns, A2 = HALF_B rounded up to
-//     4); its own 64 columns go to HBM, all MW columns to the mid row-pair buffer (which aliases
-//     the input row-pair buffer: the input chunk has been read, the next one is stored after the
-//     second H pass), mid columns left of 0 / right of W-1 replaced by columns 0 / W-1
+//     4); its own 64 columns go to HBM, all MW columns to the mid row-pair buffer (its own LDS:
+//     a mid buffer aliased onto the input row-pair buffer measured nondeterministic level-B
+//     differences on gfx950, r03 tests/diag/pair_diff2.py), mid columns left of 0 / right of W-1 replaced by columns 0 / W-1
 //     (FilterH's clamp-to-edge on level k+1);
 //   stage B (level k+2): k_gauss_lean's H pass on the mid rows into ring B, and its V pass, which
 //     reads the mid rows clamped to 0 .. H-1 (FilterV's clamp on level k+1) -- the mid stream has
@@ -846,7 +846,7 @@ __global__ __launch_bounds__(64 * kGpWaves) void k_gauss_pair(
     constexpr int NVA = MW / 2, NTV = 2 * NVA;        // stage-A V tasks (4 rows x 2 columns)
     static_assert(NTA <= 128 && NTV <= 128, "two rounds of 64 lanes");
     constexpr int NST = 4;
-    constexpr int SIN = (NPAIR * IN_SA > NPAIR * IN_SB ? NPAIR * IN_SA : NPAIR * IN_SB) + 4;
+    constexpr int SIN = NPAIR * IN_SA + 4 + NPAIR * IN_SB;   // input pairs, then mid pairs
     __shared__ __attribute__((aligned(16))) f2v s_in_all[kGpWaves][SIN];
     __shared__ __attribute__((aligned(16))) float s_ha_all[kGpWaves][RS * HSA];
     __shared__ __attribute__((aligned(16))) float s_hb_all[kGpWaves][RS * HSB];
@@ -862,7 +862,7 @@ __global__ __launch_bounds__(64 * kGpWaves) void k_gauss_pair(
     const int ye = min(H, yb + gg.rows_per_band);
     const int nchunk_out = (ye - yb + WCH - 1) / WCH;
     f2v* s_in = s_in_all[wave];
-    f2v* s_mid = s_in_all[wave];                     // aliases s_in (see above)
+    f2v* s_mid = s_in_all[wave] + NPAIR * IN_SA + 4;
     float* s_ha = s_ha_all[wave];
     float* s_hb = s_hb_all[wave];
 

@@ -6,7 +6,7 @@ from sift_synth import synth_batch
 ctx = sgpu.SiftContext(0)
 img = synth_batch(1, 1920, 1080, 5)[0]
 out = {}
-for name, fl in (("single", ctx.DEBUG_GAUSS_SINGLE), ("pair", 0), ("pair2", 0)):
+for name, fl in (("single", 0), ("pair", ctx.DEBUG_GAUSS_PAIR), ("pair2", ctx.DEBUG_GAUSS_PAIR)):
     ctx.set_debug_flags(fl)
     ctx.extract(img)
     w, h, wa = ctx.geometry()[0]

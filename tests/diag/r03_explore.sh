@@ -1,11 +1,14 @@
 # Round-3 exploration on the GPU box: lean Gaussian + wave orientation parity, then A/B timings.
 set -o pipefail
 mkdir -p gpurun_out
+echo "== pair kernel determinism (1080p, octave 0 level 5)"
+timeout -k 10 120 python tests/diag/pair_diff2.py > gpurun_out/pair_diff2.log 2>&1 || exit 1
+sed -n 1p gpurun_out/pair_diff2.log
 timeout -k 10 500 python -u -m pytest tests/test_gpu_gauss.py tests/test_gpu_parity.py -k "gauss or levels or golden or first_octave or orientation_wave or compacts" -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_lean.log 2>&1; rc=$?
 tail -3 gpurun_out/pytest_lean.log
 [ $rc -eq 0 ] || exit $rc
 echo "== gauss A/B (single levels vs pairs)"
-timeout -k 10 600 bash tests/diag/ab_env.sh "SGPU_GAUSS=single" "SGPU_GAUSS=pair" 3 || exit 1
+timeout -k 10 600 bash tests/diag/ab_env.sh "SGPU_GAUSS=lean" "SGPU_GAUSS=pair" 3 || exit 1
 echo "== c2"
 timeout -k 10 100 python -c "import bench, json; print(json.dumps(bench.bench_c2(cpu=False)))"
 echo "== kernel trace (pairs)"

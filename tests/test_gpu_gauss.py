@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 BLOCK = sgpu.SiftContext.DEBUG_GAUSS_BLOCK
 WAVE1 = sgpu.SiftContext.DEBUG_GAUSS_WAVE1
-SINGLE = sgpu.SiftContext.DEBUG_GAUSS_SINGLE
+PAIR = sgpu.SiftContext.DEBUG_GAUSS_PAIR
 
 
 def _bits(a):
@@ -62,9 +62,9 @@ def test_wave_levels_equal_block_kernel(gpu_ctx, rows, n, w, h):
     ref = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
     k_ref = [gpu_ctx.features(i)[0].copy() for i in range(n)]
     try:
-        # k_gauss_wave, k_gauss_lean one level per launch, then the shipped mix of two-level
-        # k_gauss_pair launches and k_gauss_lean
-        for kernel in (WAVE1 | SINGLE, SINGLE, 0):
+        # k_gauss_wave, the shipped k_gauss_lean (one level per launch), then the two-level
+        # k_gauss_pair launches with k_gauss_lean for the unpaired levels
+        for kernel in (WAVE1, 0, PAIR):
             gpu_ctx.set_debug_flags((rows << 16) | kernel)
             gpu_ctx.extract(imgs)
             got = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
