@@ -264,6 +264,9 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
 #define SGPU_DEBUG_GAUSS_PAIR 1024 /* two Gaussian levels per launch (k_gauss_pair) where the
                                       widths have a compiled pair: same levels, bit for bit;
                                       measured slower than one level per launch */
+#define SGPU_DEBUG_MATCH_REGSTAGE 2048 /* keyless plain matching through the register-staged
+                                          k_match_rows<..., RAW> instead of the LDS-DMA
+                                          k_match_raw: same pairs */
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);

@@ -310,6 +310,8 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
         else if (!strcmp(ev, "wave")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_WAVE1;
         else if (!strcmp(ev, "pair")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_PAIR;
     }
+    if (const char* ev = getenv("SGPU_MATCH"))
+        if (!strcmp(ev, "reg")) ctx->debug_flags |= SGPU_DEBUG_MATCH_REGSTAGE;
     int rc = sgpu_ctx_set_options(ctx, opt);
     if (rc != SGPU_OK) {
         sgpu_ctx_destroy(ctx);
@@ -1074,10 +1076,12 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     ALLOCCHK(ctx, ctx->m_part.ensure(std::max((size_t)ca * n1, part_b) * sizeof(sgk::Top2)));
     if (fused) ALLOCCHK(ctx, ctx->m_colpart.ensure((size_t)panels * n2 * sizeof(sgk::Top2)));
     if (compact) ALLOCCHK(ctx, ctx->m_cols.ensure((size_t)(2 * n2 + 1) * sizeof(int)));
-    ALLOCCHK(ctx, ctx->m_terms.ensure((size_t)2 * (n1 + n2) * sizeof(int)));
+    ALLOCCHK(ctx, ctx->m_terms.ensure(((size_t)2 * (n1 + n2) + 2 * sgk::match_ct_pad()) * sizeof(int)));
     ALLOCCHK(ctx, ctx->m_match.ensure((size_t)(n1 + n2) * sizeof(int)));
     int* row1 = ctx->m_terms.as<int>();          // row terms 128 * sum(d1), column terms
     int* col2 = row1 + n1;                       // 128 * sum(d2) - 2^21
+    int* ct1 = col2 + n2;                        // k_match_raw's column terms of each set
+    int* ct2 = ct1 + n1 + sgk::match_ct_pad();
     int* match1 = ctx->m_match.as<int>();
     int* match2 = match1 + n1;
     sgk::Top2* part = ctx->m_part.as<sgk::Top2>();
@@ -1094,18 +1098,20 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     // (two GEMMs: 128 * sum(d2), the row terms of the swapped launch; fused: the column terms
     // 128 * sum(d2) - 2^21, guided: 0) and the matched-column flags cleared
     int* cw = compact ? ctx->m_cols.as<int>() : nullptr;   // [flag n2][count][list n2]
-    HIPCHK(ctx, sgk::launch_prep_set(a, n1, ctx->m_s1.as<uint8_t>(), row1, 128, 0, nullptr, 0, st));
-    if (mbm)
-        HIPCHK(ctx, sgk::launch_prep_set(b, n2, ctx->m_s2.as<uint8_t>(), col2,
+    // keyless folding (k_match_raw / k_match_rows<..., RAW>): exact whenever a tied maximum
+    // cannot pass the ratio test, i.e. ratiomax <= 1 (the reference's default 0.8);
+    // SGPU_DEBUG_KEYED_MATCH keeps the keyed epilogue
+    const bool raw = !guided && !(ratiomax > 1.0f) && !(ctx->debug_flags & SGPU_DEBUG_KEYED_MATCH);
+    const bool dma = raw && !(ctx->debug_flags & SGPU_DEBUG_MATCH_REGSTAGE);
+    HIPCHK(ctx, sgk::launch_prep_set(a, n1, ctx->m_s1.as<uint8_t>(), row1, 128, 0, nullptr, 0, st,
+                                     dma && mbm && !fused ? ct1 : nullptr));
+    if (mbm || dma)
+        HIPCHK(ctx, sgk::launch_prep_set(b, n2, ctx->m_s2.as<uint8_t>(), mbm ? col2 : nullptr,
                                          guided && fused ? 0 : 128,
                                          fused && !guided ? -2097152 : 0,
-                                         cw, compact ? n2 + 1 : 0, st));
+                                         cw, compact ? n2 + 1 : 0, st, dma ? ct2 : nullptr));
     else
         HIPCHK(ctx, sgk::launch_to_s8(b, n2, ctx->m_s2.as<uint8_t>(), st));
-    // keyless folding (k_match_rows<..., RAW>): exact whenever a tied maximum cannot pass the
-    // ratio test, i.e. ratiomax <= 1 (the reference's default 0.8); SGPU_DEBUG_KEYED_MATCH keeps
-    // the keyed epilogue
-    const bool raw = !guided && !(ratiomax > 1.0f) && !(ctx->debug_flags & SGPU_DEBUG_KEYED_MATCH);
     if (mbm && !fused) {
         // The mutual check below reads the column decision match2[j] only for j = match1[i] >=
         // 0, so the column GEMM runs over those columns alone: the row finish appends each
@@ -1123,12 +1129,13 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
             cols.map = claim.list;
         }
         HIPCHK(ctx, sgk::launch_match_rows(s1, n1, s2, n2, ca, part, st, nullptr, true, nullptr,
-                                           nullptr, raw));
+                                           nullptr, raw, nullptr, nullptr, dma ? ct2 : nullptr));
         HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, row1, ctx->m_dist.as<float>(), distmax,
                                              ratiomax, match1, nullptr, st, true,
                                              raw ? a : nullptr, raw ? b : nullptr, n2, claim));
         HIPCHK(ctx, sgk::launch_match_rows(s2, n2, s1, n1, cb, part, st, nullptr, false, nullptr,
-                                           nullptr, raw, cols.map, cols.count));
+                                           nullptr, raw, cols.map, cols.count,
+                                           dma ? ct1 : nullptr));
         HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, col2, ctx->m_dist.as<float>(), distmax,
                                              ratiomax, match2, nullptr, st, false,
                                              raw ? b : nullptr, raw ? a : nullptr, n1, cols));
@@ -1144,7 +1151,8 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     } else {
         const bool r1 = raw && !rmask;
         HIPCHK(ctx, sgk::launch_match_rows(s1, n1, s2, n2, ca, part, st, rmask, true, nullptr,
-                                           nullptr, r1));
+                                           nullptr, r1, nullptr, nullptr,
+                                           r1 && dma ? ct2 : nullptr));
         HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, row1, ctx->m_dist.as<float>(), distmax,
                                              ratiomax, match1, nullptr, st, true,
                                              r1 ? a : nullptr, r1 ? b : nullptr, n2));

@@ -154,10 +154,13 @@ struct Top2 { int max, idx, second; };
 hipError_t launch_to_s8(const uint8_t* src, int n, uint8_t* dst, hipStream_t stream);
 // s[i] = scale * sum_k d[i][k] + bias
 hipError_t launch_rowsums(const uint8_t* d, int n, int* s, int scale, int bias, hipStream_t stream);
-// both at once, for one set: dst = s8 form, sums[i] = scale * sum_k src[i][k] + bias, and
-// zero[0 .. nzero) = 0
+// both at once, for one set: dst = s8 form, sums[i] = scale * sum_k src[i][k] + bias (sums may
+// be null), zero[0 .. nzero) = 0, and ctp (optional, n + match_ct_pad() entries) the biased
+// column terms of a raw launch_match_rows with this set as B
 hipError_t launch_prep_set(const uint8_t* src, int n, uint8_t* dst, int* sums, int scale,
-                           int bias, int* zero, int nzero, hipStream_t stream);
+                           int bias, int* zero, int nzero, hipStream_t stream,
+                           int* ctp = nullptr);
+int match_ct_pad();
 int match_chunks(int nA, int nB);
 // part[chunk][nA]: per-row top-2 of (A_i . B_j + col_term[j]) over each column chunk, with
 // col_term[j] = 128 * sum(B_j) - 2^21 formed in the kernel from the staged bytes.  A and B are
@@ -170,6 +173,7 @@ int match_chunks(int nA, int nB);
 // (dot - column term) (guided: of the guided value), for launch_match_cols.
 // raw (plain matching with ratiomax <= 1 only): values folded without keys; part.idx is then
 // (tile + lane) and k_match_finish recovers the column (pass raw_A / raw_B to it).
+// ctp (raw only; launch_prep_set of B): the LDS-DMA kernel k_match_raw, same partials.
 // amap / an (plain matching only): the rows are A[amap[r]] for r < *an (a count on the device,
 // at most nA); the launch covers every count and the split is chunks_for(*an, nB), which
 // launch_match_finish with ColumnList{map, count} derives again.  part needs
@@ -178,7 +182,8 @@ hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
                              int chunks, Top2* part, hipStream_t stream,
                              const uint8_t* mask, bool row_side, const int* row_term = nullptr,
                              Top2* colpart = nullptr, bool raw = false,
-                             const int* amap = nullptr, const int* an = nullptr);
+                             const int* amap = nullptr, const int* an = nullptr,
+                             const int* ctp = nullptr);
 size_t match_part_bound(int nA, int nB);
 int match_panels(int nA);
 // Column decisions from the panels' partials: col_term[j] = 128 * sum(B_j) - 2^21 (guided: 0).

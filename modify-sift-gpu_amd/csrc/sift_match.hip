@@ -15,6 +15,7 @@
 // once per row at the end (it does not change a row's ordering).  Results equal the reference's
 // integer dot products exactly.
 #include <algorithm>
+#include <type_traits>
 
 #include "sift_kernels.h"
 
@@ -25,7 +26,18 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 
 constexpr int kPanel = 128;      // A rows per workgroup (4 waves x 32)
 constexpr int kTile = 128;       // B columns per LDS tile
-constexpr int kLdsRow = 128 + 16;// bytes per staged B row (padding against bank conflicts)
+constexpr int kCtPad = kTile;    // k_match_raw: zero column terms past nB (launch_prep_set)
+#ifndef SGK_MATCH_LDSROW
+#define SGK_MATCH_LDSROW 144
+#endif
+constexpr int kLdsRow = SGK_MATCH_LDSROW;   // bytes per staged B row (padding against bank conflicts)
+#ifndef SGK_MATCH_PF
+#define SGK_MATCH_PF 1     // RAW kernel: tiles of staging loads in flight (1 or 2)
+#endif
+#ifndef SGK_MATCH_PKEY
+#define SGK_MATCH_PKEY 1   // RAW fold: the tile index packed below the tile maximum (see k_match_rows)
+#endif
+constexpr int kMaxChunkTiles = 256;   // RAW packed keys: tiles per column chunk fit 8 bits
 // Running maxima hold keys (acc << 7) | low, acc = dot - row term (- guided bias) in
 // [-2^23 - 2^22, 2^23]: every key fits in int32 and INT_MIN is below all of them.
 constexpr int kNeg = INT_MIN;
@@ -72,7 +84,8 @@ __host__ __device__ inline int chunks_for(int nA, int nB) {
     const int panels = (nA + kPanel - 1) / kPanel;
     const int chunks = (kMatchWg + panels - 1) / panels;
     const int max_chunks = max(1, (nB + 2 * kTile - 1) / (2 * kTile));
-    return max(1, min(chunks, max_chunks));
+    const int min_chunks = (nB + kMaxChunkTiles * kTile - 1) / (kMaxChunkTiles * kTile);
+    return max(min_chunks, max(1, min(chunks, max_chunks)));
 }
 
 // u8 descriptors -> s8 (s = u - 128, xor 0x80), once per match call for both sets
@@ -91,7 +104,7 @@ __global__ __launch_bounds__(256) void k_to_s8(const uint4* __restrict__ src, si
 __global__ __launch_bounds__(256) void k_prep_set(const uint4* __restrict__ src, size_t n16,
                                                   uint4* __restrict__ dst, int* __restrict__ sums,
                                                   int scale, int bias, int* __restrict__ zero,
-                                                  int nzero) {
+                                                  int nzero, int* __restrict__ ctp, int n) {
     const size_t stride = (size_t)gridDim.x * 256;
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) {
         uint4 v = src[i];
@@ -104,9 +117,14 @@ __global__ __launch_bounds__(256) void k_prep_set(const uint4* __restrict__ src,
         t += __shfl_xor(t, 1, 64);
         t += __shfl_xor(t, 2, 64);
         t += __shfl_xor(t, 4, 64);
-        if ((i & 7) == 0) sums[i >> 3] = scale * t + bias;
+        if ((i & 7) == 0) {
+            if (sums) sums[i >> 3] = scale * t + bias;
+            if (ctp) ctp[i >> 3] = 128 * t + 4194304;   // k_match_raw's biased column term
+        }
     }
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < (size_t)nzero; i += stride) zero[i] = 0;
+    if (ctp)
+        for (int i = blockIdx.x * 256 + threadIdx.x; i < kCtPad; i += (int)stride) ctp[n + i] = 0;
 }
 
 // Equal-dot order of the two decisions: does column a come before column b (-1 = none)?
@@ -152,7 +170,8 @@ __device__ __forceinline__ bool tie_before(int a, int b) {
 // RAW (plain matching with ratiomax <= 1): the values are folded as they are, no key -- the
 // accumulators start at the column term, a lane takes each row's maximum over its 8 columns of
 // the tile (v_max3 chains, half a VALU per value) and folds only that into its running (max,
-// second), recording the tile in which the maximum last grew.  The second is then the second
+// second), recording the tile in which the maximum last grew (as the low 8 bits of the folded
+// key: (tile maximum << 8) | tile index in the chunk).  The second is then the second
 // largest (tile, lane) maximum -- a lower bound of the row's second, exact unless the row's two
 // largest values share the winning lane's tile.  k_match_finish recomputes the dot products of
 // those 8 columns for every row that passes the ratio test with the lower bound (a row that
@@ -233,13 +252,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAW ? SGK_M
         for (int i = 0; i < 4; i++) { M[rb][i] = kNeg; S[rb][i] = kNeg; I[rb][i] = -1; W[rb][i] = 0; }
     constexpr uint32_t kPrefix = TIE32 ? 4u : 128u;   // keys differing below this bit tie
 
-    // staging: thread t copies 64 bytes: column t>>1, half (t&1)
+    // staging: thread t copies 64 bytes: column t>>1, half (t&1).  The loads are unconditional
+    // (columns past the set clamped to its last one; stage_store zeroes columns past the chunk),
+    // so the compiler's wait before a store counts only the loads older than it.
     auto stage_load = [&](int tbase, uint4* r) {
-        const int col = tbase + (tid >> 1);
+        const int col = min(tbase + (tid >> 1), nB - 1);
         const uint8_t* src = B + (size_t)col * 128 + (tid & 1) * 64;
 #pragma unroll
-        for (int q = 0; q < 4; q++)
-            r[q] = col < c_end ? reinterpret_cast<const uint4*>(src)[q] : make_uint4(0, 0, 0, 0);
+        for (int q = 0; q < 4; q++) r[q] = reinterpret_cast<const uint4*>(src)[q];
     };
     // The column term 128 * sum(u8 B[col]) - 2^21 is formed here from the staged s8 bytes
     // (sum(u) = sum(s) + 128 * 128; byte sums by v_dot4_i32_i8, the two half-columns joined by
@@ -248,10 +268,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAW ? SGK_M
     // prefetch.
     auto stage_store = [&](int buf, const uint4* r, int tbase) {
         uint8_t* dst = &s_b[buf][(tid >> 1) * kLdsRow + (tid & 1) * 64];
+        const bool in_chunk = tbase + (tid >> 1) < c_end;
         int sum = 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const uint4 v = r[q];
+            const uint4 v = in_chunk ? r[q] : make_uint4(0, 0, 0, 0);
             sum = __builtin_amdgcn_sdot4((int)v.x, 0x01010101, sum, false);
             sum = __builtin_amdgcn_sdot4((int)v.y, 0x01010101, sum, false);
             sum = __builtin_amdgcn_sdot4((int)v.z, 0x01010101, sum, false);
@@ -274,16 +295,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAW ? SGK_M
         low[cb] = TIE32 ? ((31 - ((cb & 1) * 16 + l16)) << 2) | (3 - (cb >> 1))
                         : 127 - (cb * 16 + l16);
 
-    uint4 stg[4];
-    int buf = 0;
+    // Tile j is computed from LDS buffer j & 1.  kPf = 2 (RAW): tile j + 2's loads are issued
+    // at the start of tile j into register set j & 1 (free: tile j was stored before), and tile
+    // j + 1 (register set (j + 1) & 1, loaded during tile j - 1) is stored at its end -- two
+    // tiles of latency for every load.  kPf = 1: tile j + 1 is loaded and stored within tile j.
+    // The loop is unrolled by two so that the register sets are static.
+    constexpr int kPf = RAW ? SGK_MATCH_PF : 1;
+    uint4 stg[2][4];
     if (c_begin < c_end) {
-        stage_load(c_begin, stg);
-        stage_store(0, stg, c_begin);
+        stage_load(c_begin, stg[0]);
+        stage_store(0, stg[0], c_begin);
+        if constexpr (kPf == 2) stage_load(c_begin + kTile, stg[1]);
     }
     __syncthreads();
-    for (int tb = c_begin; tb < c_end; tb += kTile) {
+    auto tile = [&](auto par, int tb) {
+        constexpr int buf = decltype(par)::value;
         const bool has_next = tb + kTile < c_end;
-        if (has_next) stage_load(tb + kTile, stg);
+        if constexpr (kPf == 2) {
+            stage_load(tb + 2 * kTile, stg[buf]);
+            __builtin_amdgcn_sched_barrier(0);   // issue the loads here, before the MFMAs
+        } else {
+            stage_load(tb + kTile, stg[buf ^ 1]);
+        }
         uint4 rec_next = rec;
         if (rec_ok && has_next) rec_next = rec_p[(tb / kTile + 1) * 64];
         int mt[2][4], st[2][4];
@@ -333,6 +366,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAW ? SGK_M
             // and the tile where the maximum last grew.  The exact second of the row is the
             // larger of that second and the second within the winning (tile, lane) set of 8
             // columns, which k_match_finish recomputes for every row that can still pass.
+#if SGK_MATCH_PKEY
+            // keys (tile maximum << 8) | tile index in the chunk: |maximum| <= 2^22, at most
+            // kMaxChunkTiles tiles per chunk (chunks_for); one v_lshl_or instead of the
+            // compare + select that recorded the tile
+            const int tl = (tb - c_begin) / kTile;
+#pragma unroll
+            for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int key = (tmx[rb][i] << 8) | tl;
+                    S[rb][i] = med3i(S[rb][i], M[rb][i], key);
+                    M[rb][i] = max(M[rb][i], key);
+                }
+#else
 #pragma unroll
             for (int rb = 0; rb < 2; rb++)
 #pragma unroll
@@ -342,6 +389,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAW ? SGK_M
                     I[rb][i] = v > mo ? tb : I[rb][i];
                     M[rb][i] = max(mo, v);
                 }
+#endif
         } else {
         // plain: the accumulators start at 0 and the column term enters the key,
         // key = (acc << 7) + ((ct << 7) | low) = ((acc + ct) << 7) | low;
@@ -472,12 +520,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAW ? SGK_M
                     Top2{cm >> 7, panel * kPanel + 127 - (cm & 127), cs >> 7};
             }
         }
-        if (has_next) {
-            buf ^= 1;
-            stage_store(buf, stg, tb + kTile);
-        }
+        if (has_next) stage_store(buf ^ 1, stg[buf ^ 1], tb + kTile);
         rec = rec_next;
         __syncthreads();
+    };
+    for (int tb = c_begin; tb < c_end; tb += 2 * kTile) {
+        tile(std::integral_constant<int, 0>{}, tb);
+        if (tb + kTile < c_end) tile(std::integral_constant<int, 1>{}, tb + kTile);
     }
     // keys -> (acc, column); RAW: (tile, lane) -> tile + l16, the lane's columns in the tile
 #pragma unroll
@@ -485,7 +534,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAW ? SGK_M
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             if constexpr (RAW) {
+#if SGK_MATCH_PKEY
+                const int m = M[rb][i], sk = S[rb][i];
+                I[rb][i] = m == kNeg ? -1 : c_begin + (m & 255) * kTile + l16;
+                M[rb][i] = m == kNeg ? kNeg : m >> 8;
+                S[rb][i] = sk == kNeg ? kNeg : sk >> 8;
+#else
                 I[rb][i] = I[rb][i] < 0 ? -1 : I[rb][i] + l16;
+#endif
             } else {
                 const int k = W[rb][i] & 127;
                 const int in_tile = TIE32 ? (3 - (k & 3)) * 32 + (31 - (k >> 2)) : 127 - k;
@@ -509,6 +565,191 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAW ? SGK_M
                 M[rb][i] = max(m1, m2);
                 S[rb][i] = max(min(m1, m2), max(s1, s2));
                 I[rb][i] = (m2 > m1 || (!RAW && m2 == m1 && tie_before<TIE32>(i2, i1))) ? i2 : i1;
+            }
+    }
+    if (l16 == 0) {
+#pragma unroll
+        for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int row = panel * kPanel + wave * 32 + rb * 16 + quad * 4 + i;
+                if (row < nA) part[(size_t)chunk * nA + row] = Top2{M[rb][i], I[rb][i], S[rb][i]};
+            }
+    }
+}
+
+// k_match_raw: the RAW row kernel (plain matching, ratiomax <= 1) with the B tiles staged by
+// LDS-DMA (global_load_lds_dwordx4): no staging registers, so three LDS buffers keep two tiles of
+// loads in flight across each tile's barrier (counted vmcnt, raw s_barrier), where the register
+// staging of k_match_rows holds one (or two with copies the compiler adds).  Values, folds and
+// partials are k_match_rows<.., RAW>'s:
+//   * the column terms come precomputed (ctp[j] = 128 * sum(u8 B_j) + 2^22, launch_prep_set),
+//     staged beside the tile; ctp is zero for j in [nB, nB + kTile) and columns past nB stage
+//     the last column's bytes, so their values are acc - 2^22 - 2^21 < -128 * sum(u8 A_i) <=
+//     every real value of the row (no zeroing select, which a DMA cannot apply);
+//   * the tile image is XOR-swizzled by 16-B slots (slot j of column c at j ^ ((c >> 1) & 7)) so
+//     the B-fragment ds_read_b128 are conflict-free; the DMA writes lane-linear 1-KB runs, so
+//     the swizzle is applied to the per-lane global source address instead.
+constexpr int kRawBufs = 3;
+constexpr int kRawBufBytes = kTile * 128 + 4 * 256;   // tile image + 4 waves x 64 column terms
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+__global__ __launch_bounds__(256) void k_match_raw(const uint8_t* __restrict__ A, int nA,
+                                                   const uint8_t* __restrict__ B, int nB,
+                                                   const int* __restrict__ ctp, int cols_per_chunk,
+                                                   Top2* __restrict__ part,
+                                                   const int* __restrict__ amap,
+                                                   const int* __restrict__ an) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_lds[kRawBufs * kRawBufBytes];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int panel = blockIdx.x, chunk = blockIdx.y;
+    if (an) {
+        nA = *an;
+        if (nA <= 0) return;
+        const int panels = (nA + kPanel - 1) / kPanel, chunks = chunks_for(nA, nB);
+        if ((int)blockIdx.x >= panels * chunks) return;
+        panel = blockIdx.x % panels;
+        chunk = blockIdx.x / panels;
+        cols_per_chunk = ((nB + chunks - 1) / chunks + kTile - 1) / kTile * kTile;
+    }
+    const int c_begin = chunk * cols_per_chunk;
+    const int c_end = min(nB, c_begin + cols_per_chunk);
+    if (c_begin >= c_end) {
+        // a chunk past the set (the split rounds up): empty partials, which k_match_finish reads
+        if (tid < kPanel && panel * kPanel + tid < nA)
+            part[(size_t)chunk * nA + panel * kPanel + tid] = Top2{kNeg, -1, kNeg};
+        return;
+    }
+    const int quad = lane >> 4, l16 = lane & 15;
+
+    v4i afrag[2][2];
+#pragma unroll
+    for (int rb = 0; rb < 2; rb++) {
+        const int row = panel * kPanel + wave * 32 + rb * 16 + l16;
+#pragma unroll
+        for (int kh = 0; kh < 2; kh++) {
+            if (row < nA) {
+                const int src = amap ? amap[row] : row;
+                afrag[rb][kh] = *reinterpret_cast<const v4i*>(A + (size_t)src * 128 + kh * 64 + quad * 16);
+            } else {
+                afrag[rb][kh] = v4i{0, 0, 0, 0};
+            }
+        }
+    }
+    // the A loads retire before any DMA is in flight (the compiler would otherwise wait for the
+    // DMAs too at the first use of a fragment)
+    __builtin_amdgcn_s_waitcnt(0xc07f & ~0xc00f);   // vmcnt(0)
+    int M[2][4], S[2][4];
+#pragma unroll
+    for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) { M[rb][i] = kNeg; S[rb][i] = kNeg; }
+
+    // this lane's DMA sources: instruction q fills 16-B slot (wave * 4 + q) * 64 + lane of the
+    // image, i.e. column c = slot >> 3, position slot & 7, which holds the column's 16-B piece
+    // (slot & 7) ^ ((c >> 1) & 7)
+    int src_col[4], src_off[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int slot = (wave * 4 + q) * 64 + lane, c = slot >> 3;
+        src_col[q] = c;
+        src_off[q] = (((slot & 7) ^ ((c >> 1) & 7)) << 4);
+    }
+    auto issue = [&](int tb, int bi) {
+        uint8_t* base = s_lds + bi * kRawBufBytes;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int col = min(tb + src_col[q], nB - 1);
+            __builtin_amdgcn_global_load_lds(B + (size_t)col * 128 + src_off[q],
+                                             (lds_void_ptr)(base + (wave * 4 + q) * 1024), 16, 0, 0);
+        }
+        const int ci = min(tb + wave * 32 + (lane & 31), nB + kCtPad - 1);
+        __builtin_amdgcn_global_load_lds(ctp + ci, (lds_void_ptr)(base + kTile * 128 + wave * 256),
+                                         4, 0, 0);
+    };
+    // 5 DMA instructions per wave and tile: vmcnt(5) retires all but the newest tile
+    issue(c_begin, 0);
+    issue(c_begin + kTile, 1);
+    __builtin_amdgcn_s_waitcnt(0x0075);   // vmcnt(5) lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    int bi = 0;
+    for (int tb = c_begin; tb < c_end; tb += kTile) {
+        issue(tb + 2 * kTile, bi == 0 ? 2 : bi - 1);
+        const uint8_t* sb = s_lds + bi * kRawBufBytes;
+        const int* sct = reinterpret_cast<const int*>(sb + kTile * 128);
+        constexpr int CB = 8 / kMatchSplit;
+        int tmx[2][4];
+#pragma unroll
+        for (int h = 0; h < kMatchSplit; h++) {
+            v4i acc[2][CB];
+#pragma unroll
+            for (int c = 0; c < CB; c++) {
+                const int col = (h * CB + c) * 16 + l16;
+                const int ct = sct[(col >> 5) * 64 + (col & 31)] - 6291456;
+                acc[0][c] = v4i{ct, ct, ct, ct};
+                acc[1][c] = acc[0][c];
+            }
+#pragma unroll
+            for (int c = 0; c < CB; c++) {
+                const int col = (h * CB + c) * 16 + l16;
+#pragma unroll
+                for (int kh = 0; kh < 2; kh++) {
+                    const int j = kh * 4 + quad;
+                    const v4i bfrag = *reinterpret_cast<const v4i*>(
+                        sb + col * 128 + ((j ^ ((col >> 1) & 7)) << 4));
+                    acc[0][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[0][kh], bfrag, acc[0][c], 0, 0, 0);
+                    acc[1][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[1][kh], bfrag, acc[1][c], 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int c = 0; c < CB; c += 2) {
+                        const int a = acc[rb][c][i], b2 = acc[rb][c + 1][i];
+                        tmx[rb][i] = (h == 0 && c == 0) ? max(a, b2) : max(max(tmx[rb][i], a), b2);
+                    }
+        }
+        const int tl = (tb - c_begin) / kTile;
+#pragma unroll
+        for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int key = (tmx[rb][i] << 8) | tl;
+                S[rb][i] = med3i(S[rb][i], M[rb][i], key);
+                M[rb][i] = max(M[rb][i], key);
+            }
+        // tile t + 1's DMAs retired (t + 2's stay in flight), this tile's reads done
+        __builtin_amdgcn_s_waitcnt(0x0075);   // vmcnt(5) lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        bi = bi == 2 ? 0 : bi + 1;
+    }
+    // no DMA may land after the workgroup's LDS is handed to another one
+    __builtin_amdgcn_s_waitcnt(0xc07f & ~0xc00f);   // vmcnt(0)
+    int I[2][4];
+#pragma unroll
+    for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int m = M[rb][i], sk = S[rb][i];
+            I[rb][i] = m == kNeg ? -1 : c_begin + (m & 255) * kTile + l16;
+            M[rb][i] = m == kNeg ? kNeg : m >> 8;
+            S[rb][i] = sk == kNeg ? kNeg : sk >> 8;
+        }
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+#pragma unroll
+        for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int m2 = __shfl_xor(M[rb][i], off, 64);
+                const int s2 = __shfl_xor(S[rb][i], off, 64);
+                const int i2 = __shfl_xor(I[rb][i], off, 64);
+                const int m1 = M[rb][i], s1 = S[rb][i], i1 = I[rb][i];
+                M[rb][i] = max(m1, m2);
+                S[rb][i] = max(min(m1, m2), max(s1, s2));
+                I[rb][i] = m2 > m1 ? i2 : i1;
             }
     }
     if (l16 == 0) {
@@ -848,14 +1089,14 @@ hipError_t launch_to_s8(const uint8_t* src, int n, uint8_t* dst, hipStream_t str
 }
 
 hipError_t launch_prep_set(const uint8_t* src, int n, uint8_t* dst, int* sums, int scale,
-                           int bias, int* zero, int nzero, hipStream_t stream) {
+                           int bias, int* zero, int nzero, hipStream_t stream, int* ctp) {
     if (n <= 0 && nzero <= 0) return hipSuccess;
     const size_t n16 = (size_t)std::max(n, 0) * 8;
     const size_t work = std::max(n16, (size_t)std::max(nzero, 0));
     const unsigned grid = (unsigned)std::min<size_t>((work + 255) / 256, 4096);
     hipLaunchKernelGGL(k_prep_set, dim3(grid), dim3(256), 0, stream,
                        reinterpret_cast<const uint4*>(src), n16, reinterpret_cast<uint4*>(dst),
-                       sums, scale, bias, zero, nzero);
+                       sums, scale, bias, zero, nzero, ctp, std::max(n, 0));
     return hipGetLastError();
 }
 
@@ -867,6 +1108,7 @@ hipError_t launch_rowsums(const uint8_t* d, int n, int* out, int scale, int bias
 }
 
 int match_chunks(int nA, int nB) { return chunks_for(nA, nB); }
+int match_ct_pad() { return kCtPad; }
 
 // bounds over every row count m <= nA of chunks_for(m, nB) * m (partials) and of
 // panels(m) * chunks_for(m, nB) (workgroups): chunks <= max_chunks, and chunks * panels <
@@ -874,12 +1116,16 @@ int match_chunks(int nA, int nB) { return chunks_for(nA, nB); }
 size_t match_part_bound(int nA, int nB) {
     const size_t panels = (nA + kPanel - 1) / kPanel;
     const size_t max_chunks = std::max(1, (nB + 2 * kTile - 1) / (2 * kTile));
-    return std::min((kMatchWg + panels) * kPanel, max_chunks * (size_t)nA);
+    const size_t min_chunks = (nB + kMaxChunkTiles * kTile - 1) / (kMaxChunkTiles * kTile);
+    return std::max(std::min((kMatchWg + panels) * kPanel, max_chunks * (size_t)nA),
+                    min_chunks * (size_t)nA);
 }
 static unsigned match_grid_bound(int nA, int nB) {
     const size_t panels = (nA + kPanel - 1) / kPanel;
     const size_t max_chunks = std::max(1, (nB + 2 * kTile - 1) / (2 * kTile));
-    return (unsigned)std::min(kMatchWg + panels, max_chunks * panels);
+    const size_t min_chunks = (nB + kMaxChunkTiles * kTile - 1) / (kMaxChunkTiles * kTile);
+    return (unsigned)std::max(std::min(kMatchWg + panels, max_chunks * panels),
+                              min_chunks * panels);
 }
 
 int match_panels(int nA) { return (nA + kPanel - 1) / kPanel; }
@@ -887,7 +1133,8 @@ int match_panels(int nA) { return (nA + kPanel - 1) / kPanel; }
 hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
                              int chunks, Top2* part, hipStream_t stream,
                              const uint8_t* mask, bool row_side, const int* row_term,
-                             Top2* colpart, bool raw, const int* amap, const int* an) {
+                             Top2* colpart, bool raw, const int* amap, const int* an,
+                             const int* ctp) {
     if (raw && (mask || colpart)) return hipErrorInvalidValue;
     if (nA <= 0 || nB <= 0) return hipSuccess;
     if (colpart && (!row_term || !row_side)) return hipErrorInvalidValue;
@@ -905,7 +1152,10 @@ hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
 #define SGK_MRR(T)                                                                            \
     hipLaunchKernelGGL((k_match_rows<false, T, false, true>), grid, dim3(256), 0, stream, A, nA, \
                        B, nB, per, part, rec, tiles, row_term, colpart, amap, an)
-    if (raw) {
+    if (raw && ctp) {
+        hipLaunchKernelGGL(k_match_raw, grid, dim3(256), 0, stream, A, nA, B, nB, ctp, per, part,
+                           amap, an);
+    } else if (raw) {
         if (row_side) SGK_MRR(true); else SGK_MRR(false);
     } else if (an) {
         if (row_side) SGK_MR(false, true, false); else SGK_MR(false, false, false);

@@ -421,6 +421,7 @@ class SiftContext:
     DEBUG_GAUSS_WAVE1 = 256   # round 2's k_gauss_wave instead of the lean level kernel
     DEBUG_ORIENT_WAVE = 512   # orientation one wave per candidate for any candidate count
     DEBUG_GAUSS_PAIR = 1024    # two-level k_gauss_pair launches where compiled (test hook, slower)
+    DEBUG_MATCH_REGSTAGE = 2048  # keyless matcher with register staging (k_match_rows<RAW>)
 
     def set_debug_flags(self, flags: int):
         """Per-context debug flags (sgpu_debug_set_flags; 0 = shipped configuration)."""

@@ -10,8 +10,10 @@ d2 = synth_descriptors(n, 5001, base=d1, n_dup=min(20000, n // 2))
 q1, q2 = quantize(d1), quantize(d2)
 ref = None
 only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
+REG = getattr(ctx, "DEBUG_MATCH_REGSTAGE", 0)
 for name, flags, mbm in (("plain", 0, 1), ("full_columns", ctx.DEBUG_FULL_COLUMNS, 1),
-                         ("keyed", ctx.DEBUG_KEYED_MATCH, 1), ("rows_only", 0, 0)):
+                         ("keyed", ctx.DEBUG_KEYED_MATCH, 1), ("rows_only", 0, 0),
+                         ("plain_reg", REG, 1), ("rows_reg", REG, 0)):
     if only and name not in only:
         continue
     ctx.set_debug_flags(flags)

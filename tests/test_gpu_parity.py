@@ -436,6 +436,44 @@ def test_keyless_match_equals_keyed(gpu_ctx, ratiomax):
     assert len(raw[0]) > 5000
 
 
+def test_dma_matcher_equals_register_staged(gpu_ctx):
+    """The keyless matcher's LDS-DMA kernel (k_match_raw: three staged tiles, swizzled image,
+    precomputed column terms, columns past the set neutralised by a -2^22 - 2^21 column term
+    instead of zeroed bytes) against the register-staged k_match_rows<..., RAW>
+    (SGPU_DEBUG_MATCH_REGSTAGE): identical pairs for ragged sizes (one column, one partial tile,
+    chunk ends inside a tile), exact ties, and rows whose dots are all 0 with the largest
+    possible row term (the case a badly neutralised padding column would win)."""
+    d1 = synth_descriptors(20000, 5000)
+    d2 = synth_descriptors(20000, 5001, base=d1, n_dup=8000)
+    q1t, q2t, _ = synth_tie_scene(3000, 9000, 23, [(200, 129), (130, 2), (4000, 33), (8999, 1)],
+                                  [(60, 61), (1, 2995)])
+    base = quantize(synth_descriptors(400, 5))
+    ortho1 = np.zeros((300, 128), np.uint8)
+    ortho1[:, :64] = 255
+    ortho2 = np.zeros((129, 128), np.uint8)
+    ortho2[:, 64:] = 255
+    ortho2[5] = ortho1[0]
+    cases = [(quantize(d1), quantize(d2)), (q1t, q2t), (base, base[:1].copy()),
+             (base[:1].copy(), base), (base, np.concatenate([base, base[:200]])),
+             (quantize(synth_descriptors(700, 8)), quantize(synth_descriptors(129, 9))),
+             (quantize(synth_descriptors(5000, 11)), quantize(synth_descriptors(16385, 12))),
+             (ortho1, ortho2)]
+    for mbm in (0, 1):
+        for ratiomax in (0.8, 1.0):
+            dma = [gpu_ctx.match(a, b, 0.9, ratiomax, mbm) for a, b in cases]
+            try:
+                gpu_ctx.set_debug_flags(gpu_ctx.DEBUG_MATCH_REGSTAGE)
+                reg = [gpu_ctx.match(a, b, 0.9, ratiomax, mbm) for a, b in cases]
+            finally:
+                gpu_ctx.set_debug_flags(0)
+            for i, (x, y) in enumerate(zip(dma, reg)):
+                assert np.array_equal(x, y), (mbm, ratiomax, i)
+    assert len(dma[0]) > 5000
+    # the last pass (mbm 1, ratiomax 1.0) against the oracle on the ragged and orthogonal cases
+    for i in (5, 7):
+        assert np.array_equal(dma[i], O.match(*cases[i], 0.9, 1.0, 1)), i
+
+
 def test_matched_columns_equal_full_columns(gpu_ctx):
     """Mutual matching decides only the columns some row matched (a device-side list; the
     column GEMM takes its rows and their count from it).  Pairs must equal deciding every column
