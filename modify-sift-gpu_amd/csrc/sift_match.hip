@@ -590,23 +590,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAW ? SGK_M
 //   * the tile image is XOR-swizzled by 16-B slots (slot j of column c at j ^ ((c >> 1) & 7)) so
 //     the B-fragment ds_read_b128 are conflict-free; the DMA writes lane-linear 1-KB runs, so
 //     the swizzle is applied to the per-lane global source address instead.
+// NW waves per workgroup share each staged tile: a panel of 32 * NW rows of A.
+#ifndef SGK_MATCH_RAW_WAVES
+#define SGK_MATCH_RAW_WAVES 8
+#endif
+constexpr int kRawWaves = SGK_MATCH_RAW_WAVES;
 constexpr int kRawBufs = 3;
-constexpr int kRawBufBytes = kTile * 128 + 4 * 256;   // tile image + 4 waves x 64 column terms
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 
-__global__ __launch_bounds__(256) void k_match_raw(const uint8_t* __restrict__ A, int nA,
+__global__ __launch_bounds__(64 * kRawWaves) void k_match_raw(const uint8_t* __restrict__ A, int nA,
                                                    const uint8_t* __restrict__ B, int nB,
                                                    const int* __restrict__ ctp, int cols_per_chunk,
                                                    Top2* __restrict__ part,
                                                    const int* __restrict__ amap,
                                                    const int* __restrict__ an) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_lds[kRawBufs * kRawBufBytes];
+    constexpr int NW = kRawWaves;
+    constexpr int kRows = 32 * NW;        // panel rows
+    constexpr int kDmaB = 16 / NW;        // 1-KB image runs per wave and tile
+    constexpr int kCtW = kTile / NW;      // column terms staged per wave (lanes repeat them)
+    static_assert(kTile * 128 == NW * kDmaB * 1024, "the image is NW x kDmaB runs");
+    __shared__ __attribute__((aligned(16))) uint8_t s_lds[kRawBufs * (kTile * 128 + NW * 256)];
+    constexpr int kBuf = kTile * 128 + NW * 256;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int panel = blockIdx.x, chunk = blockIdx.y;
     if (an) {
         nA = *an;
         if (nA <= 0) return;
-        const int panels = (nA + kPanel - 1) / kPanel, chunks = chunks_for(nA, nB);
+        const int panels = (nA + kRows - 1) / kRows, chunks = chunks_for(nA, nB);
         if ((int)blockIdx.x >= panels * chunks) return;
         panel = blockIdx.x % panels;
         chunk = blockIdx.x / panels;
@@ -616,8 +626,8 @@ __global__ __launch_bounds__(256) void k_match_raw(const uint8_t* __restrict__ A
     const int c_end = min(nB, c_begin + cols_per_chunk);
     if (c_begin >= c_end) {
         // a chunk past the set (the split rounds up): empty partials, which k_match_finish reads
-        if (tid < kPanel && panel * kPanel + tid < nA)
-            part[(size_t)chunk * nA + panel * kPanel + tid] = Top2{kNeg, -1, kNeg};
+        if (tid < kRows && panel * kRows + tid < nA)
+            part[(size_t)chunk * nA + panel * kRows + tid] = Top2{kNeg, -1, kNeg};
         return;
     }
     const int quad = lane >> 4, l16 = lane & 15;
@@ -625,7 +635,7 @@ __global__ __launch_bounds__(256) void k_match_raw(const uint8_t* __restrict__ A
     v4i afrag[2][2];
 #pragma unroll
     for (int rb = 0; rb < 2; rb++) {
-        const int row = panel * kPanel + wave * 32 + rb * 16 + l16;
+        const int row = panel * kRows + wave * 32 + rb * 16 + l16;
 #pragma unroll
         for (int kh = 0; kh < 2; kh++) {
             if (row < nA) {
@@ -645,37 +655,39 @@ __global__ __launch_bounds__(256) void k_match_raw(const uint8_t* __restrict__ A
 #pragma unroll
         for (int i = 0; i < 4; i++) { M[rb][i] = kNeg; S[rb][i] = kNeg; }
 
-    // this lane's DMA sources: instruction q fills 16-B slot (wave * 4 + q) * 64 + lane of the
-    // image, i.e. column c = slot >> 3, position slot & 7, which holds the column's 16-B piece
-    // (slot & 7) ^ ((c >> 1) & 7)
-    int src_col[4], src_off[4];
+    // this lane's DMA sources: instruction q fills 16-B slot (wave * kDmaB + q) * 64 + lane of
+    // the image, i.e. column c = slot >> 3, position slot & 7, which holds the column's 16-B
+    // piece (slot & 7) ^ ((c >> 1) & 7)
+    int src_col[kDmaB], src_off[kDmaB];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int slot = (wave * 4 + q) * 64 + lane, c = slot >> 3;
+    for (int q = 0; q < kDmaB; q++) {
+        const int slot = (wave * kDmaB + q) * 64 + lane, c = slot >> 3;
         src_col[q] = c;
         src_off[q] = (((slot & 7) ^ ((c >> 1) & 7)) << 4);
     }
     auto issue = [&](int tb, int bi) {
-        uint8_t* base = s_lds + bi * kRawBufBytes;
+        uint8_t* base = s_lds + bi * kBuf;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
+        for (int q = 0; q < kDmaB; q++) {
             const int col = min(tb + src_col[q], nB - 1);
             __builtin_amdgcn_global_load_lds(B + (size_t)col * 128 + src_off[q],
-                                             (lds_void_ptr)(base + (wave * 4 + q) * 1024), 16, 0, 0);
+                                             (lds_void_ptr)(base + (wave * kDmaB + q) * 1024), 16, 0, 0);
         }
-        const int ci = min(tb + wave * 32 + (lane & 31), nB + kCtPad - 1);
+        const int ci = min(tb + wave * kCtW + lane % kCtW, nB + kCtPad - 1);
         __builtin_amdgcn_global_load_lds(ctp + ci, (lds_void_ptr)(base + kTile * 128 + wave * 256),
                                          4, 0, 0);
     };
-    // 5 DMA instructions per wave and tile: vmcnt(5) retires all but the newest tile
+    // kDmaB + 1 DMA instructions per wave and tile: vmcnt(kDmaB + 1) retires all but the
+    // newest tile (the immediate: vmcnt low bits, expcnt 7, lgkmcnt 0)
+    constexpr int kWaitTile = 0x0070 | (kDmaB + 1);
     issue(c_begin, 0);
     issue(c_begin + kTile, 1);
-    __builtin_amdgcn_s_waitcnt(0x0075);   // vmcnt(5) lgkmcnt(0)
+    __builtin_amdgcn_s_waitcnt(kWaitTile);
     __builtin_amdgcn_s_barrier();
     int bi = 0;
     for (int tb = c_begin; tb < c_end; tb += kTile) {
         issue(tb + 2 * kTile, bi == 0 ? 2 : bi - 1);
-        const uint8_t* sb = s_lds + bi * kRawBufBytes;
+        const uint8_t* sb = s_lds + bi * kBuf;
         const int* sct = reinterpret_cast<const int*>(sb + kTile * 128);
         constexpr int CB = 8 / kMatchSplit;
         int tmx[2][4];
@@ -685,7 +697,7 @@ __global__ __launch_bounds__(256) void k_match_raw(const uint8_t* __restrict__ A
 #pragma unroll
             for (int c = 0; c < CB; c++) {
                 const int col = (h * CB + c) * 16 + l16;
-                const int ct = sct[(col >> 5) * 64 + (col & 31)] - 6291456;
+                const int ct = sct[(col / kCtW) * 64 + col % kCtW] - 6291456;
                 acc[0][c] = v4i{ct, ct, ct, ct};
                 acc[1][c] = acc[0][c];
             }
@@ -721,7 +733,7 @@ __global__ __launch_bounds__(256) void k_match_raw(const uint8_t* __restrict__ A
                 M[rb][i] = max(M[rb][i], key);
             }
         // tile t + 1's DMAs retired (t + 2's stay in flight), this tile's reads done
-        __builtin_amdgcn_s_waitcnt(0x0075);   // vmcnt(5) lgkmcnt(0)
+        __builtin_amdgcn_s_waitcnt(kWaitTile);
         __builtin_amdgcn_s_barrier();
         bi = bi == 2 ? 0 : bi + 1;
     }
@@ -757,7 +769,7 @@ __global__ __launch_bounds__(256) void k_match_raw(const uint8_t* __restrict__ A
         for (int rb = 0; rb < 2; rb++)
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const int row = panel * kPanel + wave * 32 + rb * 16 + quad * 4 + i;
+                const int row = panel * kRows + wave * 32 + rb * 16 + quad * 4 + i;
                 if (row < nA) part[(size_t)chunk * nA + row] = Top2{M[rb][i], I[rb][i], S[rb][i]};
             }
     }
@@ -1153,8 +1165,10 @@ hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
     hipLaunchKernelGGL((k_match_rows<false, T, false, true>), grid, dim3(256), 0, stream, A, nA, \
                        B, nB, per, part, rec, tiles, row_term, colpart, amap, an)
     if (raw && ctp) {
-        hipLaunchKernelGGL(k_match_raw, grid, dim3(256), 0, stream, A, nA, B, nB, ctp, per, part,
-                           amap, an);
+        constexpr int rows = 32 * kRawWaves;
+        const dim3 rgrid = an ? grid : dim3((nA + rows - 1) / rows, chunks);
+        hipLaunchKernelGGL(k_match_raw, rgrid, dim3(64 * kRawWaves), 0, stream, A, nA,
+                           B, nB, ctp, per, part, amap, an);
     } else if (raw) {
         if (row_side) SGK_MRR(true); else SGK_MRR(false);
     } else if (an) {
