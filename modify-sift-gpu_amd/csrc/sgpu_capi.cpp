@@ -54,10 +54,15 @@ struct DevBuf {
 enum { T_UPLOAD, T_PYRAMID, T_DETECT, T_ORIENT, T_EXPAND, T_DESC, T_DOWNLOAD, T_TOTAL, T_MATCH,
        T_LIST, T_N };
 
+constexpr int kOctStreams = 3;   // streams for pyramid octaves >= 1 per part
+
 // One part of a batch: consecutive images [img0, img0 + n) with their own stream and buffers.
 struct Part {
     hipStream_t stream = nullptr;      // high priority: pyramid + detection
     hipStream_t stream_lo = nullptr;   // low priority: orientation, descriptors, readback
+    hipStream_t oct_st[kOctStreams] = {};  // high priority: pyramid octaves >= 1 (enqueue_part)
+    hipEvent_t ev_ds[sgk::kMaxOctaves] = {};  // octave o's decimating level done
+    hipEvent_t ev_oj[kOctStreams] = {};       // an octave stream's work done
     size_t cand_hint = 0, feat_hint = 0;   // counts of the previous call (launch-grid sizing)
     hipEvent_t ev[10] = {};  // start, pyramid, detect, orientation, expand, descriptor, end,
                              // extrema done (before the row scan), (spare), (spare)
@@ -84,6 +89,13 @@ struct Part {
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
         if (stream_lo) (void)hipStreamDestroy(stream_lo);
+        for (hipEvent_t& e : ev_ds)
+            if (e) (void)hipEventDestroy(e);
+        for (int i = 0; i < kOctStreams; i++) {
+            if (ev_oj[i]) (void)hipEventDestroy(ev_oj[i]);
+            if (oct_st[i]) (void)hipStreamDestroy(oct_st[i]);
+            oct_st[i] = nullptr;
+        }
         stream = stream_lo = nullptr;
     }
 };
@@ -295,11 +307,16 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     for (Part& pt : ctx->part) {
         if (hipStreamCreateWithPriority(&pt.stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-            hipStreamCreateWithPriority(&pt.stream_lo, hipStreamNonBlocking, prio_lo) != hipSuccess) {
+            hipStreamCreateWithPriority(&pt.stream_lo, hipStreamNonBlocking, prio_lo) != hipSuccess ||
+            hipStreamCreateWithPriority(&pt.oct_st[0], hipStreamNonBlocking, prio_hi) != hipSuccess ||
+            hipStreamCreateWithPriority(&pt.oct_st[1], hipStreamNonBlocking, prio_hi) != hipSuccess ||
+            hipStreamCreateWithPriority(&pt.oct_st[2], hipStreamNonBlocking, prio_hi) != hipSuccess) {
             sgpu_ctx_destroy(ctx);
             return SGPU_ENODEV;
         }
         for (hipEvent_t& e : pt.ev) (void)hipEventCreate(&e);
+        for (hipEvent_t& e : pt.ev_ds) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        for (hipEvent_t& e : pt.ev_oj) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
     }
     // test mode for the C++ replicas, which only see SiftGPU.h: the bit-exact descriptor
     if (const char* ev = getenv("SGPU_EXACT_DESCRIPTOR"))
@@ -309,6 +326,10 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
         if (!strcmp(ev, "block")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_BLOCK;
         else if (!strcmp(ev, "wave")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_WAVE1;
         else if (!strcmp(ev, "pair")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_PAIR;
+    }
+    if (const char* ev = getenv("SGPU_PYR")) {
+        if (!strcmp(ev, "serial")) ctx->debug_flags |= SGPU_DEBUG_PYR_SERIAL;
+        else if (!strcmp(ev, "multi")) ctx->debug_flags |= SGPU_DEBUG_PYR_MULTI;
     }
     if (const char* ev = getenv("SGPU_MATCH"))
         if (!strcmp(ev, "reg")) ctx->debug_flags |= SGPU_DEBUG_MATCH_REGSTAGE;
@@ -328,6 +349,8 @@ int sgpu_ctx_destroy(sgpu_ctx* ctx) {
     for (Part& pt : ctx->part) {
         if (pt.stream) (void)hipStreamSynchronize(pt.stream);
         if (pt.stream_lo) (void)hipStreamSynchronize(pt.stream_lo);
+        for (hipStream_t so : pt.oct_st)
+            if (so) (void)hipStreamSynchronize(so);
         pt.release();
     }
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
@@ -457,8 +480,23 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
         lfw[k] = sgp::make_filter(S.sigma[k - 1], O.filter_width_factor, ltaps[k].k);
     const int fw0 = sgp::make_filter(S.initial_smooth, O.filter_width_factor, taps0.k);
     const int kds = S.level_ds - S.level_min;
+    // Octaves >= 1 run on a second stream, which starts as soon as octave 0's level kds has
+    // written octave 1's base (level 0): their small, latency-bound launches run beside octave
+    // 0's last levels instead of after them, 3.64 vs 3.69-3.74 ms per 128 x 1080p (DESIGN.md
+    // 4.3).  SGPU_DEBUG_PYR_SERIAL: one stream; SGPU_DEBUG_PYR_MULTI: octave o on stream
+    // (o - 1) % 3, waiting for octave o-1's decimating level (3.83 ms: the upper octaves crowd
+    // each other).  The main stream waits for them before the extremum kernel.
+    const bool side = noct > 1 && !(ctx->debug_flags & SGPU_DEBUG_PYR_SERIAL);
+    const int nside = (ctx->debug_flags & SGPU_DEBUG_PYR_MULTI) ? kOctStreams : 1;
+    bool used[kOctStreams] = {};
     for (int o = 0; o < noct; o++) {
         const sgk::OctaveDesc& od = fp.oct[o];
+        const int si = (o - 1) % nside;
+        const hipStream_t so = side && o >= 1 ? pt.oct_st[si] : st;
+        if (side && o >= 1) {
+            HIPCHK(ctx, hipStreamWaitEvent(so, pt.ev_ds[o - 1], 0));
+            used[si] = true;
+        }
         const long long npx = (long long)od.wa * od.h;
         float* lvl0 = pyr + od.gauss_off;
         float* ds = nullptr;
@@ -514,7 +552,8 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
                                                    lvl0 + (k + 1) * od.level_stride, npx, od.wa,
                                                    od.h, fwk, taps, lfw[k + 1], ltaps[k + 1], n,
                                                    dk1 ? ds : nullptr, dk1 ? dsw : 0,
-                                                   dk1 ? dsh : 0, dk1 ? ds_stride : 0, st));
+                                                   dk1 ? dsh : 0, dk1 ? ds_stride : 0, so));
+                if (side && dk1) HIPCHK(ctx, hipEventRecord(pt.ev_ds[o], so));
                 k++;
                 continue;
             }
@@ -522,12 +561,18 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
                                           k == 0 ? in_8 : nullptr, k == 0 ? in_stride : od.wa,
                                           k == 0 ? in_img : npx, lvl0 + k * od.level_stride,
                                           npx, od.wa, od.h, fwk, taps, n, dk ? ds : nullptr,
-                                          dk ? dsw : 0, dk ? dsh : 0, dk ? ds_stride : 0, st,
+                                          dk ? dsw : 0, dk ? dsh : 0, dk ? ds_stride : 0, so,
                                           (ctx->debug_flags & SGPU_DEBUG_GAUSS_BLOCK)
                                               ? -1 : (ctx->debug_flags >> 16),
                                           !(ctx->debug_flags & SGPU_DEBUG_GAUSS_WAVE1)));
+            if (side && dk) HIPCHK(ctx, hipEventRecord(pt.ev_ds[o], so));
         }
     }
+    for (int i = 0; i < kOctStreams; i++)
+        if (used[i]) {
+            HIPCHK(ctx, hipEventRecord(pt.ev_oj[i], pt.oct_st[i]));
+            HIPCHK(ctx, hipStreamWaitEvent(st, pt.ev_oj[i], 0));
+        }
     HIPCHK(ctx, hipEventRecord(pt.ev[1], st));
 
     // ---- extrema + row scan (the strip extremum kernel only sets the bits it accepts)

@@ -44,9 +44,9 @@ def calibration():
 
 def factors(name, cal):
     """(read factor, write factor) for a kernel's access widths, (1, 1) when uncalibrated."""
-    if cal is None or "k_gauss_wave" not in name:
+    if cal is None or not re.search(r"k_gauss_(wave|lean)<", name):
         return 1.0, 1.0
-    u8 = re.search(r"k_gauss_wave<\s*\d+\s*,\s*true", name) is not None
+    u8 = re.search(r"k_gauss_(wave|lean)<\s*\d+\s*,\s*true", name) is not None
     return cal.get("read4" if u8 else "read16") or 1.0, cal.get("write8") or 1.0
 
 

@@ -1,6 +1,6 @@
-"""Gaussian pyramid kernels on the GPU: the shipped two-level kernel (k_gauss_pair) and lean level
-kernel (k_gauss_lean), round 2's wave-streaming kernel (k_gauss_wave) and the workgroup strip
-kernel (k_gauss_pk2) against each other and the oracle, bit for bit.
+"""Gaussian pyramid kernels on the GPU: the shipped level kernel (k_gauss_lean), the two-level
+k_gauss_pair (test hook SGPU_DEBUG_GAUSS_PAIR), round 2's wave-streaming kernel (k_gauss_wave) and
+the workgroup strip kernel (k_gauss_pk2) against each other and the oracle, bit for bit.
 
 Both kernels restate FilterH / FilterV (ProgramCU.cu:115-222) with the taps summed i = 0..FW-1
 and the 2x decimation of DownsampleKernel<1> (ProgramCU.cu:287-298) fused into the level that
@@ -122,6 +122,34 @@ def test_block_first_octave_float_path(gpu_ctx, fo):
                 g = gpu_ctx.gaussian(0, o, lvl)
                 r = O.gaussian(img, o, lvl, opts)
                 assert np.array_equal(_bits(g), _bits(r)), (o, lvl)
+    finally:
+        gpu_ctx.set_debug_flags(0)
+        gpu_ctx.set_options(default_options())
+
+
+@pytest.mark.parametrize("n,w,h,no", [(3, 1920, 1080, 4), (2, 517, 389, -1), (1, 4096, 4096, 6)])
+def test_octave_streams_equal_serial(gpu_ctx, n, w, h, no):
+    """Octaves >= 1 on a second stream (shipped), on one stream per octave
+    (SGPU_DEBUG_PYR_MULTI) and all on the main stream (SGPU_DEBUG_PYR_SERIAL): the same levels
+    and keypoints, bit for bit -- the side streams only reorder launches whose inputs are
+    complete (octave o waits for octave o-1's decimating level; the extremum kernel for all)."""
+    imgs = synth_batch(n, w, h, 90 + n)
+    opts = default_options(octave_num=no) if no > 0 else default_options()
+    gpu_ctx.set_options(opts)
+    try:
+        gpu_ctx.set_debug_flags(gpu_ctx.DEBUG_PYR_SERIAL)
+        gpu_ctx.extract(imgs)
+        ref = _levels(gpu_ctx, n - 1, opts)
+        k_ref = [gpu_ctx.features(i)[0].copy() for i in range(n)]
+        for flags in (0, gpu_ctx.DEBUG_PYR_MULTI):
+            gpu_ctx.set_debug_flags(flags)
+            gpu_ctx.extract(imgs)
+            got = _levels(gpu_ctx, n - 1, opts)
+            for o, (la, lb) in enumerate(zip(ref, got)):
+                for lvl, (x, y) in enumerate(zip(la, lb)):
+                    assert np.array_equal(_bits(x), _bits(y)), (flags, o, lvl)
+            for i in range(n):
+                assert np.array_equal(_bits(gpu_ctx.features(i)[0]), _bits(k_ref[i])), flags
     finally:
         gpu_ctx.set_debug_flags(0)
         gpu_ctx.set_options(default_options())
