@@ -270,9 +270,6 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
 #define SGPU_DEBUG_PYR_SERIAL 4096 /* every pyramid octave on the part's main stream (the
                                       shipped path runs octaves >= 1 on a second stream beside
                                       octave 0's last levels): same levels */
-#define SGPU_DEBUG_PYR_MULTI 8192 /* pyramid octave o >= 1 on its own stream from the moment
-                                     octave o-1 has written its base (shipped: all octaves >= 1
-                                     on one second stream; measured faster) */
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);

@@ -54,15 +54,13 @@ struct DevBuf {
 enum { T_UPLOAD, T_PYRAMID, T_DETECT, T_ORIENT, T_EXPAND, T_DESC, T_DOWNLOAD, T_TOTAL, T_MATCH,
        T_LIST, T_N };
 
-constexpr int kOctStreams = 3;   // streams for pyramid octaves >= 1 per part
-
 // One part of a batch: consecutive images [img0, img0 + n) with their own stream and buffers.
 struct Part {
     hipStream_t stream = nullptr;      // high priority: pyramid + detection
     hipStream_t stream_lo = nullptr;   // low priority: orientation, descriptors, readback
-    hipStream_t oct_st[kOctStreams] = {};  // high priority: pyramid octaves >= 1 (enqueue_part)
-    hipEvent_t ev_ds[sgk::kMaxOctaves] = {};  // octave o's decimating level done
-    hipEvent_t ev_oj[kOctStreams] = {};       // an octave stream's work done
+    hipStream_t stream_oct = nullptr;  // high priority: pyramid octaves >= 1 (enqueue_part)
+    hipEvent_t ev_ds = nullptr;        // octave 0's decimating level done
+    hipEvent_t ev_oct = nullptr;       // octaves >= 1 done
     size_t cand_hint = 0, feat_hint = 0;   // counts of the previous call (launch-grid sizing)
     hipEvent_t ev[10] = {};  // start, pyramid, detect, orientation, expand, descriptor, end,
                              // extrema done (before the row scan), (spare), (spare)
@@ -89,14 +87,11 @@ struct Part {
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
         if (stream_lo) (void)hipStreamDestroy(stream_lo);
-        for (hipEvent_t& e : ev_ds)
-            if (e) (void)hipEventDestroy(e);
-        for (int i = 0; i < kOctStreams; i++) {
-            if (ev_oj[i]) (void)hipEventDestroy(ev_oj[i]);
-            if (oct_st[i]) (void)hipStreamDestroy(oct_st[i]);
-            oct_st[i] = nullptr;
-        }
-        stream = stream_lo = nullptr;
+        if (ev_ds) (void)hipEventDestroy(ev_ds);
+        if (ev_oct) (void)hipEventDestroy(ev_oct);
+        ev_ds = ev_oct = nullptr;
+        if (stream_oct) (void)hipStreamDestroy(stream_oct);
+        stream = stream_lo = stream_oct = nullptr;
     }
 };
 
@@ -287,6 +282,25 @@ int sgpu_ctx_set_options(sgpu_ctx* ctx, const sgpu_options* opt) {
     return SGPU_OK;
 }
 
+// A part's streams and events, created when the part is first used: the pyramid/detection
+// stream gets the dispatch priority over the orientation/descriptor stream (of the previous
+// part, when a batch runs in parts); octaves >= 1 of the pyramid run on a third stream.
+static int part_streams(Part& pt) {
+    if (pt.stream) return SGPU_OK;
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    if (hipStreamCreateWithPriority(&pt.stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&pt.stream_lo, hipStreamNonBlocking, prio_lo) != hipSuccess ||
+        hipStreamCreateWithPriority(&pt.stream_oct, hipStreamNonBlocking, prio_hi) != hipSuccess)
+        return SGPU_ENODEV;
+    for (hipEvent_t& e : pt.ev)
+        if (hipEventCreate(&e) != hipSuccess) return SGPU_ENODEV;
+    if (hipEventCreateWithFlags(&pt.ev_ds, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&pt.ev_oct, hipEventDisableTiming) != hipSuccess)
+        return SGPU_ENODEV;
+    return SGPU_OK;
+}
+
 int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     if (!out) return SGPU_EINVAL;
     *out = nullptr;
@@ -301,22 +315,12 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
         return SGPU_ENODEV;
     }
     for (int i = 0; i <= T_N; i++) (void)hipEventCreate(&ctx->ev[i]);
-    // the HBM-bound pyramid/detection stream of a part gets the dispatch priority over the
-    // VALU-bound orientation/descriptor stream of the previous part
-    int prio_lo = 0, prio_hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    for (Part& pt : ctx->part) {
-        if (hipStreamCreateWithPriority(&pt.stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-            hipStreamCreateWithPriority(&pt.stream_lo, hipStreamNonBlocking, prio_lo) != hipSuccess ||
-            hipStreamCreateWithPriority(&pt.oct_st[0], hipStreamNonBlocking, prio_hi) != hipSuccess ||
-            hipStreamCreateWithPriority(&pt.oct_st[1], hipStreamNonBlocking, prio_hi) != hipSuccess ||
-            hipStreamCreateWithPriority(&pt.oct_st[2], hipStreamNonBlocking, prio_hi) != hipSuccess) {
-            sgpu_ctx_destroy(ctx);
-            return SGPU_ENODEV;
-        }
-        for (hipEvent_t& e : pt.ev) (void)hipEventCreate(&e);
-        for (hipEvent_t& e : pt.ev_ds) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-        for (hipEvent_t& e : pt.ev_oj) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    // part 0's streams now (a part's streams are created when it is first used, see
+    // part_streams): a context that runs one part holds 4 streams, which the runtime spreads
+    // over distinct hardware queues (4 on the GPU box)
+    if (part_streams(ctx->part[0]) != SGPU_OK) {
+        sgpu_ctx_destroy(ctx);
+        return SGPU_ENODEV;
     }
     // test mode for the C++ replicas, which only see SiftGPU.h: the bit-exact descriptor
     if (const char* ev = getenv("SGPU_EXACT_DESCRIPTOR"))
@@ -329,7 +333,6 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     }
     if (const char* ev = getenv("SGPU_PYR")) {
         if (!strcmp(ev, "serial")) ctx->debug_flags |= SGPU_DEBUG_PYR_SERIAL;
-        else if (!strcmp(ev, "multi")) ctx->debug_flags |= SGPU_DEBUG_PYR_MULTI;
     }
     if (const char* ev = getenv("SGPU_MATCH"))
         if (!strcmp(ev, "reg")) ctx->debug_flags |= SGPU_DEBUG_MATCH_REGSTAGE;
@@ -349,8 +352,7 @@ int sgpu_ctx_destroy(sgpu_ctx* ctx) {
     for (Part& pt : ctx->part) {
         if (pt.stream) (void)hipStreamSynchronize(pt.stream);
         if (pt.stream_lo) (void)hipStreamSynchronize(pt.stream_lo);
-        for (hipStream_t so : pt.oct_st)
-            if (so) (void)hipStreamSynchronize(so);
+        if (pt.stream_oct) (void)hipStreamSynchronize(pt.stream_oct);
         pt.release();
     }
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
@@ -483,20 +485,13 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     // Octaves >= 1 run on a second stream, which starts as soon as octave 0's level kds has
     // written octave 1's base (level 0): their small, latency-bound launches run beside octave
     // 0's last levels instead of after them, 3.64 vs 3.69-3.74 ms per 128 x 1080p (DESIGN.md
-    // 4.3).  SGPU_DEBUG_PYR_SERIAL: one stream; SGPU_DEBUG_PYR_MULTI: octave o on stream
-    // (o - 1) % 3, waiting for octave o-1's decimating level (3.83 ms: the upper octaves crowd
-    // each other).  The main stream waits for them before the extremum kernel.
+    // 4.3; one stream per octave measured 3.83 ms).  SGPU_DEBUG_PYR_SERIAL: one stream.  The
+    // main stream waits for them before the extremum kernel.
     const bool side = noct > 1 && !(ctx->debug_flags & SGPU_DEBUG_PYR_SERIAL);
-    const int nside = (ctx->debug_flags & SGPU_DEBUG_PYR_MULTI) ? kOctStreams : 1;
-    bool used[kOctStreams] = {};
     for (int o = 0; o < noct; o++) {
         const sgk::OctaveDesc& od = fp.oct[o];
-        const int si = (o - 1) % nside;
-        const hipStream_t so = side && o >= 1 ? pt.oct_st[si] : st;
-        if (side && o >= 1) {
-            HIPCHK(ctx, hipStreamWaitEvent(so, pt.ev_ds[o - 1], 0));
-            used[si] = true;
-        }
+        const hipStream_t so = side && o >= 1 ? pt.stream_oct : st;
+        if (side && o == 1) HIPCHK(ctx, hipStreamWaitEvent(so, pt.ev_ds, 0));
         const long long npx = (long long)od.wa * od.h;
         float* lvl0 = pyr + od.gauss_off;
         float* ds = nullptr;
@@ -553,7 +548,7 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
                                                    od.h, fwk, taps, lfw[k + 1], ltaps[k + 1], n,
                                                    dk1 ? ds : nullptr, dk1 ? dsw : 0,
                                                    dk1 ? dsh : 0, dk1 ? ds_stride : 0, so));
-                if (side && dk1) HIPCHK(ctx, hipEventRecord(pt.ev_ds[o], so));
+                if (side && o == 0 && dk1) HIPCHK(ctx, hipEventRecord(pt.ev_ds, st));
                 k++;
                 continue;
             }
@@ -565,14 +560,13 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
                                           (ctx->debug_flags & SGPU_DEBUG_GAUSS_BLOCK)
                                               ? -1 : (ctx->debug_flags >> 16),
                                           !(ctx->debug_flags & SGPU_DEBUG_GAUSS_WAVE1)));
-            if (side && dk) HIPCHK(ctx, hipEventRecord(pt.ev_ds[o], so));
+            if (side && o == 0 && dk) HIPCHK(ctx, hipEventRecord(pt.ev_ds, st));
         }
     }
-    for (int i = 0; i < kOctStreams; i++)
-        if (used[i]) {
-            HIPCHK(ctx, hipEventRecord(pt.ev_oj[i], pt.oct_st[i]));
-            HIPCHK(ctx, hipStreamWaitEvent(st, pt.ev_oj[i], 0));
-        }
+    if (side) {
+        HIPCHK(ctx, hipEventRecord(pt.ev_oct, pt.stream_oct));
+        HIPCHK(ctx, hipStreamWaitEvent(st, pt.ev_oct, 0));
+    }
     HIPCHK(ctx, hipEventRecord(pt.ev[1], st));
 
     // ---- extrema + row scan (the strip extremum kernel only sets the bits it accepts)
@@ -712,6 +706,9 @@ static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
     if ((ctx->debug_flags & SGPU_DEBUG_PARTS2) && n >= 2) np = 2;
     if ((ctx->debug_flags & SGPU_DEBUG_PARTS4) && n >= 4) np = 4;
     ctx->nparts = np;
+    for (int p = 0; p < np; p++)
+        if (part_streams(ctx->part[p]) != SGPU_OK)
+            return ctx->fail(SGPU_ENODEV, "stream creation failed");
     for (int p = 0, i0 = 0; p < np; p++) {
         const int cnt = n / np + (p < n % np ? 1 : 0);
         ctx->part[p].img0 = i0;
@@ -868,6 +865,8 @@ static int extract_stream_body(sgpu_ctx* ctx, const uint8_t* const* batches, int
         }
         return result;
     }
+    if (part_streams(ctx->part[1]) != SGPU_OK)
+        return ctx->fail(SGPU_ENODEV, "stream creation failed");
     if (!ctx->h2d) {
         HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->h2d, hipStreamNonBlocking));
         HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->d2h, hipStreamNonBlocking));

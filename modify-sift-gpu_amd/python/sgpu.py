@@ -423,7 +423,6 @@ class SiftContext:
     DEBUG_GAUSS_PAIR = 1024    # two-level k_gauss_pair launches where compiled (test hook, slower)
     DEBUG_MATCH_REGSTAGE = 2048  # keyless matcher with register staging (k_match_rows<RAW>)
     DEBUG_PYR_SERIAL = 4096    # all pyramid octaves on one stream
-    DEBUG_PYR_MULTI = 8192     # pyramid octave o >= 1 on stream (o - 1) % 3 (slower)
 
     def set_debug_flags(self, flags: int):
         """Per-context debug flags (sgpu_debug_set_flags; 0 = shipped configuration)."""

@@ -129,10 +129,10 @@ def test_block_first_octave_float_path(gpu_ctx, fo):
 
 @pytest.mark.parametrize("n,w,h,no", [(3, 1920, 1080, 4), (2, 517, 389, -1), (1, 4096, 4096, 6)])
 def test_octave_streams_equal_serial(gpu_ctx, n, w, h, no):
-    """Octaves >= 1 on a second stream (shipped), on one stream per octave
-    (SGPU_DEBUG_PYR_MULTI) and all on the main stream (SGPU_DEBUG_PYR_SERIAL): the same levels
-    and keypoints, bit for bit -- the side streams only reorder launches whose inputs are
-    complete (octave o waits for octave o-1's decimating level; the extremum kernel for all)."""
+    """Octaves >= 1 on a second stream (shipped) and all on the main stream
+    (SGPU_DEBUG_PYR_SERIAL): the same levels and keypoints, bit for bit -- the side stream only
+    reorders launches whose inputs are complete (octave 1 waits for octave 0's decimating level,
+    the extremum kernel for every octave)."""
     imgs = synth_batch(n, w, h, 90 + n)
     opts = default_options(octave_num=no) if no > 0 else default_options()
     gpu_ctx.set_options(opts)
@@ -141,7 +141,7 @@ def test_octave_streams_equal_serial(gpu_ctx, n, w, h, no):
         gpu_ctx.extract(imgs)
         ref = _levels(gpu_ctx, n - 1, opts)
         k_ref = [gpu_ctx.features(i)[0].copy() for i in range(n)]
-        for flags in (0, gpu_ctx.DEBUG_PYR_MULTI):
+        for flags in (0,):
             gpu_ctx.set_debug_flags(flags)
             gpu_ctx.extract(imgs)
             got = _levels(gpu_ctx, n - 1, opts)
