@@ -285,19 +285,26 @@ int sgpu_ctx_set_options(sgpu_ctx* ctx, const sgpu_options* opt) {
 // A part's streams and events, created when the part is first used: the pyramid/detection
 // stream gets the dispatch priority over the orientation/descriptor stream (of the previous
 // part, when a batch runs in parts); octaves >= 1 of the pyramid run on a third stream.
-static int part_streams(Part& pt) {
-    if (pt.stream) return SGPU_OK;
+enum { PS_MAIN = 1, PS_LO = 2, PS_OCT = 4, PS_ALL = 7 };
+static int part_streams(Part& pt, int which = PS_ALL) {
     int prio_lo = 0, prio_hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    if (hipStreamCreateWithPriority(&pt.stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&pt.stream_lo, hipStreamNonBlocking, prio_lo) != hipSuccess ||
+    if ((which & PS_MAIN) && !pt.stream &&
+        hipStreamCreateWithPriority(&pt.stream, hipStreamNonBlocking, prio_hi) != hipSuccess)
+        return SGPU_ENODEV;
+    if ((which & PS_LO) && !pt.stream_lo &&
+        hipStreamCreateWithPriority(&pt.stream_lo, hipStreamNonBlocking, prio_lo) != hipSuccess)
+        return SGPU_ENODEV;
+    if ((which & PS_OCT) && !pt.stream_oct &&
         hipStreamCreateWithPriority(&pt.stream_oct, hipStreamNonBlocking, prio_hi) != hipSuccess)
         return SGPU_ENODEV;
-    for (hipEvent_t& e : pt.ev)
-        if (hipEventCreate(&e) != hipSuccess) return SGPU_ENODEV;
-    if (hipEventCreateWithFlags(&pt.ev_ds, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&pt.ev_oct, hipEventDisableTiming) != hipSuccess)
-        return SGPU_ENODEV;
+    if (!pt.ev_ds) {
+        for (hipEvent_t& e : pt.ev)
+            if (hipEventCreate(&e) != hipSuccess) return SGPU_ENODEV;
+        if (hipEventCreateWithFlags(&pt.ev_ds, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&pt.ev_oct, hipEventDisableTiming) != hipSuccess)
+            return SGPU_ENODEV;
+    }
     return SGPU_OK;
 }
 
@@ -315,12 +322,32 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
         return SGPU_ENODEV;
     }
     for (int i = 0; i <= T_N; i++) (void)hipEventCreate(&ctx->ev[i]);
-    // part 0's streams now (a part's streams are created when it is first used, see
-    // part_streams): a context that runs one part holds 4 streams, which the runtime spreads
-    // over distinct hardware queues (4 on the GPU box)
-    if (part_streams(ctx->part[0]) != SGPU_OK) {
-        sgpu_ctx_destroy(ctx);
-        return SGPU_ENODEV;
+    // Streams in an order that puts the concurrently busy ones on distinct hardware queues: the
+    // runtime hands a process's streams the hardware queues in turn (4 on the GPU box), so the
+    // i-th stream created here shares a queue with the (i+4)-th.  Busy together: a part's
+    // pyramid stream and its octave stream (extract), and in sgpu_extract_stream also the copy
+    // streams h2d / d2h (a batch's orientation / descriptor stream runs beside the copies
+    // only).  Order (queue = index mod 4): 0 context stream, 1 part 0 main, 2 part 0 octaves,
+    // 3 h2d, 4 d2h, 5 part 0 low, 6 part 1 octaves, 7-8 part 2 main / low (idle unless
+    // SGPU_DEBUG_PARTS4), 9 part 1 main, 10 part 1 low: the main and octave streams on queues
+    // 1 and 2, the copies on 3 and 0.  Measured: the same streams created part by part put a
+    // copy stream beside a pyramid stream and cost the host-in / host-out stream 13 % (DESIGN.md
+    // 4.3).  The rest are created when first used (part_streams).
+    {
+        Part* p = ctx->part;
+        bool ok = part_streams(p[0], PS_MAIN) == SGPU_OK && part_streams(p[0], PS_OCT) == SGPU_OK &&
+                  hipStreamCreateWithFlags(&ctx->h2d, hipStreamNonBlocking) == hipSuccess &&
+                  hipStreamCreateWithFlags(&ctx->d2h, hipStreamNonBlocking) == hipSuccess &&
+                  part_streams(p[0], PS_LO) == SGPU_OK && part_streams(p[1], PS_OCT) == SGPU_OK &&
+                  part_streams(p[2], PS_MAIN) == SGPU_OK && part_streams(p[2], PS_LO) == SGPU_OK &&
+                  part_streams(p[1], PS_MAIN) == SGPU_OK && part_streams(p[1], PS_LO) == SGPU_OK;
+        for (int i = 0; ok && i < 2; i++)
+            ok = hipEventCreateWithFlags(&ctx->up_ev[i], hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreateWithFlags(&ctx->down_ev[i], hipEventDisableTiming) == hipSuccess;
+        if (!ok) {
+            sgpu_ctx_destroy(ctx);
+            return SGPU_ENODEV;
+        }
     }
     // test mode for the C++ replicas, which only see SiftGPU.h: the bit-exact descriptor
     if (const char* ev = getenv("SGPU_EXACT_DESCRIPTOR"))
@@ -867,7 +894,7 @@ static int extract_stream_body(sgpu_ctx* ctx, const uint8_t* const* batches, int
     }
     if (part_streams(ctx->part[1]) != SGPU_OK)
         return ctx->fail(SGPU_ENODEV, "stream creation failed");
-    if (!ctx->h2d) {
+    if (!ctx->h2d) {   // created with the context; kept for a context whose creation order changes
         HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->h2d, hipStreamNonBlocking));
         HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->d2h, hipStreamNonBlocking));
         for (int i = 0; i < 2; i++) {
