@@ -58,6 +58,9 @@ enum { T_UPLOAD, T_PYRAMID, T_DETECT, T_ORIENT, T_EXPAND, T_DESC, T_DOWNLOAD, T_
 struct Part {
     hipStream_t stream = nullptr;      // high priority: pyramid + detection
     hipStream_t stream_lo = nullptr;   // low priority: orientation, descriptors, readback
+    // a small batch (one image through SiftGPU::RunSIFT) runs every stage on `stream`: the
+    // cross-stream event waits cost more than the overlap gains there (extract_body)
+    bool one_stream = false;
     hipStream_t stream_oct = nullptr;  // high priority: pyramid octaves >= 1 (enqueue_part)
     hipEvent_t ev_ds = nullptr;        // octave 0's decimating level done
     hipEvent_t ev_oct = nullptr;       // octaves >= 1 done
@@ -108,6 +111,8 @@ struct sgpu_ctx {
     sgp::Schedule sched{};
     sgp::InputPlan plan{};                 // first octave of the last extract (plan_input)
     int debug_flags = 0;                   // SGPU_DEBUG_* test hooks
+    bool multi_stream = false;             // SGPU_STREAMS=multi: no one-stream small batches
+    bool one_stream_all = false;           // SGPU_STREAMS=one: every single-part batch on one stream
     std::string err;
     // last extract
     int batch = 0, w = 0, h = 0, nparts = 0;
@@ -286,6 +291,8 @@ int sgpu_ctx_set_options(sgpu_ctx* ctx, const sgpu_options* opt) {
 // stream gets the dispatch priority over the orientation/descriptor stream (of the previous
 // part, when a batch runs in parts); octaves >= 1 of the pyramid run on a third stream.
 enum { PS_MAIN = 1, PS_LO = 2, PS_OCT = 4, PS_ALL = 7 };
+// batches of at most this many first-octave pixels run on one stream (extract_body)
+static constexpr size_t kOneStreamPixels = (size_t)4 << 20;
 static int part_streams(Part& pt, int which = PS_ALL) {
     int prio_lo = 0, prio_hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
@@ -360,6 +367,10 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     }
     if (const char* ev = getenv("SGPU_PYR")) {
         if (!strcmp(ev, "serial")) ctx->debug_flags |= SGPU_DEBUG_PYR_SERIAL;
+    }
+    if (const char* ev = getenv("SGPU_STREAMS")) {
+        ctx->multi_stream = !strcmp(ev, "multi");
+        ctx->one_stream_all = !strcmp(ev, "one");
     }
     if (const char* ev = getenv("SGPU_MATCH"))
         if (!strcmp(ev, "reg")) ctx->debug_flags |= SGPU_DEBUG_MATCH_REGSTAGE;
@@ -514,7 +525,7 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     // 0's last levels instead of after them, 3.64 vs 3.69-3.74 ms per 128 x 1080p (DESIGN.md
     // 4.3; one stream per octave measured 3.83 ms).  SGPU_DEBUG_PYR_SERIAL: one stream.  The
     // main stream waits for them before the extremum kernel.
-    const bool side = noct > 1 && !(ctx->debug_flags & SGPU_DEBUG_PYR_SERIAL);
+    const bool side = noct > 1 && !pt.one_stream && !(ctx->debug_flags & SGPU_DEBUG_PYR_SERIAL);
     for (int o = 0; o < noct; o++) {
         const sgk::OctaveDesc& od = fp.oct[o];
         const hipStream_t so = side && o >= 1 ? pt.stream_oct : st;
@@ -597,8 +608,12 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     HIPCHK(ctx, hipEventRecord(pt.ev[1], st));
 
     // ---- extrema + row scan (the strip extremum kernel only sets the bits it accepts)
-    HIPCHK(ctx, hipMemsetAsync(pt.row_count.p, 0, (size_t)pt.total_rows * 4, st));
-    HIPCHK(ctx, hipMemsetAsync(pt.mask.p, 0, (size_t)moff * sizeof(uint32_t), st));
+    // (one launch zeroes the row counts and the mask, and on a single stream also the
+    // orientation counts, which otherwise are zeroed on the feature stream after its waits)
+    HIPCHK(ctx, sgk::launch_zero(pt.row_count.as<uint32_t>(), (size_t)pt.total_rows,
+                                 pt.mask.as<uint32_t>(), (size_t)moff,
+                                 pt.one_stream ? pt.ocount.as<uint32_t>() : nullptr,
+                                 pt.one_stream ? nc : 0, st));
     HIPCHK(ctx, sgk::launch_extrema(pyr, pt.mask.as<uint32_t>(), pt.row_count.as<uint32_t>(),
                                     fp, st));
     if (O.feature_count_threshold > 0)   // -tc: GenerateFeatureList skip + LimitFeatureCount(0)
@@ -612,11 +627,14 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     // ---- orientation (+ keypoint refinement), expansion, descriptors on the low-priority
     // stream: counts stay on the device, grids come from the previous call's counts (the
     // kernels grid-stride over whatever the device count is)
-    st = pt.stream_lo;
-    HIPCHK(ctx, hipStreamWaitEvent(st, pt.ev[2], 0));
+    if (!pt.one_stream) {
+        st = pt.stream_lo;
+        HIPCHK(ctx, hipStreamWaitEvent(st, pt.ev[2], 0));
+    }
     if (wait_lo) HIPCHK(ctx, hipStreamWaitEvent(st, wait_lo, 0));   // previous features read out
     const uint32_t* n_cand_dev = pt.row_base.as<uint32_t>() + pt.total_rows;
-    HIPCHK(ctx, hipMemsetAsync(pt.ocount.p, 0, nc * sizeof(uint32_t), st));
+    if (!pt.one_stream)
+        HIPCHK(ctx, sgk::launch_zero(pt.ocount.as<uint32_t>(), nc, nullptr, 0, nullptr, 0, st));
     const int cand_grid = (int)std::min(nc, pt.cand_hint ? pt.cand_hint : nc);
     // few candidates (a single image): one wave per candidate instead of a quad, so that the
     // SIMDs are filled and each window is walked 64 samples at a time (same bits)
@@ -654,7 +672,7 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
 
 // Queue the (pinned) readback of a part's counts and offsets.
 static int enqueue_readback(sgpu_ctx* ctx, Part& pt) {
-    hipStream_t st = pt.stream_lo;
+    hipStream_t st = pt.one_stream ? pt.stream : pt.stream_lo;
     pt.h_read[0] = 0;
     HIPCHK(ctx, hipMemcpyAsync(pt.h_read, pt.row_base.as<uint32_t>() + pt.total_rows, 4,
                                hipMemcpyDeviceToHost, st));
@@ -740,17 +758,28 @@ static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
         const int cnt = n / np + (p < n % np ? 1 : 0);
         ctx->part[p].img0 = i0;
         ctx->part[p].n = cnt;
+        ctx->part[p].one_stream = false;
         i0 += cnt;
     }
+    // A small batch -- one image from SiftGPU::RunSIFT, config C2 -- runs upload, pyramid and
+    // feature stages on one stream: there every kernel is short and latency-bound, and each
+    // cross-stream event wait (upload -> pyramid, octave 0 -> octaves >= 1 -> extrema, detection ->
+    // orientation) left the GPU idle for 30-45 us in the C2 kernel trace (profiles/r03c_c2_*).
+    // SGPU_STREAMS=multi keeps the batch layout, SGPU_STREAMS=one uses one stream for any batch
+    // (A/B runs).
+    const bool one = np == 1 && !ctx->multi_stream &&
+                     ((size_t)n * plan.w * plan.h <= kOneStreamPixels || ctx->one_stream_all);
+    ctx->part[0].one_stream = one;
+    const hipStream_t up = one ? ctx->part[0].stream : ctx->stream;
 
     // input: host batches are uploaded first on the context stream
     const size_t in_bytes = (size_t)n * h * stride * (is_f32 ? sizeof(float) : 1);
-    HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+    HIPCHK(ctx, hipEventRecord(ctx->ev[0], up));
     const void* src_in = staged ? ctx->input.p : images;
     if (!(flags & (SGPU_INPUT_DEVICE | SGPU_INPUT_STAGED))) {
         ctx->staged_bytes = 0;
         ALLOCCHK(ctx, ctx->input.ensure(in_bytes));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->input.p, images, in_bytes, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->input.p, images, in_bytes, hipMemcpyHostToDevice, up));
         src_in = ctx->input.p;
     }
     if (color) {
@@ -759,7 +788,7 @@ static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
         ALLOCCHK(ctx, ctx->gray.ensure((size_t)n * h * tw * sizeof(float)));
         HIPCHK(ctx, sgk::launch_color_to_gray((const uint8_t*)src_in, n, w, h, stride, channels,
                                               color == SGPU_BGR || color == SGPU_BGRA,
-                                              ctx->gray.as<float>(), ctx->stream));
+                                              ctx->gray.as<float>(), up));
         src_in = ctx->gray.p;
         is_f32 = true;
         stride = tw;
@@ -774,16 +803,16 @@ static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
                                                    is_f32 ? nullptr : (const uint8_t*)src_in,
                                                    stride, (long long)stride * h, w & ~3, h, plan.ds,
                                                    ctx->pre.as<float>(), plan.w, plan.h,
-                                                   (long long)px, n, ctx->stream));
+                                                   (long long)px, n, up));
         src_in = ctx->pre.p;
         is_f32 = true;
         stride = plan.w;
     }
-    HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
+    HIPCHK(ctx, hipEventRecord(ctx->ev[1], up));
 
     // part p's pyramid starts when part p-1 has finished detection
     for (int p = 0; p < np; p++) {
-        hipEvent_t wait = p == 0 ? ctx->ev[1] : ctx->part[p - 1].ev[2];
+        hipEvent_t wait = p == 0 ? (one ? nullptr : ctx->ev[1]) : ctx->part[p - 1].ev[2];
         int rc = enqueue_part(ctx, ctx->part[p], src_in, is_f32, stride, wait);
         if (rc != SGPU_OK) return rc;
     }
@@ -903,6 +932,7 @@ static int extract_stream_body(sgpu_ctx* ctx, const uint8_t* const* batches, int
         }
     }
     const size_t in_bytes = (size_t)batch * h * stride;
+    ctx->part[0].one_stream = ctx->part[1].one_stream = false;   // the slots overlap on streams
     ctx->staged_bytes = 0;
     ALLOCCHK(ctx, ctx->input.ensure(in_bytes));
     ALLOCCHK(ctx, ctx->input2.ensure(in_bytes));

@@ -87,6 +87,10 @@ hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
 // Exclusive scan of n uint32 values into out[0..n]; out[n] = total.  tmp needs
 // scan_tmp_words(n) words.
 size_t scan_tmp_words(size_t n);
+// Zero up to three u32 buffers (null / 0 words: skipped) in one launch: hipMemsetAsync is two
+// fill dispatches per buffer, which a single-image extract pays three times.
+hipError_t launch_zero(uint32_t* a, size_t na, uint32_t* b, size_t nb, uint32_t* c, size_t nc,
+                       hipStream_t stream);
 hipError_t launch_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
                        hipStream_t stream);
 

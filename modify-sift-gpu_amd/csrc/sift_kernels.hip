@@ -2419,7 +2419,8 @@ __device__ __forceinline__ float quad_sum(float v) {
 #ifndef SGK_DESC_RSTEP
 #define SGK_DESC_RSTEP 4
 #endif
-static_assert(SGK_DESC_RSTEP == 1 || SGK_DESC_RSTEP == 2 || SGK_DESC_RSTEP == 4, "rows per quad step");
+static_assert(SGK_DESC_RSTEP == 0 || SGK_DESC_RSTEP == 1 || SGK_DESC_RSTEP == 2 ||
+                  SGK_DESC_RSTEP == 4, "rows per quad step (0: flat strip order)");
 
 template <bool RECT>
 __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
@@ -2558,17 +2559,41 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
     // (rsub, csub) walks rows rsub, rsub + RSTEP, ... in strips starting 4 csub columns into the
     // span, 4 LPR apart (RSTEP 4: every lane its own rows; 2: two lanes on adjacent strips of one
     // row, so a load instruction touches half the cache lines)
-    constexpr int RSTEP = SGK_DESC_RSTEP, LPR = 4 / RSTEP;
-    const int rsub = sub / LPR, c4 = 4 * (sub % LPR);
-    int r = rsub, c = 0, lo = 0, len = 0;
+    // RSTEP 0 (flat): the cell's strips in row-major order, strip f to lane f mod 4, so the
+    // quad's 4 lanes read 16 consecutive columns of one row (or the end of one row and the start
+    // of the next): one or two cache lines per quad and load instead of four, and no lane idles
+    // on a short row.  Each lane keeps its own cursor (row r, strip s of the row) and moves it 4
+    // strips per step.
+    constexpr int RSTEP = SGK_DESC_RSTEP, LPR = 4 / (RSTEP ? RSTEP : 4);
+    const int rsub = RSTEP ? sub / LPR : 0, c4 = RSTEP ? 4 * (sub % LPR) : 0;
+    int r = rsub, c = 0, lo = 0, len = 0, s = sub, ns = 0;
     auto next_row = [&]() {   // advance r (by RSTEP) to the next row with samples for this lane
         for (; r < nrows; r += RSTEP) {
             row_span(r, lo, len);
             if (len > c4) break;
         }
     };
-    if (ncols > 0) next_row(); else r = nrows;
-    c = lo + c4;
+    auto flat_norm = [&]() {   // move (r, s) forward over rows until strip s exists in row r
+        while (s >= ns && r < nrows) {
+            s -= ns;
+            if (++r < nrows) {
+                row_span(r, lo, len);
+                ns = (len + 3) >> 2;
+            }
+        }
+    };
+    if (RSTEP == 0) {
+        r = ncols > 0 ? 0 : nrows;
+        if (r < nrows) {
+            row_span(0, lo, len);
+            ns = (len + 3) >> 2;
+        }
+        flat_norm();
+        c = lo + 4 * s;
+    } else {
+        if (ncols > 0) next_row(); else r = nrows;
+        c = lo + c4;
+    }
     f4v na, nb, nu, nd;
     // the address loaded when no sample is left: row 1, column 1 of the plane, whose 4 loads
     // (columns 0 .. 5 of row 1, columns 1 .. 4 of rows 0 and 2) stay inside it for any feature --
@@ -2587,11 +2612,17 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
         const float dy = (ymin + (float)r) - pty;
         const int nv = lo + len - c;   // samples of this strip inside the span
         const float dx0 = (xmin + (float)c) - ptx;
-        c += 4 * LPR;
-        if (c >= lo + len) {
-            r += RSTEP;
-            next_row();
-            c = lo + c4;
+        if (RSTEP == 0) {
+            s += 4;
+            flat_norm();
+            c = lo + 4 * s;
+        } else {
+            c += 4 * LPR;
+            if (c >= lo + len) {
+                r += RSTEP;
+                next_row();
+                c = lo + c4;
+            }
         }
         fetch();
         sample(dx0, dy, b.x - a.x, dn.x - up.x, true);
@@ -2960,6 +2991,38 @@ size_t scan_tmp_words(size_t n) {
         n = nb;
     }
     return words + 16;
+}
+
+__device__ __forceinline__ void zero_words(uint32_t* p, size_t n, size_t q) {
+    if (q * 4 + 4 <= n) {
+        *reinterpret_cast<uint4*>(p + q * 4) = make_uint4(0, 0, 0, 0);
+    } else {
+        for (size_t i = q * 4; i < n; i++) p[i] = 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_zero(uint32_t* __restrict__ a, size_t na,
+                                              uint32_t* __restrict__ b, size_t nb,
+                                              uint32_t* __restrict__ c, size_t nc) {
+    const size_t step = (size_t)gridDim.x * 256;
+    for (size_t q = (size_t)blockIdx.x * 256 + threadIdx.x; q * 4 < na; q += step) zero_words(a, na, q);
+    for (size_t q = (size_t)blockIdx.x * 256 + threadIdx.x; q * 4 < nb; q += step) zero_words(b, nb, q);
+    for (size_t q = (size_t)blockIdx.x * 256 + threadIdx.x; q * 4 < nc; q += step) zero_words(c, nc, q);
+}
+
+hipError_t launch_zero(uint32_t* a, size_t na, uint32_t* b, size_t nb, uint32_t* c, size_t nc,
+                       hipStream_t stream) {
+    // the uint4 stores need 16-byte aligned buffers (hipMalloc's are)
+    for (const uint32_t* p : {(const uint32_t*)a, (const uint32_t*)b, (const uint32_t*)c})
+        if ((uintptr_t)p % 16) return hipErrorInvalidValue;
+    if (!a) na = 0;
+    if (!b) nb = 0;
+    if (!c) nc = 0;
+    const size_t quads = (std::max(na, std::max(nb, nc)) + 3) / 4;
+    if (quads == 0) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<size_t>((quads + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_zero, dim3(grid), dim3(256), 0, stream, a, na, b, nb, c, nc);
+    return hipGetLastError();
 }
 
 hipError_t launch_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
