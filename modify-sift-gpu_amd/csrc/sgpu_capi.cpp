@@ -834,7 +834,7 @@ static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
             int rc = enqueue_part(ctx, pt, src_in, is_f32, stride, nullptr);
             if (rc == SGPU_OK) rc = enqueue_readback(ctx, pt);
             if (rc != SGPU_OK) return rc;
-            HIPCHK(ctx, hipStreamSynchronize(pt.stream_lo));
+            HIPCHK(ctx, hipStreamSynchronize(pt.one_stream ? pt.stream : pt.stream_lo));
             nc = (uint32_t)pt.h_read[0];
             if (nc > pt.cand_cap) return ctx->fail(SGPU_ERANGE, "keypoint capacity overflow");
         }

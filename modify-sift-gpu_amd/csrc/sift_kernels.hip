@@ -14,6 +14,8 @@
 //     (image, octave, level, row, column) order -- no histogram pyramid, no host round trips.
 // Floating-point conventions are those of oracle/sift_oracle.cpp (fma contractions written
 // out, transcendentals from sift_math.h); the build uses -ffp-contract=off.
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "sift_kernels.h"
@@ -533,7 +535,13 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_wave(
 }
 
 // band height of the wave kernel: rows_hint > 0 forces it (test / tuning hook), else bands of
-// the whole image unless that leaves fewer than ~8 waves per CU, then as many bands as needed
+// the whole image unless that leaves fewer than ~8 waves per CU, then as many bands as needed.
+// A band re-reads the level's FW-1 halo rows, so bands stay >= 4 chunks high while the level
+// streams from HBM; a level of at most kShortBandBytes (one image of a small batch, which the
+// previous level left in the 256 MB Infinity Cache) may go down to one chunk: its launches are
+// latency-bound (a wave walks band + lag chunks one after the other), and shorter bands are
+// fewer steps per wave.  SGPU_GAUSS_BANDS=long keeps the 4-chunk minimum (A/B hook).
+static constexpr long long kShortBandBytes = 64ll << 20;
 static GaussWaveGrid gauss_wave_grid(int w, int h, int batch, int rows_hint, int nw) {
     GaussWaveGrid g{};
     g.strips_x = (w + GT * nw - 1) / (GT * nw);
@@ -542,9 +550,14 @@ static GaussWaveGrid gauss_wave_grid(int w, int h, int batch, int rows_hint, int
     if (rows_hint > 0) {
         rows = rows_hint;
     } else {
+        static const bool long_bands = [] {
+            const char* e = getenv("SGPU_GAUSS_BANDS");
+            return e && !strcmp(e, "long");
+        }();
+        const bool short_ok = !long_bands && 4ll * w * h * batch <= kShortBandBytes;
         const long long want = 8 * 256;
         const int nsy = (int)std::min<long long>((want + per_band - 1) / per_band,
-                                                 std::max(1, h / (4 * WCH)));
+                                                 std::max(1, h / ((short_ok ? 1 : 4) * WCH)));
         rows = (h + std::max(nsy, 1) - 1) / std::max(nsy, 1);
     }
     rows = std::max(WCH, (rows + WCH - 1) / WCH * WCH);
@@ -2419,6 +2432,13 @@ __device__ __forceinline__ float quad_sum(float v) {
 #ifndef SGK_DESC_RSTEP
 #define SGK_DESC_RSTEP 4
 #endif
+// SGK_DESC_LDSBIN: each sample adds its two interpolated weights to the lane's own 8-bin
+// histogram in LDS (two no-return ds_add_f32 at computed addresses) instead of the branch-free
+// tent over all 8 register bins (4 VALU per bin: 33 per sample of the ~100 it costs; the kernel is
+// VALU-issue bound)
+#ifndef SGK_DESC_LDSBIN
+#define SGK_DESC_LDSBIN 0
+#endif
 static_assert(SGK_DESC_RSTEP == 0 || SGK_DESC_RSTEP == 1 || SGK_DESC_RSTEP == 2 ||
                   SGK_DESC_RSTEP == 4, "rows per quad step (0: flat strip order)");
 
@@ -2428,7 +2448,8 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
                                                 const float4* __restrict__ feat,
                                                 const int2* __restrict__ feat_info,
                                                 const FeatureParams& fp,
-                                                float* __restrict__ desc, uint32_t out) {
+                                                float* __restrict__ desc, uint32_t out,
+                                                float* hist) {
     const int cell = lane >> 2, sub = lane & 3;
     const int ix = cell & 3, iy = cell >> 2;
     const float4 key = feat[e];
@@ -2534,12 +2555,23 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
         // outside the rotated square (|n| >= 1) or theta == 8 (the reference's fidx == 8 is
         // dropped) the sample adds nothing
         w = (valid && wx > 0.0f && wy > 0.0f && theta < 8.0f) ? w : 0.0f;
+#if SGK_DESC_LDSBIN
+        // bins floor(theta) and floor(theta) + 1 (mod 8) get w (1 - f) and w f; a dropped sample
+        // (w = 0, theta possibly 8 or NaN) adds 0 to some bin of the lane's own histogram
+        const float fl = __builtin_floorf(theta);
+        const float f = theta - fl;
+        const int fi = (int)fl;
+        atomicAdd(hist + ((fi & 7) << 6) + lane, (1.0f - f) * w);
+        atomicAdd(hist + (((fi + 1) & 7) << 6) + lane, f * w);
+        (void)acc;
+#else
         acc[0] = fma_(__builtin_amdgcn_fmed3f(fmax_(1.0f - theta, theta - 7.0f), 0.0f, 1.0f), w,
                       acc[0]);
 #pragma unroll
         for (int k = 1; k < 8; k++)
             acc[k] = fma_(__builtin_amdgcn_fmed3f(1.0f - fabs_(theta - (float)k), 0.0f, 1.0f), w,
                           acc[k]);
+#endif
     };
     // Lane sub walks rows sub, sub + 4, ... of its cell's box, each row's span in strips of 4
     // consecutive samples: the strip's gradient neighbours come from 4 vector loads -- row y at
@@ -2630,6 +2662,15 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
         sample(dx0 + 2.0f, dy, b.z - a.z, dn.z - up.z, nv > 2);
         sample(dx0 + 3.0f, dy, b.w - a.w, dn.w - up.w, nv > 3);
     }
+#if SGK_DESC_LDSBIN
+    // the lane's histogram back to registers (the lane's own adds, in order), cleared for the
+    // wave's next feature
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        acc[k] = hist[(k << 6) + lane];
+        hist[(k << 6) + lane] = 0.0f;
+    }
+#endif
 #pragma unroll
     for (int k = 0; k < 8; k++) acc[k] = quad_sum(acc[k]);
     // lane sub owns bins 2 sub, 2 sub + 1 of its cell
@@ -2668,9 +2709,17 @@ __global__ __launch_bounds__(256) void k_descriptor_fast(const float* __restrict
     // the feature index is wave-uniform: say so, so that the feature's record, level pointer and
     // geometry live in SGPRs and the gathers use the SGPR-base + 32-bit-offset form
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if SGK_DESC_LDSBIN
+    __shared__ float s_hist[4 * 8 * 64];   // per wave: bin k of lane l at k * 64 + l
+    float* hist = s_hist + wave * 512;
+#pragma unroll
+    for (int k = 0; k < 8; k++) hist[(k << 6) + lane] = 0.0f;
+#else
+    float* hist = nullptr;
+#endif
     for (uint32_t e = blockIdx.x * 4 + wave; e < n; e += gridDim.x * 4)
         descriptor_fast<RECT>(e, lane, pyr, feat, feat_info, fp, desc,
-                              out_index ? (uint32_t)out_index[e] : e);
+                              out_index ? (uint32_t)out_index[e] : e, hist);
 }
 
 // One wave per feature, grid-stride over the features (count read on the device).

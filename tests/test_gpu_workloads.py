@@ -202,3 +202,29 @@ def test_extract_stream_without_descriptors(gpu_ctx):
             gpu_ctx.extract_stream(batches, desc=np.zeros((10, 128), np.float32))
     finally:
         gpu_ctx.set_options(default_options())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2])
+def test_one_stream_small_batch_equals_stream_layout(n):
+    """A small batch (C2: one image through RunSIFT) runs every stage on one stream; the batch
+    layout (octaves >= 1 and the feature stages on their own streams, SGPU_STREAMS=multi) gives the
+    same keys and descriptors bit for bit."""
+    import os
+    import sgpu
+    imgs = np.stack([synth_image(1920, 1080, 2000 + i) for i in range(n)])
+    out = {}
+    for mode in ("", "multi"):
+        os.environ["SGPU_STREAMS"] = mode   # read at context creation
+        try:
+            ctx = sgpu.SiftContext(0)
+        finally:
+            del os.environ["SGPU_STREAMS"]
+        try:
+            ctx.extract(imgs)
+            out[mode] = [ctx.features(i) for i in range(n)]
+        finally:
+            ctx.close()
+    for i in range(n):
+        assert out[""][i][0].shape[0] > 100
+        assert _equal(out[""][i], out["multi"][i]), i
