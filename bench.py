@@ -221,8 +221,7 @@ def main():
         "stage_ms_per_step": {k: v / args.steps for k, v in stage_acc.items() if k != "match"},
         "roofline": {
             "kernel": f"k_gauss_lean (separable Gaussian level; all {n_gauss} launches of a step, "
-                      "HIP events around them on the library's stream: octaves >= 1 run on "
-                      "side streams beside the octaves below, so this is the stage's span)",
+                      "back to back on the library's stream, HIP events around them)",
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,

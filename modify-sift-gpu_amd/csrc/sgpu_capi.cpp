@@ -111,8 +111,7 @@ struct sgpu_ctx {
     sgp::Schedule sched{};
     sgp::InputPlan plan{};                 // first octave of the last extract (plan_input)
     int debug_flags = 0;                   // SGPU_DEBUG_* test hooks
-    bool multi_stream = false;             // SGPU_STREAMS=multi: no one-stream small batches
-    bool one_stream_all = false;           // SGPU_STREAMS=one: every single-part batch on one stream
+    bool multi_stream = false;             // SGPU_STREAMS=multi: octave and feature streams
     std::string err;
     // last extract
     int batch = 0, w = 0, h = 0, nparts = 0;
@@ -291,8 +290,6 @@ int sgpu_ctx_set_options(sgpu_ctx* ctx, const sgpu_options* opt) {
 // stream gets the dispatch priority over the orientation/descriptor stream (of the previous
 // part, when a batch runs in parts); octaves >= 1 of the pyramid run on a third stream.
 enum { PS_MAIN = 1, PS_LO = 2, PS_OCT = 4, PS_ALL = 7 };
-// batches of at most this many first-octave pixels run on one stream (extract_body)
-static constexpr size_t kOneStreamPixels = (size_t)4 << 20;
 static int part_streams(Part& pt, int which = PS_ALL) {
     int prio_lo = 0, prio_hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
@@ -368,10 +365,7 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     if (const char* ev = getenv("SGPU_PYR")) {
         if (!strcmp(ev, "serial")) ctx->debug_flags |= SGPU_DEBUG_PYR_SERIAL;
     }
-    if (const char* ev = getenv("SGPU_STREAMS")) {
-        ctx->multi_stream = !strcmp(ev, "multi");
-        ctx->one_stream_all = !strcmp(ev, "one");
-    }
+    if (const char* ev = getenv("SGPU_STREAMS")) ctx->multi_stream = !strcmp(ev, "multi");
     if (const char* ev = getenv("SGPU_MATCH"))
         if (!strcmp(ev, "reg")) ctx->debug_flags |= SGPU_DEBUG_MATCH_REGSTAGE;
     int rc = sgpu_ctx_set_options(ctx, opt);
@@ -520,11 +514,11 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
         lfw[k] = sgp::make_filter(S.sigma[k - 1], O.filter_width_factor, ltaps[k].k);
     const int fw0 = sgp::make_filter(S.initial_smooth, O.filter_width_factor, taps0.k);
     const int kds = S.level_ds - S.level_min;
-    // Octaves >= 1 run on a second stream, which starts as soon as octave 0's level kds has
-    // written octave 1's base (level 0): their small, latency-bound launches run beside octave
-    // 0's last levels instead of after them, 3.64 vs 3.69-3.74 ms per 128 x 1080p (DESIGN.md
-    // 4.3; one stream per octave measured 3.83 ms).  SGPU_DEBUG_PYR_SERIAL: one stream.  The
-    // main stream waits for them before the extremum kernel.
+    // Stream layout (SGPU_STREAMS=multi, not the default: extract_body): octaves >= 1 run on a
+    // second stream, which starts as soon as octave 0's level kds has written octave 1's base
+    // (level 0), so their small launches run beside octave 0's last levels (pyramid 3.64 vs
+    // 3.69-3.74 ms per 128 x 1080p), and the main stream waits for them before
+    // the extremum kernel.  SGPU_DEBUG_PYR_SERIAL: one stream for the pyramid only.
     const bool side = noct > 1 && !pt.one_stream && !(ctx->debug_flags & SGPU_DEBUG_PYR_SERIAL);
     for (int o = 0; o < noct; o++) {
         const sgk::OctaveDesc& od = fp.oct[o];
@@ -761,14 +755,13 @@ static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
         ctx->part[p].one_stream = false;
         i0 += cnt;
     }
-    // A small batch -- one image from SiftGPU::RunSIFT, config C2 -- runs upload, pyramid and
-    // feature stages on one stream: there every kernel is short and latency-bound, and each
-    // cross-stream event wait (upload -> pyramid, octave 0 -> octaves >= 1 -> extrema, detection ->
-    // orientation) left the GPU idle for 30-45 us in the C2 kernel trace (profiles/r03c_c2_*).
-    // SGPU_STREAMS=multi keeps the batch layout, SGPU_STREAMS=one uses one stream for any batch
-    // (A/B runs).
-    const bool one = np == 1 && !ctx->multi_stream &&
-                     ((size_t)n * plan.w * plan.h <= kOneStreamPixels || ctx->one_stream_all);
+    // A single-part batch runs upload, pyramid and feature stages on one stream.  Measured
+    // (alternating processes): the octave stream and the feature stream, each
+    // joined by a cross-stream event wait, cost more than their overlap gains -- C2 (one image
+    // through SiftGPU::RunSIFT) 0.50 vs 0.56-0.61 ms per image, the 128 x 1080p batch 15.26-15.33k
+    // vs 14.50-14.75k images/s (extrema 1.72 vs 1.92 ms, orientation 0.50 vs 0.55 ms after the
+    // waits).  SGPU_STREAMS=multi keeps the stream layout (A/B hook).
+    const bool one = np == 1 && !ctx->multi_stream;
     ctx->part[0].one_stream = one;
     const hipStream_t up = one ? ctx->part[0].stream : ctx->stream;
 
@@ -932,7 +925,8 @@ static int extract_stream_body(sgpu_ctx* ctx, const uint8_t* const* batches, int
         }
     }
     const size_t in_bytes = (size_t)batch * h * stride;
-    ctx->part[0].one_stream = ctx->part[1].one_stream = false;   // the slots overlap on streams
+    // each slot's kernels on its own stream (extract_body's measurement); slots and copies overlap
+    ctx->part[0].one_stream = ctx->part[1].one_stream = !ctx->multi_stream;
     ctx->staged_bytes = 0;
     ALLOCCHK(ctx, ctx->input.ensure(in_bytes));
     ALLOCCHK(ctx, ctx->input2.ensure(in_bytes));
@@ -948,7 +942,7 @@ static int extract_stream_body(sgpu_ctx* ctx, const uint8_t* const* batches, int
             int r = enqueue_part(ctx, pt, din[k & 1], false, stride, nullptr, nullptr);
             if (r == SGPU_OK) r = enqueue_readback(ctx, pt);
             if (r != SGPU_OK) return r;
-            HIPCHK(ctx, hipStreamSynchronize(pt.stream_lo));
+            HIPCHK(ctx, hipStreamSynchronize(pt.one_stream ? pt.stream : pt.stream_lo));
             nc = (uint32_t)pt.h_read[0];
             if (nc > pt.cand_cap) return ctx->fail(SGPU_ERANGE, "keypoint capacity overflow");
         }

@@ -2432,13 +2432,6 @@ __device__ __forceinline__ float quad_sum(float v) {
 #ifndef SGK_DESC_RSTEP
 #define SGK_DESC_RSTEP 4
 #endif
-// SGK_DESC_LDSBIN: each sample adds its two interpolated weights to the lane's own 8-bin
-// histogram in LDS (two no-return ds_add_f32 at computed addresses) instead of the branch-free
-// tent over all 8 register bins (4 VALU per bin: 33 per sample of the ~100 it costs; the kernel is
-// VALU-issue bound)
-#ifndef SGK_DESC_LDSBIN
-#define SGK_DESC_LDSBIN 0
-#endif
 static_assert(SGK_DESC_RSTEP == 0 || SGK_DESC_RSTEP == 1 || SGK_DESC_RSTEP == 2 ||
                   SGK_DESC_RSTEP == 4, "rows per quad step (0: flat strip order)");
 
@@ -2448,8 +2441,7 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
                                                 const float4* __restrict__ feat,
                                                 const int2* __restrict__ feat_info,
                                                 const FeatureParams& fp,
-                                                float* __restrict__ desc, uint32_t out,
-                                                float* hist) {
+                                                float* __restrict__ desc, uint32_t out) {
     const int cell = lane >> 2, sub = lane & 3;
     const int ix = cell & 3, iy = cell >> 2;
     const float4 key = feat[e];
@@ -2555,23 +2547,12 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
         // outside the rotated square (|n| >= 1) or theta == 8 (the reference's fidx == 8 is
         // dropped) the sample adds nothing
         w = (valid && wx > 0.0f && wy > 0.0f && theta < 8.0f) ? w : 0.0f;
-#if SGK_DESC_LDSBIN
-        // bins floor(theta) and floor(theta) + 1 (mod 8) get w (1 - f) and w f; a dropped sample
-        // (w = 0, theta possibly 8 or NaN) adds 0 to some bin of the lane's own histogram
-        const float fl = __builtin_floorf(theta);
-        const float f = theta - fl;
-        const int fi = (int)fl;
-        atomicAdd(hist + ((fi & 7) << 6) + lane, (1.0f - f) * w);
-        atomicAdd(hist + (((fi + 1) & 7) << 6) + lane, f * w);
-        (void)acc;
-#else
         acc[0] = fma_(__builtin_amdgcn_fmed3f(fmax_(1.0f - theta, theta - 7.0f), 0.0f, 1.0f), w,
                       acc[0]);
 #pragma unroll
         for (int k = 1; k < 8; k++)
             acc[k] = fma_(__builtin_amdgcn_fmed3f(1.0f - fabs_(theta - (float)k), 0.0f, 1.0f), w,
                           acc[k]);
-#endif
     };
     // Lane sub walks rows sub, sub + 4, ... of its cell's box, each row's span in strips of 4
     // consecutive samples: the strip's gradient neighbours come from 4 vector loads -- row y at
@@ -2662,15 +2643,6 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
         sample(dx0 + 2.0f, dy, b.z - a.z, dn.z - up.z, nv > 2);
         sample(dx0 + 3.0f, dy, b.w - a.w, dn.w - up.w, nv > 3);
     }
-#if SGK_DESC_LDSBIN
-    // the lane's histogram back to registers (the lane's own adds, in order), cleared for the
-    // wave's next feature
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        acc[k] = hist[(k << 6) + lane];
-        hist[(k << 6) + lane] = 0.0f;
-    }
-#endif
 #pragma unroll
     for (int k = 0; k < 8; k++) acc[k] = quad_sum(acc[k]);
     // lane sub owns bins 2 sub, 2 sub + 1 of its cell
@@ -2709,17 +2681,9 @@ __global__ __launch_bounds__(256) void k_descriptor_fast(const float* __restrict
     // the feature index is wave-uniform: say so, so that the feature's record, level pointer and
     // geometry live in SGPRs and the gathers use the SGPR-base + 32-bit-offset form
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if SGK_DESC_LDSBIN
-    __shared__ float s_hist[4 * 8 * 64];   // per wave: bin k of lane l at k * 64 + l
-    float* hist = s_hist + wave * 512;
-#pragma unroll
-    for (int k = 0; k < 8; k++) hist[(k << 6) + lane] = 0.0f;
-#else
-    float* hist = nullptr;
-#endif
     for (uint32_t e = blockIdx.x * 4 + wave; e < n; e += gridDim.x * 4)
         descriptor_fast<RECT>(e, lane, pyr, feat, feat_info, fp, desc,
-                              out_index ? (uint32_t)out_index[e] : e, hist);
+                              out_index ? (uint32_t)out_index[e] : e);
 }
 
 // One wave per feature, grid-stride over the features (count read on the device).

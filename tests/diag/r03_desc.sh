@@ -13,7 +13,7 @@ for V in desc_flat desc_r1; do
 done
 for V in desc_flat desc_r1; do
   echo "== A = shipped (RSTEP 4), B = $V"
-  timeout -k 10 400 bash tests/diag/ab_bench.sh build_exp/$V/libsiftgpu.so 2 || exit 1
+  timeout -k 10 300 bash tests/diag/ab_bench.sh build_exp/$V/libsiftgpu.so 2 || exit 1
 done
 export TMPDIR=/tmp
 for V in shipped desc_flat desc_r1; do
