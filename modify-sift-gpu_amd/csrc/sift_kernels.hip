@@ -537,11 +537,15 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_wave(
 // band height of the wave kernel: rows_hint > 0 forces it (test / tuning hook), else bands of
 // the whole image unless that leaves fewer than ~8 waves per CU, then as many bands as needed.
 // A band re-reads the level's FW-1 halo rows, so bands stay >= 4 chunks high while the level
-// streams from HBM; a level of at most kShortBandBytes (one image of a small batch, which the
-// previous level left in the 256 MB Infinity Cache) may go down to one chunk: its launches are
+// streams from HBM; a level of at most SGK_SHORT_BAND_MB (one image of a small batch, or the
+// upper octaves of a batch, largely still in the 256 MB Infinity Cache from the previous level)
+// may go down to one chunk: its launches are
 // latency-bound (a wave walks band + lag chunks one after the other), and shorter bands are
-// fewer steps per wave.  SGPU_GAUSS_BANDS=long keeps the 4-chunk minimum (A/B hook).
-static constexpr long long kShortBandBytes = 64ll << 20;
+// fewer steps per wave.  Measured against 128 MB with ~8,192 waves on such levels (alternating
+// processes, tests/diag/r03h.sh): pyramid 3.69 vs 3.73-3.76 ms per 128 x 1080p, C4 3.55 vs 3.65.
+#ifndef SGK_SHORT_BAND_MB
+#define SGK_SHORT_BAND_MB 64
+#endif
 static GaussWaveGrid gauss_wave_grid(int w, int h, int batch, int rows_hint, int nw) {
     GaussWaveGrid g{};
     g.strips_x = (w + GT * nw - 1) / (GT * nw);
@@ -550,11 +554,12 @@ static GaussWaveGrid gauss_wave_grid(int w, int h, int batch, int rows_hint, int
     if (rows_hint > 0) {
         rows = rows_hint;
     } else {
+        // A/B hook: SGPU_GAUSS_BANDS=long keeps bands >= 4 chunks on every level (round 2)
         static const bool long_bands = [] {
             const char* e = getenv("SGPU_GAUSS_BANDS");
             return e && !strcmp(e, "long");
         }();
-        const bool short_ok = !long_bands && 4ll * w * h * batch <= kShortBandBytes;
+        const bool short_ok = !long_bands && 4ll * w * h * batch <= ((long long)SGK_SHORT_BAND_MB << 20);
         const long long want = 8 * 256;
         const int nsy = (int)std::min<long long>((want + per_band - 1) / per_band,
                                                  std::max(1, h / ((short_ok ? 1 : 4) * WCH)));
