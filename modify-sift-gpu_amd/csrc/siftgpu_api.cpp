@@ -41,6 +41,45 @@ struct HostImage {
     std::vector<float> f32;
 };
 
+// The object's feature arrays (the reference's host key / descriptor buffers, which
+// GetFeatureVector copies out): page-locked and grow-only, so the per-image downloads run at
+// DMA speed instead of through the runtime's pageable staging (C2: one image per RunSIFT).
+// Falls back to ordinary memory if page-locked allocation fails.
+class HostFloats {
+  public:
+    HostFloats() = default;
+    HostFloats(const HostFloats&) = delete;
+    HostFloats& operator=(const HostFloats&) = delete;
+    ~HostFloats() { release(); }
+    void resize(size_t n) {
+        if (n > cap_) {
+            release();
+            size_t c = std::max(n, cap_ + cap_ / 2);
+            p_ = static_cast<float*>(sgpu_host_alloc(c * sizeof(float)));
+            pinned_ = p_ != nullptr;
+            if (!p_) p_ = static_cast<float*>(std::malloc(c * sizeof(float)));
+            if (!p_) throw std::bad_alloc();
+            cap_ = c;
+        }
+        n_ = n;
+    }
+    float* data() { return p_; }
+    const float* data() const { return p_; }
+    size_t size() const { return n_; }
+  private:
+    void release() {
+        if (p_) {
+            if (pinned_) sgpu_host_free(p_);
+            else std::free(p_);
+        }
+        p_ = nullptr;
+        cap_ = n_ = 0;
+    }
+    float* p_ = nullptr;
+    size_t cap_ = 0, n_ = 0;
+    bool pinned_ = false;
+};
+
 // Runtime state, stored in the slot of the reference's SiftPyramid* member.
 struct Runtime {
     sgpu_options opt;
@@ -49,7 +88,7 @@ struct Runtime {
     int binary = 0;             // -b
     int verbose = 1;
     int feature_num = 0;
-    std::vector<float> keys, desc;
+    HostFloats keys, desc;
     // SetKeypointList (SiftPyramid::SetKeypointList, SiftPyramid.cpp:293-310): applied by the
     // next RunSIFT on a new image, then cleared (SiftPyramid.cpp:204)
     std::vector<float> pending;
