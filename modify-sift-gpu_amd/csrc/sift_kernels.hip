@@ -2673,8 +2673,18 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
 }
 
 // One wave per feature, grid-stride over the features (count read on the device).
+// SGK_DESC_WPE: waves per SIMD the register allocation must allow (0: the compiler's choice, 91
+// VGPRs = 5 waves; A/B knob)
+#ifndef SGK_DESC_WPE
+#define SGK_DESC_WPE 0
+#endif
+#if SGK_DESC_WPE
+#define SGK_DESC_ATTR __attribute__((amdgpu_waves_per_eu(SGK_DESC_WPE)))
+#else
+#define SGK_DESC_ATTR
+#endif
 template <bool RECT>
-__global__ __launch_bounds__(256) void k_descriptor_fast(const float* __restrict__ pyr,
+__global__ __launch_bounds__(256) SGK_DESC_ATTR void k_descriptor_fast(const float* __restrict__ pyr,
                                                          const float4* __restrict__ feat,
                                                          const int2* __restrict__ feat_info,
                                                          const uint32_t* __restrict__ n_feat_dev,
