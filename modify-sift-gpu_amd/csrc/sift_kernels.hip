@@ -2440,14 +2440,21 @@ __device__ __forceinline__ float quad_sum(float v) {
 static_assert(SGK_DESC_RSTEP == 0 || SGK_DESC_RSTEP == 1 || SGK_DESC_RSTEP == 2 ||
                   SGK_DESC_RSTEP == 4, "rows per quad step (0: flat strip order)");
 
-template <bool RECT>
+// LPC lanes per cell: 4 (one wave per feature, the 16 cells) or 8 (two waves per feature, wave
+// `half` takes cells 8 half .. 8 half + 7, lane sub walks rows sub, sub + 8, ...: half the strips
+// per lane, for batches with few features, where one wave per feature leaves most SIMDs idle and
+// the kernel takes two rounds of the per-feature latency); with LPC 8 the bins are written
+// unnormalised and k_desc_normalize finishes them.
+template <bool RECT, int LPC = 4>
 __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
                                                 const float* __restrict__ pyr,
                                                 const float4* __restrict__ feat,
                                                 const int2* __restrict__ feat_info,
                                                 const FeatureParams& fp,
-                                                float* __restrict__ desc, uint32_t out) {
-    const int cell = lane >> 2, sub = lane & 3;
+                                                float* __restrict__ desc, uint32_t out,
+                                                int half = 0) {
+    static_assert(LPC == 4 || LPC == 8, "lanes per cell");
+    const int cell = LPC == 4 ? lane >> 2 : half * 8 + (lane >> 3), sub = lane & (LPC - 1);
     const int ix = cell & 3, iy = cell >> 2;
     const float4 key = feat[e];
     const int2 in = feat_info[e];
@@ -2582,7 +2589,8 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
     // of the next): one or two cache lines per quad and load instead of four, and no lane idles
     // on a short row.  Each lane keeps its own cursor (row r, strip s of the row) and moves it 4
     // strips per step.
-    constexpr int RSTEP = SGK_DESC_RSTEP, LPR = 4 / (RSTEP ? RSTEP : 4);
+    constexpr int RSTEP = LPC == 8 ? 8 : SGK_DESC_RSTEP;
+    constexpr int LPR = LPC == 8 ? 1 : 4 / (RSTEP ? RSTEP : 4);
     const int rsub = RSTEP ? sub / LPR : 0, c4 = RSTEP ? 4 * (sub % LPR) : 0;
     int r = rsub, c = 0, lo = 0, len = 0, s = sub, ns = 0;
     auto next_row = [&]() {   // advance r (by RSTEP) to the next row with samples for this lane
@@ -2650,6 +2658,16 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
     }
 #pragma unroll
     for (int k = 0; k < 8; k++) acc[k] = quad_sum(acc[k]);
+    if (LPC == 8) {
+        // the cell's 8 lanes: quads summed, then the two quads; lane sub owns bin sub
+#pragma unroll
+        for (int k = 0; k < 8; k++) acc[k] += __shfl_xor(acc[k], 4, 64);
+        float b = acc[0];
+#pragma unroll
+        for (int k = 1; k < 8; k++) b = sub == k ? acc[k] : b;
+        desc[(size_t)out * 128 + cell * 8 + sub] = b;
+        return;
+    }
     // lane sub owns bins 2 sub, 2 sub + 1 of its cell
     float b0 = acc[0], b1 = acc[1];
     b0 = sub == 1 ? acc[2] : b0; b1 = sub == 1 ? acc[3] : b1;
@@ -2699,6 +2717,44 @@ __global__ __launch_bounds__(256) SGK_DESC_ATTR void k_descriptor_fast(const flo
     for (uint32_t e = blockIdx.x * 4 + wave; e < n; e += gridDim.x * 4)
         descriptor_fast<RECT>(e, lane, pyr, feat, feat_info, fp, desc,
                               out_index ? (uint32_t)out_index[e] : e);
+}
+
+// Two waves per feature (few features: C2's single image), unnormalised bins.
+__global__ __launch_bounds__(256) void k_descriptor_half(const float* __restrict__ pyr,
+                                                         const float4* __restrict__ feat,
+                                                         const int2* __restrict__ feat_info,
+                                                         const uint32_t* __restrict__ n_feat_dev,
+                                                         const FeatureParams fp,
+                                                         float* __restrict__ desc) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t n = *n_feat_dev;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint32_t g = blockIdx.x * 4 + wave; (g >> 1) < n; g += gridDim.x * 4)
+        descriptor_fast<false, 8>(g >> 1, lane, pyr, feat, feat_info, fp, desc, g >> 1,
+                                  (int)(g & 1));
+}
+
+// descriptor_fast's normalisation (ProgramCU.cu:1173-1208: L2, clamp at 0.2, L2 again) for the
+// two-wave form: one wave per feature, lane l holds bins 2 l, 2 l + 1.
+__global__ __launch_bounds__(256) void k_desc_normalize(const uint32_t* __restrict__ n_feat_dev,
+                                                        float* __restrict__ desc) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t n = *n_feat_dev;
+    for (uint32_t e = blockIdx.x * 4 + (threadIdx.x >> 6); e < n; e += gridDim.x * 4) {
+        float2* p = reinterpret_cast<float2*>(desc + (size_t)e * 128) + lane;
+        float2 b = *p;
+        float s = fma_(b.x, b.x, b.y * b.y);
+#pragma unroll
+        for (int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k, 64);
+        const float n1 = __builtin_amdgcn_rsqf(s);
+        b.x = fmin_(0.2f, b.x * n1);
+        b.y = fmin_(0.2f, b.y * n1);
+        s = fma_(b.x, b.x, b.y * b.y);
+#pragma unroll
+        for (int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k, 64);
+        const float n2 = __builtin_amdgcn_rsqf(s);
+        *p = make_float2(b.x * n2, b.y * n2);
+    }
 }
 
 // One wave per feature, grid-stride over the features (count read on the device).
@@ -3108,12 +3164,30 @@ hipError_t launch_orient_keys(const float* pyr, float4* feat, const int2* feat_i
     return hipGetLastError();
 }
 
+// up to this many features (from the previous call's count) the descriptor can run two waves per
+// feature (k_descriptor_half + k_desc_normalize): opt-in with SGPU_DESC_HALF=1 (not yet measured
+// on the GPU)
+static constexpr int kHalfDescriptorMax = 16384;
 hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* feat_info,
                              const uint32_t* n_feat_dev, int n_feat_cap, const FeatureParams& fp,
                              float* desc, hipStream_t stream, const int* out_index,
                              bool rect, bool exact) {
     if (n_feat_cap <= 0) return hipSuccess;
     const unsigned grid = (unsigned)std::min(((long long)n_feat_cap + 3) / 4, 65536LL);
+    static const bool use_half = [] {
+        const char* e = getenv("SGPU_DESC_HALF");
+        return e && !strcmp(e, "1");
+    }();
+    if (!exact && !rect && !out_index && n_feat_cap <= kHalfDescriptorMax && use_half) {
+        // few features (the grid comes from the previous call's count): two waves per feature
+        const unsigned g2 = (unsigned)((2LL * n_feat_cap + 3) / 4);
+        hipLaunchKernelGGL(k_descriptor_half, dim3(g2), dim3(256), 0, stream, pyr, feat,
+                           feat_info, n_feat_dev, fp, desc);
+        if (fp.normalize)
+            hipLaunchKernelGGL(k_desc_normalize, dim3(grid), dim3(256), 0, stream, n_feat_dev,
+                               desc);
+        return hipGetLastError();
+    }
     if (!exact) {
         if (rect)
             hipLaunchKernelGGL(k_descriptor_fast<true>, dim3(grid), dim3(256), 0, stream, pyr,
