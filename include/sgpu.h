@@ -249,7 +249,7 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
                                    creation by the environment variable SGPU_EXACT_DESCRIPTOR=1 */
 #define SGPU_DEBUG_GAUSS_BLOCK 32 /* Gaussian levels through the workgroup strip kernel
                                    (k_gauss_pk2) instead of the shipped wave-streaming one
-                                   (k_gauss_wave); both are bit-identical.  Bits 16.. of the
+                                   (k_gauss_lean); both are bit-identical.  Bits 16.. of the
                                    flags, when not 0, force the wave kernel's band height in
                                    rows (test / tuning hook)                              */
 #define SGPU_DEBUG_KEYED_MATCH 64 /* plain matching through the keyed epilogue (every value
@@ -257,13 +257,10 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
                                    ratiomax <= 1, where the keyless one is exact and used     */
 #define SGPU_DEBUG_FULL_COLUMNS 128 /* plain mutual matching decides every column of set 2, not
                                    only the columns some row of set 1 matched                 */
-#define SGPU_DEBUG_GAUSS_WAVE1 256 /* Gaussian levels through k_gauss_wave (round 2's wave-streaming
-                                     kernel) instead of k_gauss_lean: same levels, bit for bit */
+/* 256: retired (round 2's k_gauss_wave, removed from the library in round 4) */
 #define SGPU_DEBUG_ORIENT_WAVE 512 /* orientation one wave per candidate for any count (the shipped
                                      path picks it for few candidates only): same bits */
-#define SGPU_DEBUG_GAUSS_PAIR 1024 /* two Gaussian levels per launch (k_gauss_pair) where the
-                                      widths have a compiled pair: same levels, bit for bit;
-                                      measured slower than one level per launch */
+/* 1024: retired (the two-level k_gauss_pair, measured slower, removed in round 4) */
 #define SGPU_DEBUG_MATCH_REGSTAGE 2048 /* keyless plain matching through the register-staged
                                           k_match_rows<..., RAW> instead of the LDS-DMA
                                           k_match_raw: same pairs */

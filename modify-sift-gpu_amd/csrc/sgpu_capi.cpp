@@ -359,8 +359,6 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     // A/B hook for the Gaussian kernels (bench / probe runs in one process tree)
     if (const char* ev = getenv("SGPU_GAUSS")) {
         if (!strcmp(ev, "block")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_BLOCK;
-        else if (!strcmp(ev, "wave")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_WAVE1;
-        else if (!strcmp(ev, "pair")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_PAIR;
     }
     if (const char* ev = getenv("SGPU_PYR")) {
         if (!strcmp(ev, "serial")) ctx->debug_flags |= SGPU_DEBUG_PYR_SERIAL;
@@ -559,39 +557,13 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
             const float* tk = k == 0 ? taps0.k : ltaps[k].k;
             for (int i = 0; i < fwk; i++) taps.k[i] = tk[i];
             const bool dk = ds && kds == k;
-            // test hook SGPU_DEBUG_GAUSS_PAIR: ops k and k+1 in one launch (k_gauss_pair) when
-            // their widths have a compiled pair,
-            // op k does not feed the next octave (only the second level of a pair decimates),
-            // and op k does not read the buffer op k+1 writes (-fo != 0 stages its resampled
-            // input in level 1's storage)
-            const float* src_k = k == 0 ? in_f : lvl0 + (k - 1) * od.level_stride;
-            const uint8_t* src8_k = k == 0 ? in_8 : nullptr;
-            const int stride_k = k == 0 ? in_stride : od.wa;
-            const long long img_k = k == 0 ? in_img : npx;
-            if (k + 1 < nlev && kds != k && (ctx->debug_flags & SGPU_DEBUG_GAUSS_PAIR) &&
-                !(ctx->debug_flags & (SGPU_DEBUG_GAUSS_BLOCK | SGPU_DEBUG_GAUSS_WAVE1)) &&
-                !(o == 0 && k == 0 && ctx->plan.octave_min != 0) &&
-                sgk::gauss_pair_supported(fwk, lfw[k + 1], stride_k, img_k, od.wa,
-                                          src8_k ? (const void*)src8_k : (const void*)src_k)) {
-                const bool dk1 = ds && kds == k + 1;
-                HIPCHK(ctx, sgk::launch_gauss_pair(src_k, src8_k, stride_k, img_k,
-                                                   lvl0 + k * od.level_stride,
-                                                   lvl0 + (k + 1) * od.level_stride, npx, od.wa,
-                                                   od.h, fwk, taps, lfw[k + 1], ltaps[k + 1], n,
-                                                   dk1 ? ds : nullptr, dk1 ? dsw : 0,
-                                                   dk1 ? dsh : 0, dk1 ? ds_stride : 0, so));
-                if (side && o == 0 && dk1) HIPCHK(ctx, hipEventRecord(pt.ev_ds, st));
-                k++;
-                continue;
-            }
             HIPCHK(ctx, sgk::launch_gauss(k == 0 ? in_f : lvl0 + (k - 1) * od.level_stride,
                                           k == 0 ? in_8 : nullptr, k == 0 ? in_stride : od.wa,
                                           k == 0 ? in_img : npx, lvl0 + k * od.level_stride,
                                           npx, od.wa, od.h, fwk, taps, n, dk ? ds : nullptr,
                                           dk ? dsw : 0, dk ? dsh : 0, dk ? ds_stride : 0, so,
                                           (ctx->debug_flags & SGPU_DEBUG_GAUSS_BLOCK)
-                                              ? -1 : (ctx->debug_flags >> 16),
-                                          !(ctx->debug_flags & SGPU_DEBUG_GAUSS_WAVE1)));
+                                              ? -1 : (ctx->debug_flags >> 16)));
             if (side && o == 0 && dk) HIPCHK(ctx, hipEventRecord(pt.ev_ds, st));
         }
     }
@@ -714,6 +686,7 @@ static int abandon_batch(sgpu_ctx* ctx, int rc) {
     for (Part& pt : ctx->part) {
         if (pt.stream) (void)hipStreamSynchronize(pt.stream);
         if (pt.stream_lo) (void)hipStreamSynchronize(pt.stream_lo);
+        if (pt.stream_oct) (void)hipStreamSynchronize(pt.stream_oct);
         pt.img_off.clear();
     }
     ctx->batch = 0;
@@ -722,8 +695,10 @@ static int abandon_batch(sgpu_ctx* ctx, int rc) {
     return rc;
 }
 
-static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, int w, int h,
-                        int stride, int flags, int color) {
+// Argument checks of sgpu_extract*: a rejected call queues nothing and leaves the previous
+// extract's results readable.
+static int check_extract_args(sgpu_ctx* ctx, const void* images, bool is_f32, int n, int w, int h,
+                              int stride, int flags, int color) {
     const bool staged = (flags & SGPU_INPUT_STAGED) != 0;
     const int channels = color == SGPU_RGB || color == SGPU_BGR ? 3 : color ? 4 : 1;
     if ((!images && !staged) || n <= 0 || w < 8 || h < 8 || stride < w * channels)
@@ -732,6 +707,13 @@ static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
         return ctx->fail(SGPU_EINVAL, "bad color input");
     if (staged && (is_f32 || ctx->staged_bytes < (size_t)n * h * stride))
         return ctx->fail(SGPU_EINVAL, "staged input does not match the batch");
+    return SGPU_OK;
+}
+
+static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, int w, int h,
+                        int stride, int flags, int color) {
+    const bool staged = (flags & SGPU_INPUT_STAGED) != 0;
+    const int channels = color == SGPU_RGB || color == SGPU_BGR ? 3 : color ? 4 : 1;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     int rc0 = plan_batch(ctx, n, w, h);
     if (rc0 != SGPU_OK) return rc0;
@@ -861,6 +843,8 @@ static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
 static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, int w, int h,
                         int stride, int flags, int color = 0) {
     if (!ctx) return SGPU_EINVAL;
+    const int rc_args = check_extract_args(ctx, images, is_f32, n, w, h, stride, flags, color);
+    if (rc_args != SGPU_OK) return rc_args;
     const int rc = extract_body(ctx, images, is_f32, n, w, h, stride, flags, color);
     return rc == SGPU_OK ? rc : abandon_batch(ctx, rc);
 }

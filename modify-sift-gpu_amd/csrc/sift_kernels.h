@@ -42,26 +42,14 @@ struct FeatureParams {
 // src_u8 != nullptr selects the ingest variant (src value = u8 / 255.0f).  src_stride is the
 // row stride in elements of whichever source is used.
 // ds_dst != nullptr additionally writes the 2x point-downsampled output (next octave level 0).
-// wave_rows < 0: the workgroup strip kernel (k_gauss_pk2); >= 0: the wave-streaming kernels
-// with bands of wave_rows rows (0: chosen from the grid size) -- k_gauss_lean (lean, FW <= 25)
-// or k_gauss_wave.  All give bit-identical levels; unaligned sources always take k_gauss_pk2.
+// wave_rows < 0: the workgroup strip kernel (k_gauss_pk2); >= 0: the wave-streaming level
+// kernel k_gauss_lean (FW <= 33) with bands of wave_rows rows (0: chosen from the grid size).
+// Both give bit-identical levels; unaligned sources always take k_gauss_pk2.
 hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         long long src_img_stride, float* dst, long long dst_img_stride,
                         int w, int h, int fw, const Taps& taps, int batch,
                         float* ds_dst, int ds_w, int ds_h, long long ds_img_stride,
-                        hipStream_t stream, int wave_rows = -1, bool lean = true);
-
-// Two levels per launch (k_gauss_pair): dst_a = V(H(src)) with taps_a, dst_b = V(H(dst_a))
-// with taps_b (+ the 2x decimation of dst_b into ds_dst when given), bit-identical to two
-// launch_gauss calls; level a is written once and never read back.  Compiled for the width pairs
-// of the default schedule: gauss_pair_supported() says whether a call can take it.
-bool gauss_pair_supported(int fw_a, int fw_b, int src_stride, long long src_img_stride, int w,
-                          const void* src);
-hipError_t launch_gauss_pair(const float* src, const uint8_t* src_u8, int src_stride,
-                             long long src_img_stride, float* dst_a, float* dst_b,
-                             long long dst_img_stride, int w, int h, int fw_a, const Taps& taps_a,
-                             int fw_b, const Taps& taps_b, int batch, float* ds_dst, int ds_w,
-                             int ds_h, long long ds_img_stride, hipStream_t stream);
+                        hipStream_t stream, int wave_rows = -1);
 
 // First octave of -fo != 0 (BuildPyramid, PyramidCU.cpp:1011-1016): the batch's input
 // (u8 p/255 or f32; tw = w & ~3 columns used, rows `stride` apart) resampled into dst

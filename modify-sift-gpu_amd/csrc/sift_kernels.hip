@@ -267,21 +267,22 @@ __global__ __launch_bounds__(256) void k_gauss_pk2(
 }
 
 // ------------------------------------------------------------------------------------------
-// Gaussian level, wave-streaming form: the same H-then-V filter as k_gauss_pk2 (same taps, same
-// summation order i = 0..FW-1, so bit-identical outputs), but every WAVE owns a 64-column strip
-// band and walks it on its own with a wave-private LDS row-pair buffer and H ring -- no
-// workgroup barriers, so each wave keeps its row loads in flight independently of the other
-// waves of its workgroup (the extremum kernel gained 3.9 -> 5.9 TB/s from the same change).
-// Per step a wave:
+// Gaussian level, wave-streaming form (k_gauss_lean below): the same H-then-V filter as
+// k_gauss_pk2 (same taps, same summation order i = 0..FW-1, so bit-identical outputs), but every
+// WAVE owns a 64-column strip band and walks it on its own with a wave-private LDS row-pair buffer
+// and H ring -- no workgroup barriers, so each wave keeps its row loads in flight independently
+// of the other waves of its workgroup (the extremum kernel gained 3.9 -> 5.9 TB/s from the same
+// change).  Per step a wave:
 //   * H-filters input chunk c (8 rows: 4 row pairs x 16 lanes x 4 columns, packed FMAs) from
 //     the row-pair buffer into ring rows 8c .. 8c+7;
 //   * V-filters output chunk c - L (L = ceil((FW-1)/8) chunks of lag: 2 row groups x 32 lanes
 //     x 2 columns x 4 rows) from the ring and stores it (plus the decimated next-octave level);
 //   * moves input chunk c+1 from registers into the row-pair buffer and issues the loads of
-//     chunk c+2.
+//     chunk c+4.
 // LDS ops of one wave execute in issue order, so a wave needs no barrier between writing a
 // buffer and reading what other lanes wrote; the empty asm statements only stop the compiler
-// from moving LDS accesses across the phase boundaries.
+// from moving LDS accesses across the phase boundaries.  Every LDS access of a wave stays inside
+// its own buffers (round 3's pad-slot overrun, fixed in k_gauss_lean's loaders).
 // XCD-aware block order: blocks are dealt round-robin over the 8 XCDs (observed placement,
 // MI355X_MICROARCH.md; speed only, never correctness), so logical block xcd * q + k runs on XCD
 // xcd and a run of consecutive logical blocks -- neighbouring image regions -- shares one L2.
@@ -302,239 +303,9 @@ struct GaussWaveGrid {
 #ifndef SGK_GW_HSPAD
 #define SGK_GW_HSPAD 4
 #endif
-constexpr int kGwWaves = SGK_GW_WPB;   // waves per workgroup of k_gauss_wave
+constexpr int kGwWaves = SGK_GW_WPB;   // waves per workgroup of k_gauss_lean
 
-template <int FW, bool U8, int NW>
-__global__ __launch_bounds__(64 * kGwWaves) void k_gauss_wave(
-    const float* __restrict__ src, const uint8_t* __restrict__ src8, int src_stride,
-    long long src_img_stride, float* __restrict__ dst, long long dst_img_stride, int W, int H,
-    Taps taps, float* __restrict__ ds, int dsw, int dsh, long long ds_img_stride,
-    GaussWaveGrid gg) {
-    constexpr int HALF = FW >> 1;
-    constexpr int OFF = (-HALF) & 3;                  // LDS column of the strip's first input
-    constexpr int SW = GT * NW;                       // columns loaded per strip
-    constexpr int IN_W = SW + FW - 1 + OFF;           // input columns held per row
-    constexpr int NQ = (IN_W + 3) / 4;                // aligned quads per row
-    constexpr int NRD = (FW + 3) / 2;                 // ds_read_b128 per H-pass lane
-    // LDS layout of a row pair: input column a0 + j at float2 index j + SH, SH = OFF & 1, so
-    // that every H-pass read (index 4 l + OFF + SH + 2 q) is a 16-byte aligned ds_read_b128; the
-    // row-pair stride is = 2 (mod 32) float2, so that the 16 lanes of one row pair and the lanes
-    // of the next one fill disjoint 16-byte bank slots (ds_read_b128 lane groups, LDS table of
-    // MI355X_MICROARCH.md): measured 2-way bank conflicts with the plain stride
-    constexpr int SH = OFF & 1;
-    constexpr int IN_S0 = (4 * NQ + SH + 3) & ~3;
-    constexpr int IN_S = IN_S0 + ((2 - IN_S0) & 31);  // float2 per row pair
-    static_assert(IN_S % 32 == 2 && 4 * NQ + SH <= IN_S, "row-pair stride");
-    constexpr int LAG = (FW - 1 + WCH - 1) / WCH;     // chunks between H and V of a row
-    constexpr int RS0 = WCH * (LAG + 1);
-    constexpr int RS = RS0 <= 32 ? 32 : 64;           // ring rows (power of two)
-    static_assert(RS0 <= RS, "ring holds the lag");
-    constexpr int HS = GT + SGK_GW_HSPAD;             // ring row stride (floats)
-    constexpr int NPAIR = WCH / 2;
-    constexpr int NLD = (NPAIR * NQ + 64 * NW - 1) / (64 * NW);   // staged quads per lane
-#ifndef SGK_GW_NST
-#define SGK_GW_NST 4
-#endif
-    constexpr int NST = SGK_GW_NST;                   // chunks in registers (loads NST-1 ahead)
-    static_assert(NW == 1 || NW == kGwWaves, "one strip per wave, or one per workgroup");
-    static_assert(NW == 1 || NST % 2 == 0, "shared input buffers alternate by step parity");
-    // NW == 1: a wave-private row-pair buffer per wave; NW > 1: the NW waves of a workgroup
-    // share one double-buffered buffer of their NW * 64 columns
-    constexpr int NBUF = NW == 1 ? kGwWaves : 2;
-    __shared__ __attribute__((aligned(16))) f2v s_in_all[NBUF][NPAIR * IN_S + 4];   // + pad slot
-    __shared__ __attribute__((aligned(16))) float s_h_all[kGwWaves][RS * HS];
-
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int ld = NW == 1 ? lane : threadIdx.x;     // index among the strip's loaders
-    int sx, rest, x0, xs;                            // xs: first column of the loaded strip
-    if (NW == 1) {
-        // XCD-aware order: blocks are dealt round-robin over the 8 XCDs (observed placement;
-        // speed only), so logical block (xcd, k) -> xcd * q + k keeps neighbouring strips and
-        // their column halos in one L2 (pyramid 3.80-3.84 -> 3.76-3.79 ms)
-        const int gw = xcd_block(blockIdx.x, gridDim.x) * kGwWaves + wave;
-        if (gw >= gg.total_waves) return;             // uniform per wave
-        sx = gw % gg.strips_x;
-        rest = gw / gg.strips_x;
-        xs = x0 = sx * GT;
-    } else {
-        sx = blockIdx.x % gg.strips_x;                // strips of NW * 64 columns
-        rest = blockIdx.x / gg.strips_x;
-        xs = sx * SW;
-        x0 = xs + GT * wave;
-    }
-    float* s_h = s_h_all[wave];
-    const int sy = rest % gg.nsy, b = rest / gg.nsy;
-    const int yb = sy * gg.rows_per_band;
-    const int ye = min(H, yb + gg.rows_per_band);
-    const int nchunk_out = (ye - yb + WCH - 1) / WCH;
-
-    const float* sf = U8 ? nullptr : src + (long long)b * src_img_stride;
-    const uint8_t* s8 = U8 ? src8 + (long long)b * src_img_stride : nullptr;
-    const int a0 = xs - HALF - OFF;
-    // a staged element is the raw fetch of one aligned quad of rows 2p, 2p+1; the u8 -> f32
-    // conversion and the clamp-to-edge selects happen when it is written to LDS, so that nothing
-    // consumes the registers right after the loads are issued (the compiler would wait for them
-    // there, one step early, and the prefetch would hide nothing)
-    struct Elem { float4 v0, v1; };
-    Elem st[NST][NLD];
-    auto load_chunk = [&](Elem (&stage)[NLD], int c) {
-#pragma unroll
-        for (int m = 0; m < NLD; m++) {
-            const int e = min(ld + 64 * NW * m, NPAIR * NQ - 1);
-            const int p = e / NQ, j = e - p * NQ;
-            const int gy0 = clampi(yb - HALF + c * WCH + 2 * p, 0, H - 1);
-            const int gy1 = clampi(yb - HALF + c * WCH + 2 * p + 1, 0, H - 1);
-            const int lq = clampi(a0 + 4 * j, 0, W - 4);          // aligned first column
-            if (U8) {
-                stage[m].v0.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(s8 + (long long)gy0 * src_stride + lq));
-                stage[m].v1.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(s8 + (long long)gy1 * src_stride + lq));
-            } else {
-                stage[m].v0 = *reinterpret_cast<const float4*>(sf + (long long)gy0 * src_stride + lq);
-                stage[m].v1 = *reinterpret_cast<const float4*>(sf + (long long)gy1 * src_stride + lq);
-            }
-        }
-    };
-    // every lane writes every staged element (lanes past the chunk's last quad write a pad
-    // slot): a lane-conditional write would leave the registers "maybe pending" on the skip
-    // path, and the next load into them would wait for everything in flight
-    auto store_chunk = [&](const Elem (&stage)[NLD], f2v* s_in) {
-#pragma unroll
-        for (int m = 0; m < NLD; m++) {
-            const int e = ld + 64 * NW * m;
-            {
-                const bool real = e < NPAIR * NQ;
-                const int p = e / NQ, j = e - p * NQ;
-                const int gq = a0 + 4 * j;
-                float r0[4], r1[4];
-                if (U8) {
-                    const uint32_t w0 = __float_as_uint(stage[m].v0.x), w1 = __float_as_uint(stage[m].v1.x);
-#pragma unroll
-                    for (int t = 0; t < 4; t++) {
-                        r0[t] = u8_to_unit((w0 >> (8 * t)) & 255u);
-                        r1[t] = u8_to_unit((w1 >> (8 * t)) & 255u);
-                    }
-                } else {
-                    r0[0] = stage[m].v0.x; r0[1] = stage[m].v0.y; r0[2] = stage[m].v0.z; r0[3] = stage[m].v0.w;
-                    r1[0] = stage[m].v1.x; r1[1] = stage[m].v1.y; r1[2] = stage[m].v1.z; r1[3] = stage[m].v1.w;
-                }
-                // clamp-to-edge: a quad left of column 0 repeats column 0, right of W-1 repeats W-1
-                const bool left = gq < 0, right = gq > W - 4;
-                float u0[4], u1[4];
-#pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    u0[t] = left ? r0[0] : (right ? r0[3] : r0[t]);
-                    u1[t] = left ? r1[0] : (right ? r1[3] : r1[t]);
-                }
-                f2v* q = &s_in[real ? p * IN_S + 4 * j + SH : NPAIR * IN_S];
-                if (SH == 0) {
-                    reinterpret_cast<float4*>(q)[0] = make_float4(u0[0], u1[0], u0[1], u1[1]);
-                    reinterpret_cast<float4*>(q)[1] = make_float4(u0[2], u1[2], u0[3], u1[3]);
-                } else {   // 8-byte aligned
-#pragma unroll
-                    for (int t = 0; t < 4; t++) q[t] = f2v{u0[t], u1[t]};
-                }
-            }
-        }
-    };
-
-#pragma unroll
-    for (int k = 0; k < NST; k++) load_chunk(st[k], k);
-    store_chunk(st[0], s_in_all[NW == 1 ? wave : 0]);
-    if (NW > 1) __syncthreads();
-    float* d = dst + (long long)b * dst_img_stride;
-    float* dd = ds ? ds + (long long)b * ds_img_stride : nullptr;
-    const int hp = lane >> 4, hc = (lane & 15) * 4;    // H pass: rows 2hp, 2hp+1; columns hc..hc+3
-    const int vq = lane >> 5, vc = (lane & 31) * 2;    // V pass: rows 4vq..4vq+3; columns vc, vc+1
-    const int x = x0 + vc;
-    // Loads, the H pass and the LDS store run unconditionally (past the band's last input
-    // chunk they fetch clamped rows and fill ring rows no output reads): with a conditional
-    // load block the compiler's wait counting must assume no loads were issued after `cur`'s
-    // and waits for everything in flight before storing `cur`.
-    // Order inside a step: H pass, V pass + its global stores, THEN the loads of chunk c+2,
-    // then `cur` (chunk c+1, loaded a step ago) into LDS.  The wait before that LDS store then
-    // leaves the 4 loads just issued in flight (only older ops are waited for); loads issued
-    // before the (branchy, variable-count) stores would be waited for too.
-    const bool active = x0 < W;                      // a wave right of the image only loads
-    auto step = [&](int c, Elem (&cur)[NLD], Elem (&nxt)[NLD], int par) {
-        f2v* s_in = s_in_all[NW == 1 ? wave : par];
-        f2v* s_in_next = s_in_all[NW == 1 ? wave : 1 - par];
-        {   // H pass of input chunk c -> ring rows c*WCH .. c*WCH+7
-            const f2v* rowp = &s_in[hp * IN_S + hc + OFF + SH + (NW == 1 ? 0 : GT * wave)];
-            f2v a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};   // columns hc+i
-#pragma unroll
-            for (int q = 0; q < NRD; q++) {
-                f2v e[2];                            // pair columns hc+2q, hc+2q+1
-                {
-                    const float4 v = reinterpret_cast<const float4*>(rowp)[q];
-                    e[0] = f2v{v.x, v.y};
-                    e[1] = f2v{v.z, v.w};
-                }
-#pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    const int m = 2 * q + u;
-#pragma unroll
-                    for (int i = 0; i < 4; i++)
-                        if (m - i >= 0 && m - i < FW) a[i] = pk_fma(e[u], taps.k[m - i], a[i]);
-                }
-            }
-            const int r0 = (c * WCH + 2 * hp) & (RS - 1);
-            *reinterpret_cast<float4*>(&s_h[r0 * HS + hc]) = make_float4(a[0].x, a[1].x, a[2].x, a[3].x);
-            *reinterpret_cast<float4*>(&s_h[(r0 + 1) * HS + hc]) = make_float4(a[0].y, a[1].y, a[2].y, a[3].y);
-        }
-        asm volatile("" ::: "memory");
-        const int kout = c - LAG;
-        if (active && kout >= 0 && kout < nchunk_out) {   // V pass of output chunk kout
-            const int t0 = kout * WCH + 4 * vq;
-            f2v acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};   // rows t0+j
-#pragma unroll
-            for (int m = 0; m < FW + 3; m++) {
-                const f2v v = *reinterpret_cast<const f2v*>(&s_h[((t0 + m) & (RS - 1)) * HS + vc]);
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    if (m - j >= 0 && m - j < FW) acc[j] = pk_fma(v, taps.k[m - j], acc[j]);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++) asm volatile("" : "+v"(acc[j]));
-            if (x < W) {
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int y = yb + t0 + j;
-                    if (y < ye) {
-                        *reinterpret_cast<f2v*>(&d[(long long)y * W + x]) = acc[j];
-                        // DownsampleKernel<1> (ProgramCU.cu:287-298), as in k_gauss_pk2
-                        if (dd && !(y & 1) && (y >> 1) < dsh) {
-                            float* drow = dd + (long long)(y >> 1) * dsw;
-                            if ((x >> 1) < dsw) drow[x >> 1] = acc[j].x;
-                            if (x + 1 == W - 1)
-                                for (int cc = W >> 1; cc < dsw; cc++) drow[cc] = acc[j].y;
-                        }
-                    }
-                }
-            }
-        }
-        asm volatile("" ::: "memory");
-        load_chunk(nxt, c + NST);
-        store_chunk(cur, s_in_next);
-        if (NW > 1) {
-            // LDS-only barrier: chunk c+1 is in the other buffer for every wave, and every wave
-            // is done reading this step's buffer (no vmcnt wait: the loads stay in flight)
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-        }
-        asm volatile("" ::: "memory");
-    };
-    // NST register stages, rotated by unrolling: step c stores chunk c+1 from st[(c+1) % NST]
-    // and loads chunk c+NST into st[c % NST].  Every step of the unrolled group runs (a
-    // conditional one would turn the stages into phis, and their copies wait for the loads in
-    // flight).
-    const int nsteps = nchunk_out + LAG;
-    for (int c = 0; c < nsteps; c += NST) {
-#pragma unroll
-        for (int k = 0; k < NST; k++) step(c + k, st[(k + 1) % NST], st[k], k & 1);
-    }
-}
-
-// band height of the wave kernel: rows_hint > 0 forces it (test / tuning hook), else bands of
+// band height of the level kernel: rows_hint > 0 forces it (test / tuning hook), else bands of
 // the whole image unless that leaves fewer than ~8 waves per CU, then as many bands as needed.
 // A band re-reads the level's FW-1 halo rows, so bands stay >= 4 chunks high while the level
 // streams from HBM; a level of at most SGK_SHORT_BAND_MB (one image of a small batch, or the
@@ -573,7 +344,7 @@ static GaussWaveGrid gauss_wave_grid(int w, int h, int batch, int rows_hint, int
 }
 
 // ------------------------------------------------------------------------------------------
-// Gaussian level, lean form (the shipped kernel for FW <= 25): k_gauss_wave's filter -- same
+// Gaussian level, lean form (the shipped kernel, FW <= 33): round 2's k_gauss_wave filter -- same
 // strips, bands, chunks, row-pair buffer, H ring and lag, the same taps in the same order, so the
 // levels are bit-identical -- with the per-step work that is not filtering taken off the vector
 // ALU.  The kernel traces showed k_gauss_wave issuing ~150 non-FMA VALU instructions per 8-row
@@ -586,8 +357,8 @@ static GaussWaveGrid gauss_wave_grid(int w, int h, int batch, int rows_hint, int
 //     so a lane's column (and its clamp) is fixed for the whole kernel, and a chunk's rows are
 //     uniform; only chunks that reach above row 0 or below row H-1 clamp per lane;
 //   * clamp-to-edge column selects only in the strips at the image's left / right edge;
-//   * the ring holds 4 chunk slots (RS = 32, LAG <= 3) and the step's slot is compile-time (the
-//     main loop is unrolled by 4), so ring reads and writes are lane-constant base + immediate
+//   * the ring holds 4 chunk slots (RS = 32, LAG <= 3; 8 slots, RS = 64, for FW 27 .. 33) and the
+//     step's slot is compile-time (the main loop is unrolled by the slot count), so ring reads and writes are lane-constant base + immediate
 //     offset; the half-wave whose rows wrap first (vq = 1, 4 rows ahead) reads through a second
 //     base for the 4 rows where only it has wrapped;
 //   * u8 -> f32 (the ingest level) on row pairs with packed multiply / fma;
@@ -609,17 +380,19 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
     constexpr int IN_S = IN_S0 + ((2 - IN_S0) & 31);  // float2 per row pair (= 2 mod 32)
     static_assert(IN_S % 32 == 2 && 4 * NQ + SH <= IN_S, "row-pair stride");
     constexpr int LAG = (FW - 1 + WCH - 1) / WCH;     // chunks between H and V of a row
-    static_assert(WCH * (LAG + 1) <= 32, "the ring's 4 chunk slots hold the lag");
-    constexpr int RS = 32;                            // ring rows: 4 slots of WCH
+    // ring rows: 4 slots of WCH for FW <= 25, 8 slots for FW 27 .. 33 (LAG 4)
+    constexpr int RS = WCH * (LAG + 1) <= 32 ? 32 : 64;
+    constexpr int NSLOT = RS / WCH;
+    static_assert(WCH * (LAG + 1) <= RS && FW <= 33, "the ring's chunk slots hold the lag");
     constexpr int HS = GT + SGK_GW_HSPAD;             // ring row stride (floats)
     constexpr int NPAIR = WCH / 2;
-    constexpr int NST = 4;                            // chunks in registers = ring slots
-    __shared__ __attribute__((aligned(16))) f2v s_in_all[kGwWaves][NPAIR * IN_S + 4];   // + pad slot
+    constexpr int NST = 4;                            // chunks in registers
+    __shared__ __attribute__((aligned(16))) f2v s_in_all[kGwWaves][NPAIR * IN_S + 8];   // + 2 pad slots
     __shared__ __attribute__((aligned(16))) float s_h_all[kGwWaves][RS * HS];
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // XCD-aware order as in k_gauss_wave
+    // XCD-aware order (xcd_block)
     const int gw = xcd_block(blockIdx.x, gridDim.x) * kGwWaves + wave;
     if (gw >= gg.total_waves) return;                 // uniform per wave
     const int sx = gw % gg.strips_x, rest = gw / gg.strips_x;
@@ -644,7 +417,14 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
     const bool edge = a0 < 0 || a0 + 4 * NQ > W;      // uniform: this strip clamps columns
     // element offsets of the lane's quad in rows 2 g and 2 g + 1 of a row group
     const uint32_t loff0 = (uint32_t)(2 * lg * src_stride + lq), loff1 = loff0 + (uint32_t)src_stride;
-    const int s_off = lreal ? lg * IN_S + 4 * lj + SH : NPAIR * IN_S;   // LDS float2 index
+    // LDS float2 index of the lane's quad in row pairs lg (m = 0) and lg + 2 (m = 1); a lane past
+    // the row's last quad stores into its own pad slot per m.  (Round 3 used one pad slot and
+    // added the m = 1 pair offset to it too: those stores landed 2 IN_S float2 past the wave's
+    // buffer -- in the next wave's row-pair padding, or past the workgroup's LDS for the last
+    // wave -- harmless only by layout; the same pattern made k_gauss_pair's aliased mid buffer
+    // nondeterministic)
+    const int s_off0 = lreal ? lg * IN_S + 4 * lj + SH : NPAIR * IN_S;
+    const int s_off1 = lreal ? s_off0 + 2 * IN_S : NPAIR * IN_S + 4;
 
     struct Elem { float4 v0, v1; };   // the raw fetch of rows 2p, 2p+1 (u8: .x as the u32)
     Elem st[NST][2];
@@ -705,7 +485,7 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
 #pragma unroll
                 for (int t = 0; t < 4; t++) pr[t] = left ? e0 : (right ? e3 : pr[t]);
             }
-            f2v* q = s_in + s_off + 2 * m * IN_S;
+            f2v* q = s_in + (m ? s_off1 : s_off0);
             if (SH == 0) {
                 reinterpret_cast<float4*>(q)[0] = make_float4(pr[0].x, pr[0].y, pr[1].x, pr[1].y);
                 reinterpret_cast<float4*>(q)[1] = make_float4(pr[2].x, pr[2].y, pr[3].x, pr[3].y);
@@ -756,7 +536,7 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
         asm volatile("" ::: "memory");
         const int kout = c - LAG;
         if (active && kout >= 0 && kout < nchunk_out) {   // V pass of output chunk kout (uniform)
-            constexpr int KV = (K - LAG) & 3;                // its ring slot
+            constexpr int KV = (K - LAG) & (NSLOT - 1);      // its ring slot
             f2v acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};   // rows t0+j
 #pragma unroll
             for (int m = 0; m < FW + 3; m++) {
@@ -806,418 +586,30 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
         asm volatile("" ::: "memory");
     };
     const int nsteps = nchunk_out + LAG;
-    for (int c = 0; c < nsteps; c += NST) {
+    // slot K = c mod NSLOT, register set c mod NST (steps past the end filter clamped rows and
+    // store nothing)
+    for (int c = 0; c < nsteps; c += NSLOT) {
         step(c + 0, std::integral_constant<int, 0>{}, st[1], st[0]);
         step(c + 1, std::integral_constant<int, 1>{}, st[2], st[1]);
         step(c + 2, std::integral_constant<int, 2>{}, st[3], st[2]);
         step(c + 3, std::integral_constant<int, 3>{}, st[0], st[3]);
-    }
-}
-
-// ------------------------------------------------------------------------------------------
-// Two Gaussian levels per launch (level k -> k+1 -> k+2), wave-streaming: moves fewer bytes than
-// two level launches -- level k+1 is written once and never read back (the second filter takes
-// it from LDS): 12 B per pixel for two f32 levels instead of 16, 9 instead of 13 for the u8 ingest
-// pair (input -> level 0 -> level 1).  Each wave owns a 64-column strip band as in k_gauss_lean:
-//   stage A (level k+1): the H pass on the input chunk into ring A and the V pass from it, over
-//     the strip plus the second filter's halo (MW = 64 + 2 A2 columns, A2 = HALF_B rounded up to
-//     4); its own 64 columns go to HBM, all MW columns to the mid row-pair buffer (its own LDS:
-//     a mid buffer aliased onto the input row-pair buffer measured nondeterministic level-B
-//     differences on gfx950, r03 tests/diag/pair_diff2.py), mid columns left of 0 / right of W-1 replaced by columns 0 / W-1
-//     (FilterH's clamp-to-edge on level k+1);
-//   stage B (level k+2): k_gauss_lean's H pass on the mid rows into ring B, and its V pass, which
-//     reads the mid rows clamped to 0 .. H-1 (FilterV's clamp on level k+1) -- the mid stream has
-//     a row per stream position, the rows outside the image are never read.
-// Same taps in the same order as the level kernels: bit-identical levels.
-#ifndef SGK_GP_WAVES
-#define SGK_GP_WAVES 2
-#endif
-constexpr int kGpWaves = SGK_GP_WAVES;   // waves per workgroup of k_gauss_pair
-
-template <int FWA, int FWB, bool U8, bool DSB>
-__global__ __launch_bounds__(64 * kGpWaves) void k_gauss_pair(
-    const float* __restrict__ src, const uint8_t* __restrict__ src8, int src_stride,
-    long long src_img_stride, float* __restrict__ dstA, float* __restrict__ dstB,
-    long long dst_img_stride, int W, int H, Taps tapsA, Taps tapsB, float* __restrict__ ds,
-    int dsw, int dsh, long long ds_img_stride, GaussWaveGrid gg) {
-    constexpr int HA = FWA >> 1, HB = FWB >> 1;
-    constexpr int OFFB = (-HB) & 3;
-    constexpr int A2 = HB + OFFB;                     // mid halo per side (multiple of 4)
-    constexpr int MW = GT + 2 * A2;                   // mid columns per strip
-    constexpr int OFFA = (-HA) & 3;
-    constexpr int IN_WA = MW + FWA - 1 + OFFA;        // input columns per row
-    constexpr int NQA = (IN_WA + 3) / 4;
-    static_assert(NQA <= 32, "a row's quads fit half a wave");
-    constexpr int SHA = OFFA & 1;
-    constexpr int IN_SA0 = (4 * NQA + SHA + 3) & ~3;
-    constexpr int IN_SA = IN_SA0 + ((2 - IN_SA0) & 31);
-    constexpr int SHB = OFFB & 1;                     // mid LDS index j + SHB <-> mid column m0 + j
-    constexpr int IN_SB0 = (MW + SHB + 3) & ~3;
-    constexpr int IN_SB = IN_SB0 + ((2 - IN_SB0) & 31);
-    constexpr int NRDA = (FWA + 3) / 2, NRDB = (FWB + 3) / 2;
-    constexpr int LAGA = (FWA - 1 + WCH - 1) / WCH, LAGB = (FWB - 1 + WCH - 1) / WCH;
-    static_assert(WCH * (LAGA + 1) <= 32 && WCH * (LAGB + 1) <= 32, "4 ring slots");
-    constexpr int RS = 32;
-    constexpr int HSA = MW + 4, HSB = GT + SGK_GW_HSPAD;
-    constexpr int NPAIR = WCH / 2;
-    constexpr int NGA = MW / 4, NTA = NPAIR * NGA;    // stage-A H tasks (2 rows x 4 columns)
-    constexpr int NVA = MW / 2, NTV = 2 * NVA;        // stage-A V tasks (4 rows x 2 columns)
-    static_assert(NTA <= 128 && NTV <= 128, "two rounds of 64 lanes");
-    constexpr int NST = 4;
-    constexpr int SIN = NPAIR * IN_SA + 4 + NPAIR * IN_SB;   // input pairs, then mid pairs
-    __shared__ __attribute__((aligned(16))) f2v s_in_all[kGpWaves][SIN];
-    __shared__ __attribute__((aligned(16))) float s_ha_all[kGpWaves][RS * HSA];
-    __shared__ __attribute__((aligned(16))) float s_hb_all[kGpWaves][RS * HSB];
-
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int gw = xcd_block(blockIdx.x, gridDim.x) * kGpWaves + wave;
-    if (gw >= gg.total_waves) return;
-    const int sx = gw % gg.strips_x, rest = gw / gg.strips_x;
-    const int x0 = sx * GT, m0 = x0 - A2;
-    const int sy = rest % gg.nsy, b = rest / gg.nsy;
-    const int yb = sy * gg.rows_per_band;
-    const int ye = min(H, yb + gg.rows_per_band);
-    const int nchunk_out = (ye - yb + WCH - 1) / WCH;
-    f2v* s_in = s_in_all[wave];
-    f2v* s_mid = s_in_all[wave] + NPAIR * IN_SA + 4;
-    float* s_ha = s_ha_all[wave];
-    float* s_hb = s_hb_all[wave];
-
-    const float* sf = U8 ? nullptr : src + (long long)b * src_img_stride;
-    const uint8_t* s8 = U8 ? src8 + (long long)b * src_img_stride : nullptr;
-    const int a0 = m0 - HA - OFFA;                    // first input column (4-aligned)
-    const int ys0 = yb - HB - HA;                     // input row of stream position 0
-    // loaders: as k_gauss_lean
-    const int lg = lane >> 5, lj = min(lane & 31, NQA - 1);
-    const bool lreal = (lane & 31) < NQA;
-    const int gq = a0 + 4 * lj;
-    const int lq = clampi(gq, 0, W - 4);
-    const bool left = gq < 0, right = gq > W - 4;
-    const bool edge_in = a0 < 0 || a0 + 4 * NQA > W;
-    const uint32_t loff0 = (uint32_t)(2 * lg * src_stride + lq), loff1 = loff0 + (uint32_t)src_stride;
-    const int s_off = lreal ? lg * IN_SA + 4 * lj + SHA : NPAIR * IN_SA;
-
-    struct Elem { float4 v0, v1; };
-    Elem st[NST][2];
-    auto load_chunk = [&](Elem (&stage)[2], int c) {
-        const int rb = ys0 + WCH * c;
-        if (rb >= 0 && rb + WCH <= H) {
-#pragma unroll
-            for (int m = 0; m < 2; m++) {
-                const long long ro = (long long)(rb + 4 * m) * src_stride;
-                if (U8) {
-                    const uint8_t* r = s8 + ro;
-                    stage[m].v0.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(r + loff0));
-                    stage[m].v1.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(r + loff1));
-                } else {
-                    const float* r = sf + ro;
-                    stage[m].v0 = *reinterpret_cast<const float4*>(r + loff0);
-                    stage[m].v1 = *reinterpret_cast<const float4*>(r + loff1);
-                }
-            }
-        } else {
-#pragma unroll
-            for (int m = 0; m < 2; m++) {
-                const int y0 = clampi(rb + 4 * m + 2 * lg, 0, H - 1);
-                const int y1 = clampi(rb + 4 * m + 2 * lg + 1, 0, H - 1);
-                if (U8) {
-                    stage[m].v0.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(s8 + (long long)y0 * src_stride + lq));
-                    stage[m].v1.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(s8 + (long long)y1 * src_stride + lq));
-                } else {
-                    stage[m].v0 = *reinterpret_cast<const float4*>(sf + (long long)y0 * src_stride + lq);
-                    stage[m].v1 = *reinterpret_cast<const float4*>(sf + (long long)y1 * src_stride + lq);
-                }
-            }
+        if constexpr (NSLOT == 8) {
+            step(c + 4, std::integral_constant<int, 4>{}, st[1], st[0]);
+            step(c + 5, std::integral_constant<int, 5>{}, st[2], st[1]);
+            step(c + 6, std::integral_constant<int, 6>{}, st[3], st[2]);
+            step(c + 7, std::integral_constant<int, 7>{}, st[0], st[3]);
         }
-    };
-    auto store_chunk = [&](const Elem (&stage)[2]) {
-#pragma unroll
-        for (int m = 0; m < 2; m++) {
-            f2v pr[4];
-            if (U8) {
-                const uint32_t w0 = __float_as_uint(stage[m].v0.x), w1 = __float_as_uint(stage[m].v1.x);
-                const float c = 1.0f / 255.0f;
-#pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    const f2v x{(float)((w0 >> (8 * t)) & 255u), (float)((w1 >> (8 * t)) & 255u)};
-                    const f2v q = x * f2v{c, c};
-                    const f2v r = __builtin_elementwise_fma(-q, f2v{255.0f, 255.0f}, x);
-                    pr[t] = __builtin_elementwise_fma(r, f2v{c, c}, q);
-                }
-            } else {
-                pr[0] = f2v{stage[m].v0.x, stage[m].v1.x};
-                pr[1] = f2v{stage[m].v0.y, stage[m].v1.y};
-                pr[2] = f2v{stage[m].v0.z, stage[m].v1.z};
-                pr[3] = f2v{stage[m].v0.w, stage[m].v1.w};
-            }
-            if (edge_in) {
-                const f2v e0 = pr[0], e3 = pr[3];
-#pragma unroll
-                for (int t = 0; t < 4; t++) pr[t] = left ? e0 : (right ? e3 : pr[t]);
-            }
-            f2v* q = s_in + s_off + 2 * m * IN_SA;
-            if (SHA == 0) {
-                reinterpret_cast<float4*>(q)[0] = make_float4(pr[0].x, pr[0].y, pr[1].x, pr[1].y);
-                reinterpret_cast<float4*>(q)[1] = make_float4(pr[2].x, pr[2].y, pr[3].x, pr[3].y);
-            } else {
-#pragma unroll
-                for (int t = 0; t < 4; t++) q[t] = pr[t];
-            }
-        }
-    };
-
-#pragma unroll
-    for (int k = 0; k < NST; k++) load_chunk(st[k], k);
-    store_chunk(st[0]);
-    float* dA = dstA + (long long)b * dst_img_stride;
-    float* dB = dstB + (long long)b * dst_img_stride;
-    float* dd = DSB ? ds + (long long)b * ds_img_stride : nullptr;
-    // stage-A lane tasks, two rounds (round 1: lanes past the last task repeat it and store nothing)
-    int haR[2], haW[2], vaR[2], vaRa[2], vaM[2], vaC[2], vaQ[2];
-    bool vaOut[2], vaAny[2];
-#pragma unroll
-    for (int rd = 0; rd < 2; rd++) {
-        const int t = min(lane + 64 * rd, NTA - 1);
-        const int hp = t / NGA, hc = (t - hp * NGA) * 4;
-        haR[rd] = hp * IN_SA + hc + OFFA + SHA;       // f2v index of the first H_A read
-        haW[rd] = 2 * hp * HSA + hc;                  // ring A float index of row 2hp, column hc
-        const int tv = lane + 64 * rd;
-        vaAny[rd] = tv < NTV;
-        const int tvc = min(tv, NTV - 1);
-        const int vq = tvc / NVA, vc = (tvc - vq * NVA) * 2;   // mid column m0 + vc
-        vaQ[rd] = vq;
-        vaC[rd] = vc;
-        vaR[rd] = 4 * vq * HSA + vc;
-        vaRa[rd] = vaR[rd] - (vq ? RS * HSA : 0);
-        vaM[rd] = (2 * vq) * IN_SB + vc + SHB;        // f2v index of the mid pair (rows 4vq, 4vq+1)
-        const int xo = x0 + vc - A2;                  // own output column
-        vaOut[rd] = tv < NTV && vc >= A2 && vc < A2 + GT && xo < W;
     }
-    const bool edge_mid = m0 < 0 || m0 + MW > W;      // uniform
-    // stage B lanes: as k_gauss_lean
-    const int hp = lane >> 4, hc = (lane & 15) * 4;
-    const int vq = lane >> 5, vc = (lane & 31) * 2;
-    const int x = x0 + vc;
-    const bool full_cols = x0 + GT <= W;
-    const f2v* hb_rd = s_mid + hp * IN_SB + hc + OFFB + SHB;
-    float* hb_wr = s_hb + 2 * hp * HSB + hc;
-    const float* vb_rd = s_hb + 4 * vq * HSB + vc;
-    const float* vb_rd_amb = vb_rd - (vq ? RS * HSB : 0);
-    const uint32_t st_off = (uint32_t)(4 * vq * W + x);
-    const uint32_t ds_off = (uint32_t)(2 * vq * dsw + (x >> 1));
-    const int ym0 = yb - HB;                          // mid row of mid stream position 0
-
-    auto step = [&](int c, auto KC, Elem (&cur)[2], Elem (&nxt)[2]) {
-        constexpr int K = decltype(KC)::value;
-        constexpr int KA = (K - LAGA) & 3;            // ring slot of the V_A chunk / H_B chunk
-        constexpr int KB = (K - LAGA - LAGB) & 3;     // ring-B slot of the V_B chunk
-        // ---- H_A: input chunk c -> ring A slot K
-#pragma unroll
-        for (int rd = 0; rd < 2; rd++) {
-            if (rd == 1 && NTA <= 64) break;
-            const f2v* rp = s_in + haR[rd];
-            f2v a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
-#pragma unroll
-            for (int q = 0; q < NRDA; q++) {
-                const float4 v = reinterpret_cast<const float4*>(rp)[q];
-                const f2v e[2] = {f2v{v.x, v.y}, f2v{v.z, v.w}};
-#pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    const int m = 2 * q + u;
-#pragma unroll
-                    for (int i = 0; i < 4; i++)
-                        if (m - i >= 0 && m - i < FWA) a[i] = pk_fma(e[u], tap<FWA>(tapsA, m - i), a[i]);
-                }
-            }
-            float* w = s_ha + haW[rd] + WCH * K * HSA;
-            *reinterpret_cast<float4*>(w) = make_float4(a[0].x, a[1].x, a[2].x, a[3].x);
-            *reinterpret_cast<float4*>(w + HSA) = make_float4(a[0].y, a[1].y, a[2].y, a[3].y);
-        }
-        asm volatile("" ::: "memory");
-        const int kA = c - LAGA;                      // mid chunk (uniform)
-        if (kA >= 0) {
-            // ---- V_A: mid chunk kA (stream positions 8 kA ..) from ring A slot KA
-#pragma unroll
-            for (int rd = 0; rd < 2; rd++) {
-                if (rd == 1 && NTV <= 64) break;
-                const float* vr = s_ha + vaR[rd];
-                const float* vra = s_ha + vaRa[rd];
-                f2v acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
-#pragma unroll
-                for (int m = 0; m < FWA + 3; m++) {
-                    const int rc = WCH * KA + m;
-                    const float* pp = rc < RS - 4 ? vr + rc * HSA
-                                    : rc >= RS ? vr + (rc - RS) * HSA : vra + rc * HSA;
-                    const f2v v = *reinterpret_cast<const f2v*>(pp);
-#pragma unroll
-                    for (int j = 0; j < 4; j++)
-                        if (m - j >= 0 && m - j < FWA) acc[j] = pk_fma(v, tap<FWA>(tapsA, m - j), acc[j]);
-                }
-#pragma unroll
-                for (int j = 0; j < 4; j++) asm volatile("" : "+v"(acc[j]));
-                // mid rows -> the row-pair buffer (pairs 2vq, 2vq+1), all MW columns
-                f2v* mp = s_mid + vaM[rd];
-                if (SHB == 0) {
-                    reinterpret_cast<float4*>(mp)[0] = make_float4(acc[0].x, acc[1].x, acc[0].y, acc[1].y);
-                    reinterpret_cast<float4*>(mp + IN_SB)[0] = make_float4(acc[2].x, acc[3].x, acc[2].y, acc[3].y);
-                } else {
-                    mp[0] = f2v{acc[0].x, acc[1].x};
-                    mp[1] = f2v{acc[0].y, acc[1].y};
-                    mp[IN_SB] = f2v{acc[2].x, acc[3].x};
-                    mp[IN_SB + 1] = f2v{acc[2].y, acc[3].y};
-                }
-                // level k+1: the strip's own columns, rows [yb, ye)
-                if (vaOut[rd]) {
-                    const int xo = x0 + vaC[rd] - A2;
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const int y = ym0 + WCH * kA + 4 * vaQ[rd] + j;
-                        if (y >= yb && y < ye)
-                            *reinterpret_cast<f2v*>(&dA[(long long)y * W + xo]) = acc[j];
-                    }
-                }
-            }
-            asm volatile("" ::: "memory");
-            if (edge_mid) {
-                // FilterH's clamp-to-edge on level k+1: every mid column left of 0 takes column
-                // 0, every one right of W-1 takes column W-1 (the copies never read a position
-                // that is written here)
-                const int j_lo = max(0, -m0), j_hi = min(MW, W - m0);   // in-image mid indices
-                for (int e = lane; e < NPAIR * MW; e += 64) {
-                    const int p = e / MW, j = e - p * MW;
-                    const int js = j < j_lo ? j_lo : (j >= j_hi ? j_hi - 1 : j);
-                    if (js != j) s_mid[p * IN_SB + j + SHB] = s_mid[p * IN_SB + js + SHB];
-                }
-            }
-            asm volatile("" ::: "memory");
-            // ---- H_B: mid chunk kA -> ring B slot KA
-            {
-                f2v a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
-#pragma unroll
-                for (int q = 0; q < NRDB; q++) {
-                    const float4 v = reinterpret_cast<const float4*>(hb_rd)[q];
-                    const f2v e[2] = {f2v{v.x, v.y}, f2v{v.z, v.w}};
-#pragma unroll
-                    for (int u = 0; u < 2; u++) {
-                        const int m = 2 * q + u;
-#pragma unroll
-                        for (int i = 0; i < 4; i++)
-                            if (m - i >= 0 && m - i < FWB) a[i] = pk_fma(e[u], tap<FWB>(tapsB, m - i), a[i]);
-                    }
-                }
-                float* w = hb_wr + WCH * KA * HSB;
-                *reinterpret_cast<float4*>(w) = make_float4(a[0].x, a[1].x, a[2].x, a[3].x);
-                *reinterpret_cast<float4*>(w + HSB) = make_float4(a[0].y, a[1].y, a[2].y, a[3].y);
-            }
-            asm volatile("" ::: "memory");
-            const int kB = kA - LAGB;                 // output chunk (uniform)
-            if (kB >= 0 && kB < nchunk_out) {
-                // ---- V_B: output chunk kB; mid rows clamped to 0 .. H-1 near the image's top /
-                // bottom (FilterV's clamp on level k+1)
-                const int yu = yb + WCH * kB;
-                f2v acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
-                if (yu - HB >= 0 && yu + WCH - 1 + HB <= H - 1) {
-#pragma unroll
-                    for (int m = 0; m < FWB + 3; m++) {
-                        const int rc = WCH * KB + m;
-                        const float* pp = rc < RS - 4 ? vb_rd + rc * HSB
-                                        : rc >= RS ? vb_rd + (rc - RS) * HSB : vb_rd_amb + rc * HSB;
-                        const f2v v = *reinterpret_cast<const f2v*>(pp);
-#pragma unroll
-                        for (int j = 0; j < 4; j++)
-                            if (m - j >= 0 && m - j < FWB) acc[j] = pk_fma(v, tap<FWB>(tapsB, m - j), acc[j]);
-                    }
-                } else {
-                    // row of output row yu + 4vq + j, tap i: mid row clamp(yu + 4vq + j - HB + i),
-                    // stream position (that row - ym0), ring row (position & 31)
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-#pragma unroll
-                        for (int i = 0; i < FWB; i++) {
-                            const int mr = clampi(yu + 4 * vq + j - HB + i, 0, H - 1);
-                            const int pos = mr - ym0;
-                            const f2v v = *reinterpret_cast<const f2v*>(s_hb + (pos & (RS - 1)) * HSB + vc);
-                            acc[j] = pk_fma(v, tap<FWB>(tapsB, i), acc[j]);
-                        }
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < 4; j++) asm volatile("" : "+v"(acc[j]));
-                if (full_cols && yu + WCH <= ye && (!DSB || (yu + WCH) / 2 <= dsh)) {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        float* row = dB + (long long)(yu + j) * W;
-                        *reinterpret_cast<f2v*>(row + st_off) = acc[j];
-                        if (DSB && !(j & 1)) {
-                            float* drow = dd + (long long)((yu + j) >> 1) * dsw;
-                            if ((x >> 1) < dsw) drow[ds_off] = acc[j].x;
-                            if (x + 1 == W - 1)
-                                for (int cc = W >> 1; cc < dsw; cc++) drow[2 * vq * dsw + cc] = acc[j].y;
-                        }
-                    }
-                } else if (x < W) {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const int y = yu + 4 * vq + j;
-                        if (y < ye) {
-                            *reinterpret_cast<f2v*>(&dB[(long long)y * W + x]) = acc[j];
-                            if (DSB && !(y & 1) && (y >> 1) < dsh) {
-                                float* drow = dd + (long long)(y >> 1) * dsw;
-                                if ((x >> 1) < dsw) drow[x >> 1] = acc[j].x;
-                                if (x + 1 == W - 1)
-                                    for (int cc = W >> 1; cc < dsw; cc++) drow[cc] = acc[j].y;
-                            }
-                        }
-                    }
-                }
-            }
-        }
-        asm volatile("" ::: "memory");
-        load_chunk(nxt, c + NST);
-        store_chunk(cur);
-        asm volatile("" ::: "memory");
-    };
-    const int nsteps = nchunk_out + LAGA + LAGB;
-    for (int c = 0; c < nsteps; c += NST) {
-        step(c + 0, std::integral_constant<int, 0>{}, st[1], st[0]);
-        step(c + 1, std::integral_constant<int, 1>{}, st[2], st[1]);
-        step(c + 2, std::integral_constant<int, 2>{}, st[3], st[2]);
-        step(c + 3, std::integral_constant<int, 3>{}, st[0], st[3]);
-    }
-}
-
-template <int FWA, int FWB>
-hipError_t gauss_pair_dispatch(const float* src, const uint8_t* src8, int src_stride,
-                               long long src_img_stride, float* dstA, float* dstB,
-                               long long dst_img_stride, int w, int h, const Taps& tapsA,
-                               const Taps& tapsB, int batch, float* ds, int dsw, int dsh,
-                               long long ds_img_stride, hipStream_t stream) {
-    const GaussWaveGrid gg = gauss_wave_grid(w, h, batch, 0, 1);
-    const dim3 grid((unsigned)((gg.total_waves + kGpWaves - 1) / kGpWaves));
-#define SGK_PAIR(U8, DS)                                                                      \
-    hipLaunchKernelGGL((k_gauss_pair<FWA, FWB, U8, DS>), grid, dim3(64 * kGpWaves), 0, stream, \
-                       src, src8, src_stride, src_img_stride, dstA, dstB, dst_img_stride, w, h, \
-                       tapsA, tapsB, ds, dsw, dsh, ds_img_stride, gg)
-    if (src8) {
-        if (ds) SGK_PAIR(true, true); else SGK_PAIR(true, false);
-    } else {
-        if (ds) SGK_PAIR(false, true); else SGK_PAIR(false, false);
-    }
-#undef SGK_PAIR
-    return hipGetLastError();
 }
 
 template <int FW>
 hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
                           long long src_img_stride, float* dst, long long dst_img_stride, int w,
                           int h, const Taps& taps, int batch, float* ds, int dsw, int dsh,
-                          long long ds_img_stride, hipStream_t stream, int wave_rows,
-                          bool lean) {
+                          long long ds_img_stride, hipStream_t stream, int wave_rows) {
     const bool vec = (src_stride % 4) == 0 && (src_img_stride % 4) == 0 && (w % 4) == 0 &&
                      w >= 4 && ((uintptr_t)(src8 ? (const void*)src8 : (const void*)src) % 16) == 0;
-    constexpr int LAG_W = (FW - 1 + WCH - 1) / WCH;
-    if constexpr (WCH * (LAG_W + 1) <= 32) if (vec && wave_rows >= 0 && lean) {
+    if (vec && wave_rows >= 0) {
         const GaussWaveGrid gg = gauss_wave_grid(w, h, batch, wave_rows, 1);
         const dim3 wgrid((unsigned)((gg.total_waves + kGwWaves - 1) / kGwWaves));
 #define SGK_LEAN(U8, DS)                                                                      \
@@ -1230,23 +622,6 @@ hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
             if (ds) SGK_LEAN(false, true); else SGK_LEAN(false, false);
         }
 #undef SGK_LEAN
-        return hipGetLastError();
-    }
-    if (vec && wave_rows >= 0) {
-#ifndef SGK_GW_NW
-#define SGK_GW_NW 1
-#endif
-        constexpr int NW = SGK_GW_NW;
-        const GaussWaveGrid gg = gauss_wave_grid(w, h, batch, wave_rows, NW);
-        const dim3 wgrid((unsigned)((gg.total_waves + kGwWaves - 1) / kGwWaves));
-        if (src8)
-            hipLaunchKernelGGL((k_gauss_wave<FW, true, NW>), wgrid, dim3(64 * kGwWaves), 0, stream, src,
-                               src8, src_stride, src_img_stride, dst, dst_img_stride, w, h, taps,
-                               ds, dsw, dsh, ds_img_stride, gg);
-        else
-            hipLaunchKernelGGL((k_gauss_wave<FW, false, NW>), wgrid, dim3(64 * kGwWaves), 0, stream, src,
-                               src8, src_stride, src_img_stride, dst, dst_img_stride, w, h, taps,
-                               ds, dsw, dsh, ds_img_stride, gg);
         return hipGetLastError();
     }
     // bands of at most 17 chunks (544 rows), and at least 1024 workgroups when the image is
@@ -2690,6 +2065,310 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
     *reinterpret_cast<float2*>(desc + (size_t)out * 128 + cell * 8 + sub * 2) = make_float2(b0, b1);
 }
 
+// ------------------------------------------------------------------------------------------
+// Pixel-major descriptor (round 4, the shipped default for detected features).  descriptor_fast
+// visits a window pixel once per cell whose rotated square holds it -- 2.56 times on average, up to
+// 4 -- and pays the pixel's gradient magnitude, atan2, Gaussian weight and bin split on every visit,
+// while only the spatial weight (1 - |nx|)(1 - |ny|) depends on the cell.  Here every pixel is
+// evaluated once: the window |dnx|, |dny| < 2.5 (feature frame, cell units, dnx = nx + ox) is cut
+// into the 5 x 5 "dual" cells of the half-cell-shifted grid, dual cell (a, b) = floor(dnx + 2.5),
+// floor(dny + 2.5); a pixel of dual cell (a, b) lies in the squares of exactly the cells (a-1, b-1),
+// (a, b-1), (a-1, b), (a, b), with the bilinear weights (1-u)(1-v), u(1-v), (1-u)v, uv (u, v its
+// offsets inside the dual cell), which are the reference's (1 - |nx|)(1 - |ny|) for those cells
+// (ProgramCU.cu:1044-1094).  Two lanes own each dual cell (lanes 0..49, alternate rows); a pixel's
+// 8 contributions (4 cells x the 2 interpolated orientation bins) go to the wave's LDS histogram
+// as no-return ds_add_f32 (IEEE adds in the LDS), laid out [bin][6 x 6 cells][lane copy]: the
+// 6 x 6 grid gives the 4 cells of a dual cell constant offsets (0, 1, 6, 7 cells) and absorbs the
+// border cells -1 and 4, which are never read; the two lanes of a dual cell add to their own copy,
+// so no two lanes of an instruction hit one address.  Membership of a pixel is decided from dnx,
+// dny, which every lane computes with the same operations, so each pixel is counted by exactly one
+// lane.  Same samples, weights and bins as descriptor_fast (relaxed order and transcendentals):
+// L2 ~1e-6 from the oracle; descriptor_one remains the bit-exact mode.
+constexpr int kDualWords = 50 * 33;   // reduction words per wave
+#ifndef SGK_DUAL_REF
+#define SGK_DUAL_REF 1   // cell weights from the reference's rounded cell centres
+#endif
+#ifndef SGK_DUAL_WPE
+#define SGK_DUAL_WPE 0   // waves per SIMD the allocation must allow (0: compiler's choice, 90 VGPRs)
+#endif
+#if SGK_DUAL_WPE
+#define SGK_DUAL_ATTR __attribute__((amdgpu_waves_per_eu(SGK_DUAL_WPE)))
+#else
+#define SGK_DUAL_ATTR
+#endif
+__device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const float* __restrict__ pyr,
+                                                const float4* __restrict__ feat,
+                                                const int2* __restrict__ feat_info,
+                                                const FeatureParams& fp, float* __restrict__ desc,
+                                                uint32_t out, float* __restrict__ hist) {
+    const float4 key = feat[e];
+    const int2 in = feat_info[e];
+    const int o = in.y / fp.d, j = in.y - o * fp.d;
+    const OctaveDesc& od = fp.oct[o];
+    const int W = od.wa, H = od.h;
+    const float* g = pyr + od.gauss_off + (long long)(1 + j) * od.level_stride +
+                     (long long)in.x * W * H;
+    const float rpi = (float)(4.0 / 3.14159265358979323846);
+    const float spt = fabs_(key.z * fp.window_factor);
+    float s, c;
+    sincos_(key.w, &s, &c);
+    const float anglef = (double)key.w > 3.14159265358979323846
+                             ? (float)((double)key.w - (2.0 * 3.14159265358979323846))
+                             : key.w;
+    const float cspt = c * spt, sspt = s * spt, crspt = c / spt, srspt = s / spt;
+    // this lane's dual cell (a, b) and histogram copy; lanes 50..63 walk nothing
+    const int q = lane >> 1, cp = lane & 1;
+    const int a = q % 5, b = q / 5;
+    const float fa = (float)a, fb = (float)b;
+    // the dual cell's square: centre (a - 2, b - 2) cells from the keypoint, side spt
+    const float fx = fa - 2.0f, fy = fb - 2.0f;
+    const float cxi = key.x + fma_(cspt, fx, -(sspt * fy));
+    const float cyi = key.y + fma_(sspt, fx, cspt * fy);
+    const float hb = 0.5f * (fabs_(cspt) + fabs_(sspt)) + 0.01f;
+    // pixel p has its sample at p + 0.5; rows and columns 1 .. H-2 / W-2 (the reference's box
+    // clamp to [1.5, W - 1.5])
+    // (clamped as floats first: a caller keypoint far outside the image must not saturate the
+    // int conversion, whose y0 + 1 would wrap)
+    const float fH = (float)H, fW = (float)W;
+    const int y0 = (int)fmax_(1.0f, fmin_(fH, ceilf(cyi - hb - 0.5f)));
+    int y1 = (int)fmin_(fH - 2.0f, fmax_(-1.0f, floor_(cyi + hb - 0.5f)));
+    const int bx0 = (int)fmax_(1.0f, fmin_(fW, ceilf(cxi - hb - 0.5f)));
+    const int bx1 = (int)fmin_(fW - 2.0f, fmax_(-1.0f, floor_(cxi + hb - 0.5f)));
+    if (q >= 25 || !(spt > 0.0f)) y1 = y0 - 1;
+    // row span: the columns whose u = dnx + 2.5 - a and v = dny + 2.5 - b can lie in [0, 1],
+    // dnx = crspt dxk + srspt dyk, dny = crspt dyk - srspt dxk (dxk, dyk from the keypoint); the
+    // 0.01-pixel margin absorbs rounding, the per-pixel test decides
+    const bool use_c = fabs_(crspt) > 1e-4f / spt, use_s = fabs_(srspt) > 1e-4f / spt;
+    const float icr = use_c ? 1.0f / crspt : 0.0f, isr = use_s ? 1.0f / srspt : 0.0f;
+    auto row_span = [&](int py, int& lo, int& len) {
+        const float dyk = ((float)py + 0.5f) - key.y;
+        float l = -1e30f, h = 1e30f;
+        if (use_c) {   // crspt dxk in [-Ku, 1 - Ku], Ku = srspt dyk + 2.5 - a
+            const float p = -fma_(srspt, dyk, 2.5f - fa) * icr;
+            l = fmax_(l, p + fmin_(0.0f, icr));
+            h = fmin_(h, p + fmax_(0.0f, icr));
+        }
+        if (use_s) {   // -srspt dxk in [-Kv, 1 - Kv], Kv = crspt dyk + 2.5 - b
+            const float p = fma_(crspt, dyk, 2.5f - fb) * isr;
+            l = fmax_(l, p + fmin_(0.0f, -isr));
+            h = fmin_(h, p + fmax_(0.0f, -isr));
+        }
+        const float xl = ceilf(l + key.x - 0.5f - 0.01f), xh = floor_(h + key.x - 0.5f + 0.01f);
+        const int il = max(bx0, (int)fmax_(xl, -1.0f)), ih = min(bx1, (int)fmin_(xh, fW));
+        lo = il;
+        len = ih >= il ? ih - il + 1 : 0;
+    };
+    const float kexp = -0.125f * 1.44269504f;   // e^(-x/8) = 2^(kexp x)
+    // lane-constant word offset of cell (a - 1, b - 1) in the 6 x 6 grid, own copy
+#if SGK_DUAL_REF
+    // The reference measures nx, ny from each cell's centre (ptx, pty), rounded to a float at
+    // image-coordinate magnitude (ulp up to 1.2e-4 pixel at x ~ 2000; ProgramCU.cu:1044-1062).
+    // Measured from the keypoint instead, the weights differ from the reference's by ~1e-5
+    // (descriptor L2 up to 1.2e-5); so the 4 cells' weights use the reference's rounded centres:
+    // nx = dnx - ox', ox' = crspt (ptx - x_key) + srspt (pty - y_key) (both differences exact),
+    // and for the dual cell's left / right cells |nx| = nx / -nx, so that 1 - |nx| is one
+    // subtraction (at the dual cell's edges the weights cross 0 by a rounding, continuously).
+    float oxl[4], oyl[4];   // 1 -/+ ox', 1 -/+ oy' of cells (a-1,b-1), (a,b-1), (a-1,b), (a,b)
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const float ox = (float)(a - 1 + (k & 1)) - 1.5f, oy = (float)(b - 1 + (k >> 1)) - 1.5f;
+        const float ptx = fma_(cspt, ox, -(sspt * oy)) + key.x;
+        const float pty = fma_(cspt, oy, sspt * ox) + key.y;
+        const float ex = ptx - key.x, ey = pty - key.y;
+        const float oxp = fma_(crspt, ex, srspt * ey), oyp = fma_(crspt, ey, -(srspt * ex));
+        oxl[k] = (k & 1) ? 1.0f - oxp : 1.0f + oxp;
+        oyl[k] = (k >> 1) ? 1.0f - oyp : 1.0f + oyp;
+    }
+#endif
+    // the lane's 4 cells x 8 bins, bins in pairs: acc[k][p] = bins 2p, 2p + 1 of cell slot k
+    f2v acc[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int p = 0; p < 4; p++) acc[k][p] = f2v{0.0f, 0.0f};
+    // a pixel's angle: the relaxed atan2, and within 1e-5 rad of the reference's one binning
+    // discontinuity (theta rounding to 8.0 is dropped) the oracle's atan2 (descriptor_fast's
+    // rule); the exact form is evaluated in one shared loop for the strip's flagged pixels (rare)
+    auto angle = [&](float gx, float gy, float m2, bool& need) {
+        const float rot = atan2_relaxed(gy, gx);
+        const float dd = fabs_(anglef - rot);
+        need = dd < 1e-5f || dd > 6.2831753f;
+        return m2 == 0.0f ? 0.0f : rot;
+    };
+    auto pixel = [&](float dxk, float sdy, float cdy, float m2, float rot, bool valid) {
+        const float dnx = fma_(crspt, dxk, sdy);          // sdy = srspt dyk
+        const float dny = fma_(-srspt, dxk, cdy);         // cdy = crspt dyk
+        const float t = dnx + 2.5f, tv = dny + 2.5f;
+        const float ft = floor_(t), fv = floor_(tv);
+        const float u = t - ft, v = tv - fv;
+        const float m = 0.5f * __builtin_amdgcn_sqrtf(m2);
+        const float w = m * __builtin_amdgcn_exp2f(kexp * fma_(dnx, dnx, dny * dny));
+        float theta = (anglef - rot) * rpi;
+        if (theta < 0) theta += 8.0f;
+        // theta outside [0, 8) (a caller orientation far outside (-pi, pi]) adds to no bin, as the
+        // reference's k == fidx test; it would also index outside the histogram
+        const bool take = valid && ft == fa && fv == fb && theta >= 0.0f && theta < 8.0f;
+        // branch-free: a pixel not taken adds fma(tent, 0, acc) = acc (its theta replaced by 0 so
+        // that no tent is NaN)
+        const float wt = take ? w : 0.0f;
+        const float th = take ? theta : 0.0f;
+#if SGK_DUAL_REF
+        (void)u; (void)v;
+        const float c4[4] = {wt * (oxl[0] - dnx) * (oyl[0] - dny), wt * (dnx + oxl[1]) * (oyl[1] - dny),
+                             wt * (oxl[2] - dnx) * (dny + oyl[2]), wt * (dnx + oxl[3]) * (dny + oyl[3])};
+#else
+        const float wv1 = wt * v, wv0 = wt - wv1;                    // w (1 - v), w v
+        const float c4[4] = {fma_(-wv0, u, wv0), wv0 * u, fma_(-wv1, u, wv1), wv1 * u};
+#endif
+        // tent weights max(0, 1 - |theta - k|), bin 0 also taking the wrap of bin 8
+        // (ProgramCU.cu:1094), as descriptor_fast; then the outer product with the 4 cell weights
+        f2v tp[4];
+        tp[0] = f2v{__builtin_amdgcn_fmed3f(fmax_(1.0f - th, th - 7.0f), 0.0f, 1.0f),
+                    __builtin_amdgcn_fmed3f(1.0f - fabs_(th - 1.0f), 0.0f, 1.0f)};
+#pragma unroll
+        for (int p = 1; p < 4; p++)
+            tp[p] = f2v{__builtin_amdgcn_fmed3f(1.0f - fabs_(th - (float)(2 * p)), 0.0f, 1.0f),
+                        __builtin_amdgcn_fmed3f(1.0f - fabs_(th - (float)(2 * p + 1)), 0.0f, 1.0f)};
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int p = 0; p < 4; p++) acc[k][p] = pk_fma(tp[p], c4[k], acc[k][p]);
+    };
+    // walk: rows y0 + cp, y0 + cp + 2, ...; each row's span in strips of 4 pixels whose gradient
+    // neighbours come from 4 vector loads (as descriptor_fast), the next strip's loads issued
+    // before the current strip's pixels
+    const char* gb = reinterpret_cast<const char*>(g);
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    auto ld4 = [&](uint32_t byte) { return *reinterpret_cast<const f4v*>(gb + byte); };
+    int r = y0 + cp, lo = 0, len = 0, cx = 0;
+    auto next_row = [&]() {   // advance r (by 2) to the next row with a nonempty span
+#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
+        for (; r <= y1; r += 2) {
+            row_span(r, lo, len);
+            if (len > 0) break;
+        }
+        cx = lo;
+    };
+    next_row();
+    f4v na, nb, nu, nd;
+    uint32_t npo = 4u * (uint32_t)(W + 1);   // row 1, column 1 when nothing is left (in-plane)
+    auto fetch = [&]() {
+        if (r <= y1) npo = 4u * (uint32_t)(r * W + cx);
+        na = ld4(npo - 4u);
+        nb = ld4(npo + 4u);
+        nu = ld4(npo - 4u * W);
+        nd = ld4(npo + 4u * W);
+    };
+    fetch();
+    while (r <= y1) {
+        const f4v pa = na, pb = nb, pu = nu, pd = nd;
+        const float dyk = ((float)r + 0.5f) - key.y;
+        const float sdy = srspt * dyk, cdy = crspt * dyk;
+        const int nv = lo + len - cx;
+        const float xc = (float)cx + 0.5f;   // (xc + i) - x_key: the same value in every lane
+        cx += 4;
+        if (cx >= lo + len) {
+            r += 2;
+            next_row();
+        }
+        fetch();
+        const f4v gx = pb - pa, gy = pd - pu;
+        f4v m2, rot;
+        bool need[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            m2[i] = fma_(gx[i], gx[i], gy[i] * gy[i]);
+            rot[i] = angle(gx[i], gy[i], m2[i], need[i]);
+        }
+        if (need[0] || need[1] || need[2] || need[3]) {
+#pragma unroll 1
+            for (int i = 0; i < 4; i++) {
+                const float x = i == 0 ? gx[0] : i == 1 ? gx[1] : i == 2 ? gx[2] : gx[3];
+                const float y = i == 0 ? gy[0] : i == 1 ? gy[1] : i == 2 ? gy[2] : gy[3];
+                const bool nd_i = i == 0 ? need[0] : i == 1 ? need[1] : i == 2 ? need[2] : need[3];
+                const float ex = atan2_(y, x);
+                const float mm = i == 0 ? m2[0] : i == 1 ? m2[1] : i == 2 ? m2[2] : m2[3];
+                const float rr = nd_i && mm != 0.0f ? ex
+                               : (i == 0 ? rot[0] : i == 1 ? rot[1] : i == 2 ? rot[2] : rot[3]);
+                rot[0] = i == 0 ? rr : rot[0];
+                rot[1] = i == 1 ? rr : rot[1];
+                rot[2] = i == 2 ? rr : rot[2];
+                rot[3] = i == 3 ? rr : rot[3];
+            }
+        }
+        // one pixel at a time (sched_barrier): the four interleaved took ~150 VGPRs
+        pixel((xc) - key.x, sdy, cdy, m2[0], rot[0], true);
+        __builtin_amdgcn_sched_barrier(0);
+        pixel((xc + 1.0f) - key.x, sdy, cdy, m2[1], rot[1], nv > 1);
+        __builtin_amdgcn_sched_barrier(0);
+        pixel((xc + 2.0f) - key.x, sdy, cdy, m2[2], rot[2], nv > 2);
+        __builtin_amdgcn_sched_barrier(0);
+        pixel((xc + 3.0f) - key.x, sdy, cdy, m2[3], rot[3], nv > 3);
+    }
+    // reduction: lanes 0..49 store their 32 bins ([lane][slot][bin], stride 33 floats against
+    // bank conflicts); lane L then sums bins 2 sub, 2 sub + 1 of cell L >> 2 (descriptor_fast's
+    // output layout) over the 4 dual cells x 2 lanes that hold that cell
+    if (q < 25) {
+        float* my = hist + lane * 33;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int p = 0; p < 4; p++) {
+                my[8 * k + 2 * p] = acc[k][p].x;
+                my[8 * k + 2 * p + 1] = acc[k][p].y;
+            }
+    }
+    asm volatile("" ::: "memory");
+    const int cell = lane >> 2, sub = lane & 3;
+    const int ix = cell & 3, iy = cell >> 2;
+    float b0 = 0.0f, b1 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        // slot k of dual cell (ix + 1 - (k & 1), iy + 1 - (k >> 1)) is this cell
+        const int dq = (iy + 1 - (k >> 1)) * 5 + ix + 1 - (k & 1);
+#pragma unroll
+        for (int c2 = 0; c2 < 2; c2++) {
+            const float* src = hist + (2 * dq + c2) * 33 + 8 * k + 2 * sub;
+            b0 += src[0];
+            b1 += src[1];
+        }
+    }
+    asm volatile("" ::: "memory");
+    if (fp.normalize) {
+        float sn = fma_(b0, b0, b1 * b1);
+#pragma unroll
+        for (int k = 32; k >= 1; k >>= 1) sn += __shfl_xor(sn, k, 64);
+        const float n1 = __builtin_amdgcn_rsqf(sn);
+        b0 = fmin_(0.2f, b0 * n1);
+        b1 = fmin_(0.2f, b1 * n1);
+        sn = fma_(b0, b0, b1 * b1);
+#pragma unroll
+        for (int k = 32; k >= 1; k >>= 1) sn += __shfl_xor(sn, k, 64);
+        const float n2 = __builtin_amdgcn_rsqf(sn);
+        b0 *= n2;
+        b1 *= n2;
+    }
+    *reinterpret_cast<float2*>(desc + (size_t)out * 128 + cell * 8 + sub * 2) = make_float2(b0, b1);
+}
+
+// One wave per feature (grid-stride), each wave with its own LDS histogram.
+__global__ __launch_bounds__(256) SGK_DUAL_ATTR void k_descriptor_dual(const float* __restrict__ pyr,
+                                                         const float4* __restrict__ feat,
+                                                         const int2* __restrict__ feat_info,
+                                                         const uint32_t* __restrict__ n_feat_dev,
+                                                         const FeatureParams fp,
+                                                         float* __restrict__ desc,
+                                                         const int* __restrict__ out_index) {
+    __shared__ float s_hist[4][kDualWords];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* hist = s_hist[wave];
+    const uint32_t n = *n_feat_dev;
+    for (uint32_t e = blockIdx.x * 4 + wave; e < n; e += gridDim.x * 4)
+        descriptor_dual(e, lane, pyr, feat, feat_info, fp, desc,
+                        out_index ? (uint32_t)out_index[e] : e, hist);
+}
+
 // One wave per feature, grid-stride over the features (count read on the device).
 // SGK_DESC_WPE: waves per SIMD the register allocation must allow (0: the compiler's choice, 91
 // VGPRs = 5 waves; A/B knob)
@@ -2933,13 +2612,12 @@ __global__ __launch_bounds__(64) void k_debug_candidates(
 hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         long long src_img_stride, float* dst, long long dst_img_stride, int w,
                         int h, int fw, const Taps& taps, int batch, float* ds_dst, int ds_w,
-                        int ds_h, long long ds_img_stride, hipStream_t stream, int wave_rows,
-                        bool lean) {
+                        int ds_h, long long ds_img_stride, hipStream_t stream, int wave_rows) {
 #define SGK_GAUSS(FW)                                                                       \
     case FW:                                                                                  \
         return gauss_dispatch<FW>(src, src_u8, src_stride, src_img_stride, dst, dst_img_stride, \
                                   w, h, taps, batch, ds_dst, ds_w, ds_h, ds_img_stride, stream, \
-                                  wave_rows, lean);
+                                  wave_rows);
     switch (fw) {
         SGK_GAUSS(5) SGK_GAUSS(7) SGK_GAUSS(9) SGK_GAUSS(11) SGK_GAUSS(13) SGK_GAUSS(15)
         SGK_GAUSS(17) SGK_GAUSS(19) SGK_GAUSS(21) SGK_GAUSS(23) SGK_GAUSS(25) SGK_GAUSS(27)
@@ -2947,34 +2625,6 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
         default: return hipErrorInvalidValue;
     }
 #undef SGK_GAUSS
-}
-
-hipError_t launch_gauss_pair(const float* src, const uint8_t* src_u8, int src_stride,
-                             long long src_img_stride, float* dst_a, float* dst_b,
-                             long long dst_img_stride, int w, int h, int fw_a, const Taps& taps_a,
-                             int fw_b, const Taps& taps_b, int batch, float* ds_dst, int ds_w,
-                             int ds_h, long long ds_img_stride, hipStream_t stream) {
-    if (!gauss_pair_supported(fw_a, fw_b, src_stride, src_img_stride, w,
-                              src_u8 ? (const void*)src_u8 : (const void*)src))
-        return hipErrorInvalidValue;
-#define SGK_P(A, B)                                                                           \
-    if (fw_a == A && fw_b == B)                                                               \
-        return gauss_pair_dispatch<A, B>(src, src_u8, src_stride, src_img_stride, dst_a, dst_b, \
-                                         dst_img_stride, w, h, taps_a, taps_b, batch, ds_dst,  \
-                                         ds_w, ds_h, ds_img_stride, stream);
-    // the default schedule's pairs (-f 4, -d 3): input -> levels 0, 1 of octave 0 with the
-    // initial smoothing of -fo 0 (13) or -fo -1 (11); levels 2, 3 and 4, 5 of every octave
-    SGK_P(13, 11) SGK_P(11, 11) SGK_P(13, 17) SGK_P(21, 25)
-#undef SGK_P
-    return hipErrorInvalidValue;
-}
-
-bool gauss_pair_supported(int fw_a, int fw_b, int src_stride, long long src_img_stride, int w,
-                          const void* src) {
-    const bool widths = (fw_a == 13 && fw_b == 11) || (fw_a == 11 && fw_b == 11) ||
-                        (fw_a == 13 && fw_b == 17) || (fw_a == 21 && fw_b == 25);
-    return widths && (src_stride % 4) == 0 && (src_img_stride % 4) == 0 && (w % 4) == 0 &&
-           w >= 4 && ((uintptr_t)src % 16) == 0;
 }
 
 hipError_t launch_color_to_gray(const uint8_t* src, int n, int w, int h, int stride,
@@ -3186,6 +2836,14 @@ hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* f
         if (fp.normalize)
             hipLaunchKernelGGL(k_desc_normalize, dim3(grid), dim3(256), 0, stream, n_feat_dev,
                                desc);
+        return hipGetLastError();
+    }
+#ifndef SGK_DESC_DUAL
+#define SGK_DESC_DUAL 1
+#endif
+    if (!exact && !rect && SGK_DESC_DUAL) {
+        hipLaunchKernelGGL(k_descriptor_dual, dim3(grid), dim3(256), 0, stream, pyr, feat,
+                           feat_info, n_feat_dev, fp, desc, out_index);
         return hipGetLastError();
     }
     if (!exact) {

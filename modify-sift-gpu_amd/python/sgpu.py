@@ -418,9 +418,7 @@ class SiftContext:
     DEBUG_GAUSS_BLOCK = 32    # workgroup strip Gaussian (k_gauss_pk2); wave band rows in bits 16..
     DEBUG_KEYED_MATCH = 64    # keyed matcher epilogue even when ratiomax <= 1
     DEBUG_FULL_COLUMNS = 128  # mutual matching decides every column, not only the matched ones
-    DEBUG_GAUSS_WAVE1 = 256   # round 2's k_gauss_wave instead of the lean level kernel
     DEBUG_ORIENT_WAVE = 512   # orientation one wave per candidate for any candidate count
-    DEBUG_GAUSS_PAIR = 1024    # two-level k_gauss_pair launches where compiled (test hook, slower)
     DEBUG_MATCH_REGSTAGE = 2048  # keyless matcher with register staging (k_match_rows<RAW>)
     DEBUG_PYR_SERIAL = 4096    # all pyramid octaves on one stream
 

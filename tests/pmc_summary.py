@@ -7,9 +7,7 @@ Per bench step (one extract of the batch): the Gaussian family's kernel time fro
 and its HBM bytes from FETCH_SIZE + WRITE_SIZE (kB units -> bytes), raw and corrected.  The
 correction (MI355X_MICROARCH.md, HBM section: FETCH_SIZE counts 1/2 of the bytes of a 16-B-per-lane
 streaming read) uses the factors measured by tests/pmc_calib.sh on a known byte count at each
-access width (profiles/*_pmc_calibration.json): the f32 Gaussian levels load 16 B per lane
-(read16), the u8 level 0 4 B per lane (read4), and both store 8 B per lane (write8).  Kernels of
-other access patterns keep their raw counters ("hbm_bytes_per_extract" is then the raw sum).
+access width (profiles/*_pmc_calibration.json), applied to every kernel (factors()).
 """
 import csv
 import glob
@@ -43,11 +41,22 @@ def calibration():
 
 
 def factors(name, cal):
-    """(read factor, write factor) for a kernel's access widths, (1, 1) when uncalibrated."""
-    if cal is None or not re.search(r"k_gauss_(wave|lean)<", name):
+    """(read factor, write factor) of a kernel from the calibration record.  The record measured
+    FETCH_SIZE at 1/2 of the bytes for 4-, 8- and 16-byte-per-lane reads alike (and WRITE_SIZE
+    exact), so the read factor of the kernel's access width applies to every kernel: the level
+    kernels' 16-B (f32) or 4-B (u8 level 0) rows, the extremum kernel's 8-B row pairs, the
+    feature kernels' 4- and 16-B gathers (round 3 corrected only the k_gauss family and left
+    the other kernels at half their read bytes)."""
+    if cal is None:
         return 1.0, 1.0
     u8 = re.search(r"k_gauss_(wave|lean)<\s*\d+\s*,\s*true", name) is not None
-    return cal.get("read4" if u8 else "read16") or 1.0, cal.get("write8") or 1.0
+    if u8:
+        r = cal.get("read4")
+    elif "k_extrema" in name:
+        r = cal.get("read8")
+    else:
+        r = cal.get("read16")
+    return r or 1.0, cal.get("write8") or 1.0
 
 
 def main():
@@ -96,6 +105,7 @@ def main():
     if cal is not None:
         out["hbm_bytes_per_extract"] = dict(hbm)
         out["calibration"] = cal_src
+        out["calibrated_all_kernels"] = True
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))

@@ -143,3 +143,46 @@ def test_multithread_contexts_one_device(tmp_path):
         d = raw[4 * len(rk):].reshape(-1, 128)
         assert np.array_equal(k.view(np.uint32), rk.view(np.uint32))
         assert np.linalg.norm(d.astype(np.float64) - rd, axis=1).max() < 1e-4
+
+
+def test_speed_replica_timing_slots(tmp_path):
+    """TestWin/speed.cpp's protocol (speed.cpp:60-155) through bin/speed_replica: the feature count
+    is stable over the runs and equals the oracle's, and the reference's _timing slots
+    (SiftGPU.cpp:368, printed by speed.cpp:136-153) hold the per-stage times of a RunSIFT: the
+    descriptor slot [8] is filled, the pyramid slot [2] is the largest, and the slots [2..8] add
+    up to the measured time per RunSIFT within 15 %."""
+    exe = os.path.join(ROOT, "modify-sift-gpu_amd", "bin", "speed_replica")
+    img = synth_image(1920, 1080, 2000)      # the C2 image of bench.py
+    pgm = tmp_path / "c2.pgm"
+    _write_pgm(pgm, img)
+    r = subprocess.run([exe, "20", "--", "-i", str(pgm), "-fo", "0", "-no", "4", "-d", "3"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    import json
+    sp = json.loads(r.stdout.strip().splitlines()[-1])
+    assert sp["stable"] and sp["features"] == len(O.extract(img, default_options(octave_num=4))[0])
+    t = sp["timing_ms"]
+    slots = ["build_pyramid", "detection", "feature_list", "orientation", "mo_feature_list",
+             "download_keys", "descriptor"]
+    assert t["descriptor"] > 0
+    assert t["build_pyramid"] == max(t[s] for s in slots)
+    total = sum(t[s] for s in slots)
+    assert abs(total - sp["avg_ms"]) <= 0.15 * sp["avg_ms"], (total, sp["avg_ms"], t)
+
+
+def test_rejected_extract_keeps_previous_results(gpu_ctx):
+    """An sgpu_extract call rejected for its arguments queues nothing and leaves the previous
+    extract's features readable (the C ABI's argument checks run before the batch is replaced)."""
+    import ctypes
+    import sgpu
+    img = synth_image(320, 240, 5)
+    gpu_ctx.set_options(default_options())
+    gpu_ctx.extract(img)
+    k0, d0 = gpu_ctx.features(0)
+    n0 = gpu_ctx.total()
+    buf = np.zeros((8, 8), np.uint8)
+    rc = sgpu.lib().sgpu_extract(gpu_ctx._ctx, buf.ctypes.data_as(ctypes.c_void_p), 1, 8, 8, 4, 0)
+    assert rc != 0   # stride < width
+    assert gpu_ctx.total() == n0 > 0
+    k1, d1 = gpu_ctx.features(0)
+    assert np.array_equal(k0.view(np.uint32), k1.view(np.uint32)) and np.array_equal(d0, d1)

@@ -1,6 +1,6 @@
-"""Gaussian pyramid kernels on the GPU: the shipped level kernel (k_gauss_lean), the two-level
-k_gauss_pair (test hook SGPU_DEBUG_GAUSS_PAIR), round 2's wave-streaming kernel (k_gauss_wave) and
-the workgroup strip kernel (k_gauss_pk2) against each other and the oracle, bit for bit.
+"""Gaussian pyramid kernels on the GPU: the shipped wave-streaming level kernel (k_gauss_lean) and
+the workgroup strip kernel (k_gauss_pk2, test hook SGPU_DEBUG_GAUSS_BLOCK) against each other and
+the oracle, bit for bit.
 
 Both kernels restate FilterH / FilterV (ProgramCU.cu:115-222) with the taps summed i = 0..FW-1
 and the 2x decimation of DownsampleKernel<1> (ProgramCU.cu:287-298) fused into the level that
@@ -17,8 +17,6 @@ from sift_synth import synth_batch, synth_image
 pytestmark = pytest.mark.gpu
 
 BLOCK = sgpu.SiftContext.DEBUG_GAUSS_BLOCK
-WAVE1 = sgpu.SiftContext.DEBUG_GAUSS_WAVE1
-PAIR = sgpu.SiftContext.DEBUG_GAUSS_PAIR
 
 
 def _bits(a):
@@ -62,9 +60,8 @@ def test_wave_levels_equal_block_kernel(gpu_ctx, rows, n, w, h):
     ref = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
     k_ref = [gpu_ctx.features(i)[0].copy() for i in range(n)]
     try:
-        # k_gauss_wave, the shipped k_gauss_lean (one level per launch), then the two-level
-        # k_gauss_pair launches with k_gauss_lean for the unpaired levels
-        for kernel in (WAVE1, 0, PAIR):
+        # the shipped k_gauss_lean with the forced band height
+        for kernel in (0,):
             gpu_ctx.set_debug_flags((rows << 16) | kernel)
             gpu_ctx.extract(imgs)
             got = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
@@ -78,9 +75,9 @@ def test_wave_levels_equal_block_kernel(gpu_ctx, rows, n, w, h):
         gpu_ctx.set_debug_flags(0)
 
 
-# every filter width of the lean kernel and the wave kernel's widths past it: -d changes the
-# level sigmas (FW 5 .. 25 at the default -f 4), -f 5.5 reaches FW 27 .. 33 (k_gauss_wave's
-# 64-row ring); first octaves -1 / 0 / 1 (float and u8 first levels)
+# every filter width of the lean kernel: -d changes the level sigmas (FW 5 .. 25 at the default
+# -f 4, the 32-row ring), -f 5.5 reaches FW 27 .. 33 (the 64-row ring of 8 chunk slots); first
+# octaves -1 / 0 / 1 (float and u8 first levels)
 @pytest.mark.parametrize("over", [dict(dog_level_num=1), dict(dog_level_num=2),
                                   dict(dog_level_num=5), dict(filter_width_factor=5.5),
                                   dict(filter_width_factor=2.0), dict(octave_min=-1),
