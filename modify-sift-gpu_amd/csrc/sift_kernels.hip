@@ -2089,7 +2089,7 @@ constexpr int kDualWords = 50 * 33;   // reduction words per wave
 #define SGK_DUAL_REF 1   // cell weights from the reference's rounded cell centres
 #endif
 #ifndef SGK_DUAL_WPE
-#define SGK_DUAL_WPE 0   // waves per SIMD the allocation must allow (0: compiler's choice, 90 VGPRs)
+#define SGK_DUAL_WPE 4   // waves per SIMD the allocation must allow: 4 = <= 128 VGPRs, no spills (132 free)
 #endif
 #if SGK_DUAL_WPE
 #define SGK_DUAL_ATTR __attribute__((amdgpu_waves_per_eu(SGK_DUAL_WPE)))
@@ -2180,22 +2180,25 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
         oyl[k] = (k >> 1) ? 1.0f - oyp : 1.0f + oyp;
     }
 #endif
-    // the lane's 4 cells x 8 bins, bins in pairs: acc[k][p] = bins 2p, 2p + 1 of cell slot k
-    f2v acc[4][4];
+    // the lane's 4 cells x 8 bins, cells in pairs: acc[h][k] = bin k of cell slots 2h, 2h + 1
+    // (slot 0: cell (a-1, b-1), 1: (a, b-1), 2: (a-1, b), 3: (a, b)), so that each packed fma
+    // takes one scalar tent weight and a pair of cell weights
+    f2v acc[2][8];
 #pragma unroll
-    for (int k = 0; k < 4; k++)
+    for (int h = 0; h < 2; h++)
 #pragma unroll
-        for (int p = 0; p < 4; p++) acc[k][p] = f2v{0.0f, 0.0f};
+        for (int k = 0; k < 8; k++) acc[h][k] = f2v{0.0f, 0.0f};
     // a pixel's angle: the relaxed atan2, and within 1e-5 rad of the reference's one binning
     // discontinuity (theta rounding to 8.0 is dropped) the oracle's atan2 (descriptor_fast's
     // rule); the exact form is evaluated in one shared loop for the strip's flagged pixels (rare)
-    auto angle = [&](float gx, float gy, float m2, bool& need) {
-        const float rot = atan2_relaxed(gy, gx);
+    auto pixel = [&](float dxk, float sdy, float cdy, float gx, float gy, bool valid) {
+        const float m2 = fma_(gx, gx, gy * gy);
+        // the relaxed atan2, and within 1e-5 rad of the reference's one binning discontinuity
+        // (theta rounding to 8.0 is dropped) the oracle's atan2 (descriptor_fast's rule; rare)
+        float rot = atan2_relaxed(gy, gx);
         const float dd = fabs_(anglef - rot);
-        need = dd < 1e-5f || dd > 6.2831753f;
-        return m2 == 0.0f ? 0.0f : rot;
-    };
-    auto pixel = [&](float dxk, float sdy, float cdy, float m2, float rot, bool valid) {
+        if (dd < 1e-5f || dd > 6.2831753f) rot = atan2_(gy, gx);
+        rot = m2 == 0.0f ? 0.0f : rot;
         const float dnx = fma_(crspt, dxk, sdy);          // sdy = srspt dyk
         const float dny = fma_(-srspt, dxk, cdy);         // cdy = crspt dyk
         const float t = dnx + 2.5f, tv = dny + 2.5f;
@@ -2214,25 +2217,22 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
         const float th = take ? theta : 0.0f;
 #if SGK_DUAL_REF
         (void)u; (void)v;
-        const float c4[4] = {wt * (oxl[0] - dnx) * (oyl[0] - dny), wt * (dnx + oxl[1]) * (oyl[1] - dny),
-                             wt * (oxl[2] - dnx) * (dny + oyl[2]), wt * (dnx + oxl[3]) * (dny + oyl[3])};
+        const f2v cpa = wt * (f2v{oxl[0], oxl[1]} + f2v{-dnx, dnx}) * (f2v{oyl[0], oyl[1]} - dny);
+        const f2v cpb = wt * (f2v{oxl[2], oxl[3]} + f2v{-dnx, dnx}) * (f2v{oyl[2], oyl[3]} + dny);
 #else
+        const f2v xu = f2v{1.0f - u, u};
         const float wv1 = wt * v, wv0 = wt - wv1;                    // w (1 - v), w v
-        const float c4[4] = {fma_(-wv0, u, wv0), wv0 * u, fma_(-wv1, u, wv1), wv1 * u};
+        const f2v cpa = wv0 * xu, cpb = wv1 * xu;
 #endif
         // tent weights max(0, 1 - |theta - k|), bin 0 also taking the wrap of bin 8
-        // (ProgramCU.cu:1094), as descriptor_fast; then the outer product with the 4 cell weights
-        f2v tp[4];
-        tp[0] = f2v{__builtin_amdgcn_fmed3f(fmax_(1.0f - th, th - 7.0f), 0.0f, 1.0f),
-                    __builtin_amdgcn_fmed3f(1.0f - fabs_(th - 1.0f), 0.0f, 1.0f)};
+        // (ProgramCU.cu:1094), as descriptor_fast; then the outer product with the cell weights
 #pragma unroll
-        for (int p = 1; p < 4; p++)
-            tp[p] = f2v{__builtin_amdgcn_fmed3f(1.0f - fabs_(th - (float)(2 * p)), 0.0f, 1.0f),
-                        __builtin_amdgcn_fmed3f(1.0f - fabs_(th - (float)(2 * p + 1)), 0.0f, 1.0f)};
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-#pragma unroll
-            for (int p = 0; p < 4; p++) acc[k][p] = pk_fma(tp[p], c4[k], acc[k][p]);
+        for (int k = 0; k < 8; k++) {
+            const float tk = k == 0 ? __builtin_amdgcn_fmed3f(fmax_(1.0f - th, th - 7.0f), 0.0f, 1.0f)
+                                    : __builtin_amdgcn_fmed3f(1.0f - fabs_(th - (float)k), 0.0f, 1.0f);
+            acc[0][k] = pk_fma(cpa, tk, acc[0][k]);
+            acc[1][k] = pk_fma(cpb, tk, acc[1][k]);
+        }
     };
     // walk: rows y0 + cp, y0 + cp + 2, ...; each row's span in strips of 4 pixels whose gradient
     // neighbours come from 4 vector loads (as descriptor_fast), the next strip's loads issued
@@ -2254,14 +2254,14 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
     uint32_t npo = 4u * (uint32_t)(W + 1);   // row 1, column 1 when nothing is left (in-plane)
     auto fetch = [&]() {
         if (r <= y1) npo = 4u * (uint32_t)(r * W + cx);
-        na = ld4(npo - 4u);
-        nb = ld4(npo + 4u);
-        nu = ld4(npo - 4u * W);
-        nd = ld4(npo + 4u * W);
+        na = ld4(npo - 4u);            // x-1 .. x+2
+        nb = ld4(npo + 4u);            // x+1 .. x+4
+        nu = ld4(npo - 4u * W);        // row y-1, x .. x+3
+        nd = ld4(npo + 4u * W);        // row y+1, x .. x+3
     };
     fetch();
     while (r <= y1) {
-        const f4v pa = na, pb = nb, pu = nu, pd = nd;
+        const f4v gx = nb - na, gy = nd - nu;   // the strip's gradients (dx, dy per pixel)
         const float dyk = ((float)r + 0.5f) - key.y;
         const float sdy = srspt * dyk, cdy = crspt * dyk;
         const int nv = lo + len - cx;
@@ -2272,38 +2272,14 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
             next_row();
         }
         fetch();
-        const f4v gx = pb - pa, gy = pd - pu;
-        f4v m2, rot;
-        bool need[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            m2[i] = fma_(gx[i], gx[i], gy[i] * gy[i]);
-            rot[i] = angle(gx[i], gy[i], m2[i], need[i]);
-        }
-        if (need[0] || need[1] || need[2] || need[3]) {
-#pragma unroll 1
-            for (int i = 0; i < 4; i++) {
-                const float x = i == 0 ? gx[0] : i == 1 ? gx[1] : i == 2 ? gx[2] : gx[3];
-                const float y = i == 0 ? gy[0] : i == 1 ? gy[1] : i == 2 ? gy[2] : gy[3];
-                const bool nd_i = i == 0 ? need[0] : i == 1 ? need[1] : i == 2 ? need[2] : need[3];
-                const float ex = atan2_(y, x);
-                const float mm = i == 0 ? m2[0] : i == 1 ? m2[1] : i == 2 ? m2[2] : m2[3];
-                const float rr = nd_i && mm != 0.0f ? ex
-                               : (i == 0 ? rot[0] : i == 1 ? rot[1] : i == 2 ? rot[2] : rot[3]);
-                rot[0] = i == 0 ? rr : rot[0];
-                rot[1] = i == 1 ? rr : rot[1];
-                rot[2] = i == 2 ? rr : rot[2];
-                rot[3] = i == 3 ? rr : rot[3];
-            }
-        }
-        // one pixel at a time (sched_barrier): the four interleaved took ~150 VGPRs
-        pixel((xc) - key.x, sdy, cdy, m2[0], rot[0], true);
+        // one pixel at a time (sched_barrier): four interleaved took ~150 VGPRs
+        pixel((xc) - key.x, sdy, cdy, gx.x, gy.x, true);
         __builtin_amdgcn_sched_barrier(0);
-        pixel((xc + 1.0f) - key.x, sdy, cdy, m2[1], rot[1], nv > 1);
+        pixel((xc + 1.0f) - key.x, sdy, cdy, gx.y, gy.y, nv > 1);
         __builtin_amdgcn_sched_barrier(0);
-        pixel((xc + 2.0f) - key.x, sdy, cdy, m2[2], rot[2], nv > 2);
+        pixel((xc + 2.0f) - key.x, sdy, cdy, gx.z, gy.z, nv > 2);
         __builtin_amdgcn_sched_barrier(0);
-        pixel((xc + 3.0f) - key.x, sdy, cdy, m2[3], rot[3], nv > 3);
+        pixel((xc + 3.0f) - key.x, sdy, cdy, gx.w, gy.w, nv > 3);
     }
     // reduction: lanes 0..49 store their 32 bins ([lane][slot][bin], stride 33 floats against
     // bank conflicts); lane L then sums bins 2 sub, 2 sub + 1 of cell L >> 2 (descriptor_fast's
@@ -2311,11 +2287,11 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
     if (q < 25) {
         float* my = hist + lane * 33;
 #pragma unroll
-        for (int k = 0; k < 4; k++)
+        for (int h = 0; h < 2; h++)
 #pragma unroll
-            for (int p = 0; p < 4; p++) {
-                my[8 * k + 2 * p] = acc[k][p].x;
-                my[8 * k + 2 * p + 1] = acc[k][p].y;
+            for (int k = 0; k < 8; k++) {
+                my[8 * (2 * h) + k] = acc[h][k].x;
+                my[8 * (2 * h + 1) + k] = acc[h][k].y;
             }
     }
     asm volatile("" ::: "memory");

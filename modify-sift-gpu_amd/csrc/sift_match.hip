@@ -684,6 +684,9 @@ __global__ __launch_bounds__(64 * kRawWaves) void k_match_raw(const uint8_t* __r
     issue(c_begin + kTile, 1);
     __builtin_amdgcn_s_waitcnt(kWaitTile);
     __builtin_amdgcn_s_barrier();
+    // compiler memory barrier: the s_barrier intrinsic does not order memory operations for the
+    // compiler, and no LDS read of a tile buffer may move above the barrier that publishes its DMA
+    asm volatile("" ::: "memory");
     int bi = 0;
     for (int tb = c_begin; tb < c_end; tb += kTile) {
         issue(tb + 2 * kTile, bi == 0 ? 2 : bi - 1);
@@ -735,6 +738,7 @@ __global__ __launch_bounds__(64 * kRawWaves) void k_match_raw(const uint8_t* __r
         // tile t + 1's DMAs retired (t + 2's stay in flight), this tile's reads done
         __builtin_amdgcn_s_waitcnt(kWaitTile);
         __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");   // (as above: the next tile's reads stay below it)
         bi = bi == 2 ? 0 : bi + 1;
     }
     // no DMA may land after the workgroup's LDS is handed to another one
