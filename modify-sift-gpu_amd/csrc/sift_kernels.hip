@@ -934,18 +934,21 @@ __global__ __launch_bounds__(256, SGK_EXT2_WAVES) void k_extrema_wave2(const flo
     fetch(rA, ys);
     put(rA, ys);
     rowmm(hx1, hn1, cvx);
-    fetch(rA, ys + 1);
-    fetch(rB, ys + 2);
+    // rows past ye (the row below the segment's last tested row) feed no test: they are
+    // fetched clamped to ye, a row already read (cache hit, no HBM bytes).  Round 3 read 2 more
+    // rows per segment from HBM (1.19x the algorithmic bytes with 17-row segments).
+    fetch(rA, min(ys + 1, ye));
+    fetch(rB, min(ys + 2, ye));
     // each set is refetched after the row test that follows its put: the test's atomics (a
     // data-dependent number of them) then come before, not after, the loads that the next wait
     // must leave in flight
     for (int y = ys; y < ye; y += 2) {
         put(rA, y + 1);
         body(y);
-        fetch(rA, y + 3);
+        fetch(rA, min(y + 3, ye));
         put(rB, y + 2);
         body(y + 1);
-        fetch(rB, y + 4);
+        fetch(rB, min(y + 4, ye));
     }
 }
 
@@ -2656,6 +2659,9 @@ hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
 #ifndef SGK_EXT_CPL
 #define SGK_EXT_CPL 2
 #endif
+#ifndef SGK_EXT_SEG_MIN
+#define SGK_EXT_SEG_MIN 32
+#endif
     bool pairs = SGK_EXT_CPL == 2 && ((uintptr_t)pyr % 8) == 0;
     for (int o = 0; o < fp.n_octaves; o++)
         pairs = pairs && fp.oct[o].wa % 2 == 0 && fp.oct[o].gauss_off % 2 == 0 &&
@@ -2669,6 +2675,12 @@ hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
         const long long per_col = (long long)strips_x * fp.batch;
         int nseg = (int)std::min<long long>(std::max<long long>(1, (32768 + per_col - 1) / per_col),
                                             std::max(1, od.h / 16));
+        // a segment reads one halo row above and below it: 2/17 = 12 % extra bytes on the 17-row
+        // segments of the batch's upper octaves, so there segments get >= SGK_EXT_SEG_MIN rows
+        // while the octave keeps >= 8192 waves (a single image keeps its short segments: there
+        // the latency of the longest wave is the kernel's time)
+        if (o > 0 && per_col * (od.h / SGK_EXT_SEG_MIN) >= 8192)
+            nseg = std::min(nseg, std::max(1, od.h / SGK_EXT_SEG_MIN));
         const int rows = (od.h + nseg - 1) / nseg;
         nseg = (od.h + rows - 1) / rows;
         eg.wave0[o] = nw;

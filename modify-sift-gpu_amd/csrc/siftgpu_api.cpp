@@ -94,6 +94,10 @@ struct Runtime {
     std::vector<float> pending;
     int pending_orientation = 1;
     bool have_image = false;    // a pyramid of the current image exists on the device
+    // the current u8 gray image is staged in the context's device input: the reference uploads
+    // an image into its input texture once, when it is loaded (SiftGPU.cpp:317-328,
+    // GLTexImage.cpp:918-1009), and RunSIFT() on the loaded image reuses the texture
+    bool staged = false;
     // host seconds of the last image load / conversion (SiftGPU::_timing[0], SiftGPU.cpp:249,328)
     // and of the last feature downloads (keys: _timing[7], descriptors: part of _timing[8])
     float t_load = 0.f, t_keys = 0.f, t_desc = 0.f;
@@ -528,6 +532,7 @@ int SiftGPU::RunSIFT(int width, int height, const void* data, unsigned int gl_fo
     if (!set_image(IMG(_texImage), width, height, data, gl_format, gl_type, down_sampled))
         return 0;
     RT(_pyramid)->t_load = (float)(now_s() - t0);
+    RT(_pyramid)->staged = false;
     _image_loaded = 2;
     return RunSIFT();
 }
@@ -546,18 +551,34 @@ int SiftGPU::RunSIFT() {
         }
         rt->t_load = (float)(now_s() - t0);
         _image_loaded = 1;
+        rt->staged = false;
     } else if (_image_loaded == 1) {
         rt->t_load = 0.f;   // the file is already loaded (SiftGPU.cpp:348-351)
     }
     const int ch = img->color == SGPU_RGB || img->color == SGPU_BGR ? 3 : 4;
-    int rc = img->is_float
+    int rc;
+    if (!img->is_float && !img->color) {
+        // u8 gray: uploaded once per image (the load, _timing[0]), then every RunSIFT() on it
+        // starts from the device copy, as the reference's texture
+        if (!rt->staged) {
+            const double t0 = now_s();
+            rc = sgpu_stage_input(rt->ctx, img->u8.data(), 1, img->w, img->h, img->w);
+            rt->t_load += (float)(now_s() - t0);
+            rt->staged = rc == SGPU_OK;
+        }
+        rc = rt->staged ? sgpu_extract(rt->ctx, nullptr, 1, img->w, img->h, img->w, SGPU_INPUT_STAGED)
+                        : sgpu_extract(rt->ctx, img->u8.data(), 1, img->w, img->h, img->w,
+                                       SGPU_INPUT_HOST);
+    } else {
+        rt->staged = false;   // a host-input extract reuses the context's input buffer
+        rc = img->is_float
                  ? sgpu_extract_f32(rt->ctx, img->f32.data(), 1, img->w, img->h, img->w, SGPU_INPUT_HOST)
-             : img->color
-                 ? sgpu_extract_color(rt->ctx, img->u8.data(), 1, img->w, img->h, img->w * ch,
-                                      img->color, SGPU_INPUT_HOST)
-                 : sgpu_extract(rt->ctx, img->u8.data(), 1, img->w, img->h, img->w, SGPU_INPUT_HOST);
+                 : sgpu_extract_color(rt->ctx, img->u8.data(), 1, img->w, img->h, img->w * ch,
+                                      img->color, SGPU_INPUT_HOST);
+    }
     if (rc != SGPU_OK) {
         std::cerr << "SiftGPU: " << sgpu_last_error(rt->ctx) << "\n";
+        rt->staged = false;
         rt->feature_num = 0;
         rt->have_image = false;
         rt->pending.clear();

@@ -72,6 +72,72 @@ __global__ __launch_bounds__(256) void walk(const float* __restrict__ a, float* 
     if (lds_pad[threadIdx.x] == 1234.5f) sink[1] = 1.f;
 }
 
+
+// round-4 variants of the row-major walk (halo 16 columns a side, the FW 25 case):
+//   SW  store width per lane in floats (2: the level kernel's V-pass form, 4: 16 lanes per row)
+//   NT  non-temporal stores
+//   NC  chunks in flight (register sets)
+template <int SW, bool NT, int NC>
+__global__ __launch_bounds__(256) void walk2(const float* __restrict__ a, float* __restrict__ b, int BR,
+                                             float* __restrict__ sink) {
+    extern __shared__ float lds_pad[];
+    constexpr int HALO = 16, NQ = 16 + 2 * HALO / 4;
+    const int lane = threadIdx.x & 63;
+    const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int strips = W / 64, bands = (H + BR - 1) / BR;
+    const int sx = gw % strips, rest = gw / strips, band = rest % bands, img = rest / bands;
+    if (img >= N) return;
+    const float* s = a + (size_t)img * W * H;
+    float* d = b + (size_t)img * W * H;
+    const int g = lane >> 5, j = min(lane & 31, NQ - 1);
+    const int col = min(max(sx * 64 - HALO + 4 * j, 0), W - 4);
+    const int y0 = band * BR, y1 = min(H, y0 + BR);
+    const int nch = (y1 - y0 + 7) / 8;
+    float4 st[NC][4];
+    float hs = 0.f;
+    auto load = [&](float4 (&r)[4], int c) {
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            const int y = min(y0 + 8 * c + 2 * p + g, H - 1);
+            r[p] = *reinterpret_cast<const float4*>(s + (size_t)y * W + col);
+        }
+    };
+    // SW 2: lane (32 g + l) stores columns 2l, 2l+1 of rows 2p + g; SW 4: lane (16 q + l) stores
+    // columns 4l .. 4l+3 of rows 4 (p / 2) + q, two instructions per 4 rows
+    const int scol2 = sx * 64 + 2 * (lane & 31);
+    const int scol4 = sx * 64 + 4 * (lane & 15), q4 = lane >> 4;
+    auto step = [&](float4 (&r)[4], int c) {
+        if (c < nch) {
+#pragma unroll
+            for (int p = 0; p < 4; p++) {
+                hs += r[p].z + r[p].w;
+                if (SW == 2) {
+                    const int y = y0 + 8 * c + 2 * p + g;
+                    typedef float v2 __attribute__((ext_vector_type(2)));
+                    v2* q = reinterpret_cast<v2*>(d + (size_t)y * W + scol2);
+                    const v2 v = {r[p].x, r[p].y};
+                    if (NT) __builtin_nontemporal_store(v, q); else *q = v;
+                } else if ((p & 1) == 0) {
+                    const int y = y0 + 8 * c + 4 * (p >> 1) + q4;
+                    typedef float v4 __attribute__((ext_vector_type(4)));
+                    v4* q = reinterpret_cast<v4*>(d + (size_t)y * W + scol4);
+                    const v4 v = {r[p].x, r[p].y, r[p + 1].x, r[p + 1].y};
+                    if (NT) __builtin_nontemporal_store(v, q); else *q = v;
+                }
+            }
+        }
+        load(r, c + NC);
+    };
+#pragma unroll
+    for (int k = 0; k < NC; k++) load(st[k], k);
+    for (int c = 0; c < nch; c += NC) {
+#pragma unroll
+        for (int k = 0; k < NC; k++) step(st[k], c + k);
+    }
+    if (hs == 1234.5f) sink[0] = hs;
+    if (lds_pad[threadIdx.x] == 1234.5f) sink[1] = 1.f;
+}
+
 typedef float f4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void copy_flat(const f4* __restrict__ a, f4* __restrict__ b, size_t n) {
     const size_t i = blockIdx.x * (size_t)256 + threadIdx.x;
@@ -108,21 +174,16 @@ int main() {
     };
     run("flat float4 copy", [&] { copy_flat<<<(n / 4 + 255) / 256, 256>>>((const f4*)a, (f4*)b, n / 4); });
     const size_t lds = 47 * 1024;   // 3 workgroups (12 waves) per CU, as k_gauss_lean
-    for (int br : {1080, 544, 272}) {
-        const int waves = N * (W / 64) * ((H + br - 1) / br);
-        const int blocks = (waves + 3) / 4;
-        char nm[80];
-#define RUN(L, HL, LN)                                                                       \
-        snprintf(nm, sizeof nm, "%s halo %2d band %4d", LN, HL, br);                          \
-        run(nm, [&] { walk<L, HL><<<blocks, 256, lds>>>(a, b, br, sink); });
-        RUN(0, 0, "rm  ") RUN(1, 0, "sm  ") RUN(2, 0, "tile")
-        RUN(0, 16, "rm  ") RUN(1, 16, "sm  ") RUN(2, 16, "tile")
-    }
-    // 4 waves per SIMD instead of 3 (occupancy sensitivity)
     {
         const int br = 1080, waves = N * (W / 64), blocks = (waves + 3) / 4;
-        run("rm   halo 16 band 1080 16w/CU", [&] { walk<0, 16><<<blocks, 256, 36 * 1024>>>(a, b, br, sink); });
-        run("tile halo 16 band 1080 16w/CU", [&] { walk<2, 16><<<blocks, 256, 36 * 1024>>>(a, b, br, sink); });
+        char nm[80];
+        run("rm   halo 16 band 1080 (round 4 ref)", [&] { walk<0, 16><<<blocks, 256, lds>>>(a, b, br, sink); });
+#define RUN2(SW, NT, NC, L, LN)                                                                  \
+        snprintf(nm, sizeof nm, "walk2 st%d nt%d nc%d %s", SW, NT, NC, LN);                     \
+        run(nm, [&] { walk2<SW, NT, NC><<<blocks, 256, L>>>(a, b, br, sink); });
+        RUN2(2, 0, 4, lds, "12w") RUN2(4, 0, 4, lds, "12w") RUN2(2, 1, 4, lds, "12w")
+        RUN2(4, 1, 4, lds, "12w") RUN2(2, 0, 6, lds, "12w") RUN2(2, 0, 2, lds, "12w")
+        RUN2(2, 0, 4, 0, "nolds") RUN2(4, 1, 4, 0, "nolds") RUN2(2, 0, 4, 64 * 1024, "8w")
     }
     return 0;
 }
