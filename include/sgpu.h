@@ -216,7 +216,8 @@ void sgpu_quantize_descriptors(const float* d, size_t count, uint8_t* out);
  * (SiftGPU::_timing, SiftPyramid.cpp:48-56).  times[0..7] =
  * {upload, pyramid, detect, orientation, expand, descriptor, download, total} of the last
  * extract; times[8] = the last sgpu_match call; times[9] = the feature-list (row scan) part of
- * detect.  SiftGPU::_timing[2..8] map them to the reference's slots (siftgpu_api.cpp). */
+ * detect; times[10], [11] = the key and descriptor copies of the last sgpu_copy_features.
+ * SiftGPU::_timing[2..8] map them to the reference's slots (siftgpu_api.cpp). */
 int sgpu_last_timing(const sgpu_ctx* ctx, float* times, int n);
 
 /* ---- multi-GPU batch driver (no reference counterpart: the reference
@@ -264,9 +265,10 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
 #define SGPU_DEBUG_MATCH_REGSTAGE 2048 /* keyless plain matching through the register-staged
                                           k_match_rows<..., RAW> instead of the LDS-DMA
                                           k_match_raw: same pairs */
-#define SGPU_DEBUG_PYR_SERIAL 4096 /* every pyramid octave on the part's main stream (the
-                                      shipped path runs octaves >= 1 on a second stream beside
-                                      octave 0's last levels): same levels */
+#define SGPU_DEBUG_PYR_SERIAL 4096 /* the pyramid octave by octave, one level per launch (the
+                                      shipped path runs octave o+1's first levels in the same
+                                      launches as octave o's last ones; the stream layout runs
+                                      octaves >= 1 on a second stream): same levels */
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);

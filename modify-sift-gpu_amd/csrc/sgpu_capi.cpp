@@ -52,7 +52,7 @@ struct DevBuf {
 // reference's "Detection" and "Feature List" stages, SiftPyramid.cpp:107,123); T_LIST is the
 // row-scan part of it
 enum { T_UPLOAD, T_PYRAMID, T_DETECT, T_ORIENT, T_EXPAND, T_DESC, T_DOWNLOAD, T_TOTAL, T_MATCH,
-       T_LIST, T_N };
+       T_LIST, T_COPY_KEYS, T_COPY_DESC, T_N };
 
 // One part of a batch: consecutive images [img0, img0 + n) with their own stream and buffers.
 struct Part {
@@ -505,7 +505,6 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     // (k_gauss_wave) for the whole part.  Level kds = level_ds - level_min of octave o also writes
     // its 2x decimation as level 0 of octave o+1 (PyramidCU.cpp:1024).
     float* pyr = pt.pyr.as<float>();
-    sgk::Taps taps;
     sgk::Taps ltaps[sgk::kMaxLevels], taps0;
     int lfw[sgk::kMaxLevels] = {0};
     for (int k = 1; k < nlev; k++)
@@ -518,10 +517,15 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     // 3.69-3.74 ms per 128 x 1080p), and the main stream waits for them before
     // the extremum kernel.  SGPU_DEBUG_PYR_SERIAL: one stream for the pyramid only.
     const bool side = noct > 1 && !pt.one_stream && !(ctx->debug_flags & SGPU_DEBUG_PYR_SERIAL);
+    const int wave_rows = (ctx->debug_flags & SGPU_DEBUG_GAUSS_BLOCK) ? -1 : (ctx->debug_flags >> 16);
+    // the level filters of every octave: op (o, k) filters level k-1 into level k (op (0, 0)
+    // smooths the input into level 0); level kds of octave o also writes its decimation, level 0
+    // of octave o+1
+    struct Op { sgk::LevelOp op; int o, k; };
+    std::vector<Op> ops;
+    ops.reserve((size_t)noct * nlev);
     for (int o = 0; o < noct; o++) {
         const sgk::OctaveDesc& od = fp.oct[o];
-        const hipStream_t so = side && o >= 1 ? pt.stream_oct : st;
-        if (side && o == 1) HIPCHK(ctx, hipStreamWaitEvent(so, pt.ev_ds, 0));
         const long long npx = (long long)od.wa * od.h;
         float* lvl0 = pyr + od.gauss_off;
         float* ds = nullptr;
@@ -534,8 +538,6 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
             dsh = nd.h;
             ds_stride = (long long)nd.wa * nd.h;
         }
-        // filter op k: op 0 (octave 0 only) smooths the input into level 0, op k >= 1 filters
-        // level k-1 into level k
         const float* in_f = srcf;
         const uint8_t* in_8 = src8;
         int in_stride = stride;
@@ -553,18 +555,56 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
             in_img = npx;
         }
         for (int k = (o == 0 ? 0 : 1); k < nlev; k++) {
-            const int fwk = k == 0 ? fw0 : lfw[k];
+            Op e{};
+            e.o = o;
+            e.k = k;
+            sgk::LevelOp& op = e.op;
+            op.fw = k == 0 ? fw0 : lfw[k];
             const float* tk = k == 0 ? taps0.k : ltaps[k].k;
-            for (int i = 0; i < fwk; i++) taps.k[i] = tk[i];
+            for (int i = 0; i < op.fw; i++) op.taps.k[i] = tk[i];
             const bool dk = ds && kds == k;
-            HIPCHK(ctx, sgk::launch_gauss(k == 0 ? in_f : lvl0 + (k - 1) * od.level_stride,
-                                          k == 0 ? in_8 : nullptr, k == 0 ? in_stride : od.wa,
-                                          k == 0 ? in_img : npx, lvl0 + k * od.level_stride,
-                                          npx, od.wa, od.h, fwk, taps, n, dk ? ds : nullptr,
-                                          dk ? dsw : 0, dk ? dsh : 0, dk ? ds_stride : 0, so,
-                                          (ctx->debug_flags & SGPU_DEBUG_GAUSS_BLOCK)
-                                              ? -1 : (ctx->debug_flags >> 16)));
-            if (side && o == 0 && dk) HIPCHK(ctx, hipEventRecord(pt.ev_ds, st));
+            op.src = k == 0 ? in_f : lvl0 + (k - 1) * od.level_stride;
+            op.src_u8 = k == 0 ? in_8 : nullptr;
+            op.src_stride = k == 0 ? in_stride : od.wa;
+            op.src_img_stride = k == 0 ? in_img : npx;
+            op.dst = lvl0 + k * od.level_stride;
+            op.dst_img_stride = npx;
+            op.w = od.wa;
+            op.h = od.h;
+            op.batch = n;
+            op.ds_dst = dk ? ds : nullptr;
+            op.ds_w = dk ? dsw : 0;
+            op.ds_h = dk ? dsh : 0;
+            op.ds_img_stride = dk ? ds_stride : 0;
+            ops.push_back(e);
+        }
+    }
+    if (side || (ctx->debug_flags & SGPU_DEBUG_PYR_SERIAL) || kds < 1) {
+        // octave by octave, one level per launch (octaves >= 1 on the side stream in the
+        // stream layout)
+        for (const Op& e : ops) {
+            const hipStream_t so = side && e.o >= 1 ? pt.stream_oct : st;
+            if (side && e.o == 1 && e.k == 1) HIPCHK(ctx, hipStreamWaitEvent(so, pt.ev_ds, 0));
+            HIPCHK(ctx, sgk::launch_gauss_op(e.op, so, wave_rows));
+            if (side && e.o == 0 && e.k == kds && e.op.ds_dst) HIPCHK(ctx, hipEventRecord(pt.ev_ds, st));
+        }
+    } else {
+        // Diagonal schedule: op (o, k) in slot o * kds + k.  Its inputs come
+        // from earlier slots -- (o, k-1), and for k = 1 octave o-1's level kds (slot o * kds)
+        // -- so the ops of a slot are independent and share a launch: octave o+1's levels 1, 2
+        // run beside octave o's levels kds+1, kds+2 (15 launches instead of 21 for -no 4 -d 3),
+        // the small jobs' latency-bound waves filling the large ones' CU slots.
+        int last = 0;
+        for (const Op& e : ops) last = std::max(last, e.o * kds + e.k);
+        for (int slot = 0; slot <= last; slot++) {
+            const sgk::LevelOp* in_slot[sgk::kMaxOctaves];
+            int m = 0;
+            for (const Op& e : ops)
+                if (e.o * kds + e.k == slot) in_slot[m++] = &e.op;
+            int i = 0;
+            for (; i + 1 < m; i += 2)
+                HIPCHK(ctx, sgk::launch_gauss_two(*in_slot[i], *in_slot[i + 1], st, wave_rows));
+            if (i < m) HIPCHK(ctx, sgk::launch_gauss_op(*in_slot[i], st, wave_rows));
         }
     }
     if (side) {
@@ -1571,15 +1611,21 @@ int sgpu_copy_features(sgpu_ctx* ctx, int image, float* keys, float* descriptors
     const int li = image - pt.img0;
     const int64_t a = pt.img_off[li], nf = pt.img_off[li + 1] - a;
     if (nf <= 0) return SGPU_OK;
+    if (descriptors && !ctx->opt.descriptors) return ctx->fail(SGPU_EINVAL, "descriptors disabled (-sd)");
+    // both copies, then one synchronisation; events split the time between them
+    // (sgpu_last_timing slots 10, 11)
+    HIPCHK(ctx, hipEventRecord(ctx->ev[T_COPY_KEYS], ctx->stream));
     if (keys)
         HIPCHK(ctx, hipMemcpyAsync(keys, pt.keys.as<float4>() + a, nf * sizeof(float4),
                                    hipMemcpyDeviceToHost, ctx->stream));
-    if (descriptors) {
-        if (!ctx->opt.descriptors) return ctx->fail(SGPU_EINVAL, "descriptors disabled (-sd)");
+    HIPCHK(ctx, hipEventRecord(ctx->ev[T_COPY_DESC], ctx->stream));
+    if (descriptors)
         HIPCHK(ctx, hipMemcpyAsync(descriptors, pt.desc.as<float>() + a * 128,
                                    nf * 128 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
-    }
+    HIPCHK(ctx, hipEventRecord(ctx->ev[T_N], ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    (void)hipEventElapsedTime(&ctx->timing[T_COPY_KEYS], ctx->ev[T_COPY_KEYS], ctx->ev[T_COPY_DESC]);
+    (void)hipEventElapsedTime(&ctx->timing[T_COPY_DESC], ctx->ev[T_COPY_DESC], ctx->ev[T_N]);
     return SGPU_OK;
 }
 

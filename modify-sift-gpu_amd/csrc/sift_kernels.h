@@ -51,6 +51,28 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         float* ds_dst, int ds_w, int ds_h, long long ds_img_stride,
                         hipStream_t stream, int wave_rows = -1);
 
+// One level filter of a pyramid stage (the arguments of launch_gauss).
+struct LevelOp {
+    const float* src;
+    const uint8_t* src_u8;
+    int src_stride;
+    long long src_img_stride;
+    float* dst;
+    long long dst_img_stride;
+    int w, h, fw;
+    Taps taps;
+    int batch;
+    float* ds_dst;
+    int ds_w, ds_h;
+    long long ds_img_stride;
+};
+hipError_t launch_gauss_op(const LevelOp& op, hipStream_t stream, int wave_rows);
+// Two independent level filters (no data dependence between them) in one launch of the
+// wave-streaming kernel when their widths have a compiled pair, f32 sources and no decimation
+// (the "diagonal" schedule of the pyramid: octave o+1's level k beside octave o's level k + kds);
+// otherwise two launches.  Bit-identical to two launch_gauss calls.
+hipError_t launch_gauss_two(const LevelOp& a, const LevelOp& b, hipStream_t stream, int wave_rows);
+
 // First octave of -fo != 0 (BuildPyramid, PyramidCU.cpp:1011-1016): the batch's input
 // (u8 p/255 or f32; tw = w & ~3 columns used, rows `stride` apart) resampled into dst
 // (dw x dh per image, dst_img_stride apart): SampleImageD by 2^fo for fo > 0, UpsampleKernel

@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
+#include <utility>
 
 #include "sift_kernels.h"
 #include "sift_math.h"
@@ -363,37 +364,79 @@ static GaussWaveGrid gauss_wave_grid(int w, int h, int batch, int rows_hint, int
 //     base for the 4 rows where only it has wrapped;
 //   * u8 -> f32 (the ingest level) on row pairs with packed multiply / fma;
 //   * the decimation into the next octave's level 0 is a template parameter.
+#ifndef SGK_LEAN_R24
+#define SGK_LEAN_R24 0   // 1: 3-slot ring for FW <= 17, 16 waves per CU: measured slower (3.76-3.77 vs 3.71-3.75 ms)
+#endif
+// f(integral_constant<int, I>) for I in the sequence, in order (compile-time step indices)
+template <int... I, class F>
+__device__ __forceinline__ void unrolled_steps(std::integer_sequence<int, I...>, F&& f) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+
+// One level filter job of a launch: source (u8 or f32), destination, geometry, taps, the
+// optional decimation into the next octave's level 0, and the wave grid.
+struct GaussJob {
+    const float* src;
+    const uint8_t* src8;
+    int src_stride;
+    long long src_img_stride;
+    float* dst;
+    long long dst_img_stride;
+    int W, H;
+    Taps taps;
+    float* ds;
+    int dsw, dsh;
+    long long ds_img_stride;
+    GaussWaveGrid gg;
+};
+
+// LDS geometry of the level filter for width FW (per wave)
+template <int FW>
+struct LeanGeom {
+    static constexpr int HALF = FW >> 1;
+    static constexpr int OFF = (-HALF) & 3;                  // LDS column of the strip's first input
+    static constexpr int IN_W = GT + FW - 1 + OFF;           // input columns held per row
+    static constexpr int NQ = (IN_W + 3) / 4;                // aligned quads per row
+    static constexpr int SH = OFF & 1;
+    static constexpr int IN_S0 = (4 * NQ + SH + 3) & ~3;
+    static constexpr int IN_S = IN_S0 + ((2 - IN_S0) & 31);  // float2 per row pair (= 2 mod 32)
+    static constexpr int LAG = (FW - 1 + WCH - 1) / WCH;     // chunks between H and V of a row
+    // ring rows: 3 slots of WCH for FW <= 17 (LAG <= 2; SGK_LEAN_R24), 4 for FW <= 25, 8 for
+    // FW 27 .. 33 (LAG 4)
+    static constexpr int RS = (SGK_LEAN_R24 && WCH * (LAG + 1) <= 24) ? 24
+                            : WCH * (LAG + 1) <= 32 ? 32 : 64;
+    static constexpr int HS = GT + SGK_GW_HSPAD;             // ring row stride (floats)
+    static constexpr int IN_WORDS = (WCH / 2) * IN_S + 8;    // float2: row pairs + 2 pad slots
+    static constexpr int RING_WORDS = RS * HS;               // floats
+};
+
+// The level filter of one wave (global wave index gw of job J) with its LDS buffers s_in / s_h.
 template <int FW, bool U8, bool DS>
-__global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
-    const float* __restrict__ src, const uint8_t* __restrict__ src8, int src_stride,
-    long long src_img_stride, float* __restrict__ dst, long long dst_img_stride, int W, int H,
-    Taps taps, float* __restrict__ ds, int dsw, int dsh, long long ds_img_stride,
-    GaussWaveGrid gg) {
-    constexpr int HALF = FW >> 1;
-    constexpr int OFF = (-HALF) & 3;                  // LDS column of the strip's first input
-    constexpr int IN_W = GT + FW - 1 + OFF;           // input columns held per row
-    constexpr int NQ = (IN_W + 3) / 4;                // aligned quads per row
+__device__ __forceinline__ void gauss_lean_wave(const GaussJob& J, int gw, f2v* s_in, float* s_h) {
+    using G = LeanGeom<FW>;
+    constexpr int HALF = G::HALF, OFF = G::OFF, NQ = G::NQ, SH = G::SH, IN_S = G::IN_S;
     static_assert(NQ <= 32, "a row's quads fit half a wave");
     constexpr int NRD = (FW + 3) / 2;                 // ds_read_b128 per H-pass lane
-    constexpr int SH = OFF & 1;
-    constexpr int IN_S0 = (4 * NQ + SH + 3) & ~3;
-    constexpr int IN_S = IN_S0 + ((2 - IN_S0) & 31);  // float2 per row pair (= 2 mod 32)
     static_assert(IN_S % 32 == 2 && 4 * NQ + SH <= IN_S, "row-pair stride");
-    constexpr int LAG = (FW - 1 + WCH - 1) / WCH;     // chunks between H and V of a row
-    // ring rows: 4 slots of WCH for FW <= 25, 8 slots for FW 27 .. 33 (LAG 4)
-    constexpr int RS = WCH * (LAG + 1) <= 32 ? 32 : 64;
+    constexpr int LAG = G::LAG, RS = G::RS, HS = G::HS;
     constexpr int NSLOT = RS / WCH;
     static_assert(WCH * (LAG + 1) <= RS && FW <= 33, "the ring's chunk slots hold the lag");
-    constexpr int HS = GT + SGK_GW_HSPAD;             // ring row stride (floats)
     constexpr int NPAIR = WCH / 2;
     constexpr int NST = 4;                            // chunks in registers
-    __shared__ __attribute__((aligned(16))) f2v s_in_all[kGwWaves][NPAIR * IN_S + 8];   // + 2 pad slots
-    __shared__ __attribute__((aligned(16))) float s_h_all[kGwWaves][RS * HS];
+    const float* __restrict__ src = J.src;
+    const uint8_t* __restrict__ src8 = J.src8;
+    const int src_stride = J.src_stride;
+    const long long src_img_stride = J.src_img_stride;
+    float* __restrict__ dst = J.dst;
+    const long long dst_img_stride = J.dst_img_stride;
+    const int W = J.W, H = J.H;
+    const Taps& taps = J.taps;
+    float* __restrict__ ds = J.ds;
+    const int dsw = J.dsw, dsh = J.dsh;
+    const long long ds_img_stride = J.ds_img_stride;
+    const GaussWaveGrid& gg = J.gg;
 
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // XCD-aware order (xcd_block)
-    const int gw = xcd_block(blockIdx.x, gridDim.x) * kGwWaves + wave;
     if (gw >= gg.total_waves) return;                 // uniform per wave
     const int sx = gw % gg.strips_x, rest = gw / gg.strips_x;
     const int x0 = sx * GT;
@@ -401,8 +444,6 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
     const int yb = sy * gg.rows_per_band;
     const int ye = min(H, yb + gg.rows_per_band);
     const int nchunk_out = (ye - yb + WCH - 1) / WCH;
-    f2v* s_in = s_in_all[wave];
-    float* s_h = s_h_all[wave];
 
     const float* sf = U8 ? nullptr : src + (long long)b * src_img_stride;
     const uint8_t* s8 = U8 ? src8 + (long long)b * src_img_stride : nullptr;
@@ -428,7 +469,7 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
 
     struct Elem { float4 v0, v1; };   // the raw fetch of rows 2p, 2p+1 (u8: .x as the u32)
     Elem st[NST][2];
-    auto load_chunk = [&](Elem (&stage)[2], int c) {
+    auto load_chunk = [&](Elem (&stage)[2], int c) __attribute__((always_inline)) {
         const int rb = yb - HALF + WCH * c;           // first input row of chunk c (uniform)
         if (rb >= 0 && rb + WCH <= H) {
 #pragma unroll
@@ -459,7 +500,7 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
             }
         }
     };
-    auto store_chunk = [&](const Elem (&stage)[2]) {
+    auto store_chunk = [&](const Elem (&stage)[2]) __attribute__((always_inline)) {
 #pragma unroll
         for (int m = 0; m < 2; m++) {
             f2v pr[4];   // column t of the quad: (row 2p, row 2p+1)
@@ -514,7 +555,7 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
     const uint32_t ds_off = (uint32_t)(2 * vq * dsw + (x >> 1));
     // step c (ring slot K = c mod 4): H pass of input chunk c, V pass of output chunk c - LAG,
     // loads of chunk c + NST into `nxt`, chunk c + 1 (`cur`) into the row-pair buffer
-    auto step = [&](int c, auto KC, Elem (&cur)[2], Elem (&nxt)[2]) {
+    auto step = [&](int c, auto KC, Elem (&cur)[2], Elem (&nxt)[2]) __attribute__((always_inline)) {
         constexpr int K = decltype(KC)::value;
         {   // H pass -> ring rows 8K .. 8K+7
             f2v a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};   // columns hc+i
@@ -536,7 +577,7 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
         asm volatile("" ::: "memory");
         const int kout = c - LAG;
         if (active && kout >= 0 && kout < nchunk_out) {   // V pass of output chunk kout (uniform)
-            constexpr int KV = (K - LAG) & (NSLOT - 1);      // its ring slot
+            constexpr int KV = ((K - LAG) % NSLOT + NSLOT) % NSLOT;   // its ring slot
             f2v acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};   // rows t0+j
 #pragma unroll
             for (int m = 0; m < FW + 3; m++) {
@@ -587,18 +628,49 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(
     };
     const int nsteps = nchunk_out + LAG;
     // slot K = c mod NSLOT, register set c mod NST (steps past the end filter clamped rows and
-    // store nothing)
-    for (int c = 0; c < nsteps; c += NSLOT) {
-        step(c + 0, std::integral_constant<int, 0>{}, st[1], st[0]);
-        step(c + 1, std::integral_constant<int, 1>{}, st[2], st[1]);
-        step(c + 2, std::integral_constant<int, 2>{}, st[3], st[2]);
-        step(c + 3, std::integral_constant<int, 3>{}, st[0], st[3]);
-        if constexpr (NSLOT == 8) {
-            step(c + 4, std::integral_constant<int, 4>{}, st[1], st[0]);
-            step(c + 5, std::integral_constant<int, 5>{}, st[2], st[1]);
-            step(c + 6, std::integral_constant<int, 6>{}, st[3], st[2]);
-            step(c + 7, std::integral_constant<int, 7>{}, st[0], st[3]);
-        }
+    // store nothing): the loop is unrolled by lcm(NSLOT, NST) steps
+    constexpr int U = NSLOT % NST == 0 ? NSLOT : NSLOT * NST;
+    for (int c = 0; c < nsteps; c += U) {
+        unrolled_steps(std::make_integer_sequence<int, U>{}, [&](auto KI) __attribute__((always_inline)) {
+            constexpr int k = decltype(KI)::value;
+            step(c + k, std::integral_constant<int, k % NSLOT>{}, st[(k + 1) % NST], st[k % NST]);
+        });
+    }
+}
+
+template <int FW, bool U8, bool DS>
+__global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(const GaussJob J) {
+    using G = LeanGeom<FW>;
+    __shared__ __attribute__((aligned(16))) f2v s_in_all[kGwWaves][G::IN_WORDS];
+    __shared__ __attribute__((aligned(16))) float s_h_all[kGwWaves][G::RING_WORDS];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // XCD-aware order (xcd_block)
+    const int gw = xcd_block(blockIdx.x, gridDim.x) * kGwWaves + wave;
+    gauss_lean_wave<FW, U8, DS>(J, gw, s_in_all[wave], s_h_all[wave]);
+}
+
+// Two independent level jobs in one launch ("diagonal": octave o + 1's level k beside octave o's
+// level k + kds): blocks [0, nbB) run job B (the small one, dispatched first),
+// blocks [nbB, nbB + nbA) job A; nbB is a multiple of 8, so each job keeps the XCD-aware order.
+// The LDS buffers are sized for the larger geometry; f32 levels without decimation only.
+template <int FWA, int FWB>
+__global__ __launch_bounds__(64 * kGwWaves) void k_gauss_diag(const GaussJob A, const GaussJob B,
+                                                              int nbB) {
+    using GA = LeanGeom<FWA>;
+    using GB = LeanGeom<FWB>;
+    constexpr int IW = GA::IN_WORDS > GB::IN_WORDS ? GA::IN_WORDS : GB::IN_WORDS;
+    constexpr int RW = GA::RING_WORDS > GB::RING_WORDS ? GA::RING_WORDS : GB::RING_WORDS;
+    __shared__ __attribute__((aligned(16))) f2v s_in_all[kGwWaves][IW];
+    __shared__ __attribute__((aligned(16))) float s_h_all[kGwWaves][RW];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int bid = blockIdx.x;
+    if (bid < nbB) {
+        gauss_lean_wave<FWB, false, false>(B, xcd_block(bid, nbB) * kGwWaves + wave,
+                                           s_in_all[wave], s_h_all[wave]);
+    } else {
+        const int nbA = (int)gridDim.x - nbB;
+        gauss_lean_wave<FWA, false, false>(A, xcd_block(bid - nbB, nbA) * kGwWaves + wave,
+                                           s_in_all[wave], s_h_all[wave]);
     }
 }
 
@@ -612,10 +684,10 @@ hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
     if (vec && wave_rows >= 0) {
         const GaussWaveGrid gg = gauss_wave_grid(w, h, batch, wave_rows, 1);
         const dim3 wgrid((unsigned)((gg.total_waves + kGwWaves - 1) / kGwWaves));
+        const GaussJob J{src, src8, src_stride, src_img_stride, dst, dst_img_stride, w, h, taps,
+                         ds, dsw, dsh, ds_img_stride, gg};
 #define SGK_LEAN(U8, DS)                                                                      \
-        hipLaunchKernelGGL((k_gauss_lean<FW, U8, DS>), wgrid, dim3(64 * kGwWaves), 0, stream, src, \
-                           src8, src_stride, src_img_stride, dst, dst_img_stride, w, h, taps, ds, \
-                           dsw, dsh, ds_img_stride, gg)
+        hipLaunchKernelGGL((k_gauss_lean<FW, U8, DS>), wgrid, dim3(64 * kGwWaves), 0, stream, J)
         if (src8) {
             if (ds) SGK_LEAN(true, true); else SGK_LEAN(true, false);
         } else {
@@ -2604,6 +2676,54 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
         default: return hipErrorInvalidValue;
     }
 #undef SGK_GAUSS
+}
+
+hipError_t launch_gauss_op(const LevelOp& op, hipStream_t stream, int wave_rows) {
+    return launch_gauss(op.src, op.src_u8, op.src_stride, op.src_img_stride, op.dst,
+                        op.dst_img_stride, op.w, op.h, op.fw, op.taps, op.batch, op.ds_dst,
+                        op.ds_w, op.ds_h, op.ds_img_stride, stream, wave_rows);
+}
+
+static bool diag_ok(const LevelOp& op) {
+    return !op.src_u8 && !op.ds_dst && op.src && (op.src_stride % 4) == 0 &&
+           (op.src_img_stride % 4) == 0 && (op.w % 4) == 0 && op.w >= 4 &&
+           ((uintptr_t)op.src % 16) == 0;
+}
+
+template <int FWA, int FWB>
+static hipError_t gauss_diag_launch(const LevelOp& a, const LevelOp& b, hipStream_t stream,
+                                    int wave_rows) {
+    const GaussWaveGrid ga = gauss_wave_grid(a.w, a.h, a.batch, wave_rows, 1);
+    const GaussWaveGrid gb = gauss_wave_grid(b.w, b.h, b.batch, wave_rows, 1);
+    const int nbA = (ga.total_waves + kGwWaves - 1) / kGwWaves;
+    const int nbB = (gb.total_waves + kGwWaves - 1) / kGwWaves;
+    const int nbBp = (nbB + 7) / 8 * 8;   // job A starts on XCD 0 (blocks are dealt round-robin)
+    const GaussJob A{a.src, nullptr, a.src_stride, a.src_img_stride, a.dst, a.dst_img_stride, a.w,
+                     a.h, a.taps, nullptr, 0, 0, 0, ga};
+    GaussJob B{b.src, nullptr, b.src_stride, b.src_img_stride, b.dst, b.dst_img_stride, b.w,
+               b.h, b.taps, nullptr, 0, 0, 0, gb};
+    // the padding blocks of job B map to waves past its grid (gauss_lean_wave returns)
+    B.gg.total_waves = gb.total_waves;
+    hipLaunchKernelGGL((k_gauss_diag<FWA, FWB>), dim3((unsigned)(nbBp + nbA)), dim3(64 * kGwWaves),
+                       0, stream, A, B, nbBp);
+    return hipGetLastError();
+}
+
+hipError_t launch_gauss_two(const LevelOp& a, const LevelOp& b, hipStream_t stream, int wave_rows) {
+    if (wave_rows >= 0 && diag_ok(a) && diag_ok(b)) {
+        // the default schedule's pairs (-d 3: levels 4 / 5 of octave o beside levels 1 / 2 of
+        // octave o + 1); the larger job is A
+        const bool swap = (long long)a.w * a.h * a.batch < (long long)b.w * b.h * b.batch;
+        const LevelOp& big = swap ? b : a;
+        const LevelOp& small = swap ? a : b;
+#define SGK_DIAG(A, B) \
+        if (big.fw == A && small.fw == B) return gauss_diag_launch<A, B>(big, small, stream, wave_rows);
+        SGK_DIAG(21, 11) SGK_DIAG(25, 13)
+#undef SGK_DIAG
+    }
+    hipError_t e = launch_gauss_op(a, stream, wave_rows);
+    if (e != hipSuccess) return e;
+    return launch_gauss_op(b, stream, wave_rows);
 }
 
 hipError_t launch_color_to_gray(const uint8_t* src, int n, int w, int h, int stride,

@@ -431,13 +431,16 @@ static int fetch_features(Runtime* rt) {
     rt->feature_num = sgpu_feature_count(rt->ctx, 0);
     rt->keys.resize((size_t)rt->feature_num * 4);
     rt->desc.resize(rt->opt.descriptors ? (size_t)rt->feature_num * 128 : 0);
+    // keys and descriptors in one call (one synchronisation); the key copy's event time is
+    // _timing[7], the rest of the call goes with the descriptors into _timing[8]
     const double t0 = now_s();
-    int rc = sgpu_copy_features(rt->ctx, 0, rt->keys.data(), nullptr);
-    const double t1 = now_s();
-    if (rc == SGPU_OK && rt->opt.descriptors)
-        rc = sgpu_copy_features(rt->ctx, 0, nullptr, rt->desc.data());
-    rt->t_keys = (float)(t1 - t0);
-    rt->t_desc = (float)(now_s() - t1);
+    int rc = sgpu_copy_features(rt->ctx, 0, rt->keys.data(),
+                                rt->opt.descriptors ? rt->desc.data() : nullptr);
+    const double t = now_s() - t0;
+    float ct[12] = {0};
+    sgpu_last_timing(rt->ctx, ct, 12);
+    rt->t_keys = std::min((float)t, ct[10] * 1e-3f);
+    rt->t_desc = (float)t - rt->t_keys;
     return rc;
 }
 
