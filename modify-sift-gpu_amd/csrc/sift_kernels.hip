@@ -1072,6 +1072,40 @@ __global__ __launch_bounds__(256) void k_scan_block(const uint32_t* __restrict__
     }
 }
 
+// Exclusive scan of a short array (a single image's rows or candidates: C2) by one workgroup
+// in tiles of 4096, the running total carried across tiles: one launch instead of the three of
+// the block scan (each a few microseconds of launch latency at these sizes).
+__global__ __launch_bounds__(1024) void k_scan_single(const uint32_t* __restrict__ in,
+                                                      uint32_t* __restrict__ out, size_t n) {
+    __shared__ uint32_t s_w[16];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t carry = 0;
+    for (size_t t0 = 0; t0 < n; t0 += 4096) {
+        const size_t base = t0 + (size_t)threadIdx.x * 4;
+        uint32_t v[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) v[i] = (base + i < n) ? in[base + i] : 0u;
+        const uint32_t tsum = v[0] + v[1] + v[2] + v[3];
+        const uint32_t incl = wave_incl_scan(tsum);
+        if (lane == 63) s_w[wave] = incl;
+        __syncthreads();
+        uint32_t wofs = 0, total = 0;
+        for (int w = 0; w < 16; w++) {
+            if (w < wave) wofs += s_w[w];
+            total += s_w[w];
+        }
+        uint32_t run = carry + wofs + incl - tsum;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            if (base + i < n) out[base + i] = run;
+            run += v[i];
+        }
+        carry += total;
+        __syncthreads();   // s_w is rewritten by the next tile
+    }
+    if (threadIdx.x == 0) out[n] = carry;
+}
+
 __global__ __launch_bounds__(256) void k_scan_add(uint32_t* __restrict__ out, size_t n,
                                                   const uint32_t* __restrict__ block_ofs) {
     const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x * 4;
@@ -1896,21 +1930,14 @@ __device__ __forceinline__ float quad_sum(float v) {
 static_assert(SGK_DESC_RSTEP == 0 || SGK_DESC_RSTEP == 1 || SGK_DESC_RSTEP == 2 ||
                   SGK_DESC_RSTEP == 4, "rows per quad step (0: flat strip order)");
 
-// LPC lanes per cell: 4 (one wave per feature, the 16 cells) or 8 (two waves per feature, wave
-// `half` takes cells 8 half .. 8 half + 7, lane sub walks rows sub, sub + 8, ...: half the strips
-// per lane, for batches with few features, where one wave per feature leaves most SIMDs idle and
-// the kernel takes two rounds of the per-feature latency); with LPC 8 the bins are written
-// unnormalised and k_desc_normalize finishes them.
-template <bool RECT, int LPC = 4>
+template <bool RECT>
 __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
                                                 const float* __restrict__ pyr,
                                                 const float4* __restrict__ feat,
                                                 const int2* __restrict__ feat_info,
                                                 const FeatureParams& fp,
-                                                float* __restrict__ desc, uint32_t out,
-                                                int half = 0) {
-    static_assert(LPC == 4 || LPC == 8, "lanes per cell");
-    const int cell = LPC == 4 ? lane >> 2 : half * 8 + (lane >> 3), sub = lane & (LPC - 1);
+                                                float* __restrict__ desc, uint32_t out) {
+    const int cell = lane >> 2, sub = lane & 3;
     const int ix = cell & 3, iy = cell >> 2;
     const float4 key = feat[e];
     const int2 in = feat_info[e];
@@ -2045,8 +2072,8 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
     // of the next): one or two cache lines per quad and load instead of four, and no lane idles
     // on a short row.  Each lane keeps its own cursor (row r, strip s of the row) and moves it 4
     // strips per step.
-    constexpr int RSTEP = LPC == 8 ? 8 : SGK_DESC_RSTEP;
-    constexpr int LPR = LPC == 8 ? 1 : 4 / (RSTEP ? RSTEP : 4);
+    constexpr int RSTEP = SGK_DESC_RSTEP;
+    constexpr int LPR = 4 / (RSTEP ? RSTEP : 4);
     const int rsub = RSTEP ? sub / LPR : 0, c4 = RSTEP ? 4 * (sub % LPR) : 0;
     int r = rsub, c = 0, lo = 0, len = 0, s = sub, ns = 0;
     auto next_row = [&]() {   // advance r (by RSTEP) to the next row with samples for this lane
@@ -2114,16 +2141,6 @@ __device__ __forceinline__ void descriptor_fast(uint32_t e, int lane,
     }
 #pragma unroll
     for (int k = 0; k < 8; k++) acc[k] = quad_sum(acc[k]);
-    if (LPC == 8) {
-        // the cell's 8 lanes: quads summed, then the two quads; lane sub owns bin sub
-#pragma unroll
-        for (int k = 0; k < 8; k++) acc[k] += __shfl_xor(acc[k], 4, 64);
-        float b = acc[0];
-#pragma unroll
-        for (int k = 1; k < 8; k++) b = sub == k ? acc[k] : b;
-        desc[(size_t)out * 128 + cell * 8 + sub] = b;
-        return;
-    }
     // lane sub owns bins 2 sub, 2 sub + 1 of its cell
     float b0 = acc[0], b1 = acc[1];
     b0 = sub == 1 ? acc[2] : b0; b1 = sub == 1 ? acc[3] : b1;
@@ -2177,11 +2194,18 @@ constexpr int kDualWords = 50 * 33;   // reduction words per wave
 #else
 #define SGK_DUAL_ATTR
 #endif
+// NW waves per feature: 1 (batches), or 2 for few features (a single image: one wave per feature
+// leaves most SIMDs idle), wave wh of the pair walking rows 2 wh + cp, 2 wh + cp + 4, ... of
+// every dual cell; the pair's partial bins meet in LDS across a workgroup barrier.  live =
+// false: a wave pair past the last feature (it still reaches the barriers).
+template <int NW>
 __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const float* __restrict__ pyr,
                                                 const float4* __restrict__ feat,
                                                 const int2* __restrict__ feat_info,
                                                 const FeatureParams& fp, float* __restrict__ desc,
-                                                uint32_t out, float* __restrict__ hist) {
+                                                uint32_t out, float* __restrict__ hist,
+                                                int wh = 0, bool live = true) {
+    if (!live) e = 0;   // any valid record; nothing is walked or written
     const float4 key = feat[e];
     const int2 in = feat_info[e];
     const int o = in.y / fp.d, j = in.y - o * fp.d;
@@ -2215,7 +2239,7 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
     int y1 = (int)fmin_(fH - 2.0f, fmax_(-1.0f, floor_(cyi + hb - 0.5f)));
     const int bx0 = (int)fmax_(1.0f, fmin_(fW, ceilf(cxi - hb - 0.5f)));
     const int bx1 = (int)fmin_(fW - 2.0f, fmax_(-1.0f, floor_(cxi + hb - 0.5f)));
-    if (q >= 25 || !(spt > 0.0f)) y1 = y0 - 1;
+    if (q >= 25 || !(spt > 0.0f) || !live) y1 = y0 - 1;
     // row span: the columns whose u = dnx + 2.5 - a and v = dny + 2.5 - b can lie in [0, 1],
     // dnx = crspt dxk + srspt dyk, dny = crspt dyk - srspt dxk (dxk, dyk from the keypoint); the
     // 0.01-pixel margin absorbs rounding, the per-pixel test decides
@@ -2321,10 +2345,10 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
     const char* gb = reinterpret_cast<const char*>(g);
     typedef float f4v __attribute__((ext_vector_type(4)));
     auto ld4 = [&](uint32_t byte) { return *reinterpret_cast<const f4v*>(gb + byte); };
-    int r = y0 + cp, lo = 0, len = 0, cx = 0;
-    auto next_row = [&]() {   // advance r (by 2) to the next row with a nonempty span
+    int r = y0 + 2 * wh + cp, lo = 0, len = 0, cx = 0;
+    auto next_row = [&]() {   // advance r (by 2 NW) to the next row with a nonempty span
 #pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
-        for (; r <= y1; r += 2) {
+        for (; r <= y1; r += 2 * NW) {
             row_span(r, lo, len);
             if (len > 0) break;
         }
@@ -2349,7 +2373,7 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
         const float xc = (float)cx + 0.5f;   // (xc + i) - x_key: the same value in every lane
         cx += 4;
         if (cx >= lo + len) {
-            r += 2;
+            r += 2 * NW;
             next_row();
         }
         fetch();
@@ -2376,21 +2400,31 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
             }
     }
     asm volatile("" ::: "memory");
+    if (NW == 2) __syncthreads();   // the partner wave's bins are in hist + kDualWords
     const int cell = lane >> 2, sub = lane & 3;
     const int ix = cell & 3, iy = cell >> 2;
     float b0 = 0.0f, b1 = 0.0f;
+    const float* hist_pair = hist - wh * kDualWords;   // the pair's first region
+    if (wh == 0) {
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        // slot k of dual cell (ix + 1 - (k & 1), iy + 1 - (k >> 1)) is this cell
-        const int dq = (iy + 1 - (k >> 1)) * 5 + ix + 1 - (k & 1);
+        for (int w = 0; w < NW; w++)
 #pragma unroll
-        for (int c2 = 0; c2 < 2; c2++) {
-            const float* src = hist + (2 * dq + c2) * 33 + 8 * k + 2 * sub;
-            b0 += src[0];
-            b1 += src[1];
-        }
+            for (int k = 0; k < 4; k++) {
+                // slot k of dual cell (ix + 1 - (k & 1), iy + 1 - (k >> 1)) is this cell
+                const int dq = (iy + 1 - (k >> 1)) * 5 + ix + 1 - (k & 1);
+#pragma unroll
+                for (int c2 = 0; c2 < 2; c2++) {
+                    const float* src = hist_pair + w * kDualWords + (2 * dq + c2) * 33 + 8 * k + 2 * sub;
+                    b0 += src[0];
+                    b1 += src[1];
+                }
+            }
     }
     asm volatile("" ::: "memory");
+    if (NW == 2) {
+        __syncthreads();   // both regions read before the next feature writes them
+        if (wh != 0 || !live) return;
+    }
     if (fp.normalize) {
         float sn = fma_(b0, b0, b1 * b1);
 #pragma unroll
@@ -2422,8 +2456,32 @@ __global__ __launch_bounds__(256) SGK_DUAL_ATTR void k_descriptor_dual(const flo
     float* hist = s_hist[wave];
     const uint32_t n = *n_feat_dev;
     for (uint32_t e = blockIdx.x * 4 + wave; e < n; e += gridDim.x * 4)
-        descriptor_dual(e, lane, pyr, feat, feat_info, fp, desc,
-                        out_index ? (uint32_t)out_index[e] : e, hist);
+        descriptor_dual<1>(e, lane, pyr, feat, feat_info, fp, desc,
+                           out_index ? (uint32_t)out_index[e] : e, hist);
+}
+
+// Two waves per feature (few features), two features per workgroup; the loop bound is uniform
+// over the workgroup (its barriers).
+__global__ __launch_bounds__(256) SGK_DUAL_ATTR void k_descriptor_dual2(const float* __restrict__ pyr,
+                                                          const float4* __restrict__ feat,
+                                                          const int2* __restrict__ feat_info,
+                                                          const uint32_t* __restrict__ n_feat_dev,
+                                                          const FeatureParams fp,
+                                                          float* __restrict__ desc,
+                                                          const int* __restrict__ out_index) {
+    __shared__ float s_hist[4][kDualWords];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int pair = wave >> 1, wh = wave & 1;
+    float* hist = s_hist[2 * pair];
+    const uint32_t n = *n_feat_dev;
+    for (uint32_t b0 = blockIdx.x * 2; b0 < n; b0 += gridDim.x * 2) {
+        const uint32_t e = b0 + pair;
+        const bool live = e < n;
+        descriptor_dual<2>(e, lane, pyr, feat, feat_info, fp, desc,
+                           live && out_index ? (uint32_t)out_index[e] : e, hist + wh * kDualWords,
+                           wh, live);
+    }
 }
 
 // One wave per feature, grid-stride over the features (count read on the device).
@@ -2453,44 +2511,6 @@ __global__ __launch_bounds__(256) SGK_DESC_ATTR void k_descriptor_fast(const flo
     for (uint32_t e = blockIdx.x * 4 + wave; e < n; e += gridDim.x * 4)
         descriptor_fast<RECT>(e, lane, pyr, feat, feat_info, fp, desc,
                               out_index ? (uint32_t)out_index[e] : e);
-}
-
-// Two waves per feature (few features: C2's single image), unnormalised bins.
-__global__ __launch_bounds__(256) void k_descriptor_half(const float* __restrict__ pyr,
-                                                         const float4* __restrict__ feat,
-                                                         const int2* __restrict__ feat_info,
-                                                         const uint32_t* __restrict__ n_feat_dev,
-                                                         const FeatureParams fp,
-                                                         float* __restrict__ desc) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t n = *n_feat_dev;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint32_t g = blockIdx.x * 4 + wave; (g >> 1) < n; g += gridDim.x * 4)
-        descriptor_fast<false, 8>(g >> 1, lane, pyr, feat, feat_info, fp, desc, g >> 1,
-                                  (int)(g & 1));
-}
-
-// descriptor_fast's normalisation (ProgramCU.cu:1173-1208: L2, clamp at 0.2, L2 again) for the
-// two-wave form: one wave per feature, lane l holds bins 2 l, 2 l + 1.
-__global__ __launch_bounds__(256) void k_desc_normalize(const uint32_t* __restrict__ n_feat_dev,
-                                                        float* __restrict__ desc) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t n = *n_feat_dev;
-    for (uint32_t e = blockIdx.x * 4 + (threadIdx.x >> 6); e < n; e += gridDim.x * 4) {
-        float2* p = reinterpret_cast<float2*>(desc + (size_t)e * 128) + lane;
-        float2 b = *p;
-        float s = fma_(b.x, b.x, b.y * b.y);
-#pragma unroll
-        for (int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k, 64);
-        const float n1 = __builtin_amdgcn_rsqf(s);
-        b.x = fmin_(0.2f, b.x * n1);
-        b.y = fmin_(0.2f, b.y * n1);
-        s = fma_(b.x, b.x, b.y * b.y);
-#pragma unroll
-        for (int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k, 64);
-        const float n2 = __builtin_amdgcn_rsqf(s);
-        *p = make_float2(b.x * n2, b.y * n2);
-    }
 }
 
 // One wave per feature, grid-stride over the features (count read on the device).
@@ -2880,6 +2900,10 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tm
                            (uint32_t*)nullptr);
         return hipGetLastError();
     }
+    if (n <= 32768) {   // one workgroup, <= 8 tiles
+        hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(1024), 0, stream, in, out, n);
+        return hipGetLastError();
+    }
     const size_t nb = scan_blocks(n);
     uint32_t* sums = tmp;
     uint32_t* sums_scan = tmp + nb;
@@ -2928,36 +2952,27 @@ hipError_t launch_orient_keys(const float* pyr, float4* feat, const int2* feat_i
     return hipGetLastError();
 }
 
-// up to this many features (from the previous call's count) the descriptor can run two waves per
-// feature (k_descriptor_half + k_desc_normalize): opt-in with SGPU_DESC_HALF=1 (not yet measured
-// on the GPU)
-static constexpr int kHalfDescriptorMax = 16384;
 hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* feat_info,
                              const uint32_t* n_feat_dev, int n_feat_cap, const FeatureParams& fp,
                              float* desc, hipStream_t stream, const int* out_index,
                              bool rect, bool exact) {
     if (n_feat_cap <= 0) return hipSuccess;
     const unsigned grid = (unsigned)std::min(((long long)n_feat_cap + 3) / 4, 65536LL);
-    static const bool use_half = [] {
-        const char* e = getenv("SGPU_DESC_HALF");
-        return e && !strcmp(e, "1");
-    }();
-    if (!exact && !rect && !out_index && n_feat_cap <= kHalfDescriptorMax && use_half) {
-        // few features (the grid comes from the previous call's count): two waves per feature
-        const unsigned g2 = (unsigned)((2LL * n_feat_cap + 3) / 4);
-        hipLaunchKernelGGL(k_descriptor_half, dim3(g2), dim3(256), 0, stream, pyr, feat,
-                           feat_info, n_feat_dev, fp, desc);
-        if (fp.normalize)
-            hipLaunchKernelGGL(k_desc_normalize, dim3(grid), dim3(256), 0, stream, n_feat_dev,
-                               desc);
-        return hipGetLastError();
-    }
 #ifndef SGK_DESC_DUAL
 #define SGK_DESC_DUAL 1
 #endif
+#ifndef SGK_DUAL2_MAX
+#define SGK_DUAL2_MAX 16384   // up to this many features (previous call's count): two waves each
+#endif
+    constexpr int kDual2Max = SGK_DUAL2_MAX;
     if (!exact && !rect && SGK_DESC_DUAL) {
-        hipLaunchKernelGGL(k_descriptor_dual, dim3(grid), dim3(256), 0, stream, pyr, feat,
-                           feat_info, n_feat_dev, fp, desc, out_index);
+        // few features (the grid comes from the previous call's count): two waves per feature
+        if (n_feat_cap <= kDual2Max)
+            hipLaunchKernelGGL(k_descriptor_dual2, dim3((unsigned)((n_feat_cap + 1) / 2)), dim3(256), 0,
+                               stream, pyr, feat, feat_info, n_feat_dev, fp, desc, out_index);
+        else
+            hipLaunchKernelGGL(k_descriptor_dual, dim3(grid), dim3(256), 0, stream, pyr, feat,
+                               feat_info, n_feat_dev, fp, desc, out_index);
         return hipGetLastError();
     }
     if (!exact) {

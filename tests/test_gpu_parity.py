@@ -180,22 +180,25 @@ def test_options_vs_oracle(gpu_ctx, over):
     assert np.array_equal(_bits(k), _bits(rk)) and np.array_equal(_bits(d), _bits(rd)), over
 
 
-@pytest.mark.parametrize("over", [{}, {"normalized": 0}, {"descriptor_window_factor": 2},
-                                  {"octave_min": -1}, {"dog_level_num": 5}],
-                         ids=lambda o: "-".join(f"{k}{v}" for k, v in o.items()) or "default")
-def test_shipped_descriptor_vs_exact(gpu_ctx, over):
-    """The shipped relaxed-order descriptor kernel against the bit-exact one on 4 HD images
-    (tens of thousands of features): same keypoints bit for bit, descriptors within L2 1e-5
-    (relative to |d| for -unn), i.e. 10x inside the north star's 1e-4."""
+@pytest.mark.parametrize("over,n", [({}, 4), ({"normalized": 0}, 4), ({"descriptor_window_factor": 2}, 4),
+                                    ({"octave_min": -1}, 4), ({"dog_level_num": 5}, 4), ({}, 24)],
+                         ids=lambda o: ("-".join(f"{k}{v}" for k, v in o.items()) or "default")
+                         if isinstance(o, dict) else f"n{o}")
+def test_shipped_descriptor_vs_exact(gpu_ctx, over, n):
+    """The shipped relaxed-order descriptor kernel against the bit-exact one on n HD images:
+    same keypoints bit for bit, descriptors within L2 1e-5 (relative to |d| for -unn), i.e. 10x
+    inside the north star's 1e-4.  4 images (~5k features) run the two-waves-per-feature form
+    (few features), 24 images (~30k) the one-wave form."""
     from sift_synth import synth_batch_fast
-    imgs = synth_batch_fast(4, 1280, 720, 510)
+    imgs = synth_batch_fast(n, 1280, 720, 510)
     opts = default_options(**over)
     gpu_ctx.set_options(opts)
     gpu_ctx.extract(imgs)
-    fast = [gpu_ctx.features(i) for i in range(4)]
+    gpu_ctx.extract(imgs)   # the second call sizes its grids from the first one's counts
+    fast = [gpu_ctx.features(i) for i in range(n)]
     with gpu_ctx.exact_descriptors():
         gpu_ctx.extract(imgs)
-        exact = [gpu_ctx.features(i) for i in range(4)]
+        exact = [gpu_ctx.features(i) for i in range(n)]
     kf = np.concatenate([f[0] for f in fast])
     ke = np.concatenate([e[0] for e in exact])
     df = np.concatenate([f[1] for f in fast]).astype(np.float64)
