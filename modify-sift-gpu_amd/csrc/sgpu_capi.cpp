@@ -1186,12 +1186,18 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     // second time with the sets swapped, which measured faster (1.07 vs 1.15 ms at 50k x 50k,
     // DESIGN.md section 10) because the fused epilogue halves the kernel's occupancy.
     const bool fused = mbm && (guided || (ctx->debug_flags & SGPU_DEBUG_FUSED_MATCH));
-    const int ca = sgk::match_chunks(n1, n2), panels = sgk::match_panels(n1);
-    const int cb = mbm && !fused ? sgk::match_chunks(n2, n1) : 0;
+    // keyless folding (k_match_raw / k_match_rows<..., RAW>): exact whenever a tied maximum
+    // cannot pass the ratio test, i.e. ratiomax <= 1 (the reference's default 0.8);
+    // SGPU_DEBUG_KEYED_MATCH keeps the keyed epilogue.  dma: through the LDS-DMA kernel
+    // k_match_raw (its own chunk split), unless SGPU_DEBUG_MATCH_REGSTAGE
+    const bool raw = !guided && !(ratiomax > 1.0f) && !(ctx->debug_flags & SGPU_DEBUG_KEYED_MATCH);
+    const bool dma = raw && !(ctx->debug_flags & SGPU_DEBUG_MATCH_REGSTAGE);
+    const int ca = sgk::match_chunks(n1, n2, dma && !fused), panels = sgk::match_panels(n1);
+    const int cb = mbm && !fused ? sgk::match_chunks(n2, n1, dma) : 0;
     // plain mutual matching decides only the columns some row matched (see below); their
     // count is known on the device only, so the partials are sized for any count
     const bool compact = mbm && !fused && !(ctx->debug_flags & SGPU_DEBUG_FULL_COLUMNS);
-    const size_t part_b = compact ? sgk::match_part_bound(n2, n1) : (size_t)cb * n2;
+    const size_t part_b = compact ? sgk::match_part_bound(n2, n1, dma) : (size_t)cb * n2;
     ALLOCCHK(ctx, ctx->m_part.ensure(std::max((size_t)ca * n1, part_b) * sizeof(sgk::Top2)));
     if (fused) ALLOCCHK(ctx, ctx->m_colpart.ensure((size_t)panels * n2 * sizeof(sgk::Top2)));
     if (compact) ALLOCCHK(ctx, ctx->m_cols.ensure((size_t)(2 * n2 + 1) * sizeof(int)));
@@ -1217,11 +1223,6 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     // (two GEMMs: 128 * sum(d2), the row terms of the swapped launch; fused: the column terms
     // 128 * sum(d2) - 2^21, guided: 0) and the matched-column flags cleared
     int* cw = compact ? ctx->m_cols.as<int>() : nullptr;   // [flag n2][count][list n2]
-    // keyless folding (k_match_raw / k_match_rows<..., RAW>): exact whenever a tied maximum
-    // cannot pass the ratio test, i.e. ratiomax <= 1 (the reference's default 0.8);
-    // SGPU_DEBUG_KEYED_MATCH keeps the keyed epilogue
-    const bool raw = !guided && !(ratiomax > 1.0f) && !(ctx->debug_flags & SGPU_DEBUG_KEYED_MATCH);
-    const bool dma = raw && !(ctx->debug_flags & SGPU_DEBUG_MATCH_REGSTAGE);
     HIPCHK(ctx, sgk::launch_prep_set(a, n1, ctx->m_s1.as<uint8_t>(), row1, 128, 0, nullptr, 0, st,
                                      dma && mbm && !fused ? ct1 : nullptr));
     if (mbm || dma)
@@ -1246,6 +1247,7 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
             claim.list = cw + n2 + 1;
             cols.count = claim.count;
             cols.map = claim.list;
+            cols.dma = dma ? 1 : 0;
         }
         HIPCHK(ctx, sgk::launch_match_rows(s1, n1, s2, n2, ca, part, st, nullptr, true, nullptr,
                                            nullptr, raw, nullptr, nullptr, dma ? ct2 : nullptr));

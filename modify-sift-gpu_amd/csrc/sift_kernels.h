@@ -175,7 +175,9 @@ hipError_t launch_prep_set(const uint8_t* src, int n, uint8_t* dst, int* sums, i
                            int bias, int* zero, int nzero, hipStream_t stream,
                            int* ctp = nullptr);
 int match_ct_pad();
-int match_chunks(int nA, int nB);
+// column chunks of a row launch: dma = the launch runs k_match_raw (raw with ctp), whose split
+// is its own cost model (sift_match.hip chunks_for)
+int match_chunks(int nA, int nB, bool dma = false);
 // part[chunk][nA]: per-row top-2 of (A_i . B_j + col_term[j]) over each column chunk, with
 // col_term[j] = 128 * sum(B_j) - 2^21 formed in the kernel from the staged bytes.  A and B are
 // the s8 forms of the descriptor sets (launch_to_s8).
@@ -189,16 +191,16 @@ int match_chunks(int nA, int nB);
 // (tile + lane) and k_match_finish recovers the column (pass raw_A / raw_B to it).
 // ctp (raw only; launch_prep_set of B): the LDS-DMA kernel k_match_raw, same partials.
 // amap / an (plain matching only): the rows are A[amap[r]] for r < *an (a count on the device,
-// at most nA); the launch covers every count and the split is chunks_for(*an, nB), which
-// launch_match_finish with ColumnList{map, count} derives again.  part needs
-// match_part_bound(nA, nB) entries.
+// at most nA); the launch covers every count and the split is chunks_for(*an, nB, dma), which
+// launch_match_finish with ColumnList{map, count, dma} derives again.  part needs
+// match_part_bound(nA, nB, dma) entries.
 hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
                              int chunks, Top2* part, hipStream_t stream,
                              const uint8_t* mask, bool row_side, const int* row_term = nullptr,
                              Top2* colpart = nullptr, bool raw = false,
                              const int* amap = nullptr, const int* an = nullptr,
                              const int* ctp = nullptr);
-size_t match_part_bound(int nA, int nB);
+size_t match_part_bound(int nA, int nB, bool dma = false);
 int match_panels(int nA);
 // Column decisions from the panels' partials: col_term[j] = 128 * sum(B_j) - 2^21 (guided: 0).
 hipError_t launch_match_cols(const Top2* colpart, int n, int panels, const int* col_term,
@@ -226,6 +228,7 @@ struct ColumnList {
     int* list = nullptr;
     int* count = nullptr;
     const int* map = nullptr;
+    int dma = 0;   // map launches: the rows ran through k_match_raw (its chunk split)
 };
 hipError_t launch_match_finish(const Top2* part, int n, int chunks, const int* row_term,
                                const float* dist, float distmax, float ratiomax, int* out,

@@ -34,6 +34,9 @@ constexpr int kLdsRow = SGK_MATCH_LDSROW;   // bytes per staged B row (padding a
 #ifndef SGK_MATCH_PF
 #define SGK_MATCH_PF 1     // RAW kernel: tiles of staging loads in flight (1 or 2)
 #endif
+#ifndef SGK_MATCH_PIPE
+#define SGK_MATCH_PIPE 1   // RAW kernel: column groups software-pipelined across tiles (0: tile by tile)
+#endif
 #ifndef SGK_MATCH_PKEY
 #define SGK_MATCH_PKEY 1   // RAW fold: the tile index packed below the tile maximum (see k_match_rows)
 #endif
@@ -80,12 +83,47 @@ __global__ __launch_bounds__(256) void k_rowsum(const uint8_t* __restrict__ d, i
 #define SGK_MATCH_WG 4096
 #endif
 constexpr int kMatchWg = SGK_MATCH_WG;   // workgroups aimed at per launch (tuning knob)
-__host__ __device__ inline int chunks_for(int nA, int nB) {
-    const int panels = (nA + kPanel - 1) / kPanel;
-    const int chunks = (kMatchWg + panels - 1) / panels;
+
+// k_match_raw (LDS-DMA keyless kernel): 256-row panels, and 2 workgroups resident per CU (55 KB
+// of LDS and 128 VGPRs each), 512 on the chip.  Its split is picked by a cost model instead of a
+// workgroup target: for r = 1 .. kRawMaxRounds rounds of resident workgroups, the most chunks
+// that fit r rounds; cost = rounds x (tiles per chunk + a chunk's fixed cost in tiles: its A
+// fragments, the first two tiles in flight and the partials); the cheapest wins (ties: fewer
+// chunks).  C5 rows: 5 chunks (2 rounds of 79 tiles) instead of 11 (5 rounds of 36).
+#ifndef SGK_MATCH_RAW_WAVES
+#define SGK_MATCH_RAW_WAVES 8
+#endif
+constexpr int kRawWaves = SGK_MATCH_RAW_WAVES;
+constexpr int kRawRows = 32 * kRawWaves;
+#ifndef SGK_MATCH_SLOTS
+#define SGK_MATCH_SLOTS 512
+#endif
+#ifndef SGK_MATCH_OVT
+#define SGK_MATCH_OVT 2
+#endif
+constexpr int kRawSlots = SGK_MATCH_SLOTS;
+constexpr int kRawOvt = SGK_MATCH_OVT;
+constexpr int kRawMaxRounds = 8;
+
+// dma: the split of a k_match_raw launch (above); otherwise ~kMatchWg workgroups of 128 rows
+__host__ __device__ inline int chunks_for(int nA, int nB, bool dma = false) {
     const int max_chunks = max(1, (nB + 2 * kTile - 1) / (2 * kTile));
-    const int min_chunks = (nB + kMaxChunkTiles * kTile - 1) / (kMaxChunkTiles * kTile);
-    return max(min_chunks, max(1, min(chunks, max_chunks)));
+    const int min_chunks = max(1, (nB + kMaxChunkTiles * kTile - 1) / (kMaxChunkTiles * kTile));
+    if (!dma) {
+        const int panels = (nA + kPanel - 1) / kPanel;
+        const int chunks = (kMatchWg + panels - 1) / panels;
+        return max(min_chunks, min(chunks, max_chunks));
+    }
+    const int panels = max(1, (nA + kRawRows - 1) / kRawRows);
+    int best = min_chunks, best_cost = INT_MAX;
+    for (int r = 1; r <= kRawMaxRounds; r++) {
+        const int c = max(min_chunks, min(max_chunks, r * kRawSlots / panels));
+        const int rounds = (panels * c + kRawSlots - 1) / kRawSlots;
+        const int tiles = ((nB + c - 1) / c + kTile - 1) / kTile;
+        const int cost = rounds * (tiles + kRawOvt);
+        if (cost < best_cost) { best_cost = cost; best = c; }
+    }
+    return best;
 }
 
 // u8 descriptors -> s8 (s = u - 128, xor 0x80), once per match call for both sets
@@ -119,12 +157,12 @@ __global__ __launch_bounds__(256) void k_prep_set(const uint4* __restrict__ src,
         t += __shfl_xor(t, 4, 64);
         if ((i & 7) == 0) {
             if (sums) sums[i >> 3] = scale * t + bias;
-            if (ctp) ctp[i >> 3] = 128 * t + 4194304;   // k_match_raw's biased column term
+            if (ctp) ctp[i >> 3] = 128 * t - 2097152;   // k_match_raw's biased column term
         }
     }
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < (size_t)nzero; i += stride) zero[i] = 0;
     if (ctp)
-        for (int i = blockIdx.x * 256 + threadIdx.x; i < kCtPad; i += (int)stride) ctp[n + i] = 0;
+        for (int i = blockIdx.x * 256 + threadIdx.x; i < kCtPad; i += (int)stride) ctp[n + i] = -6291456;
 }
 
 // Equal-dot order of the two decisions: does column a come before column b (-1 = none)?
@@ -583,22 +621,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAW ? SGK_M
 // loads in flight across each tile's barrier (counted vmcnt, raw s_barrier), where the register
 // staging of k_match_rows holds one (or two with copies the compiler adds).  Values, folds and
 // partials are k_match_rows<.., RAW>'s:
-//   * the column terms come precomputed (ctp[j] = 128 * sum(u8 B_j) + 2^22, launch_prep_set),
-//     staged beside the tile; ctp is zero for j in [nB, nB + kTile) and columns past nB stage
-//     the last column's bytes, so their values are acc - 2^22 - 2^21 < -128 * sum(u8 A_i) <=
-//     every real value of the row (no zeroing select, which a DMA cannot apply);
+//   * the column terms come precomputed (ctp[j] = 128 * sum(u8 B_j) - 2^21, launch_prep_set),
+//     staged beside the tile four times over (a column's term fills one 16-B slot, read as the
+//     v4i that starts the column's accumulators: no register moves); ctp is -2^22 - 2^21 for j
+//     in [nB, nB + kTile) and columns past nB stage the last column's bytes, so their values
+//     are acc - 2^22 - 2^21 < -128 * sum(u8 A_i) <= every real value of the row (no zeroing
+//     select, which a DMA cannot apply);
 //   * the tile image is XOR-swizzled by 16-B slots (slot j of column c at j ^ ((c >> 1) & 7)) so
 //     the B-fragment ds_read_b128 are conflict-free; the DMA writes lane-linear 1-KB runs, so
 //     the swizzle is applied to the per-lane global source address instead.
 // NW waves per workgroup share each staged tile: a panel of 32 * NW rows of A.
-#ifndef SGK_MATCH_RAW_WAVES
-#define SGK_MATCH_RAW_WAVES 8
-#endif
-constexpr int kRawWaves = SGK_MATCH_RAW_WAVES;
 constexpr int kRawBufs = 3;
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 
-__global__ __launch_bounds__(64 * kRawWaves) void k_match_raw(const uint8_t* __restrict__ A, int nA,
+#if SGK_MATCH_PIPE
+#define SGK_RAW_ATTR __attribute__((amdgpu_waves_per_eu(4)))   // 128 VGPRs: 2 workgroups per CU
+#else
+#define SGK_RAW_ATTR
+#endif
+__global__ __launch_bounds__(64 * kRawWaves) SGK_RAW_ATTR void k_match_raw(const uint8_t* __restrict__ A, int nA,
                                                    const uint8_t* __restrict__ B, int nB,
                                                    const int* __restrict__ ctp, int cols_per_chunk,
                                                    Top2* __restrict__ part,
@@ -609,6 +650,7 @@ __global__ __launch_bounds__(64 * kRawWaves) void k_match_raw(const uint8_t* __r
     constexpr int kDmaB = 16 / NW;        // 1-KB image runs per wave and tile
     constexpr int kCtW = kTile / NW;      // column terms staged per wave (lanes repeat them)
     static_assert(kTile * 128 == NW * kDmaB * 1024, "the image is NW x kDmaB runs");
+    static_assert(kCtW * 4 == 64, "a wave stages its column terms as 16-B slots of 4 copies");
     __shared__ __attribute__((aligned(16))) uint8_t s_lds[kRawBufs * (kTile * 128 + NW * 256)];
     constexpr int kBuf = kTile * 128 + NW * 256;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -616,7 +658,7 @@ __global__ __launch_bounds__(64 * kRawWaves) void k_match_raw(const uint8_t* __r
     if (an) {
         nA = *an;
         if (nA <= 0) return;
-        const int panels = (nA + kRows - 1) / kRows, chunks = chunks_for(nA, nB);
+        const int panels = (nA + kRows - 1) / kRows, chunks = chunks_for(nA, nB, true);
         if ((int)blockIdx.x >= panels * chunks) return;
         panel = blockIdx.x % panels;
         chunk = blockIdx.x / panels;
@@ -673,10 +715,15 @@ __global__ __launch_bounds__(64 * kRawWaves) void k_match_raw(const uint8_t* __r
             __builtin_amdgcn_global_load_lds(B + (size_t)col * 128 + src_off[q],
                                              (lds_void_ptr)(base + (wave * kDmaB + q) * 1024), 16, 0, 0);
         }
-        const int ci = min(tb + wave * kCtW + lane % kCtW, nB + kCtPad - 1);
+        const int ci = min(tb + wave * kCtW + lane / (64 / kCtW), nB + kCtPad - 1);
         __builtin_amdgcn_global_load_lds(ctp + ci, (lds_void_ptr)(base + kTile * 128 + wave * 256),
                                          4, 0, 0);
     };
+    // this lane's LDS offsets in a tile buffer: column l16 of a 16-column block, its 16-B piece
+    // j = 4 kh + quad at slot j ^ ((col >> 1) & 7) (the block's 16 columns do not change the
+    // swizzle), and the column's term slot; the block adds a constant
+    const int lane_b[2] = {l16 * 128 + ((quad ^ (l16 >> 1)) << 4), l16 * 128 + (((4 + quad) ^ (l16 >> 1)) << 4)};
+    const int lane_ct = kTile * 128 + l16 * 16;
     // kDmaB + 1 DMA instructions per wave and tile: vmcnt(kDmaB + 1) retires all but the
     // newest tile (the immediate: vmcnt low bits, expcnt 7, lgkmcnt 0)
     constexpr int kWaitTile = 0x0070 | (kDmaB + 1);
@@ -687,11 +734,67 @@ __global__ __launch_bounds__(64 * kRawWaves) void k_match_raw(const uint8_t* __r
     // compiler memory barrier: the s_barrier intrinsic does not order memory operations for the
     // compiler, and no LDS read of a tile buffer may move above the barrier that publishes its DMA
     asm volatile("" ::: "memory");
+#if SGK_MATCH_PIPE
+    // software-pipelined by column group: group 1 of tile t is issued before group 0's fold, and
+    // group 0 of tile t + 1 (after the barrier) before group 1's, so every fold's VALU work runs
+    // beside MFMAs it does not depend on (the two groups' 64 accumulator registers, as before)
+    static_assert(kMatchSplit == 2, "two column groups");
+    constexpr int CB = 4;
+    v4i g0[2][CB], g1[2][CB];
+    int tmx[2][4];
+    auto group = [&](int bi_, int h, v4i (&acc)[2][CB]) __attribute__((always_inline)) {
+        const uint8_t* sb = s_lds + bi_ * kBuf;
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            const int cb = (h * CB + c) * 16;   // the column block: immediate offsets below
+            const v4i ctv = *reinterpret_cast<const v4i*>(sb + lane_ct + cb * 16);
+#pragma unroll
+            for (int kh = 0; kh < 2; kh++) {
+                const v4i bfrag = *reinterpret_cast<const v4i*>(sb + lane_b[kh] + cb * 128);
+                acc[0][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[0][kh], bfrag, kh ? acc[0][c] : ctv, 0, 0, 0);
+                acc[1][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[1][kh], bfrag, kh ? acc[1][c] : ctv, 0, 0, 0);
+            }
+        }
+    };
+    auto fold = [&](const v4i (&acc)[2][CB], bool first) __attribute__((always_inline)) {
+#pragma unroll
+        for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int c = 0; c < CB; c += 2) {
+                    const int a = acc[rb][c][i], b2 = acc[rb][c + 1][i];
+                    tmx[rb][i] = (first && c == 0) ? max(a, b2) : max(max(tmx[rb][i], a), b2);
+                }
+    };
+    int bi = 0;
+    group(0, 0, g0);
+    for (int tb = c_begin; tb < c_end; tb += kTile) {
+        issue(tb + 2 * kTile, bi == 0 ? 2 : bi - 1);
+        group(bi, 1, g1);
+        fold(g0, true);
+        // tile t + 1's DMAs retired (t + 2's stay in flight), this tile's reads done
+        __builtin_amdgcn_s_waitcnt(kWaitTile);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");   // (as above: the next tile's reads stay below it)
+        bi = bi == 2 ? 0 : bi + 1;
+        group(bi, 0, g0);   // (past the last tile: a staged tile of clamped columns, unused)
+        fold(g1, false);
+        const int tl = (tb - c_begin) / kTile;
+#pragma unroll
+        for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int key = (tmx[rb][i] << 8) | tl;
+                S[rb][i] = med3i(S[rb][i], M[rb][i], key);
+                M[rb][i] = max(M[rb][i], key);
+            }
+    }
+#else
     int bi = 0;
     for (int tb = c_begin; tb < c_end; tb += kTile) {
         issue(tb + 2 * kTile, bi == 0 ? 2 : bi - 1);
         const uint8_t* sb = s_lds + bi * kBuf;
-        const int* sct = reinterpret_cast<const int*>(sb + kTile * 128);
         constexpr int CB = 8 / kMatchSplit;
         int tmx[2][4];
 #pragma unroll
@@ -699,21 +802,15 @@ __global__ __launch_bounds__(64 * kRawWaves) void k_match_raw(const uint8_t* __r
             v4i acc[2][CB];
 #pragma unroll
             for (int c = 0; c < CB; c++) {
-                const int col = (h * CB + c) * 16 + l16;
-                const int ct = sct[(col / kCtW) * 64 + col % kCtW] - 6291456;
-                acc[0][c] = v4i{ct, ct, ct, ct};
-                acc[1][c] = acc[0][c];
-            }
-#pragma unroll
-            for (int c = 0; c < CB; c++) {
-                const int col = (h * CB + c) * 16 + l16;
+                const int cb = (h * CB + c) * 16;   // the column block: immediate offsets below
+                const v4i ctv = *reinterpret_cast<const v4i*>(sb + lane_ct + cb * 16);
 #pragma unroll
                 for (int kh = 0; kh < 2; kh++) {
-                    const int j = kh * 4 + quad;
-                    const v4i bfrag = *reinterpret_cast<const v4i*>(
-                        sb + col * 128 + ((j ^ ((col >> 1) & 7)) << 4));
-                    acc[0][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[0][kh], bfrag, acc[0][c], 0, 0, 0);
-                    acc[1][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[1][kh], bfrag, acc[1][c], 0, 0, 0);
+                    const v4i bfrag = *reinterpret_cast<const v4i*>(sb + lane_b[kh] + cb * 128);
+                    acc[0][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[0][kh], bfrag,
+                                                                      kh ? acc[0][c] : ctv, 0, 0, 0);
+                    acc[1][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag[1][kh], bfrag,
+                                                                      kh ? acc[1][c] : ctv, 0, 0, 0);
                 }
             }
 #pragma unroll
@@ -741,6 +838,7 @@ __global__ __launch_bounds__(64 * kRawWaves) void k_match_raw(const uint8_t* __r
         asm volatile("" ::: "memory");   // (as above: the next tile's reads stay below it)
         bi = bi == 2 ? 0 : bi + 1;
     }
+#endif
     // no DMA may land after the workgroup's LDS is handed to another one
     __builtin_amdgcn_s_waitcnt(0xc07f & ~0xc00f);   // vmcnt(0)
     int I[2][4];
@@ -810,7 +908,7 @@ __global__ __launch_bounds__(kFinishThreads) void k_match_finish(const Top2* __r
                                                       int nB, ColumnList cl) {
     if (cl.map) {
         n = *cl.count;
-        chunks = chunks_for(n, nB);
+        chunks = chunks_for(n, nB, cl.dma != 0);
     }
     __shared__ int s_cnt[kFinishThreads / 64], s_base;
     if ((int)blockIdx.x * kFinishRows >= n) return;   // whole workgroups only (barriers below)
@@ -1123,23 +1221,29 @@ hipError_t launch_rowsums(const uint8_t* d, int n, int* out, int scale, int bias
     return hipGetLastError();
 }
 
-int match_chunks(int nA, int nB) { return chunks_for(nA, nB); }
+int match_chunks(int nA, int nB, bool dma) { return chunks_for(nA, nB, dma); }
 int match_ct_pad() { return kCtPad; }
 
-// bounds over every row count m <= nA of chunks_for(m, nB) * m (partials) and of
-// panels(m) * chunks_for(m, nB) (workgroups): chunks <= max_chunks, and chunks * panels <
-// 4096 + panels
-size_t match_part_bound(int nA, int nB) {
+// bounds over every row count m <= nA of chunks_for(m, nB, dma) * m (partials) and of
+// panels(m) * chunks_for(m, nB, dma) (workgroups).  Register kernels: chunks <= max_chunks,
+// and chunks * panels < kMatchWg + panels (128-row panels).  k_match_raw: chunks is min_chunks
+// or at most kRawMaxRounds * kRawSlots / panels (256-row panels), so chunks * m is at most
+// kRawMaxRounds * kRawSlots * 256 and chunks * panels at most kRawMaxRounds * kRawSlots.
+size_t match_part_bound(int nA, int nB, bool dma) {
     const size_t panels = (nA + kPanel - 1) / kPanel;
     const size_t max_chunks = std::max(1, (nB + 2 * kTile - 1) / (2 * kTile));
-    const size_t min_chunks = (nB + kMaxChunkTiles * kTile - 1) / (kMaxChunkTiles * kTile);
-    return std::max(std::min((kMatchWg + panels) * kPanel, max_chunks * (size_t)nA),
-                    min_chunks * (size_t)nA);
+    const size_t min_chunks = std::max(1, (nB + kMaxChunkTiles * kTile - 1) / (kMaxChunkTiles * kTile));
+    const size_t cap = dma ? (size_t)kRawMaxRounds * kRawSlots * kRawRows : (kMatchWg + panels) * kPanel;
+    return std::max(std::min(cap, max_chunks * (size_t)nA), min_chunks * (size_t)nA);
 }
-static unsigned match_grid_bound(int nA, int nB) {
+static unsigned match_grid_bound(int nA, int nB, bool dma) {
+    const size_t min_chunks = std::max(1, (nB + kMaxChunkTiles * kTile - 1) / (kMaxChunkTiles * kTile));
+    if (dma) {
+        const size_t panels = (nA + kRawRows - 1) / kRawRows;
+        return (unsigned)std::max((size_t)kRawMaxRounds * kRawSlots, min_chunks * panels);
+    }
     const size_t panels = (nA + kPanel - 1) / kPanel;
     const size_t max_chunks = std::max(1, (nB + 2 * kTile - 1) / (2 * kTile));
-    const size_t min_chunks = (nB + kMaxChunkTiles * kTile - 1) / (kMaxChunkTiles * kTile);
     return (unsigned)std::max(std::min(kMatchWg + panels, max_chunks * panels),
                               min_chunks * panels);
 }
@@ -1158,7 +1262,8 @@ hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
     int per = (nB + chunks - 1) / chunks;
     per = (per + kTile - 1) / kTile * kTile;
     // compacted rows (at most nA of them): a 1-D grid large enough for any count
-    const dim3 grid = an ? dim3(match_grid_bound(nA, nB))
+    const bool dma = raw && ctp;
+    const dim3 grid = an ? dim3(match_grid_bound(nA, nB, dma))
                          : dim3((nA + kPanel - 1) / kPanel, chunks);
     const int tiles = (nB + kTile - 1) / kTile;
     const uint4* rec = reinterpret_cast<const uint4*>(mask);
@@ -1168,8 +1273,8 @@ hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
 #define SGK_MRR(T)                                                                            \
     hipLaunchKernelGGL((k_match_rows<false, T, false, true>), grid, dim3(256), 0, stream, A, nA, \
                        B, nB, per, part, rec, tiles, row_term, colpart, amap, an)
-    if (raw && ctp) {
-        constexpr int rows = 32 * kRawWaves;
+    if (dma) {
+        constexpr int rows = kRawRows;
         const dim3 rgrid = an ? grid : dim3((nA + rows - 1) / rows, chunks);
         hipLaunchKernelGGL(k_match_raw, rgrid, dim3(64 * kRawWaves), 0, stream, A, nA,
                            B, nB, ctp, per, part, amap, an);
