@@ -16,6 +16,7 @@
 // out, transcendentals from sift_math.h); the build uses -ffp-contract=off.
 #include <cstdlib>
 #include <cstring>
+#include <numeric>
 #include <type_traits>
 #include <utility>
 
@@ -292,6 +293,19 @@ __device__ __forceinline__ int xcd_block(int bid, int nb) {
     return xcd < r ? xcd * (q + 1) + k : r * (q + 1) + (xcd - r) * q + k;
 }
 
+// Grouped XCD order: G logically consecutive workgroups on one XCD, dispatched within 8 G slots
+// of each other (workgroup b runs on XCD b % 8), the groups in dispatch order -- locality for
+// neighbours without xcd_block's partition of the whole grid into 8 contiguous ranges (which
+// leaves XCDs idle when the work per workgroup changes along the grid).  The last partial round
+// of 8 G keeps the identity.
+template <int G>
+__device__ __forceinline__ int xcd_group(int bid, int nb) {
+    const int full = nb / (8 * G) * (8 * G);
+    if (bid >= full) return bid;
+    const int m = bid / (8 * G), r = bid % (8 * G);
+    return m * (8 * G) + (r % 8) * G + r / 8;
+}
+
 constexpr int WCH = 8;   // rows per chunk (wave kernel)
 
 struct GaussWaveGrid {
@@ -422,7 +436,10 @@ __device__ __forceinline__ void gauss_lean_wave(const GaussJob& J, int gw, f2v* 
     constexpr int NSLOT = RS / WCH;
     static_assert(WCH * (LAG + 1) <= RS && FW <= 33, "the ring's chunk slots hold the lag");
     constexpr int NPAIR = WCH / 2;
-    constexpr int NST = 4;                            // chunks in registers
+#ifndef SGK_GW_NST_U8
+#define SGK_GW_NST_U8 4
+#endif
+    constexpr int NST = U8 ? SGK_GW_NST_U8 : 4;       // chunks in registers (u8: 1 dword per row)
     const float* __restrict__ src = J.src;
     const uint8_t* __restrict__ src8 = J.src8;
     const int src_stride = J.src_stride;
@@ -629,13 +646,24 @@ __device__ __forceinline__ void gauss_lean_wave(const GaussJob& J, int gw, f2v* 
     const int nsteps = nchunk_out + LAG;
     // slot K = c mod NSLOT, register set c mod NST (steps past the end filter clamped rows and
     // store nothing): the loop is unrolled by lcm(NSLOT, NST) steps
-    constexpr int U = NSLOT % NST == 0 ? NSLOT : NSLOT * NST;
+    constexpr int U = std::lcm(NSLOT, NST);
     for (int c = 0; c < nsteps; c += U) {
         unrolled_steps(std::make_integer_sequence<int, U>{}, [&](auto KI) __attribute__((always_inline)) {
             constexpr int k = decltype(KI)::value;
             step(c + k, std::integral_constant<int, k % NSLOT>{}, st[(k + 1) % NST], st[k % NST]);
         });
     }
+}
+
+// the level kernels' workgroup order: xcd_block (1, shipped) or xcd_group<SGK_GW_XCDG> (2)
+#ifndef SGK_GW_XCD
+#define SGK_GW_XCD 1
+#endif
+#ifndef SGK_GW_XCDG
+#define SGK_GW_XCDG 4
+#endif
+__device__ __forceinline__ int gw_order(int bid, int nb) {
+    return SGK_GW_XCD == 2 ? xcd_group<SGK_GW_XCDG>(bid, nb) : xcd_block(bid, nb);
 }
 
 template <int FW, bool U8, bool DS>
@@ -645,7 +673,7 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(const GaussJob J) 
     __shared__ __attribute__((aligned(16))) float s_h_all[kGwWaves][G::RING_WORDS];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // XCD-aware order (xcd_block)
-    const int gw = xcd_block(blockIdx.x, gridDim.x) * kGwWaves + wave;
+    const int gw = gw_order(blockIdx.x, gridDim.x) * kGwWaves + wave;
     gauss_lean_wave<FW, U8, DS>(J, gw, s_in_all[wave], s_h_all[wave]);
 }
 
@@ -665,11 +693,11 @@ __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_diag(const GaussJob A, 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int bid = blockIdx.x;
     if (bid < nbB) {
-        gauss_lean_wave<FWB, false, false>(B, xcd_block(bid, nbB) * kGwWaves + wave,
+        gauss_lean_wave<FWB, false, false>(B, gw_order(bid, nbB) * kGwWaves + wave,
                                            s_in_all[wave], s_h_all[wave]);
     } else {
         const int nbA = (int)gridDim.x - nbB;
-        gauss_lean_wave<FWA, false, false>(A, xcd_block(bid - nbB, nbA) * kGwWaves + wave,
+        gauss_lean_wave<FWA, false, false>(A, gw_order(bid - nbB, nbA) * kGwWaves + wave,
                                            s_in_all[wave], s_h_all[wave]);
     }
 }
@@ -838,7 +866,7 @@ struct ExtremaWaveGrid {
 #define SGK_EXT2_WAVES 1
 #endif
 #ifndef SGK_EXT_XCD
-#define SGK_EXT_XCD 0
+#define SGK_EXT_XCD 2   // workgroup order: 0 launch order, 1 xcd_block, 2 xcd_group<SGK_EXT_XCDG>
 #endif
 // CPL = columns per lane.  CPL = 2: lane l holds the column pair x0 - 1 + 2l, x0 + 2l (one 8-byte
 // load per plane and row instead of two 4-byte ones: the texture-address unit, ~88 % busy with
@@ -857,10 +885,21 @@ __global__ __launch_bounds__(256, SGK_EXT2_WAVES) void k_extrema_wave2(const flo
     __shared__ __attribute__((aligned(8))) float s_ring[4][ND][4][RW];   // [wave][plane][row & 3][col]
     __shared__ uint16_t s_list[4][NJ * 64 * CPL];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // SGK_EXT_XCD = 1: XCD-aware order (xcd_block), the strips of one image segment on one XCD
-    // so that the cache lines two neighbouring 128-column windows share (126 columns apart, not
-    // line-aligned) come from one L2: FETCH_SIZE -1 %, detect 1.90 vs 1.67 ms -- not used
-    const int gw = (SGK_EXT_XCD ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * 4 + wave;
+    // Workgroup order.  Two neighbouring 128-column windows (126 columns apart, not line-aligned)
+    // share a cache line of every row; the 4 waves of a workgroup are 4 neighbouring strips, so
+    // the lines at workgroup boundaries were fetched twice whenever the neighbour ran on another
+    // XCD (another L2).  SGK_EXT_XCD = 2 (shipped): xcd_group<4>, 4 consecutive workgroups -- an
+    // octave-0 segment row of 16 strips -- on one XCD, dispatched together: detect 1.55-1.56 vs
+    // 1.60-1.63 ms (alternating processes, tests/diag/r04l.sh; groups of 2 / 8 / 16 workgroups:
+    // 1.59 / 1.56 / 1.58).  SGK_EXT_XCD = 1, xcd_block's partition of the grid into 8 contiguous
+    // ranges, measured 1.90 vs 1.67 ms: the ranges hold different octaves, whose waves differ in
+    // work, so XCDs went idle.
+#ifndef SGK_EXT_XCDG
+#define SGK_EXT_XCDG 4
+#endif
+    const int gw = (SGK_EXT_XCD == 1 ? xcd_block(blockIdx.x, gridDim.x)
+                    : SGK_EXT_XCD == 2 ? xcd_group<SGK_EXT_XCDG>(blockIdx.x, gridDim.x)
+                                       : (int)blockIdx.x) * 4 + wave;
     if (gw >= eg.wave0[fp.n_octaves]) return;       // uniform per wave
     int o = 0;
     while (o + 1 < fp.n_octaves && gw >= eg.wave0[o + 1]) o++;
@@ -2186,6 +2225,15 @@ constexpr int kDualWords = 50 * 33;   // reduction words per wave
 #ifndef SGK_DUAL_REF
 #define SGK_DUAL_REF 1   // cell weights from the reference's rounded cell centres
 #endif
+// SGK_DUAL_SPLIT = 1 (shipped): the one-wave kernel walks the two row groups of the two-wave
+// kernel in turn and sums them in the same order, so both give the same bits and a batch's
+// descriptors equal a single image's (the two-wave kernel serves few features, chosen from the
+// previous call's count): 1.786 vs 1.725 ms per 128 x 1080p step for the unsplit walk, whose
+// descriptors differed from the two-wave kernel's in the last bits (tests/diag/r04m.sh;
+// 128-thread two-wave workgroups for every count: 1.854-1.865 ms)
+#ifndef SGK_DUAL_SPLIT
+#define SGK_DUAL_SPLIT 1
+#endif
 #ifndef SGK_DUAL_WPE
 #define SGK_DUAL_WPE 4   // waves per SIMD the allocation must allow: 4 = <= 128 VGPRs, no spills (132 free)
 #endif
@@ -2345,16 +2393,21 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
     const char* gb = reinterpret_cast<const char*>(g);
     typedef float f4v __attribute__((ext_vector_type(4)));
     auto ld4 = [&](uint32_t byte) { return *reinterpret_cast<const f4v*>(gb + byte); };
-    int r = y0 + 2 * wh + cp, lo = 0, len = 0, cx = 0;
-    auto next_row = [&]() {   // advance r (by 2 NW) to the next row with a nonempty span
+    // NG row groups walked in turn by this wave (NW = 1 with SGK_DUAL_SPLIT): group g holds rows
+    // y0 + 2 g + cp + 4 k, the rows wave g of a two-wave pair walks, and its bins are flushed and
+    // summed before the next group, so the sums are k_descriptor_dual2's bit for bit (a batch
+    // gives the features of a single image exactly)
+    constexpr int NG = (NW == 1 && SGK_DUAL_SPLIT) ? 2 : 1;
+    constexpr int RSTEP = 2 * NW * NG;
+    int r = 0, lo = 0, len = 0, cx = 0;
+    auto next_row = [&]() {   // advance r (by RSTEP) to the next row with a nonempty span
 #pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
-        for (; r <= y1; r += 2 * NW) {
+        for (; r <= y1; r += RSTEP) {
             row_span(r, lo, len);
             if (len > 0) break;
         }
         cx = lo;
     };
-    next_row();
     f4v na, nb, nu, nd;
     uint32_t npo = 4u * (uint32_t)(W + 1);   // row 1, column 1 when nothing is left (in-plane)
     auto fetch = [&]() {
@@ -2364,66 +2417,88 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
         nu = ld4(npo - 4u * W);        // row y-1, x .. x+3
         nd = ld4(npo + 4u * W);        // row y+1, x .. x+3
     };
-    fetch();
-    while (r <= y1) {
-        const f4v gx = nb - na, gy = nd - nu;   // the strip's gradients (dx, dy per pixel)
-        const float dyk = ((float)r + 0.5f) - key.y;
-        const float sdy = srspt * dyk, cdy = crspt * dyk;
-        const int nv = lo + len - cx;
-        const float xc = (float)cx + 0.5f;   // (xc + i) - x_key: the same value in every lane
-        cx += 4;
-        if (cx >= lo + len) {
-            r += 2 * NW;
-            next_row();
-        }
+    auto walk = [&](int r0) {
+        r = r0;
+        next_row();
         fetch();
-        // one pixel at a time (sched_barrier): four interleaved took ~150 VGPRs
-        pixel((xc) - key.x, sdy, cdy, gx.x, gy.x, true);
-        __builtin_amdgcn_sched_barrier(0);
-        pixel((xc + 1.0f) - key.x, sdy, cdy, gx.y, gy.y, nv > 1);
-        __builtin_amdgcn_sched_barrier(0);
-        pixel((xc + 2.0f) - key.x, sdy, cdy, gx.z, gy.z, nv > 2);
-        __builtin_amdgcn_sched_barrier(0);
-        pixel((xc + 3.0f) - key.x, sdy, cdy, gx.w, gy.w, nv > 3);
-    }
+        while (r <= y1) {
+            const f4v gx = nb - na, gy = nd - nu;   // the strip's gradients (dx, dy per pixel)
+            const float dyk = ((float)r + 0.5f) - key.y;
+            const float sdy = srspt * dyk, cdy = crspt * dyk;
+            const int nv = lo + len - cx;
+            const float xc = (float)cx + 0.5f;   // (xc + i) - x_key: the same value in every lane
+            cx += 4;
+            if (cx >= lo + len) {
+                r += RSTEP;
+                next_row();
+            }
+            fetch();
+            // one pixel at a time (sched_barrier): four interleaved took ~150 VGPRs
+            pixel((xc) - key.x, sdy, cdy, gx.x, gy.x, true);
+            __builtin_amdgcn_sched_barrier(0);
+            pixel((xc + 1.0f) - key.x, sdy, cdy, gx.y, gy.y, nv > 1);
+            __builtin_amdgcn_sched_barrier(0);
+            pixel((xc + 2.0f) - key.x, sdy, cdy, gx.z, gy.z, nv > 2);
+            __builtin_amdgcn_sched_barrier(0);
+            pixel((xc + 3.0f) - key.x, sdy, cdy, gx.w, gy.w, nv > 3);
+        }
+    };
     // reduction: lanes 0..49 store their 32 bins ([lane][slot][bin], stride 33 floats against
     // bank conflicts); lane L then sums bins 2 sub, 2 sub + 1 of cell L >> 2 (descriptor_fast's
-    // output layout) over the 4 dual cells x 2 lanes that hold that cell
-    if (q < 25) {
-        float* my = hist + lane * 33;
+    // output layout) over the 4 dual cells x 2 lanes that hold that cell, group by group
+    auto store_bins = [&]() {
+        if (q < 25) {
+            float* my = hist + lane * 33;
 #pragma unroll
-        for (int h = 0; h < 2; h++)
+            for (int h = 0; h < 2; h++)
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                my[8 * (2 * h) + k] = acc[h][k].x;
-                my[8 * (2 * h + 1) + k] = acc[h][k].y;
-            }
-    }
-    asm volatile("" ::: "memory");
-    if (NW == 2) __syncthreads();   // the partner wave's bins are in hist + kDualWords
+                for (int k = 0; k < 8; k++) {
+                    my[8 * (2 * h) + k] = acc[h][k].x;
+                    my[8 * (2 * h + 1) + k] = acc[h][k].y;
+                }
+        }
+        asm volatile("" ::: "memory");
+    };
     const int cell = lane >> 2, sub = lane & 3;
     const int ix = cell & 3, iy = cell >> 2;
     float b0 = 0.0f, b1 = 0.0f;
-    const float* hist_pair = hist - wh * kDualWords;   // the pair's first region
-    if (wh == 0) {
+    auto add_region = [&](const float* reg) {
 #pragma unroll
-        for (int w = 0; w < NW; w++)
+        for (int k = 0; k < 4; k++) {
+            // slot k of dual cell (ix + 1 - (k & 1), iy + 1 - (k >> 1)) is this cell
+            const int dq = (iy + 1 - (k >> 1)) * 5 + ix + 1 - (k & 1);
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                // slot k of dual cell (ix + 1 - (k & 1), iy + 1 - (k >> 1)) is this cell
-                const int dq = (iy + 1 - (k >> 1)) * 5 + ix + 1 - (k & 1);
-#pragma unroll
-                for (int c2 = 0; c2 < 2; c2++) {
-                    const float* src = hist_pair + w * kDualWords + (2 * dq + c2) * 33 + 8 * k + 2 * sub;
-                    b0 += src[0];
-                    b1 += src[1];
-                }
+            for (int c2 = 0; c2 < 2; c2++) {
+                const float* src = reg + (2 * dq + c2) * 33 + 8 * k + 2 * sub;
+                b0 += src[0];
+                b1 += src[1];
             }
-    }
-    asm volatile("" ::: "memory");
-    if (NW == 2) {
-        __syncthreads();   // both regions read before the next feature writes them
-        if (wh != 0 || !live) return;
+        }
+        asm volatile("" ::: "memory");
+    };
+    if (NG == 2) {
+#pragma clang loop unroll(disable)
+        for (int g = 0; g < 2; g++) {
+            walk(y0 + 2 * g + cp);
+            store_bins();
+            add_region(hist);
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+                for (int k = 0; k < 8; k++) acc[h][k] = f2v{0.0f, 0.0f};
+        }
+    } else {
+        walk(y0 + 2 * wh + cp);
+        store_bins();
+        if (NW == 2) __syncthreads();   // the partner wave's bins are in hist + kDualWords
+        const float* hist_pair = hist - wh * kDualWords;   // the pair's first region
+        if (wh == 0)
+#pragma unroll
+            for (int w = 0; w < NW; w++) add_region(hist_pair + w * kDualWords);
+        if (NW == 2) {
+            __syncthreads();   // both regions read before the next feature writes them
+            if (wh != 0 || !live) return;
+        }
     }
     if (fp.normalize) {
         float sn = fma_(b0, b0, b1 * b1);
@@ -2819,7 +2894,10 @@ hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
         const OctaveDesc& od = fp.oct[o];
         const int strips_x = (od.wa + sw - 1) / sw;
         const long long per_col = (long long)strips_x * fp.batch;
-        int nseg = (int)std::min<long long>(std::max<long long>(1, (32768 + per_col - 1) / per_col),
+#ifndef SGK_EXT_WAVES
+#define SGK_EXT_WAVES 32768
+#endif
+        int nseg = (int)std::min<long long>(std::max<long long>(1, (SGK_EXT_WAVES + per_col - 1) / per_col),
                                             std::max(1, od.h / 16));
         // a segment reads one halo row above and below it: 2/17 = 12 % extra bytes on the 17-row
         // segments of the batch's upper octaves, so there segments get >= SGK_EXT_SEG_MIN rows
