@@ -2225,14 +2225,18 @@ constexpr int kDualWords = 50 * 33;   // reduction words per wave
 #ifndef SGK_DUAL_REF
 #define SGK_DUAL_REF 1   // cell weights from the reference's rounded cell centres
 #endif
-// SGK_DUAL_SPLIT = 1 (shipped): the one-wave kernel walks the two row groups of the two-wave
-// kernel in turn and sums them in the same order, so both give the same bits and a batch's
-// descriptors equal a single image's (the two-wave kernel serves few features, chosen from the
-// previous call's count): 1.786 vs 1.725 ms per 128 x 1080p step for the unsplit walk, whose
-// descriptors differed from the two-wave kernel's in the last bits (tests/diag/r04m.sh;
-// 128-thread two-wave workgroups for every count: 1.854-1.865 ms)
+// The one-wave and two-wave kernels must give the same bits, so that a batch's descriptors equal
+// a single image's (the two-wave kernel serves few features, chosen from the previous call's
+// count).  Shipped: SGK_DUAL2_BINS = 1, the pair splits the bins (both waves walk every row, as
+// the one-wave kernel).  The first form split the rows between the pair (C2 30.5 vs 40.9 us) and
+// differed in the last bits; SGK_DUAL_SPLIT = 1 makes the one-wave kernel walk those two row
+// groups in turn instead: bit-identical too, but 1.786-1.80 vs 1.725-1.74 ms per 128 x 1080p step
+// (tests/diag/r04m.sh, r04n.sh; 128-thread row-split pairs for every count: 1.854-1.865 ms).
 #ifndef SGK_DUAL_SPLIT
-#define SGK_DUAL_SPLIT 1
+#define SGK_DUAL_SPLIT 0
+#endif
+#ifndef SGK_DUAL2_BINS
+#define SGK_DUAL2_BINS 1
 #endif
 #ifndef SGK_DUAL_WPE
 #define SGK_DUAL_WPE 4   // waves per SIMD the allocation must allow: 4 = <= 128 VGPRs, no spills (132 free)
@@ -2336,11 +2340,17 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
     // the lane's 4 cells x 8 bins, cells in pairs: acc[h][k] = bin k of cell slots 2h, 2h + 1
     // (slot 0: cell (a-1, b-1), 1: (a, b-1), 2: (a-1, b), 3: (a, b)), so that each packed fma
     // takes one scalar tent weight and a pair of cell weights
-    f2v acc[2][8];
+    // BINS (two waves per feature, SGK_DUAL2_BINS): each wave of the pair walks every row of the
+    // lane's dual cell, as the one-wave kernel does, and accumulates half of the bins (wave wh:
+    // bins 4 wh .. 4 wh + 3), so every bin's sum is the one-wave kernel's bit for bit
+    constexpr bool BINS = NW == 2 && SGK_DUAL2_BINS;
+    constexpr int NB = BINS ? 4 : 8;
+    const int bin0 = BINS ? 4 * wh : 0;
+    f2v acc[2][NB];
 #pragma unroll
     for (int h = 0; h < 2; h++)
 #pragma unroll
-        for (int k = 0; k < 8; k++) acc[h][k] = f2v{0.0f, 0.0f};
+        for (int k = 0; k < NB; k++) acc[h][k] = f2v{0.0f, 0.0f};
     // a pixel's angle: the relaxed atan2, and within 1e-5 rad of the reference's one binning
     // discontinuity (theta rounding to 8.0 is dropped) the oracle's atan2 (descriptor_fast's
     // rule); the exact form is evaluated in one shared loop for the strip's flagged pixels (rare)
@@ -2380,9 +2390,16 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
         // tent weights max(0, 1 - |theta - k|), bin 0 also taking the wrap of bin 8
         // (ProgramCU.cu:1094), as descriptor_fast; then the outer product with the cell weights
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const float tk = k == 0 ? __builtin_amdgcn_fmed3f(fmax_(1.0f - th, th - 7.0f), 0.0f, 1.0f)
-                                    : __builtin_amdgcn_fmed3f(1.0f - fabs_(th - (float)k), 0.0f, 1.0f);
+        for (int k = 0; k < NB; k++) {
+            float tk;
+            if (!BINS) {
+                tk = k == 0 ? __builtin_amdgcn_fmed3f(fmax_(1.0f - th, th - 7.0f), 0.0f, 1.0f)
+                            : __builtin_amdgcn_fmed3f(1.0f - fabs_(th - (float)k), 0.0f, 1.0f);
+            } else {   // the same operations on the bin's value (bin 0: wave 0, k = 0)
+                const float t0 = __builtin_amdgcn_fmed3f(fmax_(1.0f - th, th - 7.0f), 0.0f, 1.0f);
+                const float tg = __builtin_amdgcn_fmed3f(1.0f - fabs_(th - (float)(bin0 + k)), 0.0f, 1.0f);
+                tk = (k == 0 && bin0 == 0) ? t0 : tg;
+            }
             acc[0][k] = pk_fma(cpa, tk, acc[0][k]);
             acc[1][k] = pk_fma(cpb, tk, acc[1][k]);
         }
@@ -2398,7 +2415,7 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
     // summed before the next group, so the sums are k_descriptor_dual2's bit for bit (a batch
     // gives the features of a single image exactly)
     constexpr int NG = (NW == 1 && SGK_DUAL_SPLIT) ? 2 : 1;
-    constexpr int RSTEP = 2 * NW * NG;
+    constexpr int RSTEP = BINS ? 2 : 2 * NW * NG;
     int r = 0, lo = 0, len = 0, cx = 0;
     auto next_row = [&]() {   // advance r (by RSTEP) to the next row with a nonempty span
 #pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
@@ -2446,13 +2463,13 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
     // reduction: lanes 0..49 store their 32 bins ([lane][slot][bin], stride 33 floats against
     // bank conflicts); lane L then sums bins 2 sub, 2 sub + 1 of cell L >> 2 (descriptor_fast's
     // output layout) over the 4 dual cells x 2 lanes that hold that cell, group by group
-    auto store_bins = [&]() {
+    auto store_bins = [&]() {   // (BINS: both waves into the pair's first region)
         if (q < 25) {
-            float* my = hist + lane * 33;
+            float* my = (BINS ? hist - wh * kDualWords : hist) + lane * 33 + bin0;
 #pragma unroll
             for (int h = 0; h < 2; h++)
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
+                for (int k = 0; k < NB; k++) {
                     my[8 * (2 * h) + k] = acc[h][k].x;
                     my[8 * (2 * h + 1) + k] = acc[h][k].y;
                 }
@@ -2485,16 +2502,16 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
 #pragma unroll
             for (int h = 0; h < 2; h++)
 #pragma unroll
-                for (int k = 0; k < 8; k++) acc[h][k] = f2v{0.0f, 0.0f};
+                for (int k = 0; k < NB; k++) acc[h][k] = f2v{0.0f, 0.0f};
         }
     } else {
-        walk(y0 + 2 * wh + cp);
+        walk(BINS ? y0 + cp : y0 + 2 * wh + cp);
         store_bins();
         if (NW == 2) __syncthreads();   // the partner wave's bins are in hist + kDualWords
         const float* hist_pair = hist - wh * kDualWords;   // the pair's first region
         if (wh == 0)
 #pragma unroll
-            for (int w = 0; w < NW; w++) add_region(hist_pair + w * kDualWords);
+            for (int w = 0; w < (BINS ? 1 : NW); w++) add_region(hist_pair + w * kDualWords);
         if (NW == 2) {
             __syncthreads();   // both regions read before the next feature writes them
             if (wh != 0 || !live) return;
