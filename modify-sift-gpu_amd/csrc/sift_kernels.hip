@@ -1500,24 +1500,40 @@ __device__ __forceinline__ void orientation_hist_wave(const OriKey& K, const Fea
     const int nrows = ymax >= ymin ? (int)(ymax - ymin) + 1 : 0;
     const int total = ncols * nrows;
     float acc = 0.0f;   // bin `lane`
-    for (int base = 0; base < total; base += 64) {
+    // sample base + lane: its pixel and the 4 gradient neighbours, fetched one batch ahead (the
+    // loads are unconditional, at a clamped in-plane pixel, so the compiler waits only for the
+    // batch it uses); `in` = inside the window and the circle
+    struct Smp { float x, y, sq, a, b, c, d; bool in; };
+    auto fetch = [&](int base, Smp& q) {
         const int sidx = base + lane;
+        const bool valid = sidx < total;
+        const int si = valid ? sidx : 0;
+        const int r = si / max(ncols, 1), c = si - r * max(ncols, 1);
+        q.x = xmin + (float)c;
+        q.y = ymin + (float)r;
+        const float dx = q.x - K.kx, dy = q.y - K.ky;
+        q.sq = fma_(dx, dx, dy * dy);
+        q.in = valid && total > 0 && !(fp.circular && q.sq >= dist_threshold);
+        const int px = q.in ? (int)q.x : 1, py = q.in ? (int)q.y : 1;   // (1, 1): in-plane
+        const float* p = K.g + (long long)py * K.W + px;
+        q.a = p[1];
+        q.b = p[-1];
+        q.c = p[K.W];
+        q.d = p[-K.W];
+    };
+    Smp cur, nxt;
+    fetch(0, cur);
+    for (int base = 0; base < total; base += 64) {
+        fetch(base + 64, nxt);
         int bin = -1;
         float weight = 0.0f;
-        if (sidx < total) {
-            const int r = sidx / ncols, c = sidx - r * ncols;
-            const float x = xmin + (float)c, y = ymin + (float)r;
-            const float dx = x - K.kx, dy = y - K.ky;
-            const float sq = fma_(dx, dx, dy * dy);
-            if (!(fp.circular && sq >= dist_threshold)) {
-                const float* p = K.g + (long long)(int)y * K.W + (int)x;
-                const float gdx = p[1] - p[-1], gdy = p[K.W] - p[-K.W];   // grad_at
-                const float grd = 0.5f * sqrt_(fma_(gdx, gdx, gdy * gdy));
-                const float rot = grd == 0.0f ? 0.0f : atan2_(gdy, gdx);
-                weight = grd * exp_(sq * factor);
-                bin = (int)floor_(rot * ten_degree_per_radius);
-                if (bin < 0) bin += 36;
-            }
+        if (cur.in) {
+            const float gdx = cur.a - cur.b, gdy = cur.c - cur.d;   // grad_at
+            const float grd = 0.5f * sqrt_(fma_(gdx, gdx, gdy * gdy));
+            const float rot = grd == 0.0f ? 0.0f : atan2_(gdy, gdx);
+            weight = grd * exp_(cur.sq * factor);
+            bin = (int)floor_(rot * ten_degree_per_radius);
+            if (bin < 0) bin += 36;
         }
         const int nb = min(64, total - base);   // uniform
         for (int k = 0; k < nb; k++) {
@@ -1525,24 +1541,26 @@ __device__ __forceinline__ void orientation_hist_wave(const OriKey& K, const Fea
             const float wk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(weight), k));
             acc += bk == lane ? wk : 0.0f;
         }
+        cur = nxt;
     }
-    if (lane < 36) s_v[lane] = acc;
-    asm volatile("" ::: "memory");   // one wave: its LDS writes complete before its reads
+    // the 6 smoothing passes, a bin per lane: each pass is a stencil over the previous pass's
+    // values, (pre + vote[j]) + vote[j + 1] as the serial form, the ring through the wave's LDS
+    const float one_third = (float)(1.0 / 3.0);
+    const int jm = lane == 0 ? 35 : lane - 1, jp = lane == 35 ? 0 : lane + 1;
+    float v = acc;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        if (lane < 36) s_v[lane] = v;
+        asm volatile("" ::: "memory");   // one wave: its LDS writes complete before its reads
+        const float pre = s_v[min(jm, 35)], nx = s_v[min(jp, 35)];
+        asm volatile("" ::: "memory");
+        v = one_third * (pre + v + nx);
+    }
+    if (lane < 36) s_v[lane] = v;
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int i = 0; i < 36; ++i) vote[i] = s_v[i];
     asm volatile("" ::: "memory");
-    const float one_third = (float)(1.0 / 3.0);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        vote[36] = vote[0];
-        float pre = vote[35];
-#pragma unroll
-        for (int j = 0; j < 36; ++j) {
-            const float temp = one_third * (pre + vote[j] + vote[j + 1]);
-            pre = vote[j];
-            vote[j] = temp;
-        }
-    }
     vote[36] = vote[0];
 }
 
@@ -2225,19 +2243,12 @@ constexpr int kDualWords = 50 * 33;   // reduction words per wave
 #ifndef SGK_DUAL_REF
 #define SGK_DUAL_REF 1   // cell weights from the reference's rounded cell centres
 #endif
-// The one-wave and two-wave kernels must give the same bits, so that a batch's descriptors equal
-// a single image's (the two-wave kernel serves few features, chosen from the previous call's
-// count).  Shipped: SGK_DUAL2_BINS = 1, the pair splits the bins (both waves walk every row, as
-// the one-wave kernel).  The first form split the rows between the pair (C2 30.5 vs 40.9 us) and
-// differed in the last bits; SGK_DUAL_SPLIT = 1 makes the one-wave kernel walk those two row
-// groups in turn instead: bit-identical too, but 1.786-1.80 vs 1.725-1.74 ms per 128 x 1080p step
-// (tests/diag/r04m.sh, r04n.sh; 128-thread row-split pairs for every count: 1.854-1.865 ms).
-#ifndef SGK_DUAL_SPLIT
-#define SGK_DUAL_SPLIT 0
-#endif
-#ifndef SGK_DUAL2_BINS
-#define SGK_DUAL2_BINS 1
-#endif
+// One wave per feature for every feature count.  Two-wave forms for few features (a single
+// image) were measured in round 4: splitting each dual cell's rows between the
+// pair (C2 30.9 vs 41 us) changes the sums' order, so a batch's descriptors no longer equalled a
+// single image's; the bit-identical forms lost -- the pair splitting the bins 49.3 us (both waves
+// walk every row), the one-wave kernel walking the pair's row groups in turn 1.786-1.80 vs
+// 1.725-1.74 ms per 128 x 1080p step.
 #ifndef SGK_DUAL_WPE
 #define SGK_DUAL_WPE 4   // waves per SIMD the allocation must allow: 4 = <= 128 VGPRs, no spills (132 free)
 #endif
@@ -2246,18 +2257,11 @@ constexpr int kDualWords = 50 * 33;   // reduction words per wave
 #else
 #define SGK_DUAL_ATTR
 #endif
-// NW waves per feature: 1 (batches), or 2 for few features (a single image: one wave per feature
-// leaves most SIMDs idle), wave wh of the pair walking rows 2 wh + cp, 2 wh + cp + 4, ... of
-// every dual cell; the pair's partial bins meet in LDS across a workgroup barrier.  live =
-// false: a wave pair past the last feature (it still reaches the barriers).
-template <int NW>
 __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const float* __restrict__ pyr,
                                                 const float4* __restrict__ feat,
                                                 const int2* __restrict__ feat_info,
                                                 const FeatureParams& fp, float* __restrict__ desc,
-                                                uint32_t out, float* __restrict__ hist,
-                                                int wh = 0, bool live = true) {
-    if (!live) e = 0;   // any valid record; nothing is walked or written
+                                                uint32_t out, float* __restrict__ hist) {
     const float4 key = feat[e];
     const int2 in = feat_info[e];
     const int o = in.y / fp.d, j = in.y - o * fp.d;
@@ -2291,7 +2295,7 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
     int y1 = (int)fmin_(fH - 2.0f, fmax_(-1.0f, floor_(cyi + hb - 0.5f)));
     const int bx0 = (int)fmax_(1.0f, fmin_(fW, ceilf(cxi - hb - 0.5f)));
     const int bx1 = (int)fmin_(fW - 2.0f, fmax_(-1.0f, floor_(cxi + hb - 0.5f)));
-    if (q >= 25 || !(spt > 0.0f) || !live) y1 = y0 - 1;
+    if (q >= 25 || !(spt > 0.0f)) y1 = y0 - 1;
     // row span: the columns whose u = dnx + 2.5 - a and v = dny + 2.5 - b can lie in [0, 1],
     // dnx = crspt dxk + srspt dyk, dny = crspt dyk - srspt dxk (dxk, dyk from the keypoint); the
     // 0.01-pixel margin absorbs rounding, the per-pixel test decides
@@ -2340,17 +2344,11 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
     // the lane's 4 cells x 8 bins, cells in pairs: acc[h][k] = bin k of cell slots 2h, 2h + 1
     // (slot 0: cell (a-1, b-1), 1: (a, b-1), 2: (a-1, b), 3: (a, b)), so that each packed fma
     // takes one scalar tent weight and a pair of cell weights
-    // BINS (two waves per feature, SGK_DUAL2_BINS): each wave of the pair walks every row of the
-    // lane's dual cell, as the one-wave kernel does, and accumulates half of the bins (wave wh:
-    // bins 4 wh .. 4 wh + 3), so every bin's sum is the one-wave kernel's bit for bit
-    constexpr bool BINS = NW == 2 && SGK_DUAL2_BINS;
-    constexpr int NB = BINS ? 4 : 8;
-    const int bin0 = BINS ? 4 * wh : 0;
-    f2v acc[2][NB];
+    f2v acc[2][8];
 #pragma unroll
     for (int h = 0; h < 2; h++)
 #pragma unroll
-        for (int k = 0; k < NB; k++) acc[h][k] = f2v{0.0f, 0.0f};
+        for (int k = 0; k < 8; k++) acc[h][k] = f2v{0.0f, 0.0f};
     // a pixel's angle: the relaxed atan2, and within 1e-5 rad of the reference's one binning
     // discontinuity (theta rounding to 8.0 is dropped) the oracle's atan2 (descriptor_fast's
     // rule); the exact form is evaluated in one shared loop for the strip's flagged pixels (rare)
@@ -2390,16 +2388,9 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
         // tent weights max(0, 1 - |theta - k|), bin 0 also taking the wrap of bin 8
         // (ProgramCU.cu:1094), as descriptor_fast; then the outer product with the cell weights
 #pragma unroll
-        for (int k = 0; k < NB; k++) {
-            float tk;
-            if (!BINS) {
-                tk = k == 0 ? __builtin_amdgcn_fmed3f(fmax_(1.0f - th, th - 7.0f), 0.0f, 1.0f)
-                            : __builtin_amdgcn_fmed3f(1.0f - fabs_(th - (float)k), 0.0f, 1.0f);
-            } else {   // the same operations on the bin's value (bin 0: wave 0, k = 0)
-                const float t0 = __builtin_amdgcn_fmed3f(fmax_(1.0f - th, th - 7.0f), 0.0f, 1.0f);
-                const float tg = __builtin_amdgcn_fmed3f(1.0f - fabs_(th - (float)(bin0 + k)), 0.0f, 1.0f);
-                tk = (k == 0 && bin0 == 0) ? t0 : tg;
-            }
+        for (int k = 0; k < 8; k++) {
+            const float tk = k == 0 ? __builtin_amdgcn_fmed3f(fmax_(1.0f - th, th - 7.0f), 0.0f, 1.0f)
+                                    : __builtin_amdgcn_fmed3f(1.0f - fabs_(th - (float)k), 0.0f, 1.0f);
             acc[0][k] = pk_fma(cpa, tk, acc[0][k]);
             acc[1][k] = pk_fma(cpb, tk, acc[1][k]);
         }
@@ -2410,12 +2401,7 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
     const char* gb = reinterpret_cast<const char*>(g);
     typedef float f4v __attribute__((ext_vector_type(4)));
     auto ld4 = [&](uint32_t byte) { return *reinterpret_cast<const f4v*>(gb + byte); };
-    // NG row groups walked in turn by this wave (NW = 1 with SGK_DUAL_SPLIT): group g holds rows
-    // y0 + 2 g + cp + 4 k, the rows wave g of a two-wave pair walks, and its bins are flushed and
-    // summed before the next group, so the sums are k_descriptor_dual2's bit for bit (a batch
-    // gives the features of a single image exactly)
-    constexpr int NG = (NW == 1 && SGK_DUAL_SPLIT) ? 2 : 1;
-    constexpr int RSTEP = BINS ? 2 : 2 * NW * NG;
+    constexpr int RSTEP = 2;   // lane cp walks rows y0 + cp, y0 + cp + 2, ...
     int r = 0, lo = 0, len = 0, cx = 0;
     auto next_row = [&]() {   // advance r (by RSTEP) to the next row with a nonempty span
 #pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
@@ -2462,14 +2448,14 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
     };
     // reduction: lanes 0..49 store their 32 bins ([lane][slot][bin], stride 33 floats against
     // bank conflicts); lane L then sums bins 2 sub, 2 sub + 1 of cell L >> 2 (descriptor_fast's
-    // output layout) over the 4 dual cells x 2 lanes that hold that cell, group by group
-    auto store_bins = [&]() {   // (BINS: both waves into the pair's first region)
+    // output layout) over the 4 dual cells x 2 lanes that hold that cell
+    auto store_bins = [&]() {
         if (q < 25) {
-            float* my = (BINS ? hist - wh * kDualWords : hist) + lane * 33 + bin0;
+            float* my = hist + lane * 33;
 #pragma unroll
             for (int h = 0; h < 2; h++)
 #pragma unroll
-                for (int k = 0; k < NB; k++) {
+                for (int k = 0; k < 8; k++) {
                     my[8 * (2 * h) + k] = acc[h][k].x;
                     my[8 * (2 * h + 1) + k] = acc[h][k].y;
                 }
@@ -2493,30 +2479,9 @@ __device__ __forceinline__ void descriptor_dual(uint32_t e, int lane, const floa
         }
         asm volatile("" ::: "memory");
     };
-    if (NG == 2) {
-#pragma clang loop unroll(disable)
-        for (int g = 0; g < 2; g++) {
-            walk(y0 + 2 * g + cp);
-            store_bins();
-            add_region(hist);
-#pragma unroll
-            for (int h = 0; h < 2; h++)
-#pragma unroll
-                for (int k = 0; k < NB; k++) acc[h][k] = f2v{0.0f, 0.0f};
-        }
-    } else {
-        walk(BINS ? y0 + cp : y0 + 2 * wh + cp);
-        store_bins();
-        if (NW == 2) __syncthreads();   // the partner wave's bins are in hist + kDualWords
-        const float* hist_pair = hist - wh * kDualWords;   // the pair's first region
-        if (wh == 0)
-#pragma unroll
-            for (int w = 0; w < (BINS ? 1 : NW); w++) add_region(hist_pair + w * kDualWords);
-        if (NW == 2) {
-            __syncthreads();   // both regions read before the next feature writes them
-            if (wh != 0 || !live) return;
-        }
-    }
+    walk(y0 + cp);
+    store_bins();
+    add_region(hist);
     if (fp.normalize) {
         float sn = fma_(b0, b0, b1 * b1);
 #pragma unroll
@@ -2548,32 +2513,8 @@ __global__ __launch_bounds__(256) SGK_DUAL_ATTR void k_descriptor_dual(const flo
     float* hist = s_hist[wave];
     const uint32_t n = *n_feat_dev;
     for (uint32_t e = blockIdx.x * 4 + wave; e < n; e += gridDim.x * 4)
-        descriptor_dual<1>(e, lane, pyr, feat, feat_info, fp, desc,
+        descriptor_dual(e, lane, pyr, feat, feat_info, fp, desc,
                            out_index ? (uint32_t)out_index[e] : e, hist);
-}
-
-// Two waves per feature (few features), two features per workgroup; the loop bound is uniform
-// over the workgroup (its barriers).
-__global__ __launch_bounds__(256) SGK_DUAL_ATTR void k_descriptor_dual2(const float* __restrict__ pyr,
-                                                          const float4* __restrict__ feat,
-                                                          const int2* __restrict__ feat_info,
-                                                          const uint32_t* __restrict__ n_feat_dev,
-                                                          const FeatureParams fp,
-                                                          float* __restrict__ desc,
-                                                          const int* __restrict__ out_index) {
-    __shared__ float s_hist[4][kDualWords];
-    const int lane = threadIdx.x & 63;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int pair = wave >> 1, wh = wave & 1;
-    float* hist = s_hist[2 * pair];
-    const uint32_t n = *n_feat_dev;
-    for (uint32_t b0 = blockIdx.x * 2; b0 < n; b0 += gridDim.x * 2) {
-        const uint32_t e = b0 + pair;
-        const bool live = e < n;
-        descriptor_dual<2>(e, lane, pyr, feat, feat_info, fp, desc,
-                           live && out_index ? (uint32_t)out_index[e] : e, hist + wh * kDualWords,
-                           wh, live);
-    }
 }
 
 // One wave per feature, grid-stride over the features (count read on the device).
@@ -3056,18 +2997,9 @@ hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* f
 #ifndef SGK_DESC_DUAL
 #define SGK_DESC_DUAL 1
 #endif
-#ifndef SGK_DUAL2_MAX
-#define SGK_DUAL2_MAX 16384   // up to this many features (previous call's count): two waves each
-#endif
-    constexpr int kDual2Max = SGK_DUAL2_MAX;
     if (!exact && !rect && SGK_DESC_DUAL) {
-        // few features (the grid comes from the previous call's count): two waves per feature
-        if (n_feat_cap <= kDual2Max)
-            hipLaunchKernelGGL(k_descriptor_dual2, dim3((unsigned)((n_feat_cap + 1) / 2)), dim3(256), 0,
-                               stream, pyr, feat, feat_info, n_feat_dev, fp, desc, out_index);
-        else
-            hipLaunchKernelGGL(k_descriptor_dual, dim3(grid), dim3(256), 0, stream, pyr, feat,
-                               feat_info, n_feat_dev, fp, desc, out_index);
+        hipLaunchKernelGGL(k_descriptor_dual, dim3(grid), dim3(256), 0, stream, pyr, feat,
+                           feat_info, n_feat_dev, fp, desc, out_index);
         return hipGetLastError();
     }
     if (!exact) {
