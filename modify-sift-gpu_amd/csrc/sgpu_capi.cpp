@@ -303,6 +303,9 @@ static int part_streams(Part& pt, int which = PS_ALL) {
         hipStreamCreateWithPriority(&pt.stream_oct, hipStreamNonBlocking, prio_hi) != hipSuccess)
         return SGPU_ENODEV;
     if (!pt.ev_ds) {
+        // stage events.  Each record leaves the GPU idle ~4.5 us between the kernels around it
+        // (C2 kernel trace; tests/microbench/event_gap.hip), whatever its flags: a device-scope
+        // release or no timing at all measured the same
         for (hipEvent_t& e : pt.ev)
             if (hipEventCreate(&e) != hipSuccess) return SGPU_ENODEV;
         if (hipEventCreateWithFlags(&pt.ev_ds, hipEventDisableTiming) != hipSuccess ||
@@ -787,9 +790,15 @@ static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
     ctx->part[0].one_stream = one;
     const hipStream_t up = one ? ctx->part[0].stream : ctx->stream;
 
-    // input: host batches are uploaded first on the context stream
+    // input: host batches are uploaded first on the context stream.  The upload's events are
+    // recorded only when there is input work to time or a stream to join: every event record
+    // in a stream costs ~4.5 us of GPU time between the commands around it, whatever its flags
+    // (tests/microbench/event_gap.hip: 2.2 vs 6.7 us per short kernel), and a staged or device
+    // batch on one stream has neither (C2, the bench's batches)
     const size_t in_bytes = (size_t)n * h * stride * (is_f32 ? sizeof(float) : 1);
-    HIPCHK(ctx, hipEventRecord(ctx->ev[0], up));
+    const bool up_events = !one || color || plan.ds > 0 ||
+                           !(flags & (SGPU_INPUT_DEVICE | SGPU_INPUT_STAGED));
+    if (up_events) HIPCHK(ctx, hipEventRecord(ctx->ev[0], up));
     const void* src_in = staged ? ctx->input.p : images;
     if (!(flags & (SGPU_INPUT_DEVICE | SGPU_INPUT_STAGED))) {
         ctx->staged_bytes = 0;
@@ -823,7 +832,7 @@ static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
         is_f32 = true;
         stride = plan.w;
     }
-    HIPCHK(ctx, hipEventRecord(ctx->ev[1], up));
+    if (up_events) HIPCHK(ctx, hipEventRecord(ctx->ev[1], up));
 
     // part p's pyramid starts when part p-1 has finished detection
     for (int p = 0; p < np; p++) {
@@ -868,7 +877,8 @@ static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
 
     // timings: stages of part 0 (its pyramid and detection run alone), total over all parts
     Part& p0 = ctx->part[0];
-    (void)hipEventElapsedTime(&ctx->timing[T_UPLOAD], ctx->ev[0], ctx->ev[1]);
+    ctx->timing[T_UPLOAD] = 0.0f;
+    if (up_events) (void)hipEventElapsedTime(&ctx->timing[T_UPLOAD], ctx->ev[0], ctx->ev[1]);
     (void)hipEventElapsedTime(&ctx->timing[T_PYRAMID], p0.ev[0], p0.ev[1]);
     (void)hipEventElapsedTime(&ctx->timing[T_DETECT], p0.ev[1], p0.ev[2]);
     (void)hipEventElapsedTime(&ctx->timing[T_LIST], p0.ev[7], p0.ev[2]);
@@ -876,7 +886,7 @@ static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
     (void)hipEventElapsedTime(&ctx->timing[T_EXPAND], p0.ev[3], p0.ev[4]);
     (void)hipEventElapsedTime(&ctx->timing[T_DESC], p0.ev[4], p0.ev[5]);
     (void)hipEventElapsedTime(&ctx->timing[T_DOWNLOAD], p0.ev[5], p0.ev[6]);
-    (void)hipEventElapsedTime(&ctx->timing[T_TOTAL], ctx->ev[0], ctx->part[np - 1].ev[6]);
+    (void)hipEventElapsedTime(&ctx->timing[T_TOTAL], up_events ? ctx->ev[0] : p0.ev[0], ctx->part[np - 1].ev[6]);
     return SGPU_OK;
 }
 
@@ -1154,7 +1164,7 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     }
     const uint8_t* a = d1;
     const uint8_t* b = d2;
-    HIPCHK(ctx, hipEventRecord(ctx->ev[0], st));
+    // (no event before the uploads: nothing reads it, and each record costs ~4.5 us of GPU time)
     if (!(flags & SGPU_INPUT_DEVICE)) {
         ALLOCCHK(ctx, ctx->m_d1.ensure((size_t)n1 * 128));
         ALLOCCHK(ctx, ctx->m_d2.ensure((size_t)n2 * 128));
@@ -1350,7 +1360,7 @@ int sgpu_match_shard_begin(sgpu_ctx* ctx, const uint8_t* d1, int ns, int row_beg
     }
     const uint8_t* a = d1;
     const uint8_t* b = d2;
-    HIPCHK(ctx, hipEventRecord(ctx->ev[0], st));
+    // (no event before the uploads: nothing reads it, and each record costs ~4.5 us of GPU time)
     if (!(flags & SGPU_INPUT_DEVICE)) {
         ALLOCCHK(ctx, ctx->m_d1.ensure((size_t)ns * 128));
         ALLOCCHK(ctx, ctx->m_d2.ensure((size_t)n2 * 128));
