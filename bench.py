@@ -129,6 +129,11 @@ def main():
 
     B, W, H = args.batch, args.width, args.height
     opts = default_options(octave_num=args.octaves)
+    c2 = None
+    if rank == 0 and world == 1 and args.workload == "c3" and not args.no_c2:
+        # C2 is its own program (speed.cpp's protocol, a child process): it runs before this
+        # process creates its context, so that the child has the GPU to itself, as speed.cpp
+        c2 = bench_c2(cpu=not args.no_cpu_baseline)
     ctx = sgpu.SiftContext(device, opts)
     rccl = world > 1 and args.dist_backend == "rccl"
     if rccl:
@@ -274,8 +279,8 @@ def main():
         sm = bench_match_sharded(ctx, args.match_n, rank, world, None if rccl else dist)
         if rank == 0:
             result["match_sharded"] = sm
-    if rank == 0 and world == 1 and args.workload == "c3" and not args.no_c2:
-        result["c2"] = bench_c2(cpu=not args.no_cpu_baseline)
+    if c2 is not None:
+        result["c2"] = c2
     if rank == 0 and not args.no_cpu_baseline:
         # rank 0 on the host cores beside its GPU work, for every N (the line is self-contained)
         result["cpu_baseline"] = cpu_baseline(imgs, opts)
