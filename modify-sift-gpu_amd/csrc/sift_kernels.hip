@@ -1486,7 +1486,8 @@ __device__ __forceinline__ void orientation_one(uint32_t f, int sub, float* vote
 // float adds (the other samples add nothing: acc + 0.0f = acc, acc >= +0), so the histogram is
 // orientation_hist's bit for bit.  Same window, sample arithmetic and smoothing.
 __device__ __forceinline__ void orientation_hist_wave(const OriKey& K, const FeatureParams& fp,
-                                                      int lane, float* s_v, float (&vote)[37]) {
+                                                      int lane, float* s_v, float2* s_bw,
+                                                      float (&vote)[37]) {
     const float ten_degree_per_radius = (float)5.7295779513082320876798154814105;
     const float gsigma = K.kz * fp.gaussian_factor;
     const float win = fabs_(K.kz) * fp.sample_factor;
@@ -1535,12 +1536,21 @@ __device__ __forceinline__ void orientation_hist_wave(const OriKey& K, const Fea
             bin = (int)floor_(rot * ten_degree_per_radius);
             if (bin < 0) bin += 36;
         }
+        // the batch's (bin, weight) pairs through the wave's LDS (every lane writes one: samples
+        // past the window have bin -1), read back as broadcasts of 4 pairs; lane b adds the
+        // weights of bin b in sample order (the others add +0, which leaves acc >= +0 unchanged)
         const int nb = min(64, total - base);   // uniform
-        for (int k = 0; k < nb; k++) {
-            const int bk = __builtin_amdgcn_readlane(bin, k);
-            const float wk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(weight), k));
-            acc += bk == lane ? wk : 0.0f;
+        s_bw[lane] = make_float2(__int_as_float(bin), weight);
+        asm volatile("" ::: "memory");   // one wave: its LDS writes complete before its reads
+        for (int k = 0; k < nb; k += 4) {
+            const float4 q0 = *reinterpret_cast<const float4*>(&s_bw[k]);
+            const float4 q1 = *reinterpret_cast<const float4*>(&s_bw[k + 2]);
+            acc += __float_as_int(q0.x) == lane ? q0.y : 0.0f;
+            acc += __float_as_int(q0.z) == lane ? q0.w : 0.0f;
+            acc += __float_as_int(q1.x) == lane ? q1.y : 0.0f;
+            acc += __float_as_int(q1.z) == lane ? q1.w : 0.0f;
         }
+        asm volatile("" ::: "memory");   // read before the next batch overwrites them
         cur = nxt;
     }
     // the 6 smoothing passes, a bin per lane: each pass is a stencil over the previous pass's
@@ -1575,6 +1585,7 @@ __global__ __launch_bounds__(256) void k_orientation_wave(const float* __restric
                                                           int2* __restrict__ info,
                                                           uint32_t* __restrict__ ocount) {
     __shared__ float s_vote[4][64];
+    __shared__ __attribute__((aligned(16))) float2 s_pair[4][64];
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t n = min(*n_cand_dev, cap);
@@ -1584,7 +1595,7 @@ __global__ __launch_bounds__(256) void k_orientation_wave(const float* __restric
                              ocount, K))
             continue;
         float vote[37];
-        orientation_hist_wave(K, fp, lane, s_vote[wave], vote);
+        orientation_hist_wave(K, fp, lane, s_vote[wave], s_pair[wave], vote);
         if (lane == 0) orientation_finish(f, vote, K, fp, out4, ocount);
         asm volatile("" ::: "memory");   // the next candidate's votes overwrite s_vote after
     }
