@@ -100,7 +100,10 @@ struct Part {
 
 constexpr int kMaxParts = 4;
 // candidate counts (of the previous call) up to which orientation runs one wave per candidate
-constexpr size_t kWaveOrientationMax = 16384;
+#ifndef SGPU_WAVE_ORIENT_MAX
+#define SGPU_WAVE_ORIENT_MAX 16384
+#endif
+constexpr size_t kWaveOrientationMax = SGPU_WAVE_ORIENT_MAX;
 
 }  // namespace
 
