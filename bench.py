@@ -547,17 +547,25 @@ def bench_c2(repeat=30, cpu=True):
             pgm = os.path.join(td, "c2.pgm")
             with open(pgm, "wb") as f:
                 f.write(b"P5\n1920 1080\n255\n" + img.tobytes())
-            r = subprocess.run([exe, str(repeat), "--", "-i", pgm, "-fo", "0", "-no", "4", "-d", "3"],
-                               capture_output=True, text=True, timeout=300)
-        if r.returncode != 0:
-            return {"error": f"speed_replica exit {r.returncode}: {r.stderr[-300:]}"}
-        sp = json.loads(r.stdout.strip().splitlines()[-1])
+            # three runs of the protocol (each its own process, as speed.cpp), the median kept:
+            # one run's 30 calls share the box's state of the moment (one read 0.53 ms with a
+            # slow descriptor download, against 0.38-0.41 in the runs around it)
+            runs = []
+            for _ in range(3):
+                r = subprocess.run([exe, str(repeat), "--", "-i", pgm, "-fo", "0", "-no", "4", "-d", "3"],
+                                   capture_output=True, text=True, timeout=300)
+                if r.returncode != 0:
+                    return {"error": f"speed_replica exit {r.returncode}: {r.stderr[-300:]}"}
+                runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+        runs.sort(key=lambda x: x["avg_ms"])
+        sp = runs[1]
     except Exception as ex:   # never costs the main measurement
         return {"error": str(ex)}
     out = {"workload": "C2: one 1920x1080 u8 PGM, -fo 0 -no 4 -d 3, SiftGPU::RunSIFT() through "
                        "include/SiftGPU.h (TestWin/speed.cpp protocol, bin/speed_replica)",
            "value": 1e3 / sp["avg_ms"], "unit": "images/s", "ms_per_image": sp["avg_ms"],
            "features": sp["features"], "repeat": sp["repeat"], "stable": sp["stable"],
+           "runs_ms_per_image": [x["avg_ms"] for x in runs], "run_kept": "median of 3",
            "timing_ms": sp["timing_ms"],
            "note": "host image in, features in the object's host buffers; _timing slots as "
                    "SiftGPU.cpp:368 / speed.cpp:147-153"}
