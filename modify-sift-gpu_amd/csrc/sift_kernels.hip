@@ -2866,8 +2866,15 @@ hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
 #ifndef SGK_EXT_WAVES
 #define SGK_EXT_WAVES 32768
 #endif
+        // segments of >= 16 rows; a single image >= 8 (C2: its ~1,100 octave-0 waves are
+        // latency-bound walks, detection 35.6 vs 44.0 us, C2 0.371-0.377 vs 0.380-0.387 ms per
+        // image, tests/diag/r04u.sh; batches keep 16: their halo rows are HBM bytes)
+#ifndef SGK_EXT_MINROWS
+#define SGK_EXT_MINROWS 16
+#endif
+        const int minrows = fp.batch == 1 ? 8 : SGK_EXT_MINROWS;
         int nseg = (int)std::min<long long>(std::max<long long>(1, (SGK_EXT_WAVES + per_col - 1) / per_col),
-                                            std::max(1, od.h / 16));
+                                            std::max(1, od.h / minrows));
         // a segment reads one halo row above and below it: 2/17 = 12 % extra bytes on the 17-row
         // segments of the batch's upper octaves, so there segments get >= SGK_EXT_SEG_MIN rows
         // while the octave keeps >= 8192 waves (a single image keeps its short segments: there
