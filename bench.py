@@ -188,10 +188,10 @@ def main():
         dist.all_reduce(f)
         feats = int(f.item())
 
-    n_filters = 1 + args.octaves * 5                    # level 0 of octave 0 + 5 levels/octave
-    # launches: the diagonal schedule runs octave o+1's levels 1, 2 in octave o's
-    # level 4 / 5 launches (-d 3: level 3 decimates), slot o*3 + k
-    n_gauss = 3 * (args.octaves - 1) + 6
+    # level filters and their kernel launches, as the library ran them (the diagonal schedule
+    # shares launches between octaves, the paired-level kernel filters two levels per launch;
+    # DESIGN.md 4.3-4.5)
+    n_gauss, n_filters = ctx.pyramid_launches()
     total_images = B * world * args.steps
     sumN = geometry_sum(W, H, args.octaves)
     pyr_bytes = 48.0 * sumN * B * args.steps          # 48 B per pyramid px
@@ -228,9 +228,9 @@ def main():
         "features_per_image": local_feats / (B * args.steps),
         "stage_ms_per_step": {k: v / args.steps for k, v in stage_acc.items() if k != "match"},
         "roofline": {
-            "kernel": f"k_gauss_lean / k_gauss_diag (separable Gaussian levels: the {n_filters} "
-                      f"level filters of a step in {n_gauss} launches, back to back on the "
-                      "library's stream, HIP events around them)",
+            "kernel": f"k_gauss_lean / k_gauss_diag / k_gauss_duo (separable Gaussian levels: "
+                      f"the {n_filters} level filters of a step in {n_gauss} launches, back to "
+                      "back on the library's stream, HIP events around them)",
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
@@ -247,28 +247,31 @@ def main():
 
     # SURVEY.md §8(d), "full detection (reported separately)": pyramid + extremum stages.  The
     # reference moves 168 B per octave pixel there (pyramid 48 + DoG 60 + gradient writes 24 +
-    # extremum reads 36); this build never stores the DoG or gradient images and moves 48 + 24 B
-    # (the extremum kernel reads the d + 3 = 6 Gaussian planes once).  The roofline fraction is
-    # the bytes this build moves (the rocprofv3 counters of the committed profile when they match
-    # the workload, else the algorithmic 72 B) over the stage time; the reference-equivalent rate
-    # (168 B over the same time) is beside it and is not a fraction of any peak.
+    # extremum reads 36); this build never stores the DoG or gradient images, and its algorithmic
+    # bytes are 48 + 24 B (the extremum kernel reads the d + 3 = 6 Gaussian planes once).  `frac`
+    # is those algorithmic bytes over the stage time (bytes a kernel re-reads do not count as
+    # achievement); the counter bytes of the committed profile of this same tree, when there is
+    # one, are reported beside it, and the reference-equivalent rate (168 B over the same time)
+    # is not a fraction of any peak.
     det_ms = stage_acc.get("pyramid", 0.0) + stage_acc.get("detect", 0.0)
     if det_ms > 0:
         det_s = det_ms * 1e-3 / args.steps
         alg = (48.0 + 4.0 * (3 + 3)) * sumN * B
         moved, src = detection_traffic(B, W, H, args.octaves)
-        b = moved if moved else alg
         result["full_detection"] = {
             "ms_per_step": det_ms / args.steps,
             "algorithmic_bytes_per_step": alg,
+            "achieved_GBps": alg / det_s / 1e9,
+            "frac": alg / det_s / 1e9 / HBM_PEAK_GBS,
             "measured_bytes_per_step": moved, "measured_source": src,
-            "achieved_GBps": b / det_s / 1e9,
-            "frac": b / det_s / 1e9 / HBM_PEAK_GBS,
+            "measured_GBps": moved / det_s / 1e9 if moved else None,
+            "measured_over_algorithmic": moved / alg if moved else None,
             "reference_equivalent_GBps": 168.0 * sumN * B / det_s / 1e9,
-            "note": "pyramid + extremum stages; bytes this build moves (counters when profiled, "
-                    "else 72 B x sum(N) per image) over their time; the reference-equivalent "
-                    "rate counts the reference's 168 B x sum(N) per image (SURVEY.md 8d), whose "
-                    "DoG and gradient images are never stored here"}
+            "note": "pyramid + extremum stages; frac = algorithmic 72 B x sum(N) per image over "
+                    "their time; measured = calibrated rocprofv3 counter bytes of the committed "
+                    "profile of this source tree (null when none); the reference-equivalent rate "
+                    "counts the reference's 168 B x sum(N) per image (SURVEY.md 8d), whose DoG and "
+                    "gradient images are never stored here"}
     if rank == 0 and world == 1 and not args.no_match:
         result["match"] = bench_match(ctx, args.match_n, cpu=not args.no_cpu_baseline)
     if rank == 0 and world == 1 and args.workload == "c3" and not args.no_c4:
@@ -291,49 +294,61 @@ def main():
     ctx.close()
 
 
-def profiled_traffic(B, W, H, octaves):
-    """HBM bytes per Gaussian launch from the committed rocprofv3 summary of this workload
-    (tests/profile_kernels.sh + tests/pmc_summary.py), or None when no summary matches.  The
-    summary's FETCH_SIZE / WRITE_SIZE are corrected per access width with the committed
-    calibration (tests/pmc_calib.sh; MI355X_MICROARCH.md: FETCH_SIZE counts 1/2 of a 16-B-per-lane
-    streaming read): "hbm_bytes_per_extract" when the summary carries it."""
+def matching_profile(B, W, H, octaves):
+    """The newest committed calibrated rocprofv3 summary (tests/profile_kernels.sh +
+    tests/pmc_summary.py) of this workload whose source digest (tests/prof_common.py) equals the
+    tree being benchmarked, as (summary, note); (None, reason) when there is none -- counters of
+    older kernels are never divided by the current kernels' time."""
     import glob
+    from prof_common import source_digest
     if (B, W, H, octaves) != (128, 1920, 1080, 4):
         return None, "no profile for this workload"
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")))
-    for path in reversed(files):
+    here = source_digest()
+    newest = None
+    for path in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")))):
         try:
             s = json.load(open(path))
-            if "hbm_bytes_per_extract" not in s:
-                continue
-            fams = [f for f in s["launches_per_extract"] if f.startswith("k_gauss")]
-            n = sum(s["launches_per_extract"][f] for f in fams)
-            b = sum(s["hbm_bytes_per_extract"][f] for f in fams)
-            return b / n, os.path.relpath(path, ROOT)
-        except (KeyError, ValueError, OSError):
+        except (ValueError, OSError):
             continue
-    return None, "no calibrated profile summary committed"
+        if not s.get("calibrated_all_kernels") or "hbm_bytes_per_extract" not in s:
+            continue
+        newest = newest or os.path.relpath(path, ROOT)
+        if s.get("source_digest") == here:
+            return s, (f"{os.path.relpath(path, ROOT)} (source digest {here}, profiled on box "
+                       f"{s.get('box', '?')})")
+    return None, (f"no calibrated profile of this source tree (digest {here}) committed; the "
+                  f"newest, {newest}, is of another tree" if newest else
+                  "no calibrated profile summary committed")
+
+
+def profiled_traffic(B, W, H, octaves):
+    """HBM bytes per Gaussian launch from the committed calibrated summary of this tree and
+    workload, or None.  The summary's FETCH_SIZE / WRITE_SIZE are corrected per access width with
+    the committed calibration (tests/pmc_calib.sh; MI355X_MICROARCH.md: FETCH_SIZE counts 1/2 of
+    a 16-B-per-lane streaming read)."""
+    s, note = matching_profile(B, W, H, octaves)
+    if s is None:
+        return None, note
+    try:
+        fams = [f for f in s["launches_per_extract"] if f.startswith("k_gauss")]
+        n = sum(s["launches_per_extract"][f] for f in fams)
+        b = sum(s["hbm_bytes_per_extract"][f] for f in fams)
+        return b / n, note
+    except (KeyError, ZeroDivisionError):
+        return None, "malformed summary: " + note
 
 
 def detection_traffic(B, W, H, octaves):
     """HBM bytes per extract of the Gaussian and extremum kernels from the committed calibrated
-    profile summary (see profiled_traffic), or None."""
-    import glob
-    if (B, W, H, octaves) != (128, 1920, 1080, 4):
-        return None, "no profile for this workload"
-    for path in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")))):
-        try:
-            s = json.load(open(path))
-            if not s.get("calibrated_all_kernels"):
-                continue
-            h = s["hbm_bytes_per_extract"]
-            fams = [f for f in h if f.startswith("k_gauss") or f.startswith("k_extrema")]
-            if not any(f.startswith("k_extrema") for f in fams):
-                continue
-            return sum(h[f] for f in fams), os.path.relpath(path, ROOT)
-        except (KeyError, ValueError, OSError):
-            continue
-    return None, "no calibrated profile summary with the extremum kernel committed"
+    summary of this tree (see matching_profile), or None."""
+    s, note = matching_profile(B, W, H, octaves)
+    if s is None:
+        return None, note
+    h = s["hbm_bytes_per_extract"]
+    fams = [f for f in h if f.startswith("k_gauss") or f.startswith("k_extrema")]
+    if not any(f.startswith("k_extrema") for f in fams):
+        return None, "no extremum kernel in " + note
+    return sum(h[f] for f in fams), note
 
 
 def bench_match(ctx, n, cpu=True):
@@ -415,13 +430,14 @@ def bench_c4(ctx, batch=16, steps=3, cpu=True):
                 st[k] = st.get(k, 0.0) + v
         el = time.perf_counter() - t0
         sumN = geometry_sum(4096, 4096, 6)
-        n_gauss = 3 * 5 + 6   # 31 level filters in 21 launches (diagonal schedule)
+        n_gauss, n_filt = c4.pyramid_launches()   # as the library ran them
         achieved = 48.0 * sumN * batch * steps / (pyr * 1e-3) / 1e9
         out = {"workload": f"C4: {batch} x 4096x4096 u8 tiles per step, -fo 0 -no 6 -d 3, "
                             f"staged in HBM", "value": batch * steps / el, "unit": "images/s",
                 "ms_per_step": el / steps * 1e3, "features_per_image": feats / (batch * steps),
                 "stage_ms_per_step": {k: v / steps for k, v in st.items() if k != "match"},
-                "roofline": {"kernel": f"k_gauss_lean / k_gauss_diag ({n_gauss} launches per step)",
+                "roofline": {"kernel": f"k_gauss_lean / k_gauss_diag / k_gauss_duo ({n_filt} level "
+                                       f"filters in {n_gauss} launches per step)",
                              "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                              "algorithmic_bytes_per_launch": 48.0 * sumN * batch / n_gauss,

@@ -92,6 +92,21 @@ int sgpu_device_count(void);
  * buffer, so that later extract calls with SGPU_INPUT_STAGED start from HBM-resident input. */
 int sgpu_stage_input(sgpu_ctx* ctx, const uint8_t* images, int n, int w, int h, int stride);
 
+/* Allocate now every device and pinned buffer that an extract of n gray u8 images of w x h
+ * pixels (rows `stride` bytes apart, staged or uploaded) needs, so that the next
+ * sgpu_stage_input + sgpu_extract of that geometry allocates nothing unless its keypoints exceed
+ * the first-guess capacity.  Replaces SiftGPU::AllocatePyramid (SiftGPU.h:193,
+ * SiftGPU.cpp:1435-1460 -> PyramidCU::ResizePyramid, PyramidCU.cpp:178-271).  Like an extract
+ * it replaces the batch: the previous results and the staged input are gone. */
+int sgpu_reserve(sgpu_ctx* ctx, int n, int w, int h, int stride);
+/* The last extract's Gaussian pyramid (part 0): returns the number of kernel launches that
+ * filtered its levels and stores the number of level filters in *filters (the reference's
+ * FilterImage calls, PyramidCU.cpp:979-1044; several run in one launch under the diagonal and
+ * paired-level schedules).  bench.py divides the pyramid's bytes and time by it. */
+int sgpu_last_pyramid_launches(const sgpu_ctx* ctx, int* filters);
+/* Test hook: number of device and pinned-host allocations the library has made so far. */
+long long sgpu_debug_alloc_count(void);
+
 /* Extract SIFT features from n gray u8 images of w x h pixels, row stride `stride` bytes,
  * image i at images + i*stride*h.  Replaces SiftGPU::RunSIFT(w, h, data, GL_LUMINANCE,
  * GL_UNSIGNED_BYTE) (SiftGPU.h:176, SiftGPU.cpp:233-268 -> SiftPyramid::RunSIFT,
@@ -269,6 +284,15 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
                                       shipped path runs octave o+1's first levels in the same
                                       launches as octave o's last ones; the stream layout runs
                                       octaves >= 1 on a second stream): same levels */
+#define SGPU_DEBUG_GAUSS_LONG_BANDS 8192 /* Gaussian bands of >= 4 chunks on every level (round
+                                            2's band rule; the shipped rule lets cache-resident
+                                            levels use 1-chunk bands): same levels.  Also set at
+                                            context creation by SGPU_GAUSS_BANDS=long */
+#define SGPU_DEBUG_DUO_ALWAYS 16384 /* paired-level Gaussian launches (k_gauss_duo) for every
+                                        eligible level pair, whatever its size (the shipped path
+                                        pairs only levels of >= 128 MB): same levels */
+#define SGPU_DEBUG_DUO_OFF 32768 /* no paired-level launches (one level per launch, the round-4
+                                    schedule): same levels */
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);

@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -27,6 +28,21 @@
 
 namespace {
 
+// paired-level Gaussian launches in the shipped schedule (1), or only when asked for by
+// SGPU_DUO=on / the debug flags (0)
+#ifndef SGK_DUO_DEFAULT
+#define SGK_DUO_DEFAULT 0
+#endif
+// paired-level Gaussian launches only for levels of at least this many MB (smaller ones stay in
+// the Infinity Cache between launches and are latency-bound: one level per launch, 1-chunk bands)
+#ifndef SGK_DUO_MIN_MB
+#define SGK_DUO_MIN_MB 128
+#endif
+
+// device and pinned-host allocations made by the library (sgpu_debug_alloc_count): a test hook
+// for sgpu_reserve, whose point is that the extract after it allocates nothing
+std::atomic<long long> g_allocs{0};
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -36,6 +52,7 @@ struct DevBuf {
         p = nullptr;
         bytes = 0;
         n = std::max<size_t>(n, 256);
+        g_allocs++;
         hipError_t e = hipMalloc(&p, n);
         if (e == hipSuccess) bytes = n;
         return e;
@@ -65,6 +82,7 @@ struct Part {
     hipEvent_t ev_ds = nullptr;        // octave 0's decimating level done
     hipEvent_t ev_oct = nullptr;       // octaves >= 1 done
     size_t cand_hint = 0, feat_hint = 0;   // counts of the previous call (launch-grid sizing)
+    int gauss_launches = 0, gauss_filters = 0;   // the last pyramid: launches, level filters
     hipEvent_t ev[10] = {};  // start, pyramid, detect, orientation, expand, descriptor, end,
                              // extrema done (before the row scan), (spare), (spare)
     int img0 = 0, n = 0;
@@ -115,6 +133,7 @@ struct sgpu_ctx {
     sgp::InputPlan plan{};                 // first octave of the last extract (plan_input)
     int debug_flags = 0;                   // SGPU_DEBUG_* test hooks
     bool multi_stream = false;             // SGPU_STREAMS=multi: octave and feature streams
+    bool duo_on = false;                   // SGPU_DUO=on: paired-level launches (size rule)
     std::string err;
     // last extract
     int batch = 0, w = 0, h = 0, nparts = 0;
@@ -126,6 +145,7 @@ struct sgpu_ctx {
                                                   // pre: the 2^ds-sampled input (-fo > 0)
     // sgpu_extract_stream: second input slot, copy-engine streams, slot events
     DevBuf input2;
+    DevBuf duo_trash;                      // k_gauss_duo's scratch stores (kGaussDuoTrashBytes)
     hipStream_t h2d = nullptr, d2h = nullptr;
     hipEvent_t up_ev[2] = {}, down_ev[2] = {};
     bool gathered = false;
@@ -366,6 +386,13 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     if (const char* ev = getenv("SGPU_GAUSS")) {
         if (!strcmp(ev, "block")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_BLOCK;
     }
+    if (const char* ev = getenv("SGPU_DUO")) {   // A/B hook of the paired-level kernel
+        if (!strcmp(ev, "off")) ctx->debug_flags |= SGPU_DEBUG_DUO_OFF;
+        if (!strcmp(ev, "always")) ctx->debug_flags |= SGPU_DEBUG_DUO_ALWAYS;
+        if (!strcmp(ev, "on")) ctx->duo_on = true;
+    }
+    if (const char* ev = getenv("SGPU_GAUSS_BANDS"))
+        if (!strcmp(ev, "long")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_LONG_BANDS;
     if (const char* ev = getenv("SGPU_PYR")) {
         if (!strcmp(ev, "serial")) ctx->debug_flags |= SGPU_DEBUG_PYR_SERIAL;
     }
@@ -401,7 +428,7 @@ int sgpu_ctx_destroy(sgpu_ctx* ctx) {
     }
     if (ctx->h2d) (void)hipStreamDestroy(ctx->h2d);
     if (ctx->d2h) (void)hipStreamDestroy(ctx->d2h);
-    DevBuf* bufs[] = {&ctx->input, &ctx->input2, &ctx->all_keys, &ctx->all_desc, &ctx->gray, &ctx->pre, &ctx->m_d1, &ctx->m_d2, &ctx->m_s1, &ctx->m_s2,
+    DevBuf* bufs[] = {&ctx->input, &ctx->input2, &ctx->duo_trash, &ctx->all_keys, &ctx->all_desc, &ctx->gray, &ctx->pre, &ctx->m_d1, &ctx->m_d2, &ctx->m_s1, &ctx->m_s2,
                       &ctx->m_part, &ctx->m_terms, &ctx->m_match, &ctx->m_dist, &ctx->m_mask, &ctx->m_loc,
                       &ctx->m_colpart, &ctx->m_cols,
                       &ctx->c_buf};
@@ -415,16 +442,15 @@ int sgpu_ctx_destroy(sgpu_ctx* ctx) {
 
 const char* sgpu_last_error(const sgpu_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
-// Queue the whole pipeline of one part on its stream.  `wait` (may be null) is an event the
-// part's pyramid must wait for.  No host synchronisation.
-static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32, int stride,
-                        hipEvent_t wait, hipEvent_t wait_lo = nullptr) {
-    hipStream_t st = pt.stream;   // reassigned per stage below
+// Layout of one part of the planned batch (plan_batch): feature parameters, buffer offsets,
+// capacities, and every device and pinned buffer the part's pipeline needs, allocated (grow-only).
+// enqueue_part runs it first; sgpu_reserve (SiftGPU::AllocatePyramid) runs it alone.
+static int layout_part(sgpu_ctx* ctx, Part& pt) {
     const sgpu_options& O = ctx->opt;
     const sgp::Schedule& S = ctx->sched;
     const int d = S.dog_level_num, nlev = S.level_num;
     const int noct = (int)ctx->oct.size();
-    const int n = pt.n, h = ctx->h;
+    const int n = pt.n;
 
     // ---- layout: pyramid [octave][level][image][h][wa]; mask [octave][dog level][image][h][words]
     sgk::FeatureParams& fp = pt.fp;
@@ -497,9 +523,28 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     if (pt.h_read_n < (size_t)n + 2) {
         if (pt.h_read) (void)hipHostFree(pt.h_read);
         pt.h_read = nullptr;
+        g_allocs++;
         ALLOCCHK(ctx, hipHostMalloc((void**)&pt.h_read, ((size_t)n + 2) * sizeof(int64_t)));
         pt.h_read_n = (size_t)n + 2;
     }
+    return SGPU_OK;
+}
+
+// Queue the whole pipeline of one part on its stream.  `wait` (may be null) is an event the
+// part's pyramid must wait for.  No host synchronisation.
+static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32, int stride,
+                        hipEvent_t wait, hipEvent_t wait_lo = nullptr) {
+    hipStream_t st = pt.stream;   // reassigned per stage below
+    const sgpu_options& O = ctx->opt;
+    const sgp::Schedule& S = ctx->sched;
+    const int nlev = S.level_num;
+    const int noct = (int)ctx->oct.size();
+    const int n = pt.n, h = ctx->h;
+    const int rc_layout = layout_part(ctx, pt);
+    if (rc_layout != SGPU_OK) return rc_layout;
+    const sgk::FeatureParams& fp = pt.fp;
+    const long long moff = pt.mask_words;
+    const size_t nc = pt.cand_cap, ne_cap = 2 * nc;
 
     if (wait) HIPCHK(ctx, hipStreamWaitEvent(st, wait, 0));
     HIPCHK(ctx, hipEventRecord(pt.ev[0], st));
@@ -524,11 +569,13 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     // the extremum kernel.  SGPU_DEBUG_PYR_SERIAL: one stream for the pyramid only.
     const bool side = noct > 1 && !pt.one_stream && !(ctx->debug_flags & SGPU_DEBUG_PYR_SERIAL);
     const int wave_rows = (ctx->debug_flags & SGPU_DEBUG_GAUSS_BLOCK) ? -1 : (ctx->debug_flags >> 16);
+    const bool long_bands = (ctx->debug_flags & SGPU_DEBUG_GAUSS_LONG_BANDS) != 0;
     // the level filters of every octave: op (o, k) filters level k-1 into level k (op (0, 0)
     // smooths the input into level 0); level kds of octave o also writes its decimation, level 0
     // of octave o+1
     struct Op { sgk::LevelOp op; int o, k; };
     std::vector<Op> ops;
+    pt.gauss_launches = 0;   // kernel launches of the level filters (sgpu_last_pyramid_launches)
     ops.reserve((size_t)noct * nlev);
     for (int o = 0; o < noct; o++) {
         const sgk::OctaveDesc& od = fp.oct[o];
@@ -585,13 +632,15 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
             ops.push_back(e);
         }
     }
+    pt.gauss_filters = (int)ops.size();
     if (side || (ctx->debug_flags & SGPU_DEBUG_PYR_SERIAL) || kds < 1) {
         // octave by octave, one level per launch (octaves >= 1 on the side stream in the
         // stream layout)
         for (const Op& e : ops) {
             const hipStream_t so = side && e.o >= 1 ? pt.stream_oct : st;
+            pt.gauss_launches++;
             if (side && e.o == 1 && e.k == 1) HIPCHK(ctx, hipStreamWaitEvent(so, pt.ev_ds, 0));
-            HIPCHK(ctx, sgk::launch_gauss_op(e.op, so, wave_rows));
+            HIPCHK(ctx, sgk::launch_gauss_op(e.op, so, wave_rows, long_bands));
             if (side && e.o == 0 && e.k == kds && e.op.ds_dst) HIPCHK(ctx, hipEventRecord(pt.ev_ds, st));
         }
     } else {
@@ -600,17 +649,57 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
         // -- so the ops of a slot are independent and share a launch: octave o+1's levels 1, 2
         // run beside octave o's levels kds+1, kds+2 (15 launches instead of 21 for -no 4 -d 3),
         // the small jobs' latency-bound waves filling the large ones' CU slots.
+        // Paired levels: ops (o, k) and (o, k+1) of a streaming-size level
+        // (>= SGK_DUO_MIN_MB: not left in the Infinity Cache by the previous launch) with a
+        // compiled width pair run as one k_gauss_duo launch in slot o * kds + k + 1 -- level k
+        // read once, levels k+1 and k+2 written (12 instead of 16 B per pixel).
+        const bool duo_all = (ctx->debug_flags & SGPU_DEBUG_DUO_ALWAYS) != 0;
+        const bool duo_off = (ctx->debug_flags & SGPU_DEBUG_DUO_OFF) != 0 ||
+                             (!SGK_DUO_DEFAULT && !duo_all && !ctx->duo_on);
+        std::vector<int> duo_next(ops.size(), -1);   // op i pairs with op duo_next[i]
+        std::vector<char> duo_second(ops.size(), 0);
+        if (!duo_off && wave_rows >= 0) {
+            for (size_t i = 0; i + 1 < ops.size(); i++) {
+                const Op& a = ops[i];
+                const Op& b = ops[i + 1];
+                if (duo_second[i] || a.o != b.o || b.k != a.k + 1) continue;
+                const long long bytes = 4ll * a.op.w * a.op.h * a.op.batch;
+                if (!duo_all && bytes < ((long long)SGK_DUO_MIN_MB << 20)) continue;
+                if (!sgk::gauss_duo_supported(a.op, b.op)) continue;
+                duo_next[i] = (int)(i + 1);
+                duo_second[i + 1] = 1;
+            }
+        }
+        bool any_duo = false;
+        for (int v : duo_next) any_duo |= v >= 0;
+        if (any_duo)
+            ALLOCCHK(ctx, ctx->duo_trash.ensure(sgk::kGaussDuoTrashBytes));
         int last = 0;
         for (const Op& e : ops) last = std::max(last, e.o * kds + e.k);
         for (int slot = 0; slot <= last; slot++) {
             const sgk::LevelOp* in_slot[sgk::kMaxOctaves];
             int m = 0;
-            for (const Op& e : ops)
-                if (e.o * kds + e.k == slot) in_slot[m++] = &e.op;
+            for (size_t i = 0; i < ops.size(); i++) {
+                const Op& e = ops[i];
+                if (duo_second[i] && e.o * kds + e.k == slot) {   // the pair ends in this slot
+                    HIPCHK(ctx, sgk::launch_gauss_duo(ops[i - 1].op, e.op, st, wave_rows,
+                                                      ctx->duo_trash.as<float>()));
+                    pt.gauss_launches++;
+                } else if (duo_next[i] < 0 && !duo_second[i] && e.o * kds + e.k == slot) {
+                    in_slot[m++] = &e.op;
+                }
+            }
             int i = 0;
-            for (; i + 1 < m; i += 2)
-                HIPCHK(ctx, sgk::launch_gauss_two(*in_slot[i], *in_slot[i + 1], st, wave_rows));
-            if (i < m) HIPCHK(ctx, sgk::launch_gauss_op(*in_slot[i], st, wave_rows));
+            for (; i + 1 < m; i += 2) {
+                int nl = 0;
+                HIPCHK(ctx, sgk::launch_gauss_two(*in_slot[i], *in_slot[i + 1], st, wave_rows,
+                                                  long_bands, &nl));
+                pt.gauss_launches += nl;
+            }
+            if (i < m) {
+                HIPCHK(ctx, sgk::launch_gauss_op(*in_slot[i], st, wave_rows, long_bands));
+                pt.gauss_launches++;
+            }
         }
     }
     if (side) {
@@ -1592,6 +1681,42 @@ int sgpu_stage_input(sgpu_ctx* ctx, const uint8_t* images, int n, int w, int h, 
     return SGPU_OK;
 }
 
+// SiftGPU::AllocatePyramid (SiftGPU.cpp:1435-1460: PyramidCU::ResizePyramid for the first
+// octave of a width x height input): every device and pinned buffer an extract of n images of
+// w x h u8 pixels (rows `stride` bytes apart) needs -- the staged input, the pyramid, the mask,
+// the row and candidate arrays at their first-guess capacity -- allocated now, so that the next
+// sgpu_stage_input + sgpu_extract of that geometry allocates nothing (unless its keypoints
+// exceed the first-guess capacity).  Like an extract it replaces the batch: the previous
+// results are gone.
+int sgpu_reserve(sgpu_ctx* ctx, int n, int w, int h, int stride) {
+    if (!ctx) return SGPU_EINVAL;
+    if (n <= 0 || w < 8 || h < 8 || stride < w) return ctx->fail(SGPU_EINVAL, "bad reserve arguments");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int rc = abandon_batch(ctx, SGPU_OK);   // nothing queued may still use the buffers
+    ctx->staged_bytes = 0;                  // the input buffer may be reallocated
+    if (rc == SGPU_OK) rc = plan_batch(ctx, n, w, h);
+    if (rc == SGPU_OK && part_streams(ctx->part[0]) != SGPU_OK)
+        rc = ctx->fail(SGPU_ENODEV, "stream creation failed");
+    if (rc == SGPU_OK) {
+        ctx->nparts = 1;
+        Part& pt = ctx->part[0];
+        pt.img0 = 0;
+        pt.n = n;
+        rc = layout_part(ctx, pt);
+    }
+    if (rc == SGPU_OK && ctx->input.ensure((size_t)n * h * stride) != hipSuccess)
+        rc = ctx->fail(SGPU_ENOMEM, "device allocation failed");
+    return abandon_batch(ctx, rc);
+}
+
+long long sgpu_debug_alloc_count(void) { return g_allocs.load(); }
+
+int sgpu_last_pyramid_launches(const sgpu_ctx* ctx, int* filters) {
+    if (!ctx || ctx->batch <= 0) return SGPU_EINVAL;
+    if (filters) *filters = ctx->part[0].gauss_filters;
+    return ctx->part[0].gauss_launches;
+}
+
 int sgpu_extract(sgpu_ctx* ctx, const uint8_t* images, int n, int w, int h, int stride,
                  int flags) {
     return extract_impl(ctx, images, false, n, w, h, stride, flags);
@@ -1625,7 +1750,11 @@ int sgpu_copy_features(sgpu_ctx* ctx, int image, float* keys, float* descriptors
     const Part& pt = ctx->part[ctx->part_of(image)];
     const int li = image - pt.img0;
     const int64_t a = pt.img_off[li], nf = pt.img_off[li + 1] - a;
-    if (nf <= 0) return SGPU_OK;
+    if (nf <= 0) {   // nothing copied: the copy slots read 0, not the previous call's times
+        ctx->timing[T_COPY_KEYS] = 0.f;
+        ctx->timing[T_COPY_DESC] = 0.f;
+        return SGPU_OK;
+    }
     if (descriptors && !ctx->opt.descriptors) return ctx->fail(SGPU_EINVAL, "descriptors disabled (-sd)");
     // both copies, then one synchronisation; events split the time between them
     // (sgpu_last_timing slots 10, 11)

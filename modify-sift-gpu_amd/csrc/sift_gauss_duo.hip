@@ -1,0 +1,518 @@
+// sift_gauss_duo.hip -- two consecutive Gaussian levels per launch ("duo"), gfx950.
+//
+// Levels k+1 = V(H(level k)) and k+2 = V(H(level k+1)) (FilterH<FW> then FilterV<FW>,
+// ProgramCU.cu:115-222, driven per level by PyramidCU::BuildPyramid, PyramidCU.cpp:979-1044) in one
+// pass over level k: 12 B of HBM traffic per pixel for the two levels (read level k, write k+1 and
+// k+2) instead of the 16 B of two single-level launches.  Round 3's two-level kernel kept both
+// H results in LDS rings and lost to its LDS footprint (4 waves per CU); here both
+// vertical passes are register-resident ("push" form), so a wave's LDS is its input rows and
+// one mid row pair:
+//
+//   * a wave owns SW = 128 - 2 RB output columns of both levels (RB = FWB / 2) and walks a band
+//     of rows top to bottom, two rows (one row pair) per step;
+//   * stage A: the input row pair (128 + 2 RA columns, clamped to the image) arrives in LDS by
+//     LDS-DMA (global_load_lds_dword, one float per lane, laid out as (row 2p, row 2p+1) pairs),
+//     NIN - 1 steps ahead of its use -- no staging registers;  H1 (lane l: mid columns
+//     m0 + 2l, m0 + 2l + 1, packed over the row pair) reads it with ds_read_b128;
+//   * the V1 pass is pushed: each H1 row is multiplied into the FWA accumulators of the mid rows
+//     it contributes to, so mid row m receives input rows m - RA .. m + RA in that order -- the
+//     reference's tap order i = 0 .. FW-1, one fma each, bit for bit the pull form's sum.  The
+//     accumulators are an array indexed by (row - base) mod P, P = the ring period, with the
+//     step loop unrolled by P / 2 so every index is a compile-time constant (registers, no
+//     rotation copies at the loop back edge);
+//   * a completed mid row pair is written to HBM (level k+1, the wave's own SW columns) and, all
+//     128 columns, to the wave's mid slot in LDS; stage B's H2 reads it there (lane l: output
+//     columns x0 + 2l, x0 + 2l + 1) and pushes into the V2 accumulators; completed rows of level
+//     k+2 go to HBM;
+//   * clamp-to-edge: stage A's rows and columns are clamped in the DMA addresses; stage B's rows
+//     above 0 / below H-1 read two extra LDS pairs, (mid 0, mid 0) -- computed by a short
+//     prologue in the top band -- and (mid H-1, mid H-1); stage B's columns outside the image
+//     take the edge mid column's value by v_readlane in the two edge strips.
+//
+// Every VMEM instruction of a step is issued unconditionally (rows outside the band store to a
+// per-wave scratch area), so the count of memory operations younger than a step's DMA is a
+// constant and one `s_waitcnt vmcnt(OPS (NIN - 1))` waits for exactly that DMA.  Levels are
+// bit-identical to two k_gauss_lean launches (tests/test_gpu_gauss.py).
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <utility>
+
+#include "sift_kernels.h"
+
+// the DMA asm names M0 as clobbered: clang warns that M0 is reserved; nothing else in this file
+// uses M0 (no builtin LDS-DMA, no indirect register indexing), see duo_wave's dma()
+#pragma clang diagnostic ignored "-Winline-asm"
+
+namespace sgk {
+namespace {
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void* lds_ptr;
+
+__device__ __forceinline__ f2v pkf(f2v a, float k, f2v c) {
+    return __builtin_elementwise_fma(a, f2v{k, k}, c);
+}
+__device__ __forceinline__ int clampd(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// tap i of a width-FW filter (make_filter's taps are symmetric bit for bit: half the SGPRs)
+template <int FW>
+__device__ __forceinline__ float tapk(const Taps& t, int i) {
+    return t.k[i < FW - 1 - i ? i : FW - 1 - i];
+}
+
+template <int... I, class F>
+__device__ __forceinline__ void unroll_seq(std::integer_sequence<int, I...>, F&& f) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+
+// a wave-uniform pointer as one (the asm's "s" operand needs an SGPR pair)
+__device__ __forceinline__ const char* uniform_ptr(const void* p) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return reinterpret_cast<const char*>(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// workgroup order: blocks dealt round-robin over the 8 XCDs (observed, speed only), so logical
+// block xcd * q + k runs on XCD xcd and neighbouring strips share one L2 (as k_gauss_lean)
+__device__ __forceinline__ int duo_block(int bid, int nb) {
+    const int q = nb / 8, r = nb % 8, xcd = bid % 8, k = bid / 8;
+    return xcd < r ? xcd * (q + 1) + k : r * (q + 1) + (xcd - r) * q + k;
+}
+
+// the two H passes of a step in one scheduling region (their fma chains interleave) or kept
+// apart by a compiler barrier (SGK_DUO_INTERLEAVE=0)
+#ifndef SGK_DUO_INTERLEAVE
+#define SGK_DUO_INTERLEAVE 1
+#endif
+constexpr bool kDuoInterleave = SGK_DUO_INTERLEAVE != 0;
+constexpr int kDuoWaves = 4;      // waves per workgroup (each wave works alone: no barriers)
+constexpr int kMidSlot = 256;     // floats of one mid row pair: 128 columns x (row, row + 1)
+
+template <int FWA, int FWB>
+struct DuoGeom {
+    static constexpr int RA = FWA / 2, RB = FWB / 2;
+    static_assert(RB % 2 == 0, "stage B's H2 reads start on a 16-B boundary (RB even)");
+    static constexpr int SW = 128 - 2 * RB;           // output columns of a wave
+    static constexpr int IN_W = 128 + 2 * RA;         // input columns of stage A
+    static constexpr int NDMA = (IN_W + 31) / 32;     // dword DMAs per row pair (32 columns each)
+    static constexpr int IN_SLOT = NDMA * 64;         // floats of one input row pair
+    static constexpr int PMAX = FWA > FWB ? FWA : FWB;
+    static constexpr int P = (PMAX + 1) & ~1;         // accumulator ring period (rows), even
+    static constexpr int U = P / 2;                   // steps per unrolled iteration
+};
+
+struct DuoJob {
+    const float* src;            // level k
+    int src_stride;
+    long long src_img;
+    float* dst1;                 // level k + 1
+    float* dst2;                 // level k + 2 (both rows W apart, images dst_img apart)
+    long long dst_img;
+    int W, H;
+    Taps ta, tb;                 // the two filters (widths FWA, FWB)
+    int strips, nsy, rows_per_band, total_waves;
+    float* trash;                // 2,560 B per wave slot (1024 slots): stores of rows outside
+                                 // the band and the DMA prologue's count-keeping stores
+};
+
+// s_waitcnt with vmcnt = n (0 .. 63), expcnt and lgkmcnt not waited for
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt field");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+__device__ __forceinline__ void wait_lgkm0() {
+    __builtin_amdgcn_s_waitcnt((15) | (3 << 14) | (7 << 4) | (0 << 8));   // lgkmcnt(0) only
+}
+
+template <int FWA, int FWB, int NIN>
+__device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, float* s_mid) {
+    using G = DuoGeom<FWA, FWB>;
+    constexpr int RA = G::RA, RB = G::RB, SW = G::SW, NDMA = G::NDMA, IN_SLOT = G::IN_SLOT;
+    constexpr int P = G::P, U = G::U;
+    constexpr int OPS = NDMA + 4;   // VMEM instructions per step: the DMAs, 2 + 2 stores
+    static_assert(NIN >= 2 && OPS * (NIN - 1) < 64, "DMA ring (vmcnt field)");
+    const int lane = threadIdx.x & 63;
+    const int W = J.W, H = J.H;
+    const int sx = gw % J.strips, rest = gw / J.strips;
+    const int sy = rest % J.nsy, b = rest / J.nsy;
+    const int x0 = sx * SW;
+    const int yb = sy * J.rows_per_band, ye = min(H, yb + J.rows_per_band);
+    const int m0 = x0 - RB;        // mid column of lane 0's first column
+    const int a0 = m0 - RA;        // input column of the input slot's float2 0
+    const float* src = J.src + (long long)b * J.src_img;
+    float* d1 = J.dst1 + (long long)b * J.dst_img;
+    float* d2 = J.dst2 + (long long)b * J.dst_img;
+    float* trash = J.trash + (size_t)(gw & 1023) * 640;   // 5 x 512 B per wave slot
+
+    // ---- DMA lane map: instruction q, lane i -> input column a0 + 32 q + i / 2 (clamped),
+    // row i & 1 of the pair; LDS float 64 q + i of the slot = float2 index 32 q + i / 2
+    uint32_t coff[NDMA];
+#pragma unroll
+    for (int q = 0; q < NDMA; q++) coff[q] = 4u * (uint32_t)clampd(a0 + 32 * q + (lane >> 1), 0, W - 1);
+    const uint32_t rsel = (lane & 1) ? 4u * (uint32_t)J.src_stride : 0u;
+    // The DMAs are inline asm, not __builtin_amdgcn_global_load_lds: the compiler's wait
+    // insertion treats every later LDS read as possibly aliasing a pending LDS-DMA and puts an
+    // s_waitcnt vmcnt(0) before it (seen in the ISA), which would drain the whole DMA ring every
+    // step.  Hidden from the compiler, the DMAs are waited for by the explicit counted waits below
+    // only; every LDS access of the wave stays inside its own slots.  M0 holds the LDS address
+    // (nothing else in this kernel uses M0).
+    static_assert(NDMA == 5, "the asm below issues 5 DMAs per row pair");
+    auto dma = [&](int rho, float* slot) __attribute__((always_inline)) {
+        const int r0 = clampd(rho, 0, H - 1), r1 = clampd(rho + 1, 0, H - 1);
+        const char* base = uniform_ptr(src + (long long)r0 * J.src_stride);
+        const uint32_t ro = r1 != r0 ? rsel : 0u;
+        const uint32_t lds = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)slot);
+        asm volatile(
+            "s_mov_b32 m0, %[l]\n\ts_nop 0\n\t"
+            "global_load_lds_dword %[o0], %[b]\n\t"
+            "s_add_u32 m0, m0, 0x100\n\ts_nop 0\n\t"
+            "global_load_lds_dword %[o1], %[b]\n\t"
+            "s_add_u32 m0, m0, 0x100\n\ts_nop 0\n\t"
+            "global_load_lds_dword %[o2], %[b]\n\t"
+            "s_add_u32 m0, m0, 0x100\n\ts_nop 0\n\t"
+            "global_load_lds_dword %[o3], %[b]\n\t"
+            "s_add_u32 m0, m0, 0x100\n\ts_nop 0\n\t"
+            "global_load_lds_dword %[o4], %[b]"
+            :
+            : [l] "s"(lds), [b] "s"(base), [o0] "v"(coff[0] + ro), [o1] "v"(coff[1] + ro),
+              [o2] "v"(coff[2] + ro), [o3] "v"(coff[3] + ro), [o4] "v"(coff[4] + ro)
+            : "memory", "m0", "scc");
+    };
+
+    // ---- lane roles
+    const int c = m0 + 2 * lane;                       // mid columns c, c + 1 (stage A)
+    const bool own1 = c >= x0 && c < x0 + SW && c < W; // stage A stores these columns
+    const int le = lane < SW / 2 ? lane : SW / 2 - 1;  // stage B lane (idle lanes repeat the last)
+    const int e = x0 + 2 * le;                         // output columns e, e + 1 (stage B)
+    const bool own2 = lane < SW / 2 && e < W;
+    const bool left = m0 < 0, right = m0 + 128 > W;    // uniform: edge strips
+    const int l_left = left ? (-m0) >> 1 : 0;          // lane holding mid column 0 (as .x)
+    const int l_right = right ? (W - 2 - m0) >> 1 : 0; // lane holding mid column W-1 (as .y)
+    // mid row pair of one lane (columns c, c+1) clamped to the image's edge columns
+    // (in the edge strips only: the lanes' columns outside the image; l_left / l_right are 0
+    // when there is no such edge, and no lane then has c < 0 / c >= W)
+    auto fix_edges = [&](f2v& v) __attribute__((always_inline)) {
+        const float el = readlane_f(v.x, l_left), er = readlane_f(v.y, l_right);
+        v = c < 0 ? f2v{el, el} : (c >= W ? f2v{er, er} : v);
+    };
+    // the taps' distinct half (symmetric bit for bit) as wave-uniform scalars: read once from the
+    // kernel arguments (a reference into the argument struct made the compiler copy it to
+    // scratch and keep the taps in VGPRs)
+    float ka[RA + 1], kb[RB + 1];
+#pragma unroll
+    for (int i = 0; i <= RA; i++)
+        ka[i] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(J.ta.k[i])));
+#pragma unroll
+    for (int i = 0; i <= RB; i++)
+        kb[i] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(J.tb.k[i])));
+    auto tapa = [&](int i) __attribute__((always_inline)) { return ka[i <= RA ? i : FWA - 1 - i]; };
+    auto tapb = [&](int i) __attribute__((always_inline)) { return kb[i <= RB ? i : FWB - 1 - i]; };
+    // H1 of the input slot: columns c, c + 1 packed over the row pair
+    auto h1 = [&](const float* slot, f2v& o0, f2v& o1) __attribute__((always_inline)) {
+        o0 = f2v{0.f, 0.f};
+        o1 = f2v{0.f, 0.f};
+        const float4* p = reinterpret_cast<const float4*>(slot) + lane;
+#pragma unroll
+        for (int q = 0; q <= RA; q++) {
+            const float4 v = p[q];
+            const f2v ev[2] = {f2v{v.x, v.y}, f2v{v.z, v.w}};
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int m = 2 * q + u;   // input float2 2l + m: tap m of column c, m-1 of c+1
+                if (m < FWA) o0 = pkf(ev[u], tapa(m), o0);
+                if (m >= 1 && m <= FWA) o1 = pkf(ev[u], tapa(m - 1), o1);
+            }
+        }
+    };
+    auto h2 = [&](const float* slot, f2v& o0, f2v& o1) __attribute__((always_inline)) {
+        o0 = f2v{0.f, 0.f};
+        o1 = f2v{0.f, 0.f};
+        const float4* p = reinterpret_cast<const float4*>(slot) + le;
+#pragma unroll
+        for (int q = 0; q <= RB; q++) {
+            const float4 v = p[q];
+            const f2v ev[2] = {f2v{v.x, v.y}, f2v{v.z, v.w}};
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int m = 2 * q + u;
+                if (m < FWB) o0 = pkf(ev[u], tapb(m), o0);
+                if (m >= 1 && m <= FWB) o1 = pkf(ev[u], tapb(m - 1), o1);
+            }
+        }
+    };
+    // mid slots: 0, 1 alternate (stage A writes step t's pair into slot t & 1, stage B reads the
+    // previous step's from the other), 2 = (mid 0, mid 0), 3 = (mid H-1, mid H-1)
+    float* const mid_top = s_mid + 2 * kMidSlot;
+    float* const mid_bot = s_mid + 3 * kMidSlot;
+    auto put_mid = [&](float* slot, f2v r0, f2v r1) __attribute__((always_inline)) {
+        reinterpret_cast<float4*>(slot)[lane] = make_float4(r0.x, r1.x, r0.y, r1.y);
+    };
+
+    // ---- top band: mid row 0 (the rows above 0 clamp to it) before the walk, as the pull sum
+    // of rows 0 .. RA in tap order (taps 0 .. RA on row 0).  A rolled loop (one copy of the H1
+    // code; unrolled, it pushed the main loop's register allocation into spills), the tap of a
+    // row picked by uniform selects.
+    if (yb - RB < 0) {
+        auto tap_at = [&](int idx) __attribute__((always_inline)) {
+            float t = 0.f;
+#pragma unroll
+            for (int j = RA + 1; j < FWA; j++) t = idx == j ? tapa(j) : t;
+            return t;
+        };
+        f2v mz{0.f, 0.f};
+#pragma unroll 1
+        for (int p = 0; 2 * p <= RA; p++) {
+            dma(2 * p, s_in);
+            wait_vm<0>();
+            asm volatile("" ::: "memory");
+            f2v o0, o1;
+            h1(s_in, o0, o1);
+            const f2v r0{o0.x, o1.x}, r1{o0.y, o1.y};   // rows 2p, 2p + 1: columns (c, c + 1)
+            if (p == 0) {
+#pragma unroll
+                for (int i = 0; i <= RA; i++) mz = pkf(r0, tapa(i), i == 0 ? f2v{0.f, 0.f} : mz);
+            } else {
+                mz = pkf(r0, tap_at(RA + 2 * p), mz);
+            }
+            if (2 * p + 1 <= RA) mz = pkf(r1, tap_at(RA + 2 * p + 1), mz);
+            wait_lgkm0();
+            asm volatile("" ::: "memory");
+        }
+        if (left || right) fix_edges(mz);
+        put_mid(mid_top, mz, mz);
+    }
+
+    // ---- the walk.  Step t: stage A pushes input rows rho0 + 2t, + 1 and completes the mid pair
+    // mc = rho0 + 2t - RA, + 1; stage B pushes the pair stage A completed in step t - 1 (mc - 2),
+    // so the two H passes of a step are independent and their fma chains interleave.
+    const int rho0 = yb - RB - RA;
+    const int ntau = (ye - yb) + 2 * RA + 2 * RB + 2;
+    const int nsteps = (ntau + 1) / 2;
+    const int niter = (nsteps + U - 1) / U;
+    f2v accA[P], accB[P];
+#pragma unroll
+    for (int i = 0; i < P; i++) {
+        accA[i] = f2v{0.f, 0.f};
+        accB[i] = f2v{0.f, 0.f};
+    }
+    // the first NIN - 1 steps' DMAs, each followed by 4 scratch stores in place of the stores of
+    // the step that issues it, so that the wait below counts the same instructions from step 0
+    // (distinct 512-B blocks: the compiler neither drops nor merges them)
+#pragma unroll
+    for (int k = 0; k < NIN - 1; k++) {
+        dma(rho0 + 2 * k, s_in + k * IN_SLOT);
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            *reinterpret_cast<f2v*>(trash + 128 * (j + 1) + 2 * lane) = f2v{0.f, 0.f};
+    }
+    asm volatile("" ::: "memory");
+    // stores: uniform row pointers (the level's image base + row * W, updated per step) plus a
+    // lane byte offset; rows outside the band go to the wave's scratch block at lane * 8
+    const uint32_t voffA = 4u * (uint32_t)c, voffB = 4u * (uint32_t)e, vtr = 8u * (uint32_t)lane;
+    const long long W4 = 4ll * W;
+    char* pA = reinterpret_cast<char*>(d1) + (long long)(rho0 - RA) * W4;        // row mc of step 0
+    char* pB = reinterpret_cast<char*>(d2) + (long long)(rho0 - RA - 2 - RB) * W4;  // row y of step 0
+    char* const ptr = reinterpret_cast<char*>(trash);
+    int slot_use = 0;                 // input slot of step t (t mod NIN)
+    int slot_dma = NIN - 1;           // input slot of step t + NIN - 1
+    for (int it = 0; it < niter; it++) {
+        unroll_seq(std::make_integer_sequence<int, U>{}, [&](auto KI) __attribute__((always_inline)) {
+            constexpr int k = decltype(KI)::value;
+            const int t = it * U + k;
+            const int rho = rho0 + 2 * t;
+            const int mc = rho - RA;          // stage A's completed pair
+            const int mu = mc - 2;            // stage B's pair
+            asm volatile("" ::: "memory");
+            dma(rho + 2 * (NIN - 1), s_in + slot_dma * IN_SLOT);
+            slot_dma = slot_dma == NIN - 1 ? 0 : slot_dma + 1;
+            // every older VMEM instruction but the OPS (NIN - 1) youngest -- this step's DMA, the
+            // previous NIN - 2 steps' DMAs and stores, and the stores of the step that issued
+            // step t's DMA -- has completed: step t's DMA has landed
+            wait_vm<OPS * (NIN - 1)>();
+            asm volatile("" ::: "memory");
+            // both H passes: stage A on the input slot, stage B on the previous step's mid pair
+            const float* mb = mu <= -1 ? mid_top
+                            : (mu >= H - 1 ? mid_bot : s_mid + ((k + 1) & 1) * kMidSlot);
+            f2v o0, o1, q0, q1;
+            h1(s_in + slot_use * IN_SLOT, o0, o1);
+            slot_use = slot_use == NIN - 1 ? 0 : slot_use + 1;
+            // V1 push of rows rho (ring row 2k) and rho + 1 (2k + 1)
+            const f2v r0{o0.x, o1.x}, r1{o0.y, o1.y};
+#pragma unroll
+            for (int i = 0; i < FWA; i++) {
+                const int s = ((2 * k - i) % P + P) % P;
+                accA[s] = pkf(r0, tapa(i), i == 0 ? f2v{0.f, 0.f} : accA[s]);
+            }
+            f2v A0 = accA[((2 * k - (FWA - 1)) % P + P) % P];
+#pragma unroll
+            for (int i = 0; i < FWA; i++) {
+                const int s = ((2 * k + 1 - i) % P + P) % P;
+                accA[s] = pkf(r1, tapa(i), i == 0 ? f2v{0.f, 0.f} : accA[s]);
+            }
+            f2v A1 = accA[((2 * k + 1 - (FWA - 1)) % P + P) % P];
+            if constexpr (!kDuoInterleave) asm volatile("" ::: "memory");
+            h2(mb, q0, q1);
+            // V2 push of mid rows mu (ring row 2k) and mu + 1
+            const f2v g0{q0.x, q1.x}, g1{q0.y, q1.y};
+#pragma unroll
+            for (int i = 0; i < FWB; i++) {
+                const int s = ((2 * k - i) % P + P) % P;
+                accB[s] = pkf(g0, tapb(i), i == 0 ? f2v{0.f, 0.f} : accB[s]);
+            }
+            const f2v B0 = accB[((2 * k - (FWB - 1)) % P + P) % P];
+#pragma unroll
+            for (int i = 0; i < FWB; i++) {
+                const int s = ((2 * k + 1 - i) % P + P) % P;
+                accB[s] = pkf(g1, tapb(i), i == 0 ? f2v{0.f, 0.f} : accB[s]);
+            }
+            const f2v B1 = accB[((2 * k + 1 - (FWB - 1)) % P + P) % P];
+            // stage A's pair into mid slot k & 1 (and the bottom pair): edge columns clamped
+            if (mc == H - 1) A1 = A0;   // odd H: the pair (H-1, H) is (H-1, H-1)
+            if (left || right) {
+                fix_edges(A0);
+                fix_edges(A1);
+            }
+            put_mid(s_mid + (k & 1) * kMidSlot, A0, A1);
+            if (mc <= H - 1 && mc + 1 >= H - 1) {
+                const f2v Bv = mc == H - 1 ? A0 : A1;
+                put_mid(mid_bot, Bv, Bv);
+            }
+            asm volatile("" ::: "memory");
+            // level k + 1 rows mc, mc + 1 and level k + 2 rows y = mu - RB, y + 1: the wave's
+            // own columns; rows outside the band into the scratch block
+            {
+                const int y = mu - RB;
+                const bool a0ok = mc >= yb && mc < ye, a1ok = mc >= yb && mc + 1 < ye;
+                const bool b0ok = y >= yb && y < ye, b1ok = y >= yb && y + 1 < ye;
+                char* q;
+                if (own1) {
+                    q = a0ok ? pA + voffA : ptr + vtr;
+                    *reinterpret_cast<f2v*>(q) = A0;
+                    q = a1ok ? pA + W4 + voffA : ptr + vtr;
+                    *reinterpret_cast<f2v*>(q) = A1;
+                }
+                if (own2) {
+                    q = b0ok ? pB + voffB : ptr + vtr;
+                    *reinterpret_cast<f2v*>(q) = B0;
+                    q = b1ok ? pB + W4 + voffB : ptr + vtr;
+                    *reinterpret_cast<f2v*>(q) = B1;
+                }
+                pA += 2 * W4;
+                pB += 2 * W4;
+            }
+        });
+    }
+    // no DMA may land after the workgroup's LDS is handed to another workgroup
+    wait_vm<0>();
+}
+
+// waves per SIMD the register allocation must allow: 3 (<= 168 VGPRs) for (21, 25), whose
+// scheduler otherwise hoists both H passes' LDS reads (255 VGPRs, one wave per SIMD); 4 (<= 128)
+// for the narrower pairs
+#ifndef SGK_DUO_WPE_WIDE
+#define SGK_DUO_WPE_WIDE 3
+#endif
+#ifndef SGK_DUO_WPE_NARROW
+#define SGK_DUO_WPE_NARROW 4
+#endif
+template <int FWA, int FWB, int NIN>
+__global__ __launch_bounds__(64 * kDuoWaves) __attribute__((amdgpu_waves_per_eu(FWA + FWB > 30 ? SGK_DUO_WPE_WIDE : SGK_DUO_WPE_NARROW))) void k_gauss_duo(const DuoJob J) {
+    using G = DuoGeom<FWA, FWB>;
+    __shared__ __attribute__((aligned(16))) float s_in_all[kDuoWaves][NIN * G::IN_SLOT];
+    __shared__ __attribute__((aligned(16))) float s_mid_all[kDuoWaves][4 * kMidSlot];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int gw = duo_block(blockIdx.x, gridDim.x) * kDuoWaves + wave;
+    if (gw >= J.total_waves) return;   // uniform per wave
+    duo_wave<FWA, FWB, NIN>(J, gw, s_in_all[wave], s_mid_all[wave]);
+}
+
+// input row pairs in LDS: the DMA runs NIN - 1 steps ahead (compiled: 5 and 7; SGPU_DUO_NIN
+// picks one, A/B hook)
+#ifndef SGK_DUO_NIN
+#define SGK_DUO_NIN 7
+#endif
+static int duo_nin() {
+    static const int v = [] {
+        const char* e = getenv("SGPU_DUO_NIN");
+        return e ? atoi(e) : SGK_DUO_NIN;
+    }();
+    return v == 5 ? 5 : 7;
+}
+static int duo_bands_env() {
+    static const int v = [] {
+        const char* e = getenv("SGPU_DUO_BANDS");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
+template <int FWA, int FWB>
+hipError_t duo_launch(const LevelOp& a, const LevelOp& b, hipStream_t stream, int rows_hint,
+                      float* trash) {
+    using G = DuoGeom<FWA, FWB>;
+    DuoJob J{};
+    J.src = a.src;
+    J.src_stride = a.src_stride;
+    J.src_img = a.src_img_stride;
+    J.dst1 = a.dst;
+    J.dst2 = b.dst;
+    J.dst_img = a.dst_img_stride;
+    J.W = a.w;
+    J.H = a.h;
+    J.ta = a.taps;
+    J.tb = b.taps;
+    J.strips = (a.w + G::SW - 1) / G::SW;
+    const long long per_band = (long long)J.strips * a.batch;
+    // bands: the whole height while the grid has >= ~2048 waves (8 per CU); each band re-walks
+    // 2 (RA + RB) halo rows, so bands stay >= 64 rows
+    int nsy = 1;
+    if (rows_hint > 0) {
+        nsy = (a.h + rows_hint - 1) / rows_hint;
+    } else if (duo_bands_env() > 0) {
+        nsy = std::min(duo_bands_env(), std::max(1, a.h / 64));
+    } else if (per_band < 2048) {
+        nsy = (int)std::min<long long>((2048 + per_band - 1) / per_band, std::max(1, a.h / 64));
+    }
+    int rows = (a.h + nsy - 1) / nsy;
+    rows = (rows + 7) / 8 * 8;
+    J.nsy = (a.h + rows - 1) / rows;
+    J.rows_per_band = rows;
+    J.total_waves = (int)(per_band * J.nsy);
+    J.trash = trash;
+    const unsigned nb = (unsigned)((J.total_waves + kDuoWaves - 1) / kDuoWaves);
+    if (duo_nin() == 5)
+        hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 5>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
+    else
+        hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 7>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+bool gauss_duo_supported(const LevelOp& a, const LevelOp& b) {
+    const bool pair = (a.fw == 11 && b.fw == 13) || (a.fw == 21 && b.fw == 25);
+    return pair && a.src && !a.src_u8 && !a.ds_dst && !b.ds_dst && b.src == a.dst &&
+           !b.src_u8 && a.w == b.w && a.h == b.h && a.batch == b.batch && a.w >= 8 && a.h >= 8 &&
+           (a.w % 4) == 0 && b.src_stride == a.w && a.dst_img_stride == b.dst_img_stride &&
+           b.src_img_stride == a.dst_img_stride && a.dst_img_stride >= (long long)a.w * a.h;
+}
+
+hipError_t launch_gauss_duo(const LevelOp& a, const LevelOp& b, hipStream_t stream, int rows_hint,
+                            float* trash) {
+    if (!trash || !gauss_duo_supported(a, b)) return hipErrorInvalidValue;
+#define SGK_DUO(A, B) \
+    if (a.fw == A && b.fw == B) return duo_launch<A, B>(a, b, stream, rows_hint, trash);
+    SGK_DUO(11, 13) SGK_DUO(21, 25)
+#undef SGK_DUO
+    return hipErrorInvalidValue;
+}
+
+}  // namespace sgk

@@ -49,7 +49,7 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         long long src_img_stride, float* dst, long long dst_img_stride,
                         int w, int h, int fw, const Taps& taps, int batch,
                         float* ds_dst, int ds_w, int ds_h, long long ds_img_stride,
-                        hipStream_t stream, int wave_rows = -1);
+                        hipStream_t stream, int wave_rows = -1, bool long_bands = false);
 
 // One level filter of a pyramid stage (the arguments of launch_gauss).
 struct LevelOp {
@@ -66,12 +66,25 @@ struct LevelOp {
     int ds_w, ds_h;
     long long ds_img_stride;
 };
-hipError_t launch_gauss_op(const LevelOp& op, hipStream_t stream, int wave_rows);
+// long_bands: bands of >= 4 chunks on every level (the A/B hook SGPU_DEBUG_GAUSS_LONG_BANDS)
+hipError_t launch_gauss_op(const LevelOp& op, hipStream_t stream, int wave_rows,
+                           bool long_bands = false);
 // Two independent level filters (no data dependence between them) in one launch of the
 // wave-streaming kernel when their widths have a compiled pair, f32 sources and no decimation
 // (the "diagonal" schedule of the pyramid: octave o+1's level k beside octave o's level k + kds);
 // otherwise two launches.  Bit-identical to two launch_gauss calls.
-hipError_t launch_gauss_two(const LevelOp& a, const LevelOp& b, hipStream_t stream, int wave_rows);
+// *launches (optional): how many kernel launches it took (1 or 2).
+hipError_t launch_gauss_two(const LevelOp& a, const LevelOp& b, hipStream_t stream, int wave_rows,
+                            bool long_bands = false, int* launches = nullptr);
+
+// Two consecutive levels in one launch (sift_gauss_duo.hip): a = level k -> k+1, b = level
+// k+1 -> k+2 (b.src == a.dst), f32, no decimation, widths (11, 13) or (21, 25).  12 B of HBM
+// traffic per pixel for the two levels instead of 16; bit-identical to two launch_gauss_op
+// calls.  trash: kGaussDuoTrashBytes of device scratch.  rows_hint > 0 forces the band height.
+constexpr size_t kGaussDuoTrashBytes = 1024 * 2560;
+bool gauss_duo_supported(const LevelOp& a, const LevelOp& b);
+hipError_t launch_gauss_duo(const LevelOp& a, const LevelOp& b, hipStream_t stream, int rows_hint,
+                            float* trash);
 
 // First octave of -fo != 0 (BuildPyramid, PyramidCU.cpp:1011-1016): the batch's input
 // (u8 p/255 or f32; tw = w & ~3 columns used, rows `stride` apart) resampled into dst

@@ -332,7 +332,8 @@ constexpr int kGwWaves = SGK_GW_WPB;   // waves per workgroup of k_gauss_lean
 #ifndef SGK_SHORT_BAND_MB
 #define SGK_SHORT_BAND_MB 64
 #endif
-static GaussWaveGrid gauss_wave_grid(int w, int h, int batch, int rows_hint, int nw) {
+static GaussWaveGrid gauss_wave_grid(int w, int h, int batch, int rows_hint, int nw,
+                                     bool long_bands = false) {
     GaussWaveGrid g{};
     g.strips_x = (w + GT * nw - 1) / (GT * nw);
     const long long per_band = (long long)g.strips_x * nw * batch;   // waves per band
@@ -340,11 +341,8 @@ static GaussWaveGrid gauss_wave_grid(int w, int h, int batch, int rows_hint, int
     if (rows_hint > 0) {
         rows = rows_hint;
     } else {
-        // A/B hook: SGPU_GAUSS_BANDS=long keeps bands >= 4 chunks on every level (round 2)
-        static const bool long_bands = [] {
-            const char* e = getenv("SGPU_GAUSS_BANDS");
-            return e && !strcmp(e, "long");
-        }();
+        // long_bands (A/B hook, per context: SGPU_DEBUG_GAUSS_LONG_BANDS, or SGPU_GAUSS_BANDS=long
+        // read at context creation) keeps bands >= 4 chunks on every level (round 2)
         const bool short_ok = !long_bands && 4ll * w * h * batch <= ((long long)SGK_SHORT_BAND_MB << 20);
         const long long want = 8 * 256;
         const int nsy = (int)std::min<long long>((want + per_band - 1) / per_band,
@@ -706,11 +704,12 @@ template <int FW>
 hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
                           long long src_img_stride, float* dst, long long dst_img_stride, int w,
                           int h, const Taps& taps, int batch, float* ds, int dsw, int dsh,
-                          long long ds_img_stride, hipStream_t stream, int wave_rows) {
+                          long long ds_img_stride, hipStream_t stream, int wave_rows,
+                          bool long_bands) {
     const bool vec = (src_stride % 4) == 0 && (src_img_stride % 4) == 0 && (w % 4) == 0 &&
                      w >= 4 && ((uintptr_t)(src8 ? (const void*)src8 : (const void*)src) % 16) == 0;
     if (vec && wave_rows >= 0) {
-        const GaussWaveGrid gg = gauss_wave_grid(w, h, batch, wave_rows, 1);
+        const GaussWaveGrid gg = gauss_wave_grid(w, h, batch, wave_rows, 1, long_bands);
         const dim3 wgrid((unsigned)((gg.total_waves + kGwWaves - 1) / kGwWaves));
         const GaussJob J{src, src8, src_stride, src_img_stride, dst, dst_img_stride, w, h, taps,
                          ds, dsw, dsh, ds_img_stride, gg};
@@ -2733,12 +2732,13 @@ __global__ __launch_bounds__(64) void k_debug_candidates(
 hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         long long src_img_stride, float* dst, long long dst_img_stride, int w,
                         int h, int fw, const Taps& taps, int batch, float* ds_dst, int ds_w,
-                        int ds_h, long long ds_img_stride, hipStream_t stream, int wave_rows) {
+                        int ds_h, long long ds_img_stride, hipStream_t stream, int wave_rows,
+                        bool long_bands) {
 #define SGK_GAUSS(FW)                                                                       \
     case FW:                                                                                  \
         return gauss_dispatch<FW>(src, src_u8, src_stride, src_img_stride, dst, dst_img_stride, \
                                   w, h, taps, batch, ds_dst, ds_w, ds_h, ds_img_stride, stream, \
-                                  wave_rows);
+                                  wave_rows, long_bands);
     switch (fw) {
         SGK_GAUSS(5) SGK_GAUSS(7) SGK_GAUSS(9) SGK_GAUSS(11) SGK_GAUSS(13) SGK_GAUSS(15)
         SGK_GAUSS(17) SGK_GAUSS(19) SGK_GAUSS(21) SGK_GAUSS(23) SGK_GAUSS(25) SGK_GAUSS(27)
@@ -2748,10 +2748,10 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
 #undef SGK_GAUSS
 }
 
-hipError_t launch_gauss_op(const LevelOp& op, hipStream_t stream, int wave_rows) {
+hipError_t launch_gauss_op(const LevelOp& op, hipStream_t stream, int wave_rows, bool long_bands) {
     return launch_gauss(op.src, op.src_u8, op.src_stride, op.src_img_stride, op.dst,
                         op.dst_img_stride, op.w, op.h, op.fw, op.taps, op.batch, op.ds_dst,
-                        op.ds_w, op.ds_h, op.ds_img_stride, stream, wave_rows);
+                        op.ds_w, op.ds_h, op.ds_img_stride, stream, wave_rows, long_bands);
 }
 
 static bool diag_ok(const LevelOp& op) {
@@ -2762,9 +2762,9 @@ static bool diag_ok(const LevelOp& op) {
 
 template <int FWA, int FWB>
 static hipError_t gauss_diag_launch(const LevelOp& a, const LevelOp& b, hipStream_t stream,
-                                    int wave_rows) {
-    const GaussWaveGrid ga = gauss_wave_grid(a.w, a.h, a.batch, wave_rows, 1);
-    const GaussWaveGrid gb = gauss_wave_grid(b.w, b.h, b.batch, wave_rows, 1);
+                                    int wave_rows, bool long_bands) {
+    const GaussWaveGrid ga = gauss_wave_grid(a.w, a.h, a.batch, wave_rows, 1, long_bands);
+    const GaussWaveGrid gb = gauss_wave_grid(b.w, b.h, b.batch, wave_rows, 1, long_bands);
     const int nbA = (ga.total_waves + kGwWaves - 1) / kGwWaves;
     const int nbB = (gb.total_waves + kGwWaves - 1) / kGwWaves;
     const int nbBp = (nbB + 7) / 8 * 8;   // job A starts on XCD 0 (blocks are dealt round-robin)
@@ -2779,7 +2779,9 @@ static hipError_t gauss_diag_launch(const LevelOp& a, const LevelOp& b, hipStrea
     return hipGetLastError();
 }
 
-hipError_t launch_gauss_two(const LevelOp& a, const LevelOp& b, hipStream_t stream, int wave_rows) {
+hipError_t launch_gauss_two(const LevelOp& a, const LevelOp& b, hipStream_t stream, int wave_rows,
+                            bool long_bands, int* launches) {
+    if (launches) *launches = 1;
     if (wave_rows >= 0 && diag_ok(a) && diag_ok(b)) {
         // the default schedule's pairs (-d 3: levels 4 / 5 of octave o beside levels 1 / 2 of
         // octave o + 1); the larger job is A
@@ -2787,13 +2789,14 @@ hipError_t launch_gauss_two(const LevelOp& a, const LevelOp& b, hipStream_t stre
         const LevelOp& big = swap ? b : a;
         const LevelOp& small = swap ? a : b;
 #define SGK_DIAG(A, B) \
-        if (big.fw == A && small.fw == B) return gauss_diag_launch<A, B>(big, small, stream, wave_rows);
+        if (big.fw == A && small.fw == B) return gauss_diag_launch<A, B>(big, small, stream, wave_rows, long_bands);
         SGK_DIAG(21, 11) SGK_DIAG(25, 13)
 #undef SGK_DIAG
     }
-    hipError_t e = launch_gauss_op(a, stream, wave_rows);
+    if (launches) *launches = 2;
+    hipError_t e = launch_gauss_op(a, stream, wave_rows, long_bands);
     if (e != hipSuccess) return e;
-    return launch_gauss_op(b, stream, wave_rows);
+    return launch_gauss_op(b, stream, wave_rows, long_bands);
 }
 
 hipError_t launch_color_to_gray(const uint8_t* src, int n, int w, int h, int stride,

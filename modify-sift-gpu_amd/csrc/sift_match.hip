@@ -773,7 +773,11 @@ __global__ __launch_bounds__(64 * kRawWaves) SGK_RAW_ATTR void k_match_raw(const
         issue(tb + 2 * kTile, bi == 0 ? 2 : bi - 1);
         group(bi, 1, g1);
         fold(g0, true);
-        // tile t + 1's DMAs retired (t + 2's stay in flight), this tile's reads done
+        // tile t + 1's DMAs retired (t + 2's stay in flight), this tile's reads done; the
+        // compiler barrier keeps this tile's LDS reads above the wait and the s_barrier (after
+        // which other waves issue the DMA into this buffer), as the one below keeps the next
+        // tile's reads below them
+        asm volatile("" ::: "memory");
         __builtin_amdgcn_s_waitcnt(kWaitTile);
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");   // (as above: the next tile's reads stay below it)
@@ -832,7 +836,9 @@ __global__ __launch_bounds__(64 * kRawWaves) SGK_RAW_ATTR void k_match_raw(const
                 S[rb][i] = med3i(S[rb][i], M[rb][i], key);
                 M[rb][i] = max(M[rb][i], key);
             }
-        // tile t + 1's DMAs retired (t + 2's stay in flight), this tile's reads done
+        // tile t + 1's DMAs retired (t + 2's stay in flight), this tile's reads done (fenced
+        // for the compiler on both sides, as in the pipelined loop)
+        asm volatile("" ::: "memory");
         __builtin_amdgcn_s_waitcnt(kWaitTile);
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");   // (as above: the next tile's reads stay below it)

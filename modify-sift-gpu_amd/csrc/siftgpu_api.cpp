@@ -633,8 +633,22 @@ int SiftGPU::RunSIFT(int num, const SiftKeypoint* keys, int keys_have_orientatio
 }
 
 int SiftGPU::GetImageCount() { return (int)LIST(_list)->size(); }
+// SiftGPU::SetTightPyramid (SiftGPU.cpp:1430-1433) chooses how much slack ResizePyramid leaves
+// for larger images; the context's buffers are grow-only and sized per batch, so it changes
+// nothing here.
 void SiftGPU::SetTightPyramid(int) {}
-int SiftGPU::AllocatePyramid(int, int) { return 1; }
+// SiftGPU::AllocatePyramid (SiftGPU.cpp:1435-1460): the pyramid (and every other buffer) for a
+// width x height gray image is allocated now, so the first RunSIFT of that size allocates nothing
+// (sgpu_reserve).  Like the reference's ResizePyramid it drops the current image's pyramid.
+int SiftGPU::AllocatePyramid(int width, int height) {
+    if (!_initialized) InitSiftGPU();
+    if (!_initialized || width <= 0 || height <= 0) return 0;
+    Runtime* rt = RT(_pyramid);
+    rt->staged = false;
+    rt->have_image = false;
+    rt->feature_num = 0;
+    return sgpu_reserve(rt->ctx, 1, width, height, width) == SGPU_OK;
+}
 // SiftGPU::SetMaxDimension (SiftGPU.cpp:1452-1458): below the GL texture limit (14096,
 // GlobalUtil.cpp:88) it becomes _texMaxDim, which raises the first octave of larger inputs
 // (PyramidCU.cpp:129-135).

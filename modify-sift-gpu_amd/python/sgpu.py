@@ -31,7 +31,8 @@ C_API = [
     "sgpu_debug_set_flags", "sgpu_comm_unique_id", "sgpu_comm_init", "sgpu_comm_allgather_i32",
     "sgpu_comm_allreduce_f64", "sgpu_extract_keypoints", "sgpu_match_guided", "sgpu_extract_color",
     "sgpu_match_shard_begin", "sgpu_match_shard_end", "sgpu_match_sharded",
-    "sgpu_extract_stream", "sgpu_host_alloc", "sgpu_host_free",
+    "sgpu_extract_stream", "sgpu_host_alloc", "sgpu_host_free", "sgpu_reserve",
+    "sgpu_debug_alloc_count", "sgpu_last_pyramid_launches",
 ]
 
 _LIB = None
@@ -58,6 +59,10 @@ def lib():
         L.sgpu_last_error.restype = c.c_char_p
         L.sgpu_extract.argtypes = [vp, vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int]
         L.sgpu_stage_input.argtypes = [vp, vp, c.c_int, c.c_int, c.c_int, c.c_int]
+        L.sgpu_reserve.argtypes = [vp, c.c_int, c.c_int, c.c_int, c.c_int]
+        L.sgpu_debug_alloc_count.argtypes = []
+        L.sgpu_debug_alloc_count.restype = c.c_longlong
+        L.sgpu_last_pyramid_launches.argtypes = [vp, P(c.c_int)]
         L.sgpu_extract_f32.argtypes = [vp, vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int]
         L.sgpu_feature_count.argtypes = [vp, c.c_int]
         L.sgpu_feature_total.argtypes = [vp]
@@ -189,6 +194,27 @@ class SiftContext:
     def set_options(self, opts: SgpuOptions):
         self.opts = opts
         self._check(lib().sgpu_ctx_set_options(self._ctx, ctypes.byref(opts)), "set_options")
+
+    def reserve(self, n: int, w: int, h: int):
+        """Allocate every buffer an extract of n u8 images of w x h needs (sgpu_reserve, the
+        SiftGPU::AllocatePyramid entry point); drops the current batch and staged input."""
+        self._check(lib().sgpu_reserve(self._ctx, n, w, h, w), "sgpu_reserve")
+        self._staged = None
+        self.batch = 0
+        return self
+
+    def pyramid_launches(self):
+        """(kernel launches, level filters) of the last extract's Gaussian pyramid."""
+        f = ctypes.c_int(0)
+        n = lib().sgpu_last_pyramid_launches(self._ctx, ctypes.byref(f))
+        if n < 0:
+            raise RuntimeError("sgpu_last_pyramid_launches: no extract")
+        return int(n), int(f.value)
+
+    @staticmethod
+    def alloc_count() -> int:
+        """Device + pinned allocations the library has made so far (sgpu_debug_alloc_count)."""
+        return int(lib().sgpu_debug_alloc_count())
 
     def stage(self, images: np.ndarray):
         """Upload a u8 batch [n, h, w] once; extract_staged() then starts from HBM."""
@@ -421,6 +447,9 @@ class SiftContext:
     DEBUG_ORIENT_WAVE = 512   # orientation one wave per candidate for any candidate count
     DEBUG_MATCH_REGSTAGE = 2048  # keyless matcher with register staging (k_match_rows<RAW>)
     DEBUG_PYR_SERIAL = 4096    # all pyramid octaves on one stream
+    DEBUG_GAUSS_LONG_BANDS = 8192  # Gaussian bands of >= 4 chunks on every level
+    DEBUG_DUO_ALWAYS = 16384   # paired-level Gaussian launches whatever the level size
+    DEBUG_DUO_OFF = 32768      # no paired-level launches (one level per launch)
 
     def set_debug_flags(self, flags: int):
         """Per-context debug flags (sgpu_debug_set_flags; 0 = shipped configuration)."""

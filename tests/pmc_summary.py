@@ -19,6 +19,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
 def _one(pattern):
@@ -74,8 +75,11 @@ def main():
         per_family[f][0] += d
         per_family[f][1] += 1
     gauss = [f for f in per_family if f.startswith("k_gauss")]
+    from prof_common import box_name, source_digest
     out = {
         "tag": tag,
+        "source_digest": source_digest(),   # bench.py uses the counters only for this tree
+        "box": box_name(),
         "gauss_family": gauss,
         "extract_calls": n_steps,
         "ms_per_extract": {f: v[0] / n_steps for f, v in per_family.items() if v[1] >= n_steps},

@@ -24,7 +24,7 @@ def _exported(path):
 
 def test_library_exports_header_symbols():
     hdr = open(os.path.join(ROOT, "include", "sgpu.h")).read()
-    declared = set(re.findall(r"^\s*(?:int|void\*?|int64_t|const char\*)\s+(sgpu_\w+)\s*\(", hdr, re.M))
+    declared = set(re.findall(r"^\s*(?:int|void\*?|int64_t|long long|const char\*)\s+(sgpu_\w+)\s*\(", hdr, re.M))
     assert declared == set(sgpu.C_API), declared ^ set(sgpu.C_API)
     syms = _exported(sgpu.LIB_PATH)
     missing = [s for s in declared if s not in syms]

@@ -126,10 +126,11 @@ def test_block_first_octave_float_path(gpu_ctx, fo):
 
 @pytest.mark.parametrize("n,w,h,no", [(3, 1920, 1080, 4), (2, 517, 389, -1), (1, 4096, 4096, 6)])
 def test_octave_streams_equal_serial(gpu_ctx, n, w, h, no):
-    """Octaves >= 1 on a second stream (shipped) and all on the main stream
-    (SGPU_DEBUG_PYR_SERIAL): the same levels and keypoints, bit for bit -- the side stream only
-    reorders launches whose inputs are complete (octave 1 waits for octave 0's decimating level,
-    the extremum kernel for every octave)."""
+    """The shipped one-stream schedule (flags 0: the diagonal schedule, octave o+1's first
+    levels sharing k_gauss_diag launches with octave o's last ones, and the paired-level kernels
+    where they apply) against the serial one-level-per-launch order (SGPU_DEBUG_PYR_SERIAL): the
+    same levels and keypoints, bit for bit -- the schedules only reorder or fuse launches whose
+    inputs are complete."""
     imgs = synth_batch(n, w, h, 90 + n)
     opts = default_options(octave_num=no) if no > 0 else default_options()
     gpu_ctx.set_options(opts)
@@ -138,7 +139,7 @@ def test_octave_streams_equal_serial(gpu_ctx, n, w, h, no):
         gpu_ctx.extract(imgs)
         ref = _levels(gpu_ctx, n - 1, opts)
         k_ref = [gpu_ctx.features(i)[0].copy() for i in range(n)]
-        for flags in (0,):
+        for flags in (0, gpu_ctx.DEBUG_DUO_ALWAYS):
             gpu_ctx.set_debug_flags(flags)
             gpu_ctx.extract(imgs)
             got = _levels(gpu_ctx, n - 1, opts)
@@ -150,3 +151,57 @@ def test_octave_streams_equal_serial(gpu_ctx, n, w, h, no):
     finally:
         gpu_ctx.set_debug_flags(0)
         gpu_ctx.set_options(default_options())
+
+
+DUO = sgpu.SiftContext.DEBUG_DUO_ALWAYS
+DUO_OFF = sgpu.SiftContext.DEBUG_DUO_OFF
+
+
+# band heights: auto, one chunk (each band re-walks 2 (RA + RB) halo rows), not a multiple of
+# 8, taller than the image; sizes: tiny (one strip with both edges), ragged widths (not a
+# multiple of the 104- / 116-column strips), odd heights (the (H-1, H-1) bottom pair), 1080p
+@pytest.mark.parametrize("rows", [0, 8, 36, 4096])
+@pytest.mark.parametrize("n,w,h", [(2, 16, 16), (3, 203, 97), (2, 1920, 1080), (2, 300, 1203),
+                                   (1, 104, 33)])
+def test_duo_levels_equal_single_level(gpu_ctx, rows, n, w, h):
+    """The paired-level kernel (k_gauss_duo: levels k+1, k+2 from level k in one pass, both
+    vertical passes pushed into register accumulators) against one level per launch
+    (SGPU_DEBUG_DUO_OFF): every level of every octave and every keypoint, bit for bit."""
+    imgs = synth_batch(n, w, h, 140 + w % 11)
+    opts = default_options()
+    gpu_ctx.set_options(opts)
+    try:
+        gpu_ctx.set_debug_flags(DUO_OFF)
+        gpu_ctx.extract(imgs)
+        ref = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
+        k_ref = [gpu_ctx.features(i)[0].copy() for i in range(n)]
+        gpu_ctx.set_debug_flags((rows << 16) | DUO)
+        gpu_ctx.extract(imgs)
+        got = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
+        for a, b in zip(ref, got):
+            for o, (la, lb) in enumerate(zip(a, b)):
+                for lvl, (x, y) in enumerate(zip(la, lb)):
+                    assert np.array_equal(_bits(x), _bits(y)), (o, lvl)
+        for i in range(n):
+            assert np.array_equal(_bits(gpu_ctx.features(i)[0]), _bits(k_ref[i]))
+    finally:
+        gpu_ctx.set_debug_flags(0)
+
+
+@pytest.mark.parametrize("w,h,seed", [(640, 480, 1000), (1921, 1081, 5)])
+def test_duo_levels_vs_oracle(gpu_ctx, w, h, seed):
+    """k_gauss_duo's levels against the oracle (FilterH / FilterV, ProgramCU.cu:115-222), every
+    level of every octave."""
+    img = synth_image(w, h, seed)
+    opts = default_options()
+    gpu_ctx.set_options(opts)
+    gpu_ctx.set_debug_flags(DUO)
+    try:
+        gpu_ctx.extract(img)
+        for o in range(len(gpu_ctx.geometry())):
+            for lvl in range(opts.dog_level_num + 3):
+                g = gpu_ctx.gaussian(0, o, lvl)
+                r = O.gaussian(img, o, lvl, opts)
+                assert np.array_equal(_bits(g), _bits(r)), (o, lvl)
+    finally:
+        gpu_ctx.set_debug_flags(0)

@@ -187,8 +187,10 @@ def test_options_vs_oracle(gpu_ctx, over):
 def test_shipped_descriptor_vs_exact(gpu_ctx, over, n):
     """The shipped relaxed-order descriptor kernel against the bit-exact one on n HD images:
     same keypoints bit for bit, descriptors within L2 1e-5 (relative to |d| for -unn), i.e. 10x
-    inside the north star's 1e-4.  4 images (~5k features) run the two-waves-per-feature form
-    (few features), 24 images (~30k) the one-wave form."""
+    inside the north star's 1e-4.  Both counts run the same one-wave-per-feature kernel
+    (k_descriptor_dual); the 4-image case (~5k features) is kept deliberately as the small-grid
+    check (the grid is sized from the previous call's count), the 24-image one (~30k) as the
+    full-occupancy check."""
     from sift_synth import synth_batch_fast
     imgs = synth_batch_fast(n, 1280, 720, 510)
     opts = default_options(**over)
