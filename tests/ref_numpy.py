@@ -18,14 +18,18 @@ import math
 import numpy as np
 
 
-def schedule(d=3, filter_factor=4.0, dog_threshold=0.0, edge_threshold=0.0):
+def schedule(d=3, filter_factor=4.0, dog_threshold=0.0, edge_threshold=0.0, octave_min=0):
+    """SiftParam::ParseSiftParam / GetInitialSmoothSigma (SiftGPU.cpp:446-498): the first
+    level's smoothing assumes the input already carries sigma_n = 0.5 at octave 0, i.e.
+    0.5 / 2^octave_min in the first octave's pixels."""
     sigma0 = 1.6 * 2.0 ** (1.0 / d)
     sigmak = 2.0 ** (1.0 / d)
     dsigma0 = sigma0 * math.sqrt(1.0 - 1.0 / (sigmak * sigmak))
     level_min, level_max = -1, d + 1
     sig = [dsigma0 * sigmak ** i for i in range(level_min + 1, level_max + 1)]
     a = sigma0 * 2.0 ** (level_min / d)
-    initial = math.sqrt(a * a - 0.25) if a > 0.5 + 0.001 else 0.0
+    b = 0.5 / 2.0 ** octave_min
+    initial = math.sqrt(a * a - b * b) if a > b + 0.001 else 0.0
     return {
         "d": d, "nlev": d + 3, "sigma0": sigma0, "level_sigma": [sigma0 * 2.0 ** ((j + 1) / d) for j in range(d)],
         "filter_sigma": sig, "initial": initial, "factor": filter_factor,
@@ -66,11 +70,37 @@ def geometry(w, h, octave_num):
     return out
 
 
-def pyramid(img_u8, S, octave_num=-1):
-    """[octave][level] float64 Gaussian images, each wa x h."""
+def upsample(img, s):
+    """UpsampleKernel<s> (ProgramCU.cu:225-269) in float64: the image bound as one flat buffer,
+    so the right neighbour of a row's last pixel is the next row's first one and reads past
+    the buffer are 0; output row R blends source rows R >> s and (R >> s) + 1 with weight
+    (R & (S-1)) / S, and source column c fills the S outputs c S .. c S + S-1 between pixels c
+    and c + 1."""
+    S = 1 << s
+    h, w = img.shape
+    flat = np.concatenate([img.reshape(-1), np.zeros(w + 2)])
+    out = np.zeros((h * S, w * S))
+    cols = np.arange(w)
+    for R in range(h * S):
+        r, f = R >> s, (R & (S - 1)) / S
+        i = r * w + cols
+        v1 = (1 - f) * flat[i] + f * flat[i + w]
+        v2 = (1 - f) * flat[i + 1] + f * flat[i + w + 1]
+        for k in range(S):
+            out[R, cols * S + k] = v1 * (1 - k / S) + v2 * (k / S)
+    return out
+
+
+def pyramid(img_u8, S, octave_num=-1, octave_min=0):
+    """[octave][level] float64 Gaussian images, each wa x h.  octave_min < 0 (-fo): the input
+    (width truncated to a multiple of 4) upsampled by 2^-octave_min first (PyramidCU.cpp:89-112,
+    SampleImageU)."""
     h, w = img_u8.shape
-    geo = geometry(w, h, octave_num)
-    base = img_u8[:, : geo[0][2]].astype(np.float64) / 255.0
+    base = img_u8[:, : w & ~3].astype(np.float64) / 255.0
+    if octave_min < 0:
+        base = upsample(base, -octave_min)
+    geo = geometry(base.shape[1], base.shape[0], octave_num)
+    base = base[:, : geo[0][2]]
     out = []
     for o, (_, ho, wa) in enumerate(geo):
         if o == 0:
