@@ -339,8 +339,11 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
             wait_vm<OPS * (NIN - 1)>();
             asm volatile("" ::: "memory");
             // both H passes: stage A on the input slot, stage B on the previous step's mid pair
-            const float* mb = mu <= -1 ? mid_top
-                            : (mu >= H - 1 ? mid_bot : s_mid + ((k + 1) & 1) * kMidSlot);
+            // (an offset from one base: a select between the slot pointers made the compiler
+            // lose their LDS address space -- flat accesses through the lambdas' closure)
+            const int mb_off = mu <= -1 ? 2 * kMidSlot : (mu >= H - 1 ? 3 * kMidSlot
+                                                                      : ((k + 1) & 1) * kMidSlot);
+            const float* mb = s_mid + mb_off;
             f2v o0, o1, q0, q1;
             h1(s_in + slot_use * IN_SLOT, o0, o1);
             slot_use = slot_use == NIN - 1 ? 0 : slot_use + 1;
