@@ -232,8 +232,15 @@ void sgpu_quantize_descriptors(const float* d, size_t count, uint8_t* out);
  * {upload, pyramid, detect, orientation, expand, descriptor, download, total} of the last
  * extract; times[8] = the last sgpu_match call; times[9] = the feature-list (row scan) part of
  * detect; times[10], [11] = the key and descriptor copies of the last sgpu_copy_features.
- * SiftGPU::_timing[2..8] map them to the reference's slots (siftgpu_api.cpp). */
+ * SiftGPU::_timing[2..8] map them to the reference's slots (siftgpu_api.cpp).  Slots 0-7 and
+ * 9-11 read 0 after a one-stream extract / copy made with the stage timing off. */
 int sgpu_last_timing(const sgpu_ctx* ctx, float* times, int n);
+/* Stage timing on (default) or off.  Replaces the reference's GlobalUtil::_timingS (GlobalUtil.cpp:51,
+ * set by SiftGPU::SetVerbose, SiftGPU.cpp:401-429; 0 skips the per-stage finish calls,
+ * PyramidCU.cpp:439,873,1041).  Off, a one-stream extract records none of its ~10 stage events
+ * (each ~4.5 us of GPU time between two kernels); the multi-stream layouts and
+ * sgpu_extract_stream keep the events they synchronise on. */
+int sgpu_set_stage_timing(sgpu_ctx* ctx, int on);
 
 /* ---- multi-GPU batch driver (no reference counterpart: the reference
  * runs one SiftGPU per device thread, TestWin/MultiThreadSIFT.cpp:141-155).  One process per

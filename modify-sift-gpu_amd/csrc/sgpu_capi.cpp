@@ -83,6 +83,7 @@ struct Part {
     hipEvent_t ev_oct = nullptr;       // octaves >= 1 done
     size_t cand_hint = 0, feat_hint = 0;   // counts of the previous call (launch-grid sizing)
     int gauss_launches = 0, gauss_filters = 0;   // the last pyramid: launches, level filters
+    bool events = true;                    // the last enqueue recorded its stage events
     hipEvent_t ev[10] = {};  // start, pyramid, detect, orientation, expand, descriptor, end,
                              // extrema done (before the row scan), (spare), (spare)
     int img0 = 0, n = 0;
@@ -134,6 +135,12 @@ struct sgpu_ctx {
     int debug_flags = 0;                   // SGPU_DEBUG_* test hooks
     bool multi_stream = false;             // SGPU_STREAMS=multi: octave and feature streams
     bool duo_on = false;                   // SGPU_DUO=on: paired-level launches (size rule)
+    // per-stage HIP events of an extract (sgpu_last_timing's stage slots).  Each event record
+    // costs ~4.5 us of GPU time between the commands around it (tests/microbench/event_gap.hip),
+    // ~40 us per single-image extract; sgpu_set_stage_timing(ctx, 0) drops them where they only
+    // time (one-stream extracts; the multi-stream layouts need some to synchronise)
+    bool stage_timing = true;
+    bool streaming = false;                // inside sgpu_extract_stream (its waits use events)
     std::string err;
     // last extract
     int batch = 0, w = 0, h = 0, nparts = 0;
@@ -510,7 +517,7 @@ static int layout_part(sgpu_ctx* ctx, Part& pt) {
     ALLOCCHK(ctx, pt.mask.ensure((size_t)moff * sizeof(uint32_t)));
     ALLOCCHK(ctx, pt.row_count.ensure((size_t)pt.total_rows * sizeof(uint32_t)));
     ALLOCCHK(ctx, pt.row_base.ensure(((size_t)pt.total_rows + 1) * sizeof(uint32_t)));
-    ALLOCCHK(ctx, pt.img_off_dev.ensure((size_t)(n + 1) * sizeof(int64_t)));
+    ALLOCCHK(ctx, pt.img_off_dev.ensure((size_t)(n + 2) * sizeof(int64_t)));
     ALLOCCHK(ctx, pt.cand.ensure(nc * sizeof(float4)));
     ALLOCCHK(ctx, pt.info.ensure(nc * sizeof(int2)));
     ALLOCCHK(ctx, pt.ocount.ensure(nc * sizeof(uint32_t)));
@@ -547,7 +554,13 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     const size_t nc = pt.cand_cap, ne_cap = 2 * nc;
 
     if (wait) HIPCHK(ctx, hipStreamWaitEvent(st, wait, 0));
-    HIPCHK(ctx, hipEventRecord(pt.ev[0], st));
+    // stage events: always where a stream waits on them (the multi-stream layouts, the
+    // host-in / host-out stream), else only when the context times its stages
+    pt.events = ctx->stage_timing || !pt.one_stream || ctx->nparts > 1 || ctx->streaming;
+    auto rec = [&](int i, hipStream_t s_) -> hipError_t {
+        return pt.events ? hipEventRecord(pt.ev[i], s_) : hipSuccess;
+    };
+    HIPCHK(ctx, rec(0, st));
     const size_t img_elems = (size_t)stride * h;
     const uint8_t* src8 = is_f32 ? nullptr : (const uint8_t*)src_in + (size_t)pt.img0 * img_elems;
     const float* srcf = is_f32 ? (const float*)src_in + (size_t)pt.img0 * img_elems : nullptr;
@@ -629,6 +642,16 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
             op.ds_w = dk ? dsw : 0;
             op.ds_h = dk ? dsh : 0;
             op.ds_img_stride = dk ? ds_stride : 0;
+            if (o == 0 && k == 0 && pt.one_stream) {
+                // the first level launch also zeroes the extremum kernel's mask and row counts
+                // and the orientation counts (one launch fewer than launch_zero)
+                op.zero.p[0] = pt.row_count.as<uint32_t>();
+                op.zero.n[0] = (size_t)pt.total_rows;
+                op.zero.p[1] = pt.mask.as<uint32_t>();
+                op.zero.n[1] = (size_t)moff;
+                op.zero.p[2] = pt.ocount.as<uint32_t>();
+                op.zero.n[2] = nc;
+            }
             ops.push_back(e);
         }
     }
@@ -706,24 +729,24 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
         HIPCHK(ctx, hipEventRecord(pt.ev_oct, pt.stream_oct));
         HIPCHK(ctx, hipStreamWaitEvent(st, pt.ev_oct, 0));
     }
-    HIPCHK(ctx, hipEventRecord(pt.ev[1], st));
+    HIPCHK(ctx, rec(1, st));
 
     // ---- extrema + row scan (the strip extremum kernel only sets the bits it accepts)
-    // (one launch zeroes the row counts and the mask, and on a single stream also the
-    // orientation counts, which otherwise are zeroed on the feature stream after its waits)
-    HIPCHK(ctx, sgk::launch_zero(pt.row_count.as<uint32_t>(), (size_t)pt.total_rows,
-                                 pt.mask.as<uint32_t>(), (size_t)moff,
-                                 pt.one_stream ? pt.ocount.as<uint32_t>() : nullptr,
-                                 pt.one_stream ? nc : 0, st));
+    // (the row counts and the mask start zeroed: on one stream the first level launch zeroed
+    // them and the orientation counts; otherwise one launch here, and the orientation counts
+    // are zeroed on the feature stream after its waits)
+    if (!pt.one_stream)
+        HIPCHK(ctx, sgk::launch_zero(pt.row_count.as<uint32_t>(), (size_t)pt.total_rows,
+                                     pt.mask.as<uint32_t>(), (size_t)moff, nullptr, 0, st));
     HIPCHK(ctx, sgk::launch_extrema(pyr, pt.mask.as<uint32_t>(), pt.row_count.as<uint32_t>(),
                                     fp, st));
     if (O.feature_count_threshold > 0)   // -tc: GenerateFeatureList skip + LimitFeatureCount(0)
         HIPCHK(ctx, sgk::launch_limit_rows(pt.row_count.as<uint32_t>(), fp,
                                            O.feature_count_threshold, O.truncate_method, st));
-    HIPCHK(ctx, hipEventRecord(pt.ev[7], st));
+    HIPCHK(ctx, rec(7, st));
     HIPCHK(ctx, sgk::launch_scan(pt.row_count.as<uint32_t>(), pt.row_base.as<uint32_t>(),
                                  pt.total_rows, pt.scan_tmp.as<uint32_t>(), st));
-    HIPCHK(ctx, hipEventRecord(pt.ev[2], st));
+    HIPCHK(ctx, rec(2, st));
 
     // ---- orientation (+ keypoint refinement), expansion, descriptors on the low-priority
     // stream: counts stay on the device, grids come from the previous call's counts (the
@@ -750,36 +773,39 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
         HIPCHK(ctx, sgk::launch_limit_oriented(pt.ocount.as<uint32_t>(), pt.row_base.as<uint32_t>(),
                                                fp, O.feature_count_threshold, O.truncate_method,
                                                (uint32_t)nc, st));
-    HIPCHK(ctx, hipEventRecord(pt.ev[3], st));
+    HIPCHK(ctx, rec(3, st));
     HIPCHK(ctx, sgk::launch_scan(pt.ocount.as<uint32_t>(), pt.eoff.as<uint32_t>(), nc,
                                  pt.scan_tmp.as<uint32_t>(), st));
     const uint32_t* n_feat_dev = pt.eoff.as<uint32_t>() + nc;
+    // (the same launch writes the readback record: candidate count + per-image offsets)
+    sgk::ImageOffsetsArgs io;
+    io.row_base = pt.row_base.as<uint32_t>();
+    io.batch = n;
+    io.rows_per_image = fp.rows_per_image;
+    io.total_rows = pt.total_rows;
+    io.off = pt.img_off_dev.as<int64_t>();
     HIPCHK(ctx, sgk::launch_expand(pt.cand.as<float4>(), pt.info.as<int2>(),
                                    pt.eoff.as<uint32_t>(), n_cand_dev, (int)nc, fp,
                                    pt.feat.as<float4>(), pt.feat_info.as<int2>(),
-                                   pt.keys.as<float4>(), st));
-    HIPCHK(ctx, hipEventRecord(pt.ev[4], st));
+                                   pt.keys.as<float4>(), st, &io));
+    HIPCHK(ctx, rec(4, st));
     if (O.descriptors)
         HIPCHK(ctx, sgk::launch_descriptor(pyr, pt.feat.as<float4>(), pt.feat_info.as<int2>(),
                                            n_feat_dev, feat_grid, fp, pt.desc.as<float>(), st,
                                            nullptr, false,
                                            ctx->debug_flags & SGPU_DEBUG_EXACT_DESCRIPTOR));
-    HIPCHK(ctx, hipEventRecord(pt.ev[5], st));
-    HIPCHK(ctx, sgk::launch_image_offsets(pt.row_base.as<uint32_t>(), pt.eoff.as<uint32_t>(), n,
-                                          fp.rows_per_image, pt.total_rows, (int)nc,
-                                          pt.img_off_dev.as<int64_t>(), st));
+    HIPCHK(ctx, rec(5, st));
     return SGPU_OK;
 }
 
 // Queue the (pinned) readback of a part's counts and offsets.
 static int enqueue_readback(sgpu_ctx* ctx, Part& pt) {
     hipStream_t st = pt.one_stream ? pt.stream : pt.stream_lo;
-    pt.h_read[0] = 0;
-    HIPCHK(ctx, hipMemcpyAsync(pt.h_read, pt.row_base.as<uint32_t>() + pt.total_rows, 4,
+    // one copy: [0] = the candidate count, [1 .. n + 1] = the per-image feature offsets (the
+    // record k_expand writes)
+    HIPCHK(ctx, hipMemcpyAsync(pt.h_read, pt.img_off_dev.p, (size_t)(pt.n + 2) * sizeof(int64_t),
                                hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(pt.h_read + 1, pt.img_off_dev.p, (size_t)(pt.n + 1) * sizeof(int64_t),
-                               hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipEventRecord(pt.ev[6], st));
+    if (pt.events) HIPCHK(ctx, hipEventRecord(pt.ev[6], st));
     return SGPU_OK;
 }
 
@@ -888,8 +914,9 @@ static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
     // (tests/microbench/event_gap.hip: 2.2 vs 6.7 us per short kernel), and a staged or device
     // batch on one stream has neither (C2, the bench's batches)
     const size_t in_bytes = (size_t)n * h * stride * (is_f32 ? sizeof(float) : 1);
-    const bool up_events = !one || color || plan.ds > 0 ||
-                           !(flags & (SGPU_INPUT_DEVICE | SGPU_INPUT_STAGED));
+    const bool up_events = !one || ((color || plan.ds > 0 ||
+                                     !(flags & (SGPU_INPUT_DEVICE | SGPU_INPUT_STAGED))) &&
+                                    ctx->stage_timing);
     if (up_events) HIPCHK(ctx, hipEventRecord(ctx->ev[0], up));
     const void* src_in = staged ? ctx->input.p : images;
     if (!(flags & (SGPU_INPUT_DEVICE | SGPU_INPUT_STAGED))) {
@@ -970,6 +997,11 @@ static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
     // timings: stages of part 0 (its pyramid and detection run alone), total over all parts
     Part& p0 = ctx->part[0];
     ctx->timing[T_UPLOAD] = 0.0f;
+    if (!p0.events) {   // sgpu_set_stage_timing(ctx, 0): no stage events were recorded
+        for (int i = T_UPLOAD; i <= T_DOWNLOAD; i++) ctx->timing[i] = 0.0f;
+        ctx->timing[T_TOTAL] = ctx->timing[T_LIST] = 0.0f;
+        return SGPU_OK;
+    }
     if (up_events) (void)hipEventElapsedTime(&ctx->timing[T_UPLOAD], ctx->ev[0], ctx->ev[1]);
     (void)hipEventElapsedTime(&ctx->timing[T_PYRAMID], p0.ev[0], p0.ev[1]);
     (void)hipEventElapsedTime(&ctx->timing[T_DETECT], p0.ev[1], p0.ev[2]);
@@ -1123,8 +1155,10 @@ int sgpu_extract_stream(sgpu_ctx* ctx, const uint8_t* const* batches, int nbatch
                         int w, int h, int stride, float* keys, float* desc, int64_t cap,
                         int32_t* counts) {
     if (!ctx) return SGPU_EINVAL;
+    ctx->streaming = true;   // its waits use the slots' stage events
     const int rc = extract_stream_body(ctx, batches, nbatches, batch, w, h, stride, keys, desc,
                                        cap, counts);
+    ctx->streaming = false;
     // on success as on failure: every copy from the caller's batches and into the caller's
     // outputs has completed, and the per-image queries (sgpu_copy_features, ...) have no "last
     // batch" after a stream
@@ -1711,6 +1745,12 @@ int sgpu_reserve(sgpu_ctx* ctx, int n, int w, int h, int stride) {
 
 long long sgpu_debug_alloc_count(void) { return g_allocs.load(); }
 
+int sgpu_set_stage_timing(sgpu_ctx* ctx, int on) {
+    if (!ctx) return SGPU_EINVAL;
+    ctx->stage_timing = on != 0;
+    return SGPU_OK;
+}
+
 int sgpu_last_pyramid_launches(const sgpu_ctx* ctx, int* filters) {
     if (!ctx || ctx->batch <= 0) return SGPU_EINVAL;
     if (filters) *filters = ctx->part[0].gauss_filters;
@@ -1757,19 +1797,23 @@ int sgpu_copy_features(sgpu_ctx* ctx, int image, float* keys, float* descriptors
     }
     if (descriptors && !ctx->opt.descriptors) return ctx->fail(SGPU_EINVAL, "descriptors disabled (-sd)");
     // both copies, then one synchronisation; events split the time between them
-    // (sgpu_last_timing slots 10, 11)
-    HIPCHK(ctx, hipEventRecord(ctx->ev[T_COPY_KEYS], ctx->stream));
+    // (sgpu_last_timing slots 10, 11) when the context times its stages
+    const bool tm = ctx->stage_timing;
+    if (tm) HIPCHK(ctx, hipEventRecord(ctx->ev[T_COPY_KEYS], ctx->stream));
     if (keys)
         HIPCHK(ctx, hipMemcpyAsync(keys, pt.keys.as<float4>() + a, nf * sizeof(float4),
                                    hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipEventRecord(ctx->ev[T_COPY_DESC], ctx->stream));
+    if (tm) HIPCHK(ctx, hipEventRecord(ctx->ev[T_COPY_DESC], ctx->stream));
     if (descriptors)
         HIPCHK(ctx, hipMemcpyAsync(descriptors, pt.desc.as<float>() + a * 128,
                                    nf * 128 * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipEventRecord(ctx->ev[T_N], ctx->stream));
+    if (tm) HIPCHK(ctx, hipEventRecord(ctx->ev[T_N], ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    (void)hipEventElapsedTime(&ctx->timing[T_COPY_KEYS], ctx->ev[T_COPY_KEYS], ctx->ev[T_COPY_DESC]);
-    (void)hipEventElapsedTime(&ctx->timing[T_COPY_DESC], ctx->ev[T_COPY_DESC], ctx->ev[T_N]);
+    ctx->timing[T_COPY_KEYS] = ctx->timing[T_COPY_DESC] = 0.f;
+    if (tm) {
+        (void)hipEventElapsedTime(&ctx->timing[T_COPY_KEYS], ctx->ev[T_COPY_KEYS], ctx->ev[T_COPY_DESC]);
+        (void)hipEventElapsedTime(&ctx->timing[T_COPY_DESC], ctx->ev[T_COPY_DESC], ctx->ev[T_N]);
+    }
     return SGPU_OK;
 }
 

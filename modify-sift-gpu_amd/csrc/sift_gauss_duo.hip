@@ -166,7 +166,8 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
     static_assert(NDMA == 5, "the asm below issues 5 DMAs per row pair");
     auto dma = [&](int rho, float* slot) __attribute__((always_inline)) {
         const int r0 = clampd(rho, 0, H - 1), r1 = clampd(rho + 1, 0, H - 1);
-        const char* base = uniform_ptr(src + (long long)r0 * J.src_stride);
+        const char* base = uniform_ptr(reinterpret_cast<const char*>(src) +
+                                       (uint32_t)r0 * (4u * (uint32_t)J.src_stride));
         const uint32_t ro = r1 != r0 ? rsel : 0u;
         const uint32_t lds = __builtin_amdgcn_readfirstlane(
             (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)slot);
@@ -317,10 +318,14 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
     // stores: uniform row pointers (the level's image base + row * W, updated per step) plus a
     // lane byte offset; rows outside the band go to the wave's scratch block at lane * 8
     const uint32_t voffA = 4u * (uint32_t)c, voffB = 4u * (uint32_t)e, vtr = 8u * (uint32_t)lane;
-    const long long W4 = 4ll * W;
-    char* pA = reinterpret_cast<char*>(d1) + (long long)(rho0 - RA) * W4;        // row mc of step 0
-    char* pB = reinterpret_cast<char*>(d2) + (long long)(rho0 - RA - 2 - RB) * W4;  // row y of step 0
-    char* const ptr = reinterpret_cast<char*>(trash);
+    // 32-bit byte offsets of the stored rows inside an image (a level image is < 4 GB): the
+    // stores are base (SGPR pair) + offset (VGPR), with no 64-bit address arithmetic per step
+    const uint32_t W4 = 4u * (uint32_t)W;
+    uint32_t rowA = (uint32_t)(rho0 - RA) * W4;            // row mc of step 0 (mod 2^32)
+    uint32_t rowB = (uint32_t)(rho0 - RA - 2 - RB) * W4;   // row y of step 0
+    char* const bA = reinterpret_cast<char*>(d1);
+    char* const bB = reinterpret_cast<char*>(d2);
+    char* const bT = reinterpret_cast<char*>(trash);
     int slot_use = 0;                 // input slot of step t (t mod NIN)
     int slot_dma = NIN - 1;           // input slot of step t + NIN - 1
     for (int it = 0; it < niter; it++) {
@@ -395,21 +400,16 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
                 const int y = mu - RB;
                 const bool a0ok = mc >= yb && mc < ye, a1ok = mc >= yb && mc + 1 < ye;
                 const bool b0ok = y >= yb && y < ye, b1ok = y >= yb && y + 1 < ye;
-                char* q;
                 if (own1) {
-                    q = a0ok ? pA + voffA : ptr + vtr;
-                    *reinterpret_cast<f2v*>(q) = A0;
-                    q = a1ok ? pA + W4 + voffA : ptr + vtr;
-                    *reinterpret_cast<f2v*>(q) = A1;
+                    *reinterpret_cast<f2v*>((a0ok ? bA : bT) + (a0ok ? rowA + voffA : vtr)) = A0;
+                    *reinterpret_cast<f2v*>((a1ok ? bA : bT) + (a1ok ? rowA + W4 + voffA : vtr)) = A1;
                 }
                 if (own2) {
-                    q = b0ok ? pB + voffB : ptr + vtr;
-                    *reinterpret_cast<f2v*>(q) = B0;
-                    q = b1ok ? pB + W4 + voffB : ptr + vtr;
-                    *reinterpret_cast<f2v*>(q) = B1;
+                    *reinterpret_cast<f2v*>((b0ok ? bB : bT) + (b0ok ? rowB + voffB : vtr)) = B0;
+                    *reinterpret_cast<f2v*>((b1ok ? bB : bT) + (b1ok ? rowB + W4 + voffB : vtr)) = B1;
                 }
-                pA += 2 * W4;
-                pB += 2 * W4;
+                rowA += 2 * W4;
+                rowB += 2 * W4;
             }
         });
     }
@@ -502,7 +502,9 @@ hipError_t duo_launch(const LevelOp& a, const LevelOp& b, hipStream_t stream, in
 
 bool gauss_duo_supported(const LevelOp& a, const LevelOp& b) {
     const bool pair = (a.fw == 11 && b.fw == 13) || (a.fw == 21 && b.fw == 25);
-    return pair && a.src && !a.src_u8 && !a.ds_dst && !b.ds_dst && b.src == a.dst &&
+    const bool zeroes = (a.zero.n[0] | a.zero.n[1] | a.zero.n[2] | b.zero.n[0] | b.zero.n[1] |
+                         b.zero.n[2]) != 0;
+    return pair && !zeroes && a.src && !a.src_u8 && !a.ds_dst && !b.ds_dst && b.src == a.dst &&
            !b.src_u8 && a.w == b.w && a.h == b.h && a.batch == b.batch && a.w >= 8 && a.h >= 8 &&
            (a.w % 4) == 0 && b.src_stride == a.w && a.dst_img_stride == b.dst_img_stride &&
            b.src_img_stride == a.dst_img_stride && a.dst_img_stride >= (long long)a.w * a.h;

@@ -38,6 +38,12 @@ struct FeatureParams {
     OctaveDesc oct[kMaxOctaves];
 };
 
+// Up to three u32 buffers to zero (null / 0 words: none).
+struct ZeroJob {
+    uint32_t* p[3] = {nullptr, nullptr, nullptr};
+    size_t n[3] = {0, 0, 0};
+};
+
 // Gaussian level filter: dst = V(H(src)) with the reference's clamp-to-edge semantics.
 // src_u8 != nullptr selects the ingest variant (src value = u8 / 255.0f).  src_stride is the
 // row stride in elements of whichever source is used.
@@ -49,9 +55,12 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         long long src_img_stride, float* dst, long long dst_img_stride,
                         int w, int h, int fw, const Taps& taps, int batch,
                         float* ds_dst, int ds_w, int ds_h, long long ds_img_stride,
-                        hipStream_t stream, int wave_rows = -1, bool long_bands = false);
+                        hipStream_t stream, int wave_rows = -1, bool long_bands = false,
+                        const ZeroJob& zero = ZeroJob{});
 
-// One level filter of a pyramid stage (the arguments of launch_gauss).
+// One level filter of a pyramid stage (the arguments of launch_gauss).  zero (optional): the
+// launch also zeroes these buffers (the extremum kernel's mask and row counts, the orientation
+// counts) -- one launch fewer per extract than launch_zero, which a single image pays per launch.
 struct LevelOp {
     const float* src;
     const uint8_t* src_u8;
@@ -65,6 +74,7 @@ struct LevelOp {
     float* ds_dst;
     int ds_w, ds_h;
     long long ds_img_stride;
+    ZeroJob zero;
 };
 // long_bands: bands of >= 4 chunks on every level (the A/B hook SGPU_DEBUG_GAUSS_LONG_BANDS)
 hipError_t launch_gauss_op(const LevelOp& op, hipStream_t stream, int wave_rows,
@@ -128,10 +138,18 @@ hipError_t launch_orientation(const float* pyr, const uint32_t* mask, const uint
                               uint32_t* ocount, hipStream_t stream,
                               bool wave_per_candidate = false);
 
-// Expansion into oriented features (+ image-coordinate keypoints).
+// Expansion into oriented features (+ image-coordinate keypoints).  io (optional): the same
+// launch also writes the extract's readback record (io.off[0] = candidate count, io.off[1 + b]
+// = image b's first feature for b in [0, batch], the readback of an extract).
+struct ImageOffsetsArgs {
+    const uint32_t* row_base = nullptr;
+    int batch = 0, rows_per_image = 0, total_rows = 0;
+    int64_t* off = nullptr;
+};
 hipError_t launch_expand(const float4* cand, const int2* info, const uint32_t* eoff,
                          const uint32_t* n_cand_dev, int n_cand_cap, const FeatureParams& fp,
-                         float4* feat, int2* feat_info, float4* keys, hipStream_t stream);
+                         float4* feat, int2* feat_info, float4* keys, hipStream_t stream,
+                         const ImageOffsetsArgs* io = nullptr);
 
 // Descriptors (+ normalisation) of the expanded features; n_feat_cap sizes the grid (one wave
 // per feature), the kernel grid-strides over *n_feat_dev.  out_index (optional): feature e's
@@ -159,11 +177,6 @@ hipError_t launch_limit_oriented(uint32_t* ocount, const uint32_t* row_base,
                                  const FeatureParams& fp, int threshold, int method,
                                  uint32_t cand_cap, hipStream_t stream);
 
-// Per-image feature offsets: off[b] = eoff[min(row_base[b * rows_per_image], cap)] for b in
-// [0, batch] (cap = candidate capacity; the clamp only matters when the candidates overflowed).
-hipError_t launch_image_offsets(const uint32_t* row_base, const uint32_t* eoff, int batch,
-                                int rows_per_image, int total_rows, int n_cand_cap, int64_t* off,
-                                hipStream_t stream);
 
 // Debug: candidates of the orientation stage back as (col, row, level id, image) + (dx,dy,ds).
 hipError_t launch_debug_candidates(const float* pyr, const uint32_t* mask,

@@ -400,7 +400,25 @@ struct GaussJob {
     int dsw, dsh;
     long long ds_img_stride;
     GaussWaveGrid gg;
+    ZeroJob zero;   // buffers this launch zeroes besides filtering (the extract's first launch)
 };
+
+__device__ __forceinline__ void zero_words(uint32_t* p, size_t n, size_t q) {
+    if (q * 4 + 4 <= n) {
+        *reinterpret_cast<uint4*>(p + q * 4) = make_uint4(0, 0, 0, 0);
+    } else {
+        for (size_t i = q * 4; i < n; i++) p[i] = 0;
+    }
+}
+
+// a ZeroJob over the whole grid (uint4 stores; the buffers are hipMalloc'ed, 16-B aligned)
+__device__ __forceinline__ void zero_job(const ZeroJob& z) {
+    const size_t step = (size_t)gridDim.x * blockDim.x;
+    const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+        for (size_t q = t0; q * 4 < z.n[i]; q += step) zero_words(z.p[i], z.n[i], q);
+}
 
 // LDS geometry of the level filter for width FW (per wave)
 template <int FW>
@@ -667,6 +685,7 @@ __device__ __forceinline__ int gw_order(int bid, int nb) {
 template <int FW, bool U8, bool DS>
 __global__ __launch_bounds__(64 * kGwWaves) void k_gauss_lean(const GaussJob J) {
     using G = LeanGeom<FW>;
+    if (J.zero.n[0] | J.zero.n[1] | J.zero.n[2]) zero_job(J.zero);
     __shared__ __attribute__((aligned(16))) f2v s_in_all[kGwWaves][G::IN_WORDS];
     __shared__ __attribute__((aligned(16))) float s_h_all[kGwWaves][G::RING_WORDS];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -705,14 +724,14 @@ hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
                           long long src_img_stride, float* dst, long long dst_img_stride, int w,
                           int h, const Taps& taps, int batch, float* ds, int dsw, int dsh,
                           long long ds_img_stride, hipStream_t stream, int wave_rows,
-                          bool long_bands) {
+                          bool long_bands, const ZeroJob& zero) {
     const bool vec = (src_stride % 4) == 0 && (src_img_stride % 4) == 0 && (w % 4) == 0 &&
                      w >= 4 && ((uintptr_t)(src8 ? (const void*)src8 : (const void*)src) % 16) == 0;
     if (vec && wave_rows >= 0) {
         const GaussWaveGrid gg = gauss_wave_grid(w, h, batch, wave_rows, 1, long_bands);
         const dim3 wgrid((unsigned)((gg.total_waves + kGwWaves - 1) / kGwWaves));
         const GaussJob J{src, src8, src_stride, src_img_stride, dst, dst_img_stride, w, h, taps,
-                         ds, dsw, dsh, ds_img_stride, gg};
+                         ds, dsw, dsh, ds_img_stride, gg, zero};
 #define SGK_LEAN(U8, DS)                                                                      \
         hipLaunchKernelGGL((k_gauss_lean<FW, U8, DS>), wgrid, dim3(64 * kGwWaves), 0, stream, J)
         if (src8) {
@@ -722,6 +741,11 @@ hipError_t gauss_dispatch(const float* src, const uint8_t* src8, int src_stride,
         }
 #undef SGK_LEAN
         return hipGetLastError();
+    }
+    if (zero.n[0] | zero.n[1] | zero.n[2]) {   // the block kernel does not zero: its own launch
+        const hipError_t ez = launch_zero(zero.p[0], zero.n[0], zero.p[1], zero.n[1], zero.p[2],
+                                          zero.n[2], stream);
+        if (ez != hipSuccess) return ez;
     }
     // bands of at most 17 chunks (544 rows), and at least 1024 workgroups when the image is
     // short (kernel traces: 2 bands of 540 rows beat 1 band of 1080 on 1080p, and 1 band beats 2
@@ -1705,15 +1729,34 @@ __global__ __launch_bounds__(256) void k_color_gray(const uint8_t* __restrict__ 
 
 // ------------------------------------------------------------------------------------------
 // Feature expansion + image coordinates (PyramidCU.cpp:521-606 / 701-751).
+// (io.off != nullptr: the grid's last block writes the readback record instead -- off[0] = the
+// candidate count, off[1 + b] = image b's first feature for b in [0, batch] -- which one more
+// launch after the descriptors wrote before; a single image's extract pays per launch)
 __global__ __launch_bounds__(256) void k_expand(const float4* __restrict__ cand,
                                                 const int2* __restrict__ info,
                                                 const uint32_t* __restrict__ eoff,
                                                 const uint32_t* __restrict__ n_cand_dev,
                                                 const FeatureParams fp, float4* __restrict__ feat,
                                                 int2* __restrict__ feat_info,
-                                                float4* __restrict__ keys, uint32_t cap) {
+                                                float4* __restrict__ keys, uint32_t cap,
+                                                const ImageOffsetsArgs io) {
+    int nblk = (int)gridDim.x;
+    if (io.off) {
+        nblk--;
+        if ((int)blockIdx.x == nblk) {
+            for (int b = threadIdx.x; b <= io.batch + 1; b += 256) {
+                if (b == 0) {
+                    io.off[0] = (int64_t)io.row_base[io.total_rows];
+                } else {
+                    const int r = b - 1 == io.batch ? io.total_rows : (b - 1) * io.rows_per_image;
+                    io.off[b] = (int64_t)eoff[min(io.row_base[r], cap)];
+                }
+            }
+            return;
+        }
+    }
     const uint32_t ncand = min(*n_cand_dev, cap);
-    for (uint32_t f = blockIdx.x * 256 + threadIdx.x; f < ncand; f += gridDim.x * 256) {
+    for (uint32_t f = blockIdx.x * 256 + threadIdx.x; f < ncand; f += (uint32_t)nblk * 256) {
     const uint32_t e0 = eoff[f], n = eoff[f + 1] - e0;
     if (n == 0) continue;
     const float4 c = cand[f];
@@ -2705,14 +2748,6 @@ __global__ __launch_bounds__(256) void k_limit_oriented(uint32_t* __restrict__ o
     }
 }
 
-__global__ void k_image_offsets(const uint32_t* __restrict__ row_base,
-                                const uint32_t* __restrict__ eoff, int batch, int rows_per_image,
-                                int total_rows, uint32_t cap, int64_t* __restrict__ off) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b > batch) return;
-    const int r = b == batch ? total_rows : b * rows_per_image;
-    off[b] = (int64_t)eoff[min(row_base[r], cap)];   // cap: only when the candidates overflowed
-}
 
 __global__ __launch_bounds__(64) void k_debug_candidates(
     const float* __restrict__ pyr, const uint32_t* __restrict__ mask,
@@ -2733,12 +2768,12 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
                         long long src_img_stride, float* dst, long long dst_img_stride, int w,
                         int h, int fw, const Taps& taps, int batch, float* ds_dst, int ds_w,
                         int ds_h, long long ds_img_stride, hipStream_t stream, int wave_rows,
-                        bool long_bands) {
+                        bool long_bands, const ZeroJob& zero) {
 #define SGK_GAUSS(FW)                                                                       \
     case FW:                                                                                  \
         return gauss_dispatch<FW>(src, src_u8, src_stride, src_img_stride, dst, dst_img_stride, \
                                   w, h, taps, batch, ds_dst, ds_w, ds_h, ds_img_stride, stream, \
-                                  wave_rows, long_bands);
+                                  wave_rows, long_bands, zero);
     switch (fw) {
         SGK_GAUSS(5) SGK_GAUSS(7) SGK_GAUSS(9) SGK_GAUSS(11) SGK_GAUSS(13) SGK_GAUSS(15)
         SGK_GAUSS(17) SGK_GAUSS(19) SGK_GAUSS(21) SGK_GAUSS(23) SGK_GAUSS(25) SGK_GAUSS(27)
@@ -2751,13 +2786,13 @@ hipError_t launch_gauss(const float* src, const uint8_t* src_u8, int src_stride,
 hipError_t launch_gauss_op(const LevelOp& op, hipStream_t stream, int wave_rows, bool long_bands) {
     return launch_gauss(op.src, op.src_u8, op.src_stride, op.src_img_stride, op.dst,
                         op.dst_img_stride, op.w, op.h, op.fw, op.taps, op.batch, op.ds_dst,
-                        op.ds_w, op.ds_h, op.ds_img_stride, stream, wave_rows, long_bands);
+                        op.ds_w, op.ds_h, op.ds_img_stride, stream, wave_rows, long_bands, op.zero);
 }
 
 static bool diag_ok(const LevelOp& op) {
     return !op.src_u8 && !op.ds_dst && op.src && (op.src_stride % 4) == 0 &&
            (op.src_img_stride % 4) == 0 && (op.w % 4) == 0 && op.w >= 4 &&
-           ((uintptr_t)op.src % 16) == 0;
+           ((uintptr_t)op.src % 16) == 0 && !(op.zero.n[0] | op.zero.n[1] | op.zero.n[2]);
 }
 
 template <int FWA, int FWB>
@@ -2769,9 +2804,9 @@ static hipError_t gauss_diag_launch(const LevelOp& a, const LevelOp& b, hipStrea
     const int nbB = (gb.total_waves + kGwWaves - 1) / kGwWaves;
     const int nbBp = (nbB + 7) / 8 * 8;   // job A starts on XCD 0 (blocks are dealt round-robin)
     const GaussJob A{a.src, nullptr, a.src_stride, a.src_img_stride, a.dst, a.dst_img_stride, a.w,
-                     a.h, a.taps, nullptr, 0, 0, 0, ga};
+                     a.h, a.taps, nullptr, 0, 0, 0, ga, ZeroJob{}};
     GaussJob B{b.src, nullptr, b.src_stride, b.src_img_stride, b.dst, b.dst_img_stride, b.w,
-               b.h, b.taps, nullptr, 0, 0, 0, gb};
+               b.h, b.taps, nullptr, 0, 0, 0, gb, ZeroJob{}};
     // the padding blocks of job B map to waves past its grid (gauss_lean_wave returns)
     B.gg.total_waves = gb.total_waves;
     hipLaunchKernelGGL((k_gauss_diag<FWA, FWB>), dim3((unsigned)(nbBp + nbA)), dim3(64 * kGwWaves),
@@ -2918,14 +2953,6 @@ size_t scan_tmp_words(size_t n) {
     return words + 16;
 }
 
-__device__ __forceinline__ void zero_words(uint32_t* p, size_t n, size_t q) {
-    if (q * 4 + 4 <= n) {
-        *reinterpret_cast<uint4*>(p + q * 4) = make_uint4(0, 0, 0, 0);
-    } else {
-        for (size_t i = q * 4; i < n; i++) p[i] = 0;
-    }
-}
-
 __global__ __launch_bounds__(256) void k_zero(uint32_t* __restrict__ a, size_t na,
                                               uint32_t* __restrict__ b, size_t nb,
                                               uint32_t* __restrict__ c, size_t nc) {
@@ -2991,11 +3018,14 @@ hipError_t launch_orientation(const float* pyr, const uint32_t* mask, const uint
 
 hipError_t launch_expand(const float4* cand, const int2* info, const uint32_t* eoff,
                          const uint32_t* n_cand_dev, int n_cand_cap, const FeatureParams& fp,
-                         float4* feat, int2* feat_info, float4* keys, hipStream_t stream) {
+                         float4* feat, int2* feat_info, float4* keys, hipStream_t stream,
+                         const ImageOffsetsArgs* io) {
     if (n_cand_cap <= 0) return hipSuccess;
-    const unsigned grid = (unsigned)std::min(((long long)n_cand_cap + 255) / 256, 1024LL);
+    const ImageOffsetsArgs none{};
+    const unsigned grid = (unsigned)std::min(((long long)n_cand_cap + 255) / 256, 1024LL) +
+                          (io && io->off ? 1u : 0u);
     hipLaunchKernelGGL(k_expand, dim3(grid), dim3(256), 0, stream, cand, info, eoff, n_cand_dev,
-                       fp, feat, feat_info, keys, (uint32_t)n_cand_cap);
+                       fp, feat, feat_info, keys, (uint32_t)n_cand_cap, io ? *io : none);
     return hipGetLastError();
 }
 
@@ -3058,14 +3088,6 @@ hipError_t launch_limit_oriented(uint32_t* ocount, const uint32_t* row_base,
     return hipGetLastError();
 }
 
-hipError_t launch_image_offsets(const uint32_t* row_base, const uint32_t* eoff, int batch,
-                                int rows_per_image, int total_rows, int n_cand_cap, int64_t* off,
-                                hipStream_t stream) {
-    hipLaunchKernelGGL(k_image_offsets, dim3((batch + 1 + 255) / 256), dim3(256), 0, stream,
-                       row_base, eoff, batch, rows_per_image, total_rows, (uint32_t)n_cand_cap,
-                       off);
-    return hipGetLastError();
-}
 
 hipError_t launch_debug_candidates(const float* pyr, const uint32_t* mask,
                                    const uint32_t* row_base, int total_rows,

@@ -87,6 +87,10 @@ struct Runtime {
     sgpu_ctx* ctx = nullptr;
     int binary = 0;             // -b
     int verbose = 1;
+    // GlobalUtil::_timingS (GlobalUtil.cpp:51, default 1; SiftGPU::SetVerbose, SiftGPU.cpp:401-429):
+    // when 0 the reference skips its per-stage finish calls; here the extract records no stage
+    // events (sgpu_set_stage_timing), so _timing[2..8] read 0 and the call is ~40 us shorter
+    int timing_s = 1;
     int feature_num = 0;
     HostFloats keys, desc;
     // SetKeypointList (SiftPyramid::SetKeypointList, SiftPyramid.cpp:293-310): applied by the
@@ -347,6 +351,7 @@ void SiftGPU::InitSiftGPU() {
             rt->ctx = nullptr;
             return;
         }
+        sgpu_set_stage_timing(rt->ctx, rt->timing_s);
     }
     _initialized = 1;
 }
@@ -465,7 +470,27 @@ int SiftGPU::VerifyContextGL() {
 
 int SiftGPU::IsFullSupported() { return _initialized ? 1 : 0; }
 
-void SiftGPU::SetVerbose(int verbose) { RT(_pyramid)->verbose = verbose; }
+// SiftGPU::SetVerbose (SiftGPU.cpp:401-429): -1 cycles the levels, -2 silences the output but
+// keeps the stage timing, otherwise output when > 0 and stage timing when > 1
+void SiftGPU::SetVerbose(int verbose) {
+    Runtime* rt = RT(_pyramid);
+    if (verbose == -1) {
+        if (rt->verbose) {
+            rt->verbose = rt->timing_s;
+            rt->timing_s = 0;
+        } else {
+            rt->verbose = 1;
+            rt->timing_s = 1;
+        }
+    } else if (verbose == -2) {
+        rt->verbose = 0;
+        rt->timing_s = 1;
+    } else {
+        rt->verbose = verbose > 0;
+        rt->timing_s = verbose > 1;
+    }
+    if (rt->ctx) sgpu_set_stage_timing(rt->ctx, rt->timing_s);
+}
 
 // SiftGPU::ParseParam (SiftGPU.cpp:801-1246): algorithm options go through sgpu_parse_args;
 // file options (-i, -il, -o, -b) are handled here.
@@ -490,7 +515,10 @@ void SiftGPU::ParseParam(int argc, char** argv) {
         for (char& c : k) c = (char)tolower(c);
         if (k == "h" || k == "help") PrintUsage();
         else if (k == "b") rt->binary = 1;
-        else if (k == "v" && i + 1 < argc) rt->verbose = atoi(argv[i + 1]);
+        else if (k == "v" && i + 1 < argc) {   // SiftGPU.cpp:1207-1210
+            int num = 0;
+            if (sscanf(argv[i + 1], "%d", &num) == 1 && num >= 0 && num <= 4) SetVerbose(num);
+        }
         else if (k == "i" && i + 1 < argc) {
             strncpy(_imgpath, argv[++i], kMaxPath - 1);
             LIST(_list)->push_back(argv[i]);

@@ -32,7 +32,7 @@ C_API = [
     "sgpu_comm_allreduce_f64", "sgpu_extract_keypoints", "sgpu_match_guided", "sgpu_extract_color",
     "sgpu_match_shard_begin", "sgpu_match_shard_end", "sgpu_match_sharded",
     "sgpu_extract_stream", "sgpu_host_alloc", "sgpu_host_free", "sgpu_reserve",
-    "sgpu_debug_alloc_count", "sgpu_last_pyramid_launches",
+    "sgpu_debug_alloc_count", "sgpu_last_pyramid_launches", "sgpu_set_stage_timing",
 ]
 
 _LIB = None
@@ -63,6 +63,7 @@ def lib():
         L.sgpu_debug_alloc_count.argtypes = []
         L.sgpu_debug_alloc_count.restype = c.c_longlong
         L.sgpu_last_pyramid_launches.argtypes = [vp, P(c.c_int)]
+        L.sgpu_set_stage_timing.argtypes = [vp, c.c_int]
         L.sgpu_extract_f32.argtypes = [vp, vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int]
         L.sgpu_feature_count.argtypes = [vp, c.c_int]
         L.sgpu_feature_total.argtypes = [vp]
@@ -210,6 +211,10 @@ class SiftContext:
         if n < 0:
             raise RuntimeError("sgpu_last_pyramid_launches: no extract")
         return int(n), int(f.value)
+
+    def set_stage_timing(self, on: bool):
+        """Per-stage HIP events on/off (sgpu_set_stage_timing; the reference's _timingS)."""
+        self._check(lib().sgpu_set_stage_timing(self._ctx, int(bool(on))), "sgpu_set_stage_timing")
 
     @staticmethod
     def alloc_count() -> int:

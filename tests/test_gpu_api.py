@@ -150,7 +150,9 @@ def test_speed_replica_timing_slots(tmp_path):
     is stable over the runs and equals the oracle's, and the reference's _timing slots
     (SiftGPU.cpp:368, printed by speed.cpp:136-153) are filled: every stage slot is a finite
     non-negative time, the pyramid and descriptor slots are positive, and the slots add up to no
-    more than the wall time per RunSIFT (plus a small allowance for event rounding).  The
+    more than the wall time per RunSIFT of that second (stage-timed, SetVerbose(-2)) loop, plus a
+    small allowance for event rounding.  The first loop runs with the stage timing off
+    (SetVerbose(0) -> _timingS 0, SiftGPU.cpp:426-427), so it is no slower than the second.  The
     relative sizes of the slots are wall-clock properties and go to bench.py's report, not here
     (one C2 run once read 0.53 ms against 0.38-0.41 for its neighbours)."""
     exe = os.path.join(ROOT, "modify-sift-gpu_amd", "bin", "speed_replica")
@@ -169,7 +171,8 @@ def test_speed_replica_timing_slots(tmp_path):
     assert all(np.isfinite(t[s]) and t[s] >= 0 for s in slots), t
     assert t["descriptor"] > 0 and t["build_pyramid"] > 0, t
     total = sum(t[s] for s in slots)
-    assert total <= 1.10 * sp["avg_ms"] + 0.02, (total, sp["avg_ms"], t)
+    assert total <= 1.10 * sp["timed_avg_ms"] + 0.02, (total, sp["timed_avg_ms"], t)
+    assert sp["avg_ms"] <= 1.10 * sp["timed_avg_ms"] + 0.02, sp
 
 
 def test_allocate_pyramid_then_runsift_allocates_nothing(tmp_path):
