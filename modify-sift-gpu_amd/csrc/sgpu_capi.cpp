@@ -31,12 +31,16 @@ namespace {
 // paired-level Gaussian launches in the shipped schedule (1), or only when asked for by
 // SGPU_DUO=on / the debug flags (0)
 #ifndef SGK_DUO_DEFAULT
-#define SGK_DUO_DEFAULT 0
+#define SGK_DUO_DEFAULT 1
 #endif
 // paired-level Gaussian launches only for levels of at least this many MB (smaller ones stay in
 // the Infinity Cache between launches and are latency-bound: one level per launch, 1-chunk bands)
 #ifndef SGK_DUO_MIN_MB
 #define SGK_DUO_MIN_MB 128
+#endif
+// paired levels only when the two filter widths sum to at most this (24: the (11, 13) pair)
+#ifndef SGK_DUO_MAX_FW_SUM
+#define SGK_DUO_MAX_FW_SUM 24
 #endif
 
 // device and pinned-host allocations made by the library (sgpu_debug_alloc_count): a test hook
@@ -135,6 +139,8 @@ struct sgpu_ctx {
     int debug_flags = 0;                   // SGPU_DEBUG_* test hooks
     bool multi_stream = false;             // SGPU_STREAMS=multi: octave and feature streams
     bool duo_on = false;                   // SGPU_DUO=on: paired-level launches (size rule)
+    bool duo_wide = false;                 // SGPU_DUO_WIDE=1: also the (21, 25) pairs
+    bool duo_u8 = false;                   // SGPU_DUO_U8=1: the u8 ingest pair (13, 11)
     // per-stage HIP events of an extract (sgpu_last_timing's stage slots).  Each event record
     // costs ~4.5 us of GPU time between the commands around it (tests/microbench/event_gap.hip),
     // ~40 us per single-image extract; sgpu_set_stage_timing(ctx, 0) drops them where they only
@@ -397,6 +403,12 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
         if (!strcmp(ev, "off")) ctx->debug_flags |= SGPU_DEBUG_DUO_OFF;
         if (!strcmp(ev, "always")) ctx->debug_flags |= SGPU_DEBUG_DUO_ALWAYS;
         if (!strcmp(ev, "on")) ctx->duo_on = true;
+    }
+    if (const char* ev = getenv("SGPU_DUO_WIDE")) {
+        if (ev[0] == '1') ctx->duo_wide = true;
+    }
+    if (const char* ev = getenv("SGPU_DUO_U8")) {
+        if (ev[0] == '1') ctx->duo_u8 = true;
     }
     if (const char* ev = getenv("SGPU_GAUSS_BANDS"))
         if (!strcmp(ev, "long")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_LONG_BANDS;
@@ -688,6 +700,12 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
                 if (duo_second[i] || a.o != b.o || b.k != a.k + 1) continue;
                 const long long bytes = 4ll * a.op.w * a.op.h * a.op.batch;
                 if (!duo_all && bytes < ((long long)SGK_DUO_MIN_MB << 20)) continue;
+                // the (21, 25) pair's arithmetic outweighs the byte saving (1,016 us against
+                // ~960 for two single-level launches, 128 x 1080p): narrow pairs only
+                if (!duo_all && !ctx->duo_wide && a.op.fw + b.op.fw > SGK_DUO_MAX_FW_SUM) continue;
+                // the u8 ingest pair (levels 0, 1: 725 us) displaces the (11, 13) pair of levels
+                // 1, 2 (750 us, level 0 alone 390): opt-in
+                if (!duo_all && !ctx->duo_u8 && a.op.src_u8) continue;
                 if (!sgk::gauss_duo_supported(a.op, b.op)) continue;
                 duo_next[i] = (int)(i + 1);
                 duo_second[i + 1] = 1;

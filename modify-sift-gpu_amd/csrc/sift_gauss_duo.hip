@@ -91,24 +91,42 @@ __device__ __forceinline__ int duo_block(int bid, int nb) {
 #define SGK_DUO_INTERLEAVE 1
 #endif
 constexpr bool kDuoInterleave = SGK_DUO_INTERLEAVE != 0;
+// timing experiments only (wrong levels, tests/diag): 1 = DMA lanes row-contiguous (lanes 0-31 row
+// 2p, 32-63 row 2p+1), 2 = no H / V arithmetic (one LDS read per pass), 0 = the kernel
+#ifndef SGK_DUO_EXP
+#define SGK_DUO_EXP 0
+#endif
 constexpr int kDuoWaves = 4;      // waves per workgroup (each wave works alone: no barriers)
 constexpr int kMidSlot = 256;     // floats of one mid row pair: 128 columns x (row, row + 1)
 
+// 32: strips of 96 columns for both compiled pairs; 128 x 1080p, (11, 13): 784 us against 905 for
+// the unaligned 116-column strips (tests/diag/r05e.sh; 16, 64-B lines: 820)
+#ifndef SGK_DUO_SWALIGN
+#define SGK_DUO_SWALIGN 32
+#endif
 template <int FWA, int FWB>
 struct DuoGeom {
     static constexpr int RA = FWA / 2, RB = FWB / 2;
-    static_assert(RB % 2 == 0, "stage B's H2 reads start on a 16-B boundary (RB even)");
-    static constexpr int SW = 128 - 2 * RB;           // output columns of a wave
+    // mid column of lane 0 = x0 - MOFF: even (stage A's pairs of mid columns are 8-B aligned in
+    // LDS and in the level k + 1 rows); stage B's H2 reads start OB = MOFF - RB float2 past its
+    // lane's pair
+    static constexpr int MOFF = RB + (RB & 1), OB = MOFF - RB;
+    // output columns of a wave: 128 - 2 MOFF, rounded down to SGK_DUO_SWALIGN columns so that
+    // the strips' rows start on 128-B lines (a strip boundary inside a line leaves two waves
+    // writing parts of it)
+    static constexpr int SW = (128 - 2 * MOFF) / SGK_DUO_SWALIGN * SGK_DUO_SWALIGN;
     static constexpr int IN_W = 128 + 2 * RA;         // input columns of stage A
     static constexpr int NDMA = (IN_W + 31) / 32;     // dword DMAs per row pair (32 columns each)
     static constexpr int IN_SLOT = NDMA * 64;         // floats of one input row pair
     static constexpr int PMAX = FWA > FWB ? FWA : FWB;
     static constexpr int P = (PMAX + 1) & ~1;         // accumulator ring period (rows), even
     static constexpr int U = P / 2;                   // steps per unrolled iteration
+    static constexpr int NQ = IN_W / 4;               // u8 input: dword quads per row
 };
 
 struct DuoJob {
-    const float* src;            // level k
+    const float* src;            // level k (f32), or
+    const uint8_t* src8;         // the u8 image (level k = the ingest level's input)
     int src_stride;
     long long src_img;
     float* dst1;                 // level k + 1
@@ -119,7 +137,34 @@ struct DuoJob {
     int strips, nsy, rows_per_band, total_waves;
     float* trash;                // 2,560 B per wave slot (1024 slots): stores of rows outside
                                  // the band and the DMA prologue's count-keeping stores
+    ZeroJob zero;                // buffers this launch zeroes (the extract's first launch)
 };
+
+// a ZeroJob over the whole grid (uint4 stores; the buffers are hipMalloc'ed, 16-B aligned), as
+// k_gauss_lean's
+__device__ __forceinline__ void duo_zero(const ZeroJob& z) {
+    const size_t step = (size_t)gridDim.x * blockDim.x;
+    const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+        for (size_t q = t0; q * 4 < z.n[i]; q += step) {
+            if (q * 4 + 4 <= z.n[i]) {
+                *reinterpret_cast<uint4*>(z.p[i] + q * 4) = make_uint4(0, 0, 0, 0);
+            } else {
+                for (size_t j = q * 4; j < z.n[i]; j++) z.p[i][j] = 0;
+            }
+        }
+}
+
+// p / 255 correctly rounded on a pair (u8_to_unit of sift_kernels.hip, packed: the same three
+// IEEE operations per element)
+__device__ __forceinline__ f2v u8_pair_to_unit(uint32_t a, uint32_t b) {
+    const float c = 1.0f / 255.0f;
+    const f2v x{(float)a, (float)b};
+    const f2v q = x * f2v{c, c};
+    const f2v r = __builtin_elementwise_fma(-q, f2v{255.0f, 255.0f}, x);
+    return __builtin_elementwise_fma(r, f2v{c, c}, q);
+}
 
 // s_waitcnt with vmcnt = n (0 .. 63), expcnt and lgkmcnt not waited for
 template <int N>
@@ -131,11 +176,13 @@ __device__ __forceinline__ void wait_lgkm0() {
     __builtin_amdgcn_s_waitcnt((15) | (3 << 14) | (7 << 4) | (0 << 8));   // lgkmcnt(0) only
 }
 
-template <int FWA, int FWB, int NIN>
+template <int FWA, int FWB, int NIN, bool U8>
 __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, float* s_mid) {
     using G = DuoGeom<FWA, FWB>;
     constexpr int RA = G::RA, RB = G::RB, SW = G::SW, NDMA = G::NDMA, IN_SLOT = G::IN_SLOT;
-    constexpr int P = G::P, U = G::U;
+    constexpr int P = G::P, U = G::U, MOFF = G::MOFF, OB = G::OB, NQ = G::NQ;
+    static_assert(!U8 || ((MOFF + RA) % 4 == 0 && G::IN_W % 4 == 0 && NQ <= 64),
+                  "u8 input: the strip's input quads are 4-column aligned");
     constexpr int OPS = NDMA + 4;   // VMEM instructions per step: the DMAs, 2 + 2 stores
     static_assert(NIN >= 2 && OPS * (NIN - 1) < 64, "DMA ring (vmcnt field)");
     const int lane = threadIdx.x & 63;
@@ -144,9 +191,10 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
     const int sy = rest % J.nsy, b = rest / J.nsy;
     const int x0 = sx * SW;
     const int yb = sy * J.rows_per_band, ye = min(H, yb + J.rows_per_band);
-    const int m0 = x0 - RB;        // mid column of lane 0's first column
+    const int m0 = x0 - MOFF;      // mid column of lane 0's first column (even)
     const int a0 = m0 - RA;        // input column of the input slot's float2 0
-    const float* src = J.src + (long long)b * J.src_img;
+    const float* src = U8 ? nullptr : J.src + (long long)b * J.src_img;
+    const uint8_t* src8 = U8 ? J.src8 + (long long)b * J.src_img : nullptr;
     float* d1 = J.dst1 + (long long)b * J.dst_img;
     float* d2 = J.dst2 + (long long)b * J.dst_img;
     float* trash = J.trash + (size_t)(gw & 1023) * 640;   // 5 x 512 B per wave slot
@@ -155,8 +203,9 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
     // row i & 1 of the pair; LDS float 64 q + i of the slot = float2 index 32 q + i / 2
     uint32_t coff[NDMA];
 #pragma unroll
-    for (int q = 0; q < NDMA; q++) coff[q] = 4u * (uint32_t)clampd(a0 + 32 * q + (lane >> 1), 0, W - 1);
-    const uint32_t rsel = (lane & 1) ? 4u * (uint32_t)J.src_stride : 0u;
+    for (int q = 0; q < NDMA; q++)
+        coff[q] = 4u * (uint32_t)clampd(a0 + 32 * q + (SGK_DUO_EXP == 1 ? (lane & 31) : (lane >> 1)), 0, W - 1);
+    const uint32_t rsel = ((SGK_DUO_EXP == 1 ? lane >> 5 : lane) & 1) ? 4u * (uint32_t)J.src_stride : 0u;
     // The DMAs are inline asm, not __builtin_amdgcn_global_load_lds: the compiler's wait
     // insertion treats every later LDS read as possibly aliasing a pending LDS-DMA and puts an
     // s_waitcnt vmcnt(0) before it (seen in the ISA), which would drain the whole DMA ring every
@@ -186,6 +235,34 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
             : [l] "s"(lds), [b] "s"(base), [o0] "v"(coff[0] + ro), [o1] "v"(coff[1] + ro),
               [o2] "v"(coff[2] + ro), [o3] "v"(coff[3] + ro), [o4] "v"(coff[4] + ro)
             : "memory", "m0", "scc");
+    };
+    // u8 input (stage A of the ingest pair): lane j < NQ loads quad j (columns a0 + 4 j ..
+    // + 3, whole quads: W % 4 == 0 and a0 % 4 == 0) of both rows of a pair into registers; the
+    // conversion to f32 writes them into the input slot in the DMA's layout (float2 index =
+    // column - a0, (row 2p, row 2p + 1)).  A quad left of column 0 repeats column 0, right of
+    // W - 1 column W - 1 (clamp-to-edge, as k_gauss_lean's loaders).
+    const int qcol = a0 + 4 * (lane < NQ ? lane : NQ - 1);
+    const uint32_t qoff = (uint32_t)clampd(qcol, 0, W - 4);
+    const bool qleft = qcol < 0, qright = qcol > W - 4;
+    auto fetch8 = [&](int rho, uint32_t (&r)[2]) __attribute__((always_inline)) {
+        const int r0 = clampd(rho, 0, H - 1), r1 = clampd(rho + 1, 0, H - 1);
+        r[0] = *reinterpret_cast<const uint32_t*>(src8 + (size_t)r0 * J.src_stride + qoff);
+        r[1] = *reinterpret_cast<const uint32_t*>(src8 + (size_t)r1 * J.src_stride + qoff);
+    };
+    auto stage8 = [&](const uint32_t (&r)[2], float* slot) __attribute__((always_inline)) {
+        f2v pr[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) pr[t] = u8_pair_to_unit((r[0] >> (8 * t)) & 255u, (r[1] >> (8 * t)) & 255u);
+        if (qleft || qright) {
+            const f2v e0 = pr[0], e3 = pr[3];
+#pragma unroll
+            for (int t = 0; t < 4; t++) pr[t] = qleft ? e0 : e3;
+        }
+        if (lane < NQ) {
+            float4* q = reinterpret_cast<float4*>(slot) + 2 * lane;
+            q[0] = make_float4(pr[0].x, pr[0].y, pr[1].x, pr[1].y);
+            q[1] = make_float4(pr[2].x, pr[2].y, pr[3].x, pr[3].y);
+        }
     };
 
     // ---- lane roles
@@ -221,6 +298,12 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
         o0 = f2v{0.f, 0.f};
         o1 = f2v{0.f, 0.f};
         const float4* p = reinterpret_cast<const float4*>(slot) + lane;
+        if constexpr (SGK_DUO_EXP == 2) {
+            const float4 v = p[0];
+            o0 = f2v{v.x, v.y};
+            o1 = f2v{v.z, v.w};
+            return;
+        }
 #pragma unroll
         for (int q = 0; q <= RA; q++) {
             const float4 v = p[q];
@@ -233,20 +316,41 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
             }
         }
     };
+    // H2 of a mid slot: output columns e, e + 1 from mid float2 2 le + OB + m, m = 0 .. FWB
     auto h2 = [&](const float* slot, f2v& o0, f2v& o1) __attribute__((always_inline)) {
         o0 = f2v{0.f, 0.f};
         o1 = f2v{0.f, 0.f};
-        const float4* p = reinterpret_cast<const float4*>(slot) + le;
+        if constexpr (SGK_DUO_EXP == 2) {
+            const float4 v = reinterpret_cast<const float4*>(slot)[le];
+            o0 = f2v{v.x, v.y};
+            o1 = f2v{v.z, v.w};
+            return;
+        }
+        f2v ev[FWB + 2];
+        if constexpr (OB == 0) {
+            const float4* p = reinterpret_cast<const float4*>(slot) + le;
 #pragma unroll
-        for (int q = 0; q <= RB; q++) {
-            const float4 v = p[q];
-            const f2v ev[2] = {f2v{v.x, v.y}, f2v{v.z, v.w}};
-#pragma unroll
-            for (int u = 0; u < 2; u++) {
-                const int m = 2 * q + u;
-                if (m < FWB) o0 = pkf(ev[u], tapb(m), o0);
-                if (m >= 1 && m <= FWB) o1 = pkf(ev[u], tapb(m - 1), o1);
+            for (int q = 0; 2 * q <= FWB; q++) {
+                const float4 v = p[q];
+                ev[2 * q] = f2v{v.x, v.y};
+                ev[2 * q + 1] = f2v{v.z, v.w};
             }
+        } else {   // one float2, then 16-B aligned float4s, then a last float2 when needed
+            const f2v* p2 = reinterpret_cast<const f2v*>(slot) + 2 * le + 1;
+            const float4* p4 = reinterpret_cast<const float4*>(slot) + le + 1;
+            ev[0] = p2[0];
+#pragma unroll
+            for (int q = 0; 2 * q + 2 <= FWB; q++) {
+                const float4 v = p4[q];
+                ev[2 * q + 1] = f2v{v.x, v.y};
+                ev[2 * q + 2] = f2v{v.z, v.w};
+            }
+            if constexpr ((FWB & 1) == 1) ev[FWB] = p2[FWB];
+        }
+#pragma unroll
+        for (int m = 0; m <= FWB; m++) {
+            if (m < FWB) o0 = pkf(ev[m], tapb(m), o0);
+            if (m >= 1) o1 = pkf(ev[m], tapb(m - 1), o1);
         }
     };
     // mid slots: 0, 1 alternate (stage A writes step t's pair into slot t & 1, stage B reads the
@@ -271,8 +375,14 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
         f2v mz{0.f, 0.f};
 #pragma unroll 1
         for (int p = 0; 2 * p <= RA; p++) {
-            dma(2 * p, s_in);
-            wait_vm<0>();
+            if constexpr (U8) {
+                uint32_t r[2];
+                fetch8(2 * p, r);
+                stage8(r, s_in);
+            } else {
+                dma(2 * p, s_in);
+                wait_vm<0>();
+            }
             asm volatile("" ::: "memory");
             f2v o0, o1;
             h1(s_in, o0, o1);
@@ -307,12 +417,19 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
     // the first NIN - 1 steps' DMAs, each followed by 4 scratch stores in place of the stores of
     // the step that issues it, so that the wait below counts the same instructions from step 0
     // (distinct 512-B blocks: the compiler neither drops nor merges them)
+    // (u8: the first U steps' quads into registers; the compiler's own waits cover them)
+    uint32_t rg[U8 ? U : 1][2];
+    if constexpr (U8) {
 #pragma unroll
-    for (int k = 0; k < NIN - 1; k++) {
-        dma(rho0 + 2 * k, s_in + k * IN_SLOT);
+        for (int k = 0; k < U; k++) fetch8(rho0 + 2 * k, rg[k]);
+    } else {
 #pragma unroll
-        for (int j = 0; j < 4; j++)
-            *reinterpret_cast<f2v*>(trash + 128 * (j + 1) + 2 * lane) = f2v{0.f, 0.f};
+        for (int k = 0; k < NIN - 1; k++) {
+            dma(rho0 + 2 * k, s_in + k * IN_SLOT);
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                *reinterpret_cast<f2v*>(trash + 128 * (j + 1) + 2 * lane) = f2v{0.f, 0.f};
+        }
     }
     asm volatile("" ::: "memory");
     // stores: uniform row pointers (the level's image base + row * W, updated per step) plus a
@@ -327,6 +444,7 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
     char* const bB = reinterpret_cast<char*>(d2);
     char* const bT = reinterpret_cast<char*>(trash);
     int slot_use = 0;                 // input slot of step t (t mod NIN)
+    int mid_cur = 0;                  // mid slot of step t's stage A (t & 1; U may be odd)
     int slot_dma = NIN - 1;           // input slot of step t + NIN - 1
     for (int it = 0; it < niter; it++) {
         unroll_seq(std::make_integer_sequence<int, U>{}, [&](auto KI) __attribute__((always_inline)) {
@@ -336,32 +454,39 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
             const int mc = rho - RA;          // stage A's completed pair
             const int mu = mc - 2;            // stage B's pair
             asm volatile("" ::: "memory");
-            dma(rho + 2 * (NIN - 1), s_in + slot_dma * IN_SLOT);
-            slot_dma = slot_dma == NIN - 1 ? 0 : slot_dma + 1;
-            // every older VMEM instruction but the OPS (NIN - 1) youngest -- this step's DMA, the
-            // previous NIN - 2 steps' DMAs and stores, and the stores of the step that issued
-            // step t's DMA -- has completed: step t's DMA has landed
-            wait_vm<OPS * (NIN - 1)>();
+            if constexpr (U8) {
+                // step t's quads (loaded U steps ago) into the one input slot, then step t + U's
+                // loads into the same registers
+                stage8(rg[k], s_in);
+                fetch8(rho + 2 * U, rg[k]);
+            } else {
+                dma(rho + 2 * (NIN - 1), s_in + slot_dma * IN_SLOT);
+                slot_dma = slot_dma == NIN - 1 ? 0 : slot_dma + 1;
+                // every older VMEM instruction but the OPS (NIN - 1) youngest -- this step's DMA,
+                // the previous NIN - 2 steps' DMAs and stores, and the stores of the step that
+                // issued step t's DMA -- has completed: step t's DMA has landed
+                wait_vm<OPS * (NIN - 1)>();
+            }
             asm volatile("" ::: "memory");
             // both H passes: stage A on the input slot, stage B on the previous step's mid pair
             // (an offset from one base: a select between the slot pointers made the compiler
             // lose their LDS address space -- flat accesses through the lambdas' closure)
             const int mb_off = mu <= -1 ? 2 * kMidSlot : (mu >= H - 1 ? 3 * kMidSlot
-                                                                      : ((k + 1) & 1) * kMidSlot);
+                                                                      : (mid_cur ^ 1) * kMidSlot);
             const float* mb = s_mid + mb_off;
             f2v o0, o1, q0, q1;
-            h1(s_in + slot_use * IN_SLOT, o0, o1);
+            h1(s_in + (U8 ? 0 : slot_use * IN_SLOT), o0, o1);
             slot_use = slot_use == NIN - 1 ? 0 : slot_use + 1;
             // V1 push of rows rho (ring row 2k) and rho + 1 (2k + 1)
             const f2v r0{o0.x, o1.x}, r1{o0.y, o1.y};
 #pragma unroll
-            for (int i = 0; i < FWA; i++) {
+            for (int i = 0; i < (SGK_DUO_EXP == 2 ? 1 : FWA); i++) {
                 const int s = ((2 * k - i) % P + P) % P;
                 accA[s] = pkf(r0, tapa(i), i == 0 ? f2v{0.f, 0.f} : accA[s]);
             }
             f2v A0 = accA[((2 * k - (FWA - 1)) % P + P) % P];
 #pragma unroll
-            for (int i = 0; i < FWA; i++) {
+            for (int i = 0; i < (SGK_DUO_EXP == 2 ? 1 : FWA); i++) {
                 const int s = ((2 * k + 1 - i) % P + P) % P;
                 accA[s] = pkf(r1, tapa(i), i == 0 ? f2v{0.f, 0.f} : accA[s]);
             }
@@ -371,24 +496,25 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
             // V2 push of mid rows mu (ring row 2k) and mu + 1
             const f2v g0{q0.x, q1.x}, g1{q0.y, q1.y};
 #pragma unroll
-            for (int i = 0; i < FWB; i++) {
+            for (int i = 0; i < (SGK_DUO_EXP == 2 ? 1 : FWB); i++) {
                 const int s = ((2 * k - i) % P + P) % P;
                 accB[s] = pkf(g0, tapb(i), i == 0 ? f2v{0.f, 0.f} : accB[s]);
             }
             const f2v B0 = accB[((2 * k - (FWB - 1)) % P + P) % P];
 #pragma unroll
-            for (int i = 0; i < FWB; i++) {
+            for (int i = 0; i < (SGK_DUO_EXP == 2 ? 1 : FWB); i++) {
                 const int s = ((2 * k + 1 - i) % P + P) % P;
                 accB[s] = pkf(g1, tapb(i), i == 0 ? f2v{0.f, 0.f} : accB[s]);
             }
             const f2v B1 = accB[((2 * k + 1 - (FWB - 1)) % P + P) % P];
-            // stage A's pair into mid slot k & 1 (and the bottom pair): edge columns clamped
+            // stage A's pair into mid slot t & 1 (and the bottom pair): edge columns clamped
             if (mc == H - 1) A1 = A0;   // odd H: the pair (H-1, H) is (H-1, H-1)
             if (left || right) {
                 fix_edges(A0);
                 fix_edges(A1);
             }
-            put_mid(s_mid + (k & 1) * kMidSlot, A0, A1);
+            put_mid(s_mid + mid_cur * kMidSlot, A0, A1);
+            mid_cur ^= 1;
             if (mc <= H - 1 && mc + 1 >= H - 1) {
                 const f2v Bv = mc == H - 1 ? A0 : A1;
                 put_mid(mid_bot, Bv, Bv);
@@ -398,8 +524,9 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
             // own columns; rows outside the band into the scratch block
             {
                 const int y = mu - RB;
-                const bool a0ok = mc >= yb && mc < ye, a1ok = mc >= yb && mc + 1 < ye;
-                const bool b0ok = y >= yb && y < ye, b1ok = y >= yb && y + 1 < ye;
+                // (mc is odd for an odd RA + RB, as in the u8 pair: each row of a pair is tested)
+                const bool a0ok = mc >= yb && mc < ye, a1ok = mc + 1 >= yb && mc + 1 < ye;
+                const bool b0ok = y >= yb && y < ye, b1ok = y + 1 >= yb && y + 1 < ye;
                 if (own1) {
                     *reinterpret_cast<f2v*>((a0ok ? bA : bT) + (a0ok ? rowA + voffA : vtr)) = A0;
                     *reinterpret_cast<f2v*>((a1ok ? bA : bT) + (a1ok ? rowA + W4 + voffA : vtr)) = A1;
@@ -426,15 +553,17 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
 #ifndef SGK_DUO_WPE_NARROW
 #define SGK_DUO_WPE_NARROW 4
 #endif
-template <int FWA, int FWB, int NIN>
+template <int FWA, int FWB, int NIN, bool U8>
 __global__ __launch_bounds__(64 * kDuoWaves) __attribute__((amdgpu_waves_per_eu(FWA + FWB > 30 ? SGK_DUO_WPE_WIDE : SGK_DUO_WPE_NARROW))) void k_gauss_duo(const DuoJob J) {
     using G = DuoGeom<FWA, FWB>;
-    __shared__ __attribute__((aligned(16))) float s_in_all[kDuoWaves][NIN * G::IN_SLOT];
+    // u8 input: one input slot (the registers hold the prefetched rows)
+    __shared__ __attribute__((aligned(16))) float s_in_all[kDuoWaves][(U8 ? 1 : NIN) * G::IN_SLOT];
     __shared__ __attribute__((aligned(16))) float s_mid_all[kDuoWaves][4 * kMidSlot];
+    if (J.zero.n[0] | J.zero.n[1] | J.zero.n[2]) duo_zero(J.zero);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int gw = duo_block(blockIdx.x, gridDim.x) * kDuoWaves + wave;
     if (gw >= J.total_waves) return;   // uniform per wave
-    duo_wave<FWA, FWB, NIN>(J, gw, s_in_all[wave], s_mid_all[wave]);
+    duo_wave<FWA, FWB, NIN, U8>(J, gw, s_in_all[wave], s_mid_all[wave]);
 }
 
 // input row pairs in LDS: the DMA runs NIN - 1 steps ahead (compiled: 5 and 7; SGPU_DUO_NIN
@@ -456,13 +585,28 @@ static int duo_bands_env() {
     }();
     return v;
 }
+// waves a launch aims for (bands of one image added until the grid has as many): a duo wave is
+// latency-bound, so the grid wants more than the 12 resident waves per CU; 128 x 1080p, (11, 13)
+// at octave 0: 750 / 780 / 765 / 797 us for 4,096 / 6,144 / 8,192 / 12,288 (tests/diag/r05f.sh)
+#ifndef SGK_DUO_WAVES
+#define SGK_DUO_WAVES 4096
+#endif
+static long long duo_waves_target() {
+    static const long long v = [] {
+        const char* e = getenv("SGPU_DUO_WAVES");
+        return e && atoll(e) > 0 ? atoll(e) : (long long)SGK_DUO_WAVES;
+    }();
+    return v;
+}
 
-template <int FWA, int FWB>
+template <int FWA, int FWB, bool U8>
 hipError_t duo_launch(const LevelOp& a, const LevelOp& b, hipStream_t stream, int rows_hint,
                       float* trash) {
     using G = DuoGeom<FWA, FWB>;
     DuoJob J{};
     J.src = a.src;
+    J.src8 = a.src_u8;
+    J.zero = a.zero;
     J.src_stride = a.src_stride;
     J.src_img = a.src_img_stride;
     J.dst1 = a.dst;
@@ -474,15 +618,16 @@ hipError_t duo_launch(const LevelOp& a, const LevelOp& b, hipStream_t stream, in
     J.tb = b.taps;
     J.strips = (a.w + G::SW - 1) / G::SW;
     const long long per_band = (long long)J.strips * a.batch;
-    // bands: the whole height while the grid has >= ~2048 waves (8 per CU); each band re-walks
+    // bands: as many as the grid needs for duo_waves_target() waves; each band re-walks
     // 2 (RA + RB) halo rows, so bands stay >= 64 rows
     int nsy = 1;
+    const long long want = duo_waves_target();
     if (rows_hint > 0) {
         nsy = (a.h + rows_hint - 1) / rows_hint;
     } else if (duo_bands_env() > 0) {
         nsy = std::min(duo_bands_env(), std::max(1, a.h / 64));
-    } else if (per_band < 2048) {
-        nsy = (int)std::min<long long>((2048 + per_band - 1) / per_band, std::max(1, a.h / 64));
+    } else if (per_band < want) {
+        nsy = (int)std::min<long long>((want + per_band - 1) / per_band, std::max(1, a.h / 64));
     }
     int rows = (a.h + nsy - 1) / nsy;
     rows = (rows + 7) / 8 * 8;
@@ -491,30 +636,40 @@ hipError_t duo_launch(const LevelOp& a, const LevelOp& b, hipStream_t stream, in
     J.total_waves = (int)(per_band * J.nsy);
     J.trash = trash;
     const unsigned nb = (unsigned)((J.total_waves + kDuoWaves - 1) / kDuoWaves);
-    if (duo_nin() == 5)
-        hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 5>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
+    if constexpr (U8)
+        hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 2, true>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
+    else if (duo_nin() == 5)
+        hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 5, false>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
     else
-        hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 7>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
+        hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 7, false>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
     return hipGetLastError();
 }
 
 }  // namespace
 
 bool gauss_duo_supported(const LevelOp& a, const LevelOp& b) {
-    const bool pair = (a.fw == 11 && b.fw == 13) || (a.fw == 21 && b.fw == 25);
-    const bool zeroes = (a.zero.n[0] | a.zero.n[1] | a.zero.n[2] | b.zero.n[0] | b.zero.n[1] |
-                         b.zero.n[2]) != 0;
-    return pair && !zeroes && a.src && !a.src_u8 && !a.ds_dst && !b.ds_dst && b.src == a.dst &&
-           !b.src_u8 && a.w == b.w && a.h == b.h && a.batch == b.batch && a.w >= 8 && a.h >= 8 &&
-           (a.w % 4) == 0 && b.src_stride == a.w && a.dst_img_stride == b.dst_img_stride &&
-           b.src_img_stride == a.dst_img_stride && a.dst_img_stride >= (long long)a.w * a.h;
+    // f32 pairs (11, 13), (21, 25); the u8 ingest pair (13, 11) (level 0 from the image, level 1)
+    const bool u8 = a.src_u8 != nullptr;
+    const bool pair = u8 ? (a.fw == 13 && b.fw == 11)
+                         : ((a.fw == 11 && b.fw == 13) || (a.fw == 21 && b.fw == 25));
+    const bool src_ok = u8 ? (!a.src && (a.src_stride % 4) == 0 && (a.src_img_stride % 4) == 0 &&
+                              ((uintptr_t)a.src_u8 % 4) == 0)
+                           : (a.src && a.src_stride >= a.w);
+    const bool b_zeroes = (b.zero.n[0] | b.zero.n[1] | b.zero.n[2]) != 0;
+    const bool a_zeroes = (a.zero.n[0] | a.zero.n[1] | a.zero.n[2]) != 0;
+    return pair && src_ok && !b_zeroes && (u8 || !a_zeroes) && !a.ds_dst && !b.ds_dst &&
+           b.src == a.dst && !b.src_u8 && a.w == b.w && a.h == b.h && a.batch == b.batch &&
+           a.w >= 8 && a.h >= 8 && (a.w % 4) == 0 && b.src_stride == a.w &&
+           a.dst_img_stride == b.dst_img_stride && b.src_img_stride == a.dst_img_stride &&
+           a.dst_img_stride >= (long long)a.w * a.h;
 }
 
 hipError_t launch_gauss_duo(const LevelOp& a, const LevelOp& b, hipStream_t stream, int rows_hint,
                             float* trash) {
     if (!trash || !gauss_duo_supported(a, b)) return hipErrorInvalidValue;
+    if (a.src_u8) return duo_launch<13, 11, true>(a, b, stream, rows_hint, trash);
 #define SGK_DUO(A, B) \
-    if (a.fw == A && b.fw == B) return duo_launch<A, B>(a, b, stream, rows_hint, trash);
+    if (a.fw == A && b.fw == B) return duo_launch<A, B, false>(a, b, stream, rows_hint, trash);
     SGK_DUO(11, 13) SGK_DUO(21, 25)
 #undef SGK_DUO
     return hipErrorInvalidValue;

@@ -66,8 +66,8 @@ def main():
     trace = _one(os.path.join(src, "trace", "**", "*kernel_trace.csv"))
     stats = _one(os.path.join(src, "trace", "**", "*kernel_stats.csv"))
     rows = list(csv.DictReader(open(trace)))
-    # one k_image_offsets launch per extract (per batch part: the bench runs one part)
-    n_steps = sum(1 for r in rows if "k_image_offsets" in r["Kernel_Name"])
+    # one k_expand launch per extract (per batch part: the bench runs one part)
+    n_steps = sum(1 for r in rows if "k_expand" in r["Kernel_Name"])
     per_family = defaultdict(lambda: [0.0, 0])
     for r in rows:
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6   # ms
@@ -101,7 +101,7 @@ def main():
             fr, fw = factors(r["Kernel_Name"], cal)
             acc[family(r["Kernel_Name"])] += b
             cor[family(r["Kernel_Name"])] += b * (fr if kind == "fetch" else fw)
-            if "k_image_offsets" in r["Kernel_Name"]:
+            if "k_expand" in r["Kernel_Name"]:
                 calls += 1
         out[f"{kind}_bytes_per_extract"] = {f: v / max(calls, 1) for f, v in acc.items()}
         for f, v in cor.items():
