@@ -38,9 +38,12 @@ namespace {
 #ifndef SGK_DUO_MIN_MB
 #define SGK_DUO_MIN_MB 128
 #endif
-// paired levels only when the two filter widths sum to at most this (24: the (11, 13) pair)
-#ifndef SGK_DUO_MAX_FW_SUM
-#define SGK_DUO_MAX_FW_SUM 24
+// paired levels: (11, 13) from SGK_DUO_MIN_MB; (17, 21) with the decimation, whose arithmetic
+// makes it latency-bound on smaller levels, from SGK_DUO_WIDE_MIN_MB (128 x 1080p: octave 0
+// 903 us against 1,052 for two launches; octave 1 309 against ~270, tests/diag/r05i.sh); (21, 25)
+// only by SGPU_DUO_WIDE=1 (1,016 us against ~1,050, and it would take level 4 from (17, 21))
+#ifndef SGK_DUO_WIDE_MIN_MB
+#define SGK_DUO_WIDE_MIN_MB 512
 #endif
 
 // device and pinned-host allocations made by the library (sgpu_debug_alloc_count): a test hook
@@ -141,6 +144,7 @@ struct sgpu_ctx {
     bool duo_on = false;                   // SGPU_DUO=on: paired-level launches (size rule)
     bool duo_wide = false;                 // SGPU_DUO_WIDE=1: also the (21, 25) pairs
     bool duo_u8 = false;                   // SGPU_DUO_U8=1: the u8 ingest pair (13, 11)
+    int env_flags = 0;                     // debug flags set from the environment at creation
     // per-stage HIP events of an extract (sgpu_last_timing's stage slots).  Each event record
     // costs ~4.5 us of GPU time between the commands around it (tests/microbench/event_gap.hip),
     // ~40 us per single-image extract; sgpu_set_stage_timing(ctx, 0) drops them where they only
@@ -418,6 +422,7 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     if (const char* ev = getenv("SGPU_STREAMS")) ctx->multi_stream = !strcmp(ev, "multi");
     if (const char* ev = getenv("SGPU_MATCH"))
         if (!strcmp(ev, "reg")) ctx->debug_flags |= SGPU_DEBUG_MATCH_REGSTAGE;
+    ctx->env_flags = ctx->debug_flags;   // kept by sgpu_debug_set_flags (A/B runs of the probes)
     int rc = sgpu_ctx_set_options(ctx, opt);
     if (rc != SGPU_OK) {
         sgpu_ctx_destroy(ctx);
@@ -700,9 +705,11 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
                 if (duo_second[i] || a.o != b.o || b.k != a.k + 1) continue;
                 const long long bytes = 4ll * a.op.w * a.op.h * a.op.batch;
                 if (!duo_all && bytes < ((long long)SGK_DUO_MIN_MB << 20)) continue;
-                // the (21, 25) pair's arithmetic outweighs the byte saving (1,016 us against
-                // ~960 for two single-level launches, 128 x 1080p): narrow pairs only
-                if (!duo_all && !ctx->duo_wide && a.op.fw + b.op.fw > SGK_DUO_MAX_FW_SUM) continue;
+                if (!duo_all && a.op.fw + b.op.fw > 24) {
+                    const bool ds_pair = a.op.ds_dst != nullptr;
+                    if (!ds_pair && !ctx->duo_wide) continue;
+                    if (bytes < ((long long)SGK_DUO_WIDE_MIN_MB << 20)) continue;
+                }
                 // the u8 ingest pair (levels 0, 1: 725 us) displaces the (11, 13) pair of levels
                 // 1, 2 (750 us, level 0 alone 390): opt-in
                 if (!duo_all && !ctx->duo_u8 && a.op.src_u8) continue;
@@ -1886,7 +1893,7 @@ int sgpu_last_timing(const sgpu_ctx* ctx, float* times, int n) {
 
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags) {
     if (!ctx) return SGPU_EINVAL;
-    ctx->debug_flags = flags;
+    ctx->debug_flags = flags | ctx->env_flags;
     return SGPU_OK;
 }
 

@@ -134,8 +134,11 @@ struct DuoJob {
     long long dst_img;
     int W, H;
     Taps ta, tb;                 // the two filters (widths FWA, FWB)
+    float* ds;                   // level k + 1 decimated into the next octave's level 0 (DS)
+    int dsw;
+    long long ds_img;
     int strips, nsy, rows_per_band, total_waves;
-    float* trash;                // 2,560 B per wave slot (1024 slots): stores of rows outside
+    float* trash;                // 3,072 B per wave slot (1024 slots): stores of rows outside
                                  // the band and the DMA prologue's count-keeping stores
     ZeroJob zero;                // buffers this launch zeroes (the extract's first launch)
 };
@@ -176,14 +179,15 @@ __device__ __forceinline__ void wait_lgkm0() {
     __builtin_amdgcn_s_waitcnt((15) | (3 << 14) | (7 << 4) | (0 << 8));   // lgkmcnt(0) only
 }
 
-template <int FWA, int FWB, int NIN, bool U8>
+template <int FWA, int FWB, int NIN, bool U8, bool DS>
 __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, float* s_mid) {
     using G = DuoGeom<FWA, FWB>;
     constexpr int RA = G::RA, RB = G::RB, SW = G::SW, NDMA = G::NDMA, IN_SLOT = G::IN_SLOT;
     constexpr int P = G::P, U = G::U, MOFF = G::MOFF, OB = G::OB, NQ = G::NQ;
     static_assert(!U8 || ((MOFF + RA) % 4 == 0 && G::IN_W % 4 == 0 && NQ <= 64),
                   "u8 input: the strip's input quads are 4-column aligned");
-    constexpr int OPS = NDMA + 4;   // VMEM instructions per step: the DMAs, 2 + 2 stores
+    // VMEM instructions per step: the DMAs, 2 + 2 stores, the decimated row's store
+    constexpr int OPS = NDMA + 4 + (DS ? 1 : 0);
     static_assert(NIN >= 2 && OPS * (NIN - 1) < 64, "DMA ring (vmcnt field)");
     const int lane = threadIdx.x & 63;
     const int W = J.W, H = J.H;
@@ -197,7 +201,7 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
     const uint8_t* src8 = U8 ? J.src8 + (long long)b * J.src_img : nullptr;
     float* d1 = J.dst1 + (long long)b * J.dst_img;
     float* d2 = J.dst2 + (long long)b * J.dst_img;
-    float* trash = J.trash + (size_t)(gw & 1023) * 640;   // 5 x 512 B per wave slot
+    float* trash = J.trash + (size_t)(gw & 1023) * 768;   // 6 x 512 B per wave slot
 
     // ---- DMA lane map: instruction q, lane i -> input column a0 + 32 q + i / 2 (clamped),
     // row i & 1 of the pair; LDS float 64 q + i of the slot = float2 index 32 q + i / 2
@@ -427,7 +431,7 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
         for (int k = 0; k < NIN - 1; k++) {
             dma(rho0 + 2 * k, s_in + k * IN_SLOT);
 #pragma unroll
-            for (int j = 0; j < 4; j++)
+            for (int j = 0; j < 4 + (DS ? 1 : 0); j++)
                 *reinterpret_cast<f2v*>(trash + 128 * (j + 1) + 2 * lane) = f2v{0.f, 0.f};
         }
     }
@@ -443,6 +447,14 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
     char* const bA = reinterpret_cast<char*>(d1);
     char* const bB = reinterpret_cast<char*>(d2);
     char* const bT = reinterpret_cast<char*>(trash);
+    // DS: the even row of stage A's pair (mc + DSR; mc's parity is RB's, yb being even) decimated
+    // into the next octave's level 0 -- DownsampleKernel<1> (ProgramCU.cu:287-298): ds(r, cc) =
+    // level(2 r, 2 cc), stored by the lanes that own column c = 2 cc
+    constexpr int DSR = RB & 1;
+    char* const bD = DS ? reinterpret_cast<char*>(J.ds + (long long)b * J.ds_img) : nullptr;
+    const uint32_t DW4 = DS ? 4u * (uint32_t)J.dsw : 0u;
+    uint32_t rowD = DS ? (uint32_t)((rho0 - RA + DSR) / 2) * DW4 : 0u;   // (rho0 - RA + DSR even)
+    const uint32_t voffD = 2u * (uint32_t)c;
     int slot_use = 0;                 // input slot of step t (t mod NIN)
     int mid_cur = 0;                  // mid slot of step t's stage A (t & 1; U may be odd)
     int slot_dma = NIN - 1;           // input slot of step t + NIN - 1
@@ -530,6 +542,12 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
                 if (own1) {
                     *reinterpret_cast<f2v*>((a0ok ? bA : bT) + (a0ok ? rowA + voffA : vtr)) = A0;
                     *reinterpret_cast<f2v*>((a1ok ? bA : bT) + (a1ok ? rowA + W4 + voffA : vtr)) = A1;
+                    if constexpr (DS) {
+                        const int yd = mc + DSR;
+                        const bool dok = yd >= yb && yd < ye;
+                        *reinterpret_cast<float*>((dok ? bD : bT) + (dok ? rowD + voffD : vtr)) =
+                            DSR ? A1.x : A0.x;
+                    }
                 }
                 if (own2) {
                     *reinterpret_cast<f2v*>((b0ok ? bB : bT) + (b0ok ? rowB + voffB : vtr)) = B0;
@@ -537,6 +555,7 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
                 }
                 rowA += 2 * W4;
                 rowB += 2 * W4;
+                if constexpr (DS) rowD += DW4;
             }
         });
     }
@@ -553,7 +572,7 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
 #ifndef SGK_DUO_WPE_NARROW
 #define SGK_DUO_WPE_NARROW 4
 #endif
-template <int FWA, int FWB, int NIN, bool U8>
+template <int FWA, int FWB, int NIN, bool U8, bool DS>
 __global__ __launch_bounds__(64 * kDuoWaves) __attribute__((amdgpu_waves_per_eu(FWA + FWB > 30 ? SGK_DUO_WPE_WIDE : SGK_DUO_WPE_NARROW))) void k_gauss_duo(const DuoJob J) {
     using G = DuoGeom<FWA, FWB>;
     // u8 input: one input slot (the registers hold the prefetched rows)
@@ -563,7 +582,7 @@ __global__ __launch_bounds__(64 * kDuoWaves) __attribute__((amdgpu_waves_per_eu(
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int gw = duo_block(blockIdx.x, gridDim.x) * kDuoWaves + wave;
     if (gw >= J.total_waves) return;   // uniform per wave
-    duo_wave<FWA, FWB, NIN, U8>(J, gw, s_in_all[wave], s_mid_all[wave]);
+    duo_wave<FWA, FWB, NIN, U8, DS>(J, gw, s_in_all[wave], s_mid_all[wave]);
 }
 
 // input row pairs in LDS: the DMA runs NIN - 1 steps ahead (compiled: 5 and 7; SGPU_DUO_NIN
@@ -599,7 +618,7 @@ static long long duo_waves_target() {
     return v;
 }
 
-template <int FWA, int FWB, bool U8>
+template <int FWA, int FWB, bool U8, bool DS>
 hipError_t duo_launch(const LevelOp& a, const LevelOp& b, hipStream_t stream, int rows_hint,
                       float* trash) {
     using G = DuoGeom<FWA, FWB>;
@@ -616,6 +635,9 @@ hipError_t duo_launch(const LevelOp& a, const LevelOp& b, hipStream_t stream, in
     J.H = a.h;
     J.ta = a.taps;
     J.tb = b.taps;
+    J.ds = a.ds_dst;
+    J.dsw = a.ds_w;
+    J.ds_img = a.ds_img_stride;
     J.strips = (a.w + G::SW - 1) / G::SW;
     const long long per_band = (long long)J.strips * a.batch;
     // bands: as many as the grid needs for duo_waves_target() waves; each band re-walks
@@ -637,27 +659,31 @@ hipError_t duo_launch(const LevelOp& a, const LevelOp& b, hipStream_t stream, in
     J.trash = trash;
     const unsigned nb = (unsigned)((J.total_waves + kDuoWaves - 1) / kDuoWaves);
     if constexpr (U8)
-        hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 2, true>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
+        hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 2, true, DS>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
     else if (duo_nin() == 5)
-        hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 5, false>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
+        hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 5, false, DS>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
     else
-        hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 7, false>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
+        hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 7, false, DS>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
     return hipGetLastError();
 }
 
 }  // namespace
 
 bool gauss_duo_supported(const LevelOp& a, const LevelOp& b) {
-    // f32 pairs (11, 13), (21, 25); the u8 ingest pair (13, 11) (level 0 from the image, level 1)
+    // f32 pairs (11, 13), (21, 25), (17, 21) with level k + 1 decimated into the next octave; the
+    // u8 ingest pair (13, 11) (level 0 from the image, level 1)
     const bool u8 = a.src_u8 != nullptr;
-    const bool pair = u8 ? (a.fw == 13 && b.fw == 11)
+    const bool ds = a.ds_dst != nullptr;
+    const bool pair = u8 ? (a.fw == 13 && b.fw == 11 && !ds)
+                    : ds ? (a.fw == 17 && b.fw == 21 && (a.w % 2) == 0 && a.ds_w * 2 == a.w &&
+                            a.ds_h == (a.h + 1) / 2 && a.ds_img_stride >= (long long)a.ds_w * a.ds_h)
                          : ((a.fw == 11 && b.fw == 13) || (a.fw == 21 && b.fw == 25));
     const bool src_ok = u8 ? (!a.src && (a.src_stride % 4) == 0 && (a.src_img_stride % 4) == 0 &&
                               ((uintptr_t)a.src_u8 % 4) == 0)
                            : (a.src && a.src_stride >= a.w);
     const bool b_zeroes = (b.zero.n[0] | b.zero.n[1] | b.zero.n[2]) != 0;
     const bool a_zeroes = (a.zero.n[0] | a.zero.n[1] | a.zero.n[2]) != 0;
-    return pair && src_ok && !b_zeroes && (u8 || !a_zeroes) && !a.ds_dst && !b.ds_dst &&
+    return pair && src_ok && !b_zeroes && (u8 || !a_zeroes) && !b.ds_dst &&
            b.src == a.dst && !b.src_u8 && a.w == b.w && a.h == b.h && a.batch == b.batch &&
            a.w >= 8 && a.h >= 8 && (a.w % 4) == 0 && b.src_stride == a.w &&
            a.dst_img_stride == b.dst_img_stride && b.src_img_stride == a.dst_img_stride &&
@@ -667,9 +693,10 @@ bool gauss_duo_supported(const LevelOp& a, const LevelOp& b) {
 hipError_t launch_gauss_duo(const LevelOp& a, const LevelOp& b, hipStream_t stream, int rows_hint,
                             float* trash) {
     if (!trash || !gauss_duo_supported(a, b)) return hipErrorInvalidValue;
-    if (a.src_u8) return duo_launch<13, 11, true>(a, b, stream, rows_hint, trash);
+    if (a.src_u8) return duo_launch<13, 11, true, false>(a, b, stream, rows_hint, trash);
+    if (a.ds_dst) return duo_launch<17, 21, false, true>(a, b, stream, rows_hint, trash);
 #define SGK_DUO(A, B) \
-    if (a.fw == A && b.fw == B) return duo_launch<A, B, false>(a, b, stream, rows_hint, trash);
+    if (a.fw == A && b.fw == B) return duo_launch<A, B, false, false>(a, b, stream, rows_hint, trash);
     SGK_DUO(11, 13) SGK_DUO(21, 25)
 #undef SGK_DUO
     return hipErrorInvalidValue;

@@ -88,12 +88,13 @@ hipError_t launch_gauss_two(const LevelOp& a, const LevelOp& b, hipStream_t stre
                             bool long_bands = false, int* launches = nullptr);
 
 // Two consecutive levels in one launch (sift_gauss_duo.hip): a = level k -> k+1, b = level
-// k+1 -> k+2 (b.src == a.dst), no decimation; f32 widths (11, 13) or (21, 25): 12 B of HBM
-// traffic per pixel for the two levels instead of 16; or the u8 ingest pair (13, 11), level 0
+// k+1 -> k+2 (b.src == a.dst); f32 widths (11, 13) or (21, 25): 12 B of HBM
+// traffic per pixel for the two levels instead of 16 (and (17, 21) with level k+1 decimated into
+// the next octave's level 0); or the u8 ingest pair (13, 11), level 0
 // from the image and level 1 (with a's ZeroJob): 9 B instead of 13.  Bit-identical to two
 // launch_gauss_op calls.  trash: kGaussDuoTrashBytes of device scratch.  rows_hint > 0 forces
 // the band height.
-constexpr size_t kGaussDuoTrashBytes = 1024 * 2560;
+constexpr size_t kGaussDuoTrashBytes = 1024 * 3072;
 bool gauss_duo_supported(const LevelOp& a, const LevelOp& b);
 hipError_t launch_gauss_duo(const LevelOp& a, const LevelOp& b, hipStream_t stream, int rows_hint,
                             float* trash);

@@ -113,8 +113,11 @@ def main():
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    with open(os.path.join(prof, f"{tag}_summary.json"), "w") as f:
-        json.dump(out, f, indent=1, sort_keys=True)
+    # profiles/ on the GPU box does not come back (gpurun merges gpurun_out/ only): a copy beside
+    # the traces, to be moved into profiles/ after the call
+    for path in (os.path.join(prof, f"{tag}_summary.json"), os.path.join(src, "summary.json")):
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1, sort_keys=True)
     print(json.dumps(out, indent=1, sort_keys=True))
 
 
