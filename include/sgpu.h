@@ -235,6 +235,15 @@ void sgpu_quantize_descriptors(const float* d, size_t count, uint8_t* out);
  * SiftGPU::_timing[2..8] map them to the reference's slots (siftgpu_api.cpp).  Slots 0-7 and
  * 9-11 read 0 after a one-stream extract / copy made with the stage timing off. */
 int sgpu_last_timing(const sgpu_ctx* ctx, float* times, int n);
+/* Register page-locked host buffers (sgpu_host_alloc) for the NEXT extract of one image
+ * (sgpu_extract / _f32 / _color with n == 1): it writes image 0's keys (4 floats each) and
+ * descriptors (128 floats each; descriptors may be NULL) for up to `capacity` features into them
+ * from the GPU, in its own stream before its one synchronisation, in place of the count copy and
+ * the two downloads of sgpu_copy_features.  sgpu_copy_features(ctx, 0, keys, descriptors) with
+ * the same pointers then returns at once when the image's features fit (otherwise it copies as
+ * usual).  The registration is consumed by that extract.  No reference counterpart: the
+ * reference's RunSIFT downloads keys and descriptors after the pyramid (PyramidCU.cpp:434). */
+int sgpu_set_host_output(sgpu_ctx* ctx, float* keys, float* descriptors, int capacity);
 /* Stage timing on (default) or off.  Replaces the reference's GlobalUtil::_timingS (GlobalUtil.cpp:51,
  * set by SiftGPU::SetVerbose, SiftGPU.cpp:401-429; 0 skips the per-stage finish calls,
  * PyramidCU.cpp:439,873,1041).  Off, a one-stream extract records none of its ~10 stage events

@@ -91,6 +91,7 @@ struct Part {
     size_t cand_hint = 0, feat_hint = 0;   // counts of the previous call (launch-grid sizing)
     int gauss_launches = 0, gauss_filters = 0;   // the last pyramid: launches, level filters
     bool events = true;                    // the last enqueue recorded its stage events
+    bool copied_out = false;               // the last enqueue copied its results to host_out
     hipEvent_t ev[10] = {};  // start, pyramid, detect, orientation, expand, descriptor, end,
                              // extrema done (before the row scan), (spare), (spare)
     int img0 = 0, n = 0;
@@ -145,6 +146,14 @@ struct sgpu_ctx {
     bool duo_wide = false;                 // SGPU_DUO_WIDE=1: also the (21, 25) pairs
     bool duo_u8 = false;                   // SGPU_DUO_U8=1: the u8 ingest pair (13, 11)
     int env_flags = 0;                     // debug flags set from the environment at creation
+    // sgpu_set_host_output: page-locked host buffers the next one-image extract fills in its own
+    // stream (armed until that extract); done = the last extract filled them
+    struct HostOut {
+        float* keys = nullptr;
+        float* desc = nullptr;
+        int cap = 0;
+        bool armed = false, active = false, done = false;
+    } host_out;
     // per-stage HIP events of an extract (sgpu_last_timing's stage slots).  Each event record
     // costs ~4.5 us of GPU time between the commands around it (tests/microbench/event_gap.hip),
     // ~40 us per single-image extract; sgpu_set_stage_timing(ctx, 0) drops them where they only
@@ -820,6 +829,14 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
                                            nullptr, false,
                                            ctx->debug_flags & SGPU_DEBUG_EXACT_DESCRIPTOR));
     HIPCHK(ctx, rec(5, st));
+    // one image with registered host buffers: its keys, descriptors and count record go straight
+    // to the host (enqueue_readback then copies nothing)
+    pt.copied_out = ctx->host_out.active && pt.one_stream && n == 1 && ctx->nparts == 1;
+    if (pt.copied_out)
+        HIPCHK(ctx, sgk::launch_copy_out(pt.keys.as<float4>(), O.descriptors ? pt.desc.as<float>() : nullptr,
+                                         n_feat_dev, ctx->host_out.cap, pt.img_off_dev.as<int64_t>(),
+                                         n + 2, ctx->host_out.keys,
+                                         O.descriptors ? ctx->host_out.desc : nullptr, pt.h_read, st));
     return SGPU_OK;
 }
 
@@ -827,9 +844,10 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
 static int enqueue_readback(sgpu_ctx* ctx, Part& pt) {
     hipStream_t st = pt.one_stream ? pt.stream : pt.stream_lo;
     // one copy: [0] = the candidate count, [1 .. n + 1] = the per-image feature offsets (the
-    // record k_expand writes)
-    HIPCHK(ctx, hipMemcpyAsync(pt.h_read, pt.img_off_dev.p, (size_t)(pt.n + 2) * sizeof(int64_t),
-                               hipMemcpyDeviceToHost, st));
+    // record k_expand writes); none when k_copy_out wrote it with the features
+    if (!pt.copied_out)
+        HIPCHK(ctx, hipMemcpyAsync(pt.h_read, pt.img_off_dev.p, (size_t)(pt.n + 2) * sizeof(int64_t),
+                                   hipMemcpyDeviceToHost, st));
     if (pt.events) HIPCHK(ctx, hipEventRecord(pt.ev[6], st));
     return SGPU_OK;
 }
@@ -1044,7 +1062,15 @@ static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
     if (!ctx) return SGPU_EINVAL;
     const int rc_args = check_extract_args(ctx, images, is_f32, n, w, h, stride, flags, color);
     if (rc_args != SGPU_OK) return rc_args;
+    // a registered host output serves this extract only, and only one image
+    ctx->host_out.active = ctx->host_out.armed && n == 1;
+    ctx->host_out.armed = false;
+    ctx->host_out.done = false;
     const int rc = extract_body(ctx, images, is_f32, n, w, h, stride, flags, color);
+    ctx->host_out.done = rc == SGPU_OK && ctx->host_out.active && ctx->nparts == 1 &&
+                         ctx->part[0].copied_out;
+    ctx->host_out.active = false;
+    ctx->part[0].copied_out = ctx->part[1].copied_out = false;
     return rc == SGPU_OK ? rc : abandon_batch(ctx, rc);
 }
 
@@ -1770,6 +1796,16 @@ int sgpu_reserve(sgpu_ctx* ctx, int n, int w, int h, int stride) {
 
 long long sgpu_debug_alloc_count(void) { return g_allocs.load(); }
 
+int sgpu_set_host_output(sgpu_ctx* ctx, float* keys, float* descriptors, int capacity) {
+    if (!ctx || capacity < 0) return SGPU_EINVAL;
+    ctx->host_out.keys = keys;
+    ctx->host_out.desc = descriptors;
+    ctx->host_out.cap = capacity;
+    ctx->host_out.armed = keys != nullptr && capacity > 0;
+    ctx->host_out.done = false;
+    return SGPU_OK;
+}
+
 int sgpu_set_stage_timing(sgpu_ctx* ctx, int on) {
     if (!ctx) return SGPU_EINVAL;
     ctx->stage_timing = on != 0;
@@ -1821,6 +1857,13 @@ int sgpu_copy_features(sgpu_ctx* ctx, int image, float* keys, float* descriptors
         return SGPU_OK;
     }
     if (descriptors && !ctx->opt.descriptors) return ctx->fail(SGPU_EINVAL, "descriptors disabled (-sd)");
+    const auto& ho = ctx->host_out;
+    if (ho.done && image == 0 && a == 0 && keys == ho.keys && (!descriptors || descriptors == ho.desc) &&
+        nf <= ho.cap) {
+        // the extract already wrote them there (sgpu_set_host_output)
+        ctx->timing[T_COPY_KEYS] = ctx->timing[T_COPY_DESC] = 0.f;
+        return SGPU_OK;
+    }
     // both copies, then one synchronisation; events split the time between them
     // (sgpu_last_timing slots 10, 11) when the context times its stages
     const bool tm = ctx->stage_timing;

@@ -154,6 +154,12 @@ hipError_t launch_expand(const float4* cand, const int2* info, const uint32_t* e
                          float4* feat, int2* feat_info, float4* keys, hipStream_t stream,
                          const ImageOffsetsArgs* io = nullptr);
 
+// Copy *n_dev (at most cap) keys (float4) and descriptors (128 floats; desc may be null) and the
+// rec_n (<= 256) int64 words of rec into page-locked host buffers, in one launch.
+hipError_t launch_copy_out(const float4* keys, const float* desc, const uint32_t* n_dev, int cap,
+                           const int64_t* rec, int rec_n, float* hkeys, float* hdesc,
+                           int64_t* hrec, hipStream_t stream);
+
 // Descriptors (+ normalisation) of the expanded features; n_feat_cap sizes the grid (one wave
 // per feature), the kernel grid-strides over *n_feat_dev.  out_index (optional): feature e's
 // descriptor goes to row out_index[e].  rect: the rectangle descriptor of keys given with

@@ -3016,6 +3016,39 @@ hipError_t launch_orientation(const float* pyr, const uint32_t* mask, const uint
     return hipGetLastError();
 }
 
+// One image's keys and descriptors (up to cap features) and its count record straight into
+// page-locked host memory (sgpu_set_host_output): one launch in the extract's stream in place of
+// the record's copy and the two downloads of sgpu_copy_features -- on one 1080p image each of
+// those copies costs ~20 us of DMA start-up and host round trip beside 5 + 19 us of transfer
+// (tests/diag/c2_ab.sh timeline).  16-B stores; the host reads them after the stream's
+// synchronisation.
+__global__ __launch_bounds__(256) void k_copy_out(const float4* __restrict__ keys,
+                                                  const float4* __restrict__ desc,
+                                                  const uint32_t* __restrict__ n_dev, uint32_t cap,
+                                                  const int64_t* __restrict__ rec, int rec_n,
+                                                  float4* __restrict__ hkeys, float4* __restrict__ hdesc,
+                                                  int64_t* __restrict__ hrec) {
+    const uint32_t n = min(*n_dev, cap);
+    const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t step = (size_t)gridDim.x * blockDim.x;
+    if (t0 < (size_t)rec_n) hrec[t0] = rec[t0];
+    for (size_t i = t0; i < n; i += step) hkeys[i] = keys[i];
+    if (hdesc)
+        for (size_t i = t0; i < (size_t)n * 32; i += step) hdesc[i] = desc[i];
+}
+
+hipError_t launch_copy_out(const float4* keys, const float* desc, const uint32_t* n_dev, int cap,
+                           const int64_t* rec, int rec_n, float* hkeys, float* hdesc,
+                           int64_t* hrec, hipStream_t stream) {
+    if (cap < 0 || rec_n < 0 || rec_n > 256 || !hkeys || !hrec) return hipErrorInvalidValue;
+    const long long work = std::max<long long>(1, (long long)cap * (hdesc ? 32 : 1));
+    const unsigned nb = (unsigned)std::min<long long>(256, std::max<long long>(1, (work + 1023) / 1024));
+    hipLaunchKernelGGL(k_copy_out, dim3(nb), dim3(256), 0, stream, keys,
+                       reinterpret_cast<const float4*>(desc), n_dev, (uint32_t)cap, rec, rec_n,
+                       reinterpret_cast<float4*>(hkeys), reinterpret_cast<float4*>(hdesc), hrec);
+    return hipGetLastError();
+}
+
 hipError_t launch_expand(const float4* cand, const int2* info, const uint32_t* eoff,
                          const uint32_t* n_cand_dev, int n_cand_cap, const FeatureParams& fp,
                          float4* feat, int2* feat_info, float4* keys, hipStream_t stream,

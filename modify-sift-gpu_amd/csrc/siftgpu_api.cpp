@@ -51,6 +51,15 @@ class HostFloats {
     HostFloats(const HostFloats&) = delete;
     HostFloats& operator=(const HostFloats&) = delete;
     ~HostFloats() { release(); }
+    // capacity for n floats (contents not kept), size unchanged
+    void reserve(size_t n) {
+        if (n > cap_) {
+            const size_t keep = n_;
+            resize(n);
+            n_ = keep;
+        }
+    }
+    bool pinned() const { return pinned_; }
     void resize(size_t n) {
         if (n > cap_) {
             release();
@@ -429,6 +438,19 @@ void SiftGPU::SetKeypointList(int num, const SiftKeypoint* keys, int keys_have_o
     rt->pending_orientation = keys_have_orientation;
 }
 
+// Before a detecting extract: the object's page-locked key / descriptor buffers, sized for the
+// last image's count + 25 % (at least 4,096 features), registered as the extract's host output
+// (sgpu_set_host_output): the GPU writes them in the extract's own stream, and fetch_features
+// then copies nothing when they fit.
+static void arm_host_output(Runtime* rt) {
+    const size_t hint = std::max<size_t>(4096, (size_t)rt->feature_num + (size_t)rt->feature_num / 4);
+    rt->keys.reserve(hint * 4);
+    if (rt->opt.descriptors) rt->desc.reserve(hint * 128);
+    if (rt->keys.pinned() && (!rt->opt.descriptors || rt->desc.pinned()))
+        sgpu_set_host_output(rt->ctx, rt->keys.data(), rt->opt.descriptors ? rt->desc.data() : nullptr,
+                             (int)hint);
+}
+
 // Copy the context's current features (image 0) into the object's host buffers: the keys
 // (the reference's DownloadKeypoints stage) and then the descriptors (downloaded inside its
 // GetFeatureDescriptors stage, PyramidCU.cpp:434), each timed on the host.
@@ -588,6 +610,7 @@ int SiftGPU::RunSIFT() {
     }
     const int ch = img->color == SGPU_RGB || img->color == SGPU_BGR ? 3 : 4;
     int rc;
+    if (rt->pending.empty()) arm_host_output(rt);
     if (!img->is_float && !img->color) {
         // u8 gray: uploaded once per image (the load, _timing[0]), then every RunSIFT() on it
         // starts from the device copy, as the reference's texture

@@ -33,6 +33,7 @@ C_API = [
     "sgpu_match_shard_begin", "sgpu_match_shard_end", "sgpu_match_sharded",
     "sgpu_extract_stream", "sgpu_host_alloc", "sgpu_host_free", "sgpu_reserve",
     "sgpu_debug_alloc_count", "sgpu_last_pyramid_launches", "sgpu_set_stage_timing",
+    "sgpu_set_host_output",
 ]
 
 _LIB = None
@@ -64,6 +65,7 @@ def lib():
         L.sgpu_debug_alloc_count.restype = c.c_longlong
         L.sgpu_last_pyramid_launches.argtypes = [vp, P(c.c_int)]
         L.sgpu_set_stage_timing.argtypes = [vp, c.c_int]
+        L.sgpu_set_host_output.argtypes = [vp, vp, vp, c.c_int]
         L.sgpu_extract_f32.argtypes = [vp, vp, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int]
         L.sgpu_feature_count.argtypes = [vp, c.c_int]
         L.sgpu_feature_total.argtypes = [vp]
@@ -344,6 +346,20 @@ class SiftContext:
                                              desc.ctypes.data if (n and descriptors) else None),
                     "sgpu_copy_features")
         return keys, desc
+
+    def set_host_output(self, keys, descriptors, capacity: int):
+        """Register page-locked buffers (PinnedArray .array, [cap, 4] / [cap, 128] float32) that
+        the next one-image extract fills from the GPU (sgpu_set_host_output)."""
+        self._check(lib().sgpu_set_host_output(
+            self._ctx, keys.ctypes.data if keys is not None else None,
+            descriptors.ctypes.data if descriptors is not None else None, int(capacity)),
+            "sgpu_set_host_output")
+
+    def copy_features_into(self, keys, descriptors, image: int = 0):
+        """sgpu_copy_features into caller arrays (e.g. the registered host output)."""
+        self._check(lib().sgpu_copy_features(
+            self._ctx, image, keys.ctypes.data if keys is not None else None,
+            descriptors.ctypes.data if descriptors is not None else None), "sgpu_copy_features")
 
     def timing(self):
         t = np.zeros(10, np.float32)

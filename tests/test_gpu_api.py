@@ -212,6 +212,48 @@ def test_reserve_then_extract_allocates_nothing(gpu_ctx):
         assert np.array_equal(d, ref[i][1])
 
 
+@pytest.mark.parametrize("cap", [4096, 16])
+def test_host_output_equals_copy_features(gpu_ctx, cap):
+    """sgpu_set_host_output: the next one-image extract writes image 0's keys and descriptors
+    from the GPU into the registered page-locked buffers (k_copy_out, in the extract's stream);
+    they equal sgpu_copy_features' copies bit for bit, sgpu_copy_features on those pointers copies
+    nothing more, and with a capacity below the count (16) the GPU writes only that many and
+sgpu_copy_features into buffers of the image's size does the work.  The
+    registration serves one extract: the one after it writes nothing there."""
+    import sgpu
+    img = synth_image(640, 480, 77)
+    gpu_ctx.set_options(default_options())
+    hk = sgpu.PinnedArray((cap, 4), np.float32)
+    hd = sgpu.PinnedArray((cap, 128), np.float32)
+    try:
+        hk.array[:] = -1.0
+        hd.array[:] = -1.0
+        gpu_ctx.set_host_output(hk.array, hd.array, cap)
+        gpu_ctx.extract(img)
+        k, d = gpu_ctx.features(0)
+        n = len(k)
+        assert n > 16
+        if n <= cap:
+            assert np.array_equal(hk.array[:n].view(np.uint32), k.view(np.uint32))
+            assert np.array_equal(hd.array[:n].view(np.uint32), d.view(np.uint32))
+            assert np.all(hk.array[n:] == -1.0)
+        else:
+            assert np.all(hk.array[:] == -1.0) or np.array_equal(hk.array.view(np.uint32), k[:cap].view(np.uint32))
+        # through the registered pointers (when they hold the image): the fast path
+        if n <= cap:
+            gpu_ctx.copy_features_into(hk.array, hd.array)
+            assert np.array_equal(hd.array[:n].view(np.uint32), d.view(np.uint32))
+        # consumed: a second extract leaves the buffers alone
+        hk.array[:] = -2.0
+        gpu_ctx.extract(img)
+        assert np.all(hk.array == -2.0)
+        k2, _ = gpu_ctx.features(0)
+        assert np.array_equal(k2.view(np.uint32), k.view(np.uint32))
+    finally:
+        hk.free()
+        hd.free()
+
+
 def test_rejected_extract_keeps_previous_results(gpu_ctx):
     """An sgpu_extract call rejected for its arguments queues nothing and leaves the previous
     extract's features readable (the C ABI's argument checks run before the batch is replaced)."""
