@@ -98,6 +98,14 @@ def main():
         args.octaves = 6
         if args.batch == 128:
             args.batch = 16
+    c2 = None
+    if rank == 0 and world == 1 and args.workload == "c3" and not args.no_c2:
+        # C2 is its own program (speed.cpp's protocol, a child process): it runs before this
+        # process initialises the HIP runtime at all, so that the child has the GPU to itself,
+        # as speed.cpp does (with this process's runtime up beside it, idle, the child's RunSIFT
+        # read 0.313-0.316 ms against 0.289-0.293 alone: profiles/bench_r05n.json,
+        # tests/diag/c2_ab.sh)
+        c2 = bench_c2(cpu=False)
     sgpu.lib()   # libsiftgpu (and /opt/rocm's HIP runtime) before torch: torch never touches
                  # the GPU here -- torch.distributed (gloo, host) is only the rendezvous
     # Initialise /opt/rocm's HIP runtime now, before `import torch` maps torch's own copy of
@@ -129,11 +137,8 @@ def main():
 
     B, W, H = args.batch, args.width, args.height
     opts = default_options(octave_num=args.octaves)
-    c2 = None
-    if rank == 0 and world == 1 and args.workload == "c3" and not args.no_c2:
-        # C2 is its own program (speed.cpp's protocol, a child process): it runs before this
-        # process creates its context, so that the child has the GPU to itself, as speed.cpp
-        c2 = bench_c2(cpu=not args.no_cpu_baseline)
+    if c2 is not None and "error" not in c2 and not args.no_cpu_baseline:
+        c2["cpu_baseline"] = bench_c2_cpu()
     ctx = sgpu.SiftContext(device, opts)
     rccl = world > 1 and args.dist_backend == "rccl"
     if rccl:
@@ -586,19 +591,25 @@ def bench_c2(repeat=30, cpu=True):
            "note": "host image in, features in the object's host buffers; _timing slots as "
                    "SiftGPU.cpp:368 / speed.cpp:147-153"}
     if cpu:
-        import oracle_py
-        secs, feats = oracle_py.bench_extract(img[None], default_options(octave_num=4), threads=1)
-        out["cpu_baseline"] = {"value": 1.0 / secs, "unit": "images/s", "cores": 1, "kind": "port",
-                               "sample": "the same image, one thread, oracle/liboracle.so",
-                               "ms_per_image": secs * 1e3, "features": int(feats)}
-        # all cores (1 thread and all cores): copies of the image, one per thread
-        threads = max(1, min(16, os.cpu_count() or 1))
-        sa, _ = oracle_py.bench_extract(np.repeat(img[None], threads, 0),
-                                        default_options(octave_num=4), threads=threads)
-        out["cpu_baseline"]["all_cores"] = {"value": threads / sa, "unit": "images/s",
-                                            "cores": threads,
-                                            "sample": f"{threads} copies of the image, one per "
-                                                      "OpenMP thread"}
+        out["cpu_baseline"] = bench_c2_cpu()
+    return out
+
+
+def bench_c2_cpu():
+    """C2's CPU baseline: the oracle on the same image, one thread and all cores."""
+    import oracle_py
+    from sift_synth import synth_image
+    img = synth_image(1920, 1080, 2000)
+    secs, feats = oracle_py.bench_extract(img[None], default_options(octave_num=4), threads=1)
+    out = {"value": 1.0 / secs, "unit": "images/s", "cores": 1, "kind": "port",
+           "sample": "the same image, one thread, oracle/liboracle.so",
+           "ms_per_image": secs * 1e3, "features": int(feats)}
+    # all cores (SURVEY.md 8d: 1 thread and all cores): copies of the image, one per thread
+    threads = max(1, min(16, os.cpu_count() or 1))
+    sa, _ = oracle_py.bench_extract(np.repeat(img[None], threads, 0),
+                                    default_options(octave_num=4), threads=threads)
+    out["all_cores"] = {"value": threads / sa, "unit": "images/s", "cores": threads,
+                        "sample": f"{threads} copies of the image, one per OpenMP thread"}
     return out
 
 

@@ -309,6 +309,8 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
                                         pairs only levels of >= 128 MB): same levels */
 #define SGPU_DEBUG_DUO_OFF 32768 /* no paired-level launches (one level per launch, the round-4
                                     schedule): same levels */
+#define SGPU_DEBUG_DESC_DUAL 65536 /* detected features' descriptors through the round-4 dual-cell
+                                       kernel instead of the pixel-parallel k_descriptor_flat */
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);

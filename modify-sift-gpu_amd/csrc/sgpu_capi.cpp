@@ -431,6 +431,8 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     if (const char* ev = getenv("SGPU_STREAMS")) ctx->multi_stream = !strcmp(ev, "multi");
     if (const char* ev = getenv("SGPU_MATCH"))
         if (!strcmp(ev, "reg")) ctx->debug_flags |= SGPU_DEBUG_MATCH_REGSTAGE;
+    if (const char* ev = getenv("SGPU_DESC"))
+        if (!strcmp(ev, "dual")) ctx->debug_flags |= SGPU_DEBUG_DESC_DUAL;
     ctx->env_flags = ctx->debug_flags;   // kept by sgpu_debug_set_flags (A/B runs of the probes)
     int rc = sgpu_ctx_set_options(ctx, opt);
     if (rc != SGPU_OK) {
@@ -827,7 +829,8 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
         HIPCHK(ctx, sgk::launch_descriptor(pyr, pt.feat.as<float4>(), pt.feat_info.as<int2>(),
                                            n_feat_dev, feat_grid, fp, pt.desc.as<float>(), st,
                                            nullptr, false,
-                                           ctx->debug_flags & SGPU_DEBUG_EXACT_DESCRIPTOR));
+                                           ctx->debug_flags & SGPU_DEBUG_EXACT_DESCRIPTOR,
+                                           ctx->debug_flags & SGPU_DEBUG_DESC_DUAL));
     HIPCHK(ctx, rec(5, st));
     // one image with registered host buffers: its keys, descriptors and count record go straight
     // to the host (enqueue_readback then copies nothing)
@@ -885,6 +888,7 @@ static int plan_batch(sgpu_ctx* ctx, int n, int w, int h) {
 // batch geometry was already replaced): wait for every stream of the context, then forget the
 // batch.
 static int abandon_batch(sgpu_ctx* ctx, int rc) {
+    ctx->host_out.done = false;
     for (hipStream_t st : {ctx->stream, ctx->h2d, ctx->d2h})
         if (st) (void)hipStreamSynchronize(st);
     for (Part& pt : ctx->part) {
@@ -1207,6 +1211,7 @@ int sgpu_extract_stream(sgpu_ctx* ctx, const uint8_t* const* batches, int nbatch
                         int32_t* counts) {
     if (!ctx) return SGPU_EINVAL;
     ctx->streaming = true;   // its waits use the slots' stage events
+    ctx->host_out.done = false;
     const int rc = extract_stream_body(ctx, batches, nbatches, batch, w, h, stride, keys, desc,
                                        cap, counts);
     ctx->streaming = false;
@@ -1235,6 +1240,7 @@ void sgpu_host_free(void* p) {
 int sgpu_extract_keypoints(sgpu_ctx* ctx, int image, const float* keys, int num,
                            int has_orientation) {
     if (!ctx || !keys || num <= 0) return SGPU_EINVAL;
+    ctx->host_out.done = false;   // the features it writes replace what k_copy_out delivered
     if (ctx->batch <= 0 || image < 0 || image >= ctx->batch)
         return ctx->fail(SGPU_EINVAL, "no extracted image to describe keypoints on");
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -1304,7 +1310,8 @@ int sgpu_extract_keypoints(sgpu_ctx* ctx, int image, const float* keys, int num,
         HIPCHK(ctx, sgk::launch_descriptor(pt.pyr.as<float>(), pt.feat.as<float4>(),
                                            pt.feat_info.as<int2>(), d_m, std::max(m, 1), pt.fp,
                                            pt.desc.as<float>(), st, d_index, rect,
-                                           ctx->debug_flags & SGPU_DEBUG_EXACT_DESCRIPTOR));
+                                           ctx->debug_flags & SGPU_DEBUG_EXACT_DESCRIPTOR,
+                                           ctx->debug_flags & SGPU_DEBUG_DESC_DUAL));
     }
     HIPCHK(ctx, hipStreamSynchronize(st));
     // the described image now owns the context's feature list

@@ -165,11 +165,12 @@ hipError_t launch_copy_out(const float4* keys, const float* desc, const uint32_t
 // descriptor goes to row out_index[e].  rect: the rectangle descriptor of keys given with
 // keys_have_orientation == -1 (feat = (x, y, width, height) in octave coordinates).
 // exact: the reference's per-bin fma order and the oracle's transcendentals (bit-identical to the
-// oracle; the test mode); otherwise the relaxed-order kernel (L2 ~1e-6 from the oracle).
+// oracle; the test mode); otherwise the relaxed-order pixel-parallel kernel k_descriptor_flat
+// (L2 ~1e-6 from the oracle), or with dual the round-4 dual-cell kernel (A/B).
 hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* feat_info,
                              const uint32_t* n_feat_dev, int n_feat_cap, const FeatureParams& fp,
                              float* desc, hipStream_t stream, const int* out_index = nullptr,
-                             bool rect = false, bool exact = false);
+                             bool rect = false, bool exact = false, bool dual = false);
 
 // Caller-supplied keypoints: strongest orientation into feat[e].w (num_orientation != 0, else
 // 0) and the image-coordinate key at keys_out[index[e]].

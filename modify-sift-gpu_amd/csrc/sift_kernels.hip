@@ -2570,6 +2570,259 @@ __global__ __launch_bounds__(256) SGK_DUAL_ATTR void k_descriptor_dual(const flo
                            out_index ? (uint32_t)out_index[e] : e, hist);
 }
 
+// ------------------------------------------------------------------------------------------
+// Flat pixel-parallel descriptor (round 5, the shipped default for detected features).  The
+// dual-cell kernel above gives every lane one dual cell and its own register histogram: 50 of 64
+// lanes walk (lanes 50..63 idle), each lane's 4-pixel strips run past its row spans (masked
+// pixels evaluated), and its gradient loads are 16-B gathers scattered over 25 cells.  Here the
+// window's pixels are enumerated row-major over the rotated 5 x 5-cell square's row spans and
+// dealt to the 64 lanes in turn (pixel p -> lane p mod 64): every lane busy, no masked tails,
+// neighbouring lanes on neighbouring pixels (coalesced loads).  A pixel's dual cell (a, b) and
+// its weights are those of descriptor_dual (the same dnx, dny, the reference's rounded cell
+// centres, ProgramCU.cu:1044-1094, from a 6 x 6 per-feature table), its 4 cells x 2 orientation
+// bins are 8 no-return LDS float adds into the wave's histogram, kept in kFlatCopies copies
+// (lane mod kFlatCopies) against same-address serialisation and summed at the end.  Within a
+// wave the adds of one instruction to one address serialise in a fixed order, so a feature's
+// descriptor does not depend on the batch around it; against the exact kernel the sums' order
+// differs (L2 ~1e-6, tests/test_gpu_parity.py::test_shipped_descriptor_vs_exact).
+#ifndef SGK_FLAT_COPIES
+#define SGK_FLAT_COPIES 4
+#endif
+constexpr int kFlatCopies = SGK_FLAT_COPIES;
+static_assert(kFlatCopies >= 1 && kFlatCopies <= 32 && (kFlatCopies & (kFlatCopies - 1)) == 0,
+              "histogram copies");
+// [4 x 4 cells][8 bins][copies] 64-bit words, a (cell, bin)'s copies kFlatStride words apart from
+// the next's.  Measured per 128 x 1080p step (tests/diag/r05m.sh): 4 copies 1.51 ms, 1 / 2 / 8 /
+// 16 copies 2.83 / 1.91 / 2.07 / 3.79 ms; a padded stride (copies + 1) 1.68 ms
+#ifndef SGK_FLAT_PAD
+#define SGK_FLAT_PAD 0
+#endif
+constexpr int kFlatStride = kFlatCopies + SGK_FLAT_PAD;
+constexpr int kFlatHist = 16 * 8 * kFlatStride;
+constexpr int kFlatRows = 64;                      // window rows per chunk (one per lane)
+constexpr int kFlatWords = 2 * kFlatHist + 144;
+
+// A contribution as a 64-bit fixed-point word, 32 fraction bits (two's complement; |v| < 2^31):
+// the integer part by floor, the fraction (exact in float) scaled by 2^32 and truncated (error <
+// 2^-32).  LDS integer adds are full rate where float adds (ds_add_f32) serialise their lanes
+// (~4 cycles per lane, 7.8 ms per 128 x 1080p step against 1.37 with integer adds,
+// tests/diag/r05l.sh), and integer sums do not depend on their order.
+__device__ __forceinline__ unsigned long long to_fix32(float v) {
+    const float fl = floor_(v);
+    const uint32_t lo = (uint32_t)((v - fl) * 4294967296.0f);
+    return ((unsigned long long)(uint32_t)(int)fl << 32) | lo;
+}
+
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+        const int u = __shfl_up(v, k, 64);
+        if (lane >= k) v += u;
+    }
+    return v;
+}
+
+__device__ __forceinline__ void descriptor_flat(uint32_t e, int lane, const float* __restrict__ pyr,
+                                                const float4* __restrict__ feat,
+                                                const int2* __restrict__ feat_info,
+                                                const FeatureParams& fp, float* __restrict__ desc,
+                                                uint32_t out, float* __restrict__ sh) {
+    unsigned long long* hist = reinterpret_cast<unsigned long long*>(sh);   // kFlatHist
+    // 36: (1 + ox', 1 - ox', 1 + oy', 1 - oy') of cell (i, j)
+    float4* ctab = reinterpret_cast<float4*>(sh + 2 * kFlatHist);
+    const float4 key = feat[e];
+    const int2 in = feat_info[e];
+    const int o = in.y / fp.d, j = in.y - o * fp.d;
+    const OctaveDesc& od = fp.oct[o];
+    const int W = od.wa, H = od.h;
+    const float* g = pyr + od.gauss_off + (long long)(1 + j) * od.level_stride +
+                     (long long)in.x * W * H;
+    const float rpi = (float)(4.0 / 3.14159265358979323846);
+    const float spt = fabs_(key.z * fp.window_factor);
+    float s, c;
+    sincos_(key.w, &s, &c);
+    const float anglef = (double)key.w > 3.14159265358979323846
+                             ? (float)((double)key.w - (2.0 * 3.14159265358979323846))
+                             : key.w;
+    const float cspt = c * spt, sspt = s * spt, crspt = c / spt, srspt = s / spt;
+    // the histogram (every copy) to zero; the cell centre table: cell (i, j), i, j = -1 .. 4 at
+    // (j + 1) * 6 + i + 1 -- the reference's rounded centre, measured in the feature frame
+    // (descriptor_dual's oxl / oyl)
+#pragma unroll
+    for (int i = lane; i < kFlatHist / 2; i += 64)
+        reinterpret_cast<float4*>(hist)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (lane < 36) {
+        const float ox = (float)(lane % 6 - 1) - 1.5f, oy = (float)(lane / 6 - 1) - 1.5f;
+        const float ptx = fma_(cspt, ox, -(sspt * oy)) + key.x;
+        const float pty = fma_(cspt, oy, sspt * ox) + key.y;
+        const float ex = ptx - key.x, ey = pty - key.y;
+        const float oxp = fma_(crspt, ex, srspt * ey), oyp = fma_(crspt, ey, -(srspt * ex));
+        ctab[lane] = make_float4(1.0f + oxp, 1.0f - oxp, 1.0f + oyp, 1.0f - oyp);
+    }
+    // the window's bounding rows and columns: the 5 x 5-cell square (side 5 spt, rotated) around
+    // the keypoint, clamped to rows / columns 1 .. H-2 / W-2 (the reference's [1.5, W - 1.5] box)
+    const float hb = 2.5f * (fabs_(cspt) + fabs_(sspt)) + 0.01f;
+    const float fH = (float)H, fW = (float)W;
+    const int y0 = (int)fmax_(1.0f, fmin_(fH, ceilf(key.y - hb - 0.5f)));
+    int y1 = (int)fmin_(fH - 2.0f, fmax_(-1.0f, floor_(key.y + hb - 0.5f)));
+    const int bx0 = (int)fmax_(1.0f, fmin_(fW, ceilf(key.x - hb - 0.5f)));
+    const int bx1 = (int)fmin_(fW - 2.0f, fmax_(-1.0f, floor_(key.x + hb - 0.5f)));
+    if (!(spt > 0.0f)) y1 = y0 - 1;
+    // a row's span: the columns whose dnx, dny can lie in [-2.5, 2.5) (0.05-pixel margin; the
+    // per-pixel test decides)
+    const bool use_c = fabs_(crspt) > 1e-4f / spt, use_s = fabs_(srspt) > 1e-4f / spt;
+    const float icr = use_c ? 1.0f / crspt : 0.0f, isr = use_s ? 1.0f / srspt : 0.0f;
+    const float kexp = -0.125f * 1.44269504f;   // e^(-x/8) = 2^(kexp x)
+    const int copy = lane & (kFlatCopies - 1);
+    asm volatile("" ::: "memory");
+    for (int rb = y0; rb <= y1; rb += kFlatRows) {
+        // this chunk's rows: lane L holds row rb + L's first column and first pixel index
+        int lo = 0, len = 0;
+        {
+            const int py = rb + lane;
+            if (py <= y1) {
+                const float dyk = ((float)py + 0.5f) - key.y;
+                float l = -1e30f, h = 1e30f;
+                if (use_c) {   // crspt dxk in [-2.5 - srspt dyk, 2.5 - srspt dyk]
+                    const float sd = srspt * dyk;
+                    const float p0 = (-2.5f - sd) * icr, p1 = (2.5f - sd) * icr;
+                    l = fmax_(l, fmin_(p0, p1));
+                    h = fmin_(h, fmax_(p0, p1));
+                }
+                if (use_s) {   // -srspt dxk in [-2.5 - crspt dyk, 2.5 - crspt dyk]
+                    const float cd = crspt * dyk;
+                    const float p0 = (2.5f + cd) * isr, p1 = -(2.5f - cd) * isr;
+                    l = fmax_(l, fmin_(p0, p1));
+                    h = fmin_(h, fmax_(p0, p1));
+                }
+                const float xl = ceilf(l + key.x - 0.5f - 0.05f), xh = floor_(h + key.x - 0.5f + 0.05f);
+                const int il = max(bx0, (int)fmax_(xl, -1.0f)), ih = min(bx1, (int)fmin_(xh, fW));
+                lo = il;
+                len = ih >= il ? ih - il + 1 : 0;
+            }
+        }
+        const int incl = wave_incl_scan(len, lane);
+        const int rs = incl - len;                                   // row L's first pixel index
+        const int total = __builtin_amdgcn_readlane(incl, kFlatRows - 1);
+        int rcur = 0;   // the row of pixel `base` (uniform)
+        for (int base = 0; base < total; base += 64) {
+            const int p = base + lane;
+            const bool valid = p < total;
+            // pixel p's row: rcur + the rows after it starting at or before p (their starts read
+            // as uniform values; the loop stops at the first row past this step's pixels)
+            int r = rcur;
+            for (int k = rcur + 1; k < kFlatRows; k++) {
+                const int sk = __builtin_amdgcn_readlane(rs, k);
+                if (sk > base + 63 || sk >= total) break;
+                r += p >= sk ? 1 : 0;
+            }
+            rcur = __builtin_amdgcn_readlane(r, 63);
+            const int y = rb + r;
+            // (the shuffles with every lane active: a lane outside the valid ones may be the
+            // source; the asm keeps the compiler from moving them under the valid test)
+            int xr = __shfl(lo, r, 64) + (p - __shfl(rs, r, 64));
+            asm volatile("" : "+v"(xr));
+            const int x = valid ? xr : bx0;
+            const int yc = valid ? y : y0;
+            // 32-bit byte offsets from the level image's base (an image plane is < 4 GB)
+            const char* gp = reinterpret_cast<const char*>(g) + 4u * (uint32_t)(yc * W + x);
+            const uint32_t W4 = 4u * (uint32_t)W;
+            const float gx = *reinterpret_cast<const float*>(gp + 4) - *reinterpret_cast<const float*>(gp - 4);
+            const float gy = *reinterpret_cast<const float*>(gp + W4) - *reinterpret_cast<const float*>(gp - W4);
+            const float m2 = fma_(gx, gx, gy * gy);
+            float rot = atan2_relaxed(gy, gx);
+            const float dd = fabs_(anglef - rot);
+            if (dd < 1e-5f || dd > 6.2831753f) rot = atan2_(gy, gx);
+            rot = m2 == 0.0f ? 0.0f : rot;
+            const float dxk = ((float)x + 0.5f) - key.x;
+            const float dyk = ((float)yc + 0.5f) - key.y;
+            const float dnx = fma_(crspt, dxk, srspt * dyk);
+            const float dny = fma_(-srspt, dxk, crspt * dyk);
+            const float ft = floor_(dnx + 2.5f), fv = floor_(dny + 2.5f);
+            const float m = 0.5f * __builtin_amdgcn_sqrtf(m2);
+            const float w = m * __builtin_amdgcn_exp2f(kexp * fma_(dnx, dnx, dny * dny));
+            float theta = (anglef - rot) * rpi;
+            if (theta < 0) theta += 8.0f;
+            const bool take = valid && ft >= 0.0f && ft <= 4.0f && fv >= 0.0f && fv <= 4.0f &&
+                              theta >= 0.0f && theta < 8.0f;
+            if (take) {
+                const int a = (int)ft, b = (int)fv;
+                const int c00 = b * 6 + a;                 // cell (a - 1, b - 1) in the 6 x 6 table
+                const float4 t0 = ctab[c00], t1 = ctab[c00 + 1], t2 = ctab[c00 + 6], t3 = ctab[c00 + 7];
+                const float w0 = (w * (t0.x - dnx)) * (t0.z - dny);
+                const float w1 = (w * (t1.y + dnx)) * (t1.z - dny);
+                const float w2 = (w * (t2.x - dnx)) * (t2.w + dny);
+                const float w3 = (w * (t3.y + dnx)) * (t3.w + dny);
+                // orientation bins: floor(theta) and the next (8 -> 0), tent weights as
+                // descriptor_dual's max(0, 1 - |theta - k|)
+                const int b0 = min((int)theta, 7), b1 = (b0 + 1) & 7;
+                const float tk0 = 1.0f - (theta - (float)b0);
+                const float tk1 = b0 == 7 ? theta - 7.0f : 1.0f - ((float)(b0 + 1) - theta);
+                // the 4 cells (a - 1 + dx, b - 1 + dy); cells outside 0 .. 3 (the dual cells on the
+                // window's border) are not descriptor cells and take nothing
+                const bool x0in = a >= 1, x1in = a <= 3, y0in = b >= 1, y1in = b <= 3;
+                unsigned long long* hp = hist + (((b - 1) * 4 + (a - 1)) * 8) * kFlatStride + copy;
+                const int o0 = b0 * kFlatStride, o1 = b1 * kFlatStride;
+                constexpr int CX = 8 * kFlatStride, CY = 4 * 8 * kFlatStride;
+                auto add2 = [&](bool in, int off, float wc) {
+                    if (in) {
+                        __hip_atomic_fetch_add(hp + off + o0, to_fix32(wc * tk0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_add(hp + off + o1, to_fix32(wc * tk1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                };
+                add2(x0in && y0in, 0, w0);
+                add2(x1in && y0in, CX, w1);
+                add2(x0in && y1in, CY, w2);
+                add2(x1in && y1in, CY + CX, w3);
+            }
+        }
+        asm volatile("" ::: "memory");
+    }
+    // cell (ix, iy) = lane >> 2, bins 2 sub, 2 sub + 1: the copies summed in order
+    const int cell = lane >> 2, sub = lane & 3;
+    const int ix = cell & 3, iy = cell >> 2;
+    const unsigned long long* hc = hist + ((iy * 4 + ix) * 8 + 2 * sub) * kFlatStride;
+    unsigned long long s0 = hc[0], s1 = hc[kFlatStride];
+#pragma unroll
+    for (int k = 1; k < kFlatCopies; k++) {
+        s0 += hc[k];
+        s1 += hc[kFlatStride + k];
+    }
+    float b0 = (float)((double)(long long)s0 * 0x1p-32), b1 = (float)((double)(long long)s1 * 0x1p-32);
+    asm volatile("" ::: "memory");
+    if (fp.normalize) {
+        float sn = fma_(b0, b0, b1 * b1);
+#pragma unroll
+        for (int k = 32; k >= 1; k >>= 1) sn += __shfl_xor(sn, k, 64);
+        const float n1 = __builtin_amdgcn_rsqf(sn);
+        b0 = fmin_(0.2f, b0 * n1);
+        b1 = fmin_(0.2f, b1 * n1);
+        sn = fma_(b0, b0, b1 * b1);
+#pragma unroll
+        for (int k = 32; k >= 1; k >>= 1) sn += __shfl_xor(sn, k, 64);
+        const float n2 = __builtin_amdgcn_rsqf(sn);
+        b0 *= n2;
+        b1 *= n2;
+    }
+    *reinterpret_cast<float2*>(desc + (size_t)out * 128 + cell * 8 + sub * 2) = make_float2(b0, b1);
+}
+
+__global__ __launch_bounds__(256) void k_descriptor_flat(const float* __restrict__ pyr,
+                                                         const float4* __restrict__ feat,
+                                                         const int2* __restrict__ feat_info,
+                                                         const uint32_t* __restrict__ n_feat_dev,
+                                                         const FeatureParams fp,
+                                                         float* __restrict__ desc,
+                                                         const int* __restrict__ out_index) {
+    __shared__ __attribute__((aligned(16))) float s_flat[4][kFlatWords];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t n = *n_feat_dev;
+    for (uint32_t e = blockIdx.x * 4 + wave; e < n; e += gridDim.x * 4)
+        descriptor_flat(e, lane, pyr, feat, feat_info, fp, desc,
+                        out_index ? (uint32_t)out_index[e] : e, s_flat[wave]);
+}
+
 // One wave per feature, grid-stride over the features (count read on the device).
 // SGK_DESC_WPE: waves per SIMD the register allocation must allow (0: the compiler's choice, 91
 // VGPRs = 5 waves; A/B knob)
@@ -3075,12 +3328,20 @@ hipError_t launch_orient_keys(const float* pyr, float4* feat, const int2* feat_i
 hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* feat_info,
                              const uint32_t* n_feat_dev, int n_feat_cap, const FeatureParams& fp,
                              float* desc, hipStream_t stream, const int* out_index,
-                             bool rect, bool exact) {
+                             bool rect, bool exact, bool dual) {
     if (n_feat_cap <= 0) return hipSuccess;
     const unsigned grid = (unsigned)std::min(((long long)n_feat_cap + 3) / 4, 65536LL);
 #ifndef SGK_DESC_DUAL
 #define SGK_DESC_DUAL 1
 #endif
+#ifndef SGK_DESC_FLAT
+#define SGK_DESC_FLAT 1
+#endif
+    if (!exact && !rect && SGK_DESC_FLAT && !dual) {
+        hipLaunchKernelGGL(k_descriptor_flat, dim3(grid), dim3(256), 0, stream, pyr, feat,
+                           feat_info, n_feat_dev, fp, desc, out_index);
+        return hipGetLastError();
+    }
     if (!exact && !rect && SGK_DESC_DUAL) {
         hipLaunchKernelGGL(k_descriptor_dual, dim3(grid), dim3(256), 0, stream, pyr, feat,
                            feat_info, n_feat_dev, fp, desc, out_index);

@@ -471,6 +471,7 @@ class SiftContext:
     DEBUG_GAUSS_LONG_BANDS = 8192  # Gaussian bands of >= 4 chunks on every level
     DEBUG_DUO_ALWAYS = 16384   # paired-level Gaussian launches whatever the level size
     DEBUG_DUO_OFF = 32768      # no paired-level launches (one level per launch)
+    DEBUG_DESC_DUAL = 65536    # descriptors through the round-4 dual-cell kernel
 
     def set_debug_flags(self, flags: int):
         """Per-context debug flags (sgpu_debug_set_flags; 0 = shipped configuration)."""
