@@ -10,6 +10,7 @@
 // capacities); the host waits once per batch, reads the per-image offsets and, if a part's
 // candidates overflowed its capacity, grows the buffers and re-runs that part.  (The reference
 // does four host round trips per DoG level, PyramidCU.cpp:783-813.)
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -1972,6 +1973,24 @@ int sgpu_debug_gaussian(sgpu_ctx* ctx, int image, int octave, int level, float* 
     return SGPU_OK;
 }
 
+// The test-hook library beside this one (lib/libsiftgpu_debug.so, csrc/sgpu_debug.hip), loaded on
+// first use: the candidate dump's kernel is not part of the product library.
+static sgk::DebugCandidatesFn debug_candidates_hook() {
+    static sgk::DebugCandidatesFn fn = [] {
+        Dl_info info{};
+        if (!dladdr(reinterpret_cast<void*>(&sgpu_debug_candidates), &info) || !info.dli_fname)
+            return (sgk::DebugCandidatesFn) nullptr;
+        std::string path(info.dli_fname);
+        const size_t slash = path.rfind('/');
+        path = (slash == std::string::npos ? std::string(".") : path.substr(0, slash)) +
+               "/libsiftgpu_debug.so";
+        void* h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+        return h ? reinterpret_cast<sgk::DebugCandidatesFn>(dlsym(h, "sgpu_testhook_candidates"))
+                 : (sgk::DebugCandidatesFn) nullptr;
+    }();
+    return fn;
+}
+
 int sgpu_debug_candidates(sgpu_ctx* ctx, int* ints, float* floats, int cap, int* n) {
     if (!ctx || !n) return SGPU_EINVAL;
     uint32_t total = 0;
@@ -1979,6 +1998,8 @@ int sgpu_debug_candidates(sgpu_ctx* ctx, int* ints, float* floats, int cap, int*
     *n = (int)total;
     if (!ints || !floats || cap < (int)total) return total ? SGPU_ERANGE : SGPU_OK;
     if (total == 0) return SGPU_OK;
+    const sgk::DebugCandidatesFn hook = debug_candidates_hook();
+    if (!hook) return ctx->fail(SGPU_EINVAL, "test-hook library lib/libsiftgpu_debug.so not found");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     DevBuf a, b;
     ALLOCCHK(ctx, a.ensure(total * sizeof(int4)));
@@ -1987,11 +2008,10 @@ int sgpu_debug_candidates(sgpu_ctx* ctx, int* ints, float* floats, int cap, int*
     for (int p = 0; p < ctx->nparts; p++) {
         const Part& pt = ctx->part[p];
         if (!pt.n_cand) continue;
-        HIPCHK(ctx, sgk::launch_debug_candidates(pt.pyr.as<float>(), pt.mask.as<uint32_t>(),
-                                                 pt.row_base.as<uint32_t>(), pt.total_rows,
-                                                 pt.row_base.as<uint32_t>() + pt.total_rows,
-                                                 (int)pt.n_cand, pt.fp, a.as<int4>() + at,
-                                                 b.as<float4>() + at, ctx->stream));
+        HIPCHK(ctx, hook(pt.pyr.as<float>(), pt.mask.as<uint32_t>(), pt.row_base.as<uint32_t>(),
+                         pt.total_rows, pt.row_base.as<uint32_t>() + pt.total_rows,
+                         (int)pt.n_cand, &pt.fp, a.as<int4>() + at, b.as<float4>() + at,
+                         ctx->stream));
         at += pt.n_cand;
     }
     HIPCHK(ctx, hipMemcpyAsync(ints, a.p, total * sizeof(int4), hipMemcpyDeviceToHost, ctx->stream));

@@ -188,12 +188,14 @@ hipError_t launch_limit_oriented(uint32_t* ocount, const uint32_t* row_base,
                                  uint32_t cand_cap, hipStream_t stream);
 
 
-// Debug: candidates of the orientation stage back as (col, row, level id, image) + (dx,dy,ds).
-hipError_t launch_debug_candidates(const float* pyr, const uint32_t* mask,
-                                   const uint32_t* row_base, int total_rows,
-                                   const uint32_t* n_cand_dev, int n_cand_cap,
-                                   const FeatureParams& fp, int4* ints, float4* floats,
-                                   hipStream_t stream);
+// Test hook, NOT in the product library: the candidates of the orientation stage back as
+// (col, row, level id, image) + (dx, dy, ds, result), from lib/libsiftgpu_debug.so
+// (csrc/sgpu_debug.hip), which sgpu_debug_candidates loads on first use.
+typedef hipError_t (*DebugCandidatesFn)(const float* pyr, const uint32_t* mask,
+                                        const uint32_t* row_base, int total_rows,
+                                        const uint32_t* n_cand_dev, int n_cand_cap,
+                                        const FeatureParams* fp, int4* ints, float4* floats,
+                                        hipStream_t stream);
 
 // ---- matcher (sift_match.hip) ----
 // Distance table dist[v] = float(acos(min(v * 2^-18, 1.0))) for v in [0, 262144], built on the

@@ -35,6 +35,18 @@ def test_library_exports_header_symbols():
     sgpu.lib()   # loads with every argtype bound
 
 
+def test_test_hooks_live_outside_the_product_library():
+    """The candidate dump's kernel (k_debug_candidates) is not in libsiftgpu.so: it lives in
+    lib/libsiftgpu_debug.so beside it, which sgpu_debug_candidates loads on first use."""
+    lib = sgpu.LIB_PATH
+    dbg = os.path.join(os.path.dirname(lib), "libsiftgpu_debug.so")
+    with open(lib, "rb") as f:
+        assert b"k_debug_candidates" not in f.read()
+    assert "sgpu_testhook_candidates" in _exported(dbg)
+    with open(dbg, "rb") as f:
+        assert b"k_debug_candidates" in f.read()
+
+
 def test_default_options_match_reference_defaults():
     o = SgpuOptions()
     sgpu.lib().sgpu_default_options(ctypes.byref(o))
