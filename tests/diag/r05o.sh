@@ -4,7 +4,7 @@ set -o pipefail
 OUT=gpurun_out/r05o
 mkdir -p $OUT
 export TMPDIR=/tmp
-for cfg in base:X=0 ew16:SGPU_LIB_PATH=build_exp/ew16/libsiftgpu.so ew8:SGPU_LIB_PATH=build_exp/ew8/libsiftgpu.so sm64:SGPU_LIB_PATH=build_exp/sm64/libsiftgpu.so; do
+for cfg in base:X=0 ew64:SGPU_LIB_PATH=build_exp/ew64/libsiftgpu.so ew48:SGPU_LIB_PATH=build_exp/ew48/libsiftgpu.so base2:X=0 ew64b:SGPU_LIB_PATH=build_exp/ew64/libsiftgpu.so; do
   name=${cfg%%:*}; envs=${cfg#*:}
   env $envs timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $OUT/kt_$name -o run -- python3 tests/probe.py extract --reps 3 > $OUT/kt_$name.log 2>&1 || exit 1
   env $envs timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_$name -o run -- python3 tests/probe.py extract --reps 2 > $OUT/pmc_$name.log 2>&1 || exit 1
