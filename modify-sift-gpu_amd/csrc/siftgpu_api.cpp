@@ -443,6 +443,12 @@ void SiftGPU::SetKeypointList(int num, const SiftKeypoint* keys, int keys_have_o
 // (sgpu_set_host_output): the GPU writes them in the extract's own stream, and fetch_features
 // then copies nothing when they fit.
 static void arm_host_output(Runtime* rt) {
+    // A/B hook: SGPU_HOST_OUTPUT=0 keeps the copies of sgpu_copy_features
+    static const bool off = [] {
+        const char* e = getenv("SGPU_HOST_OUTPUT");
+        return e && e[0] == '0';
+    }();
+    if (off) return;
     const size_t hint = std::max<size_t>(4096, (size_t)rt->feature_num + (size_t)rt->feature_num / 4);
     rt->keys.reserve(hint * 4);
     if (rt->opt.descriptors) rt->desc.reserve(hint * 128);
