@@ -2665,7 +2665,16 @@ __device__ __forceinline__ void descriptor_flat(uint32_t e, int lane, const floa
     *reinterpret_cast<float2*>(desc + (size_t)out * 128 + cell * 8 + sub * 2) = make_float2(b0, b1);
 }
 
-__global__ __launch_bounds__(256) void k_descriptor_flat(const float* __restrict__ pyr,
+// waves per SIMD the allocation must allow (0: the compiler's choice, 70 VGPRs = 7 waves)
+#ifndef SGK_FLAT_WPE
+#define SGK_FLAT_WPE 0
+#endif
+#if SGK_FLAT_WPE
+#define SGK_FLAT_ATTR __attribute__((amdgpu_waves_per_eu(SGK_FLAT_WPE)))
+#else
+#define SGK_FLAT_ATTR
+#endif
+__global__ __launch_bounds__(256) SGK_FLAT_ATTR void k_descriptor_flat(const float* __restrict__ pyr,
                                                          const float4* __restrict__ feat,
                                                          const int2* __restrict__ feat_info,
                                                          const uint32_t* __restrict__ n_feat_dev,
