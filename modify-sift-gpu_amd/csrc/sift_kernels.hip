@@ -2665,9 +2665,11 @@ __device__ __forceinline__ void descriptor_flat(uint32_t e, int lane, const floa
     *reinterpret_cast<float2*>(desc + (size_t)out * 128 + cell * 8 + sub * 2) = make_float2(b0, b1);
 }
 
-// waves per SIMD the allocation must allow (0: the compiler's choice, 70 VGPRs = 7 waves)
+// waves per SIMD the allocation must allow: 8 (64 VGPRs, no spills): 1.448-1.451 ms per
+// 128 x 1080p step against 1.520-1.524 at the compiler's 70 VGPRs / 7 waves (alternating
+// processes, tests/diag/r05r.sh); 0 leaves it to the compiler
 #ifndef SGK_FLAT_WPE
-#define SGK_FLAT_WPE 0
+#define SGK_FLAT_WPE 8
 #endif
 #if SGK_FLAT_WPE
 #define SGK_FLAT_ATTR __attribute__((amdgpu_waves_per_eu(SGK_FLAT_WPE)))
