@@ -19,6 +19,8 @@ $H $CX -x hip -c -o "$OUT/a.o" $PKG/csrc/siftgpu_api.cpp &
 wait
 $H --offload-arch=gfx950 -shared -o "$OUT/libsiftgpu.so" "$OUT"/{k,d,m,c,a}.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -f "$OUT"/*.o
+# the test-hook library is loaded from beside the product library (sgpu_debug_candidates)
+cp "$PKG/lib/libsiftgpu_debug.so" "$OUT/"
 # a kernel whose host stub was not emitted links into the .so and fails only when loaded
 if nm -D --undefined-only "$OUT/libsiftgpu.so" | grep -q __device_stub; then echo "undefined kernel stubs in $OUT"; exit 1; fi
 echo "built $OUT/libsiftgpu.so"
