@@ -281,18 +281,25 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
                                    creation by the environment variable SGPU_EXACT_DESCRIPTOR=1 */
 #define SGPU_DEBUG_GAUSS_BLOCK 32 /* Gaussian levels through the workgroup strip kernel
                                    (k_gauss_pk2) instead of the shipped wave-streaming one
-                                   (k_gauss_lean); both are bit-identical.  Bits 16.. of the
-                                   flags, when not 0, force the wave kernel's band height in
-                                   rows (test / tuning hook)                              */
+                                   (k_gauss_lean); both are bit-identical.  Bits
+                                   SGPU_DEBUG_BAND_SHIFT.. of the flags, when not 0, force the
+                                   wave kernel's band height in rows (test / tuning hook) */
+#define SGPU_DEBUG_BAND_SHIFT 20  /* band height field: (flags >> 20) & 0x7ff rows; the flag bits
+                                     below it never reach it (DESC_DUAL at 1 << 16
+                                     used to share its bit with the band field) */
 #define SGPU_DEBUG_KEYED_MATCH 64 /* plain matching through the keyed epilogue (every value
                                    folded with its column's tie-order bits) even when
                                    ratiomax <= 1, where the keyless one is exact and used     */
 #define SGPU_DEBUG_FULL_COLUMNS 128 /* plain mutual matching decides every column of set 2, not
                                    only the columns some row of set 1 matched                 */
-/* 256: retired (round 2's k_gauss_wave, removed from the library in round 4) */
+#define SGPU_DEBUG_DESC_DUAL 256 /* detected features' descriptors through the round-4 dual-cell
+                                    kernel instead of the pixel-parallel k_descriptor_flat */
 #define SGPU_DEBUG_ORIENT_WAVE 512 /* orientation one wave per candidate for any count (the shipped
                                      path picks it for few candidates only): same bits */
-/* 1024: retired (the two-level k_gauss_pair, measured slower, removed in round 4) */
+#define SGPU_DEBUG_GAUSS_TILE_ALWAYS 1024 /* every level through the 2-D tile kernel
+                                             (k_gauss_tile), whatever its size (the shipped path
+                                             tiles levels of at most SGPU_GAUSS_TILE_MB, default
+                                             16 MB: a single image's): same levels */
 #define SGPU_DEBUG_MATCH_REGSTAGE 2048 /* keyless plain matching through the register-staged
                                           k_match_rows<..., RAW> instead of the LDS-DMA
                                           k_match_raw: same pairs */
@@ -309,8 +316,13 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
                                         pairs only levels of >= 128 MB): same levels */
 #define SGPU_DEBUG_DUO_OFF 32768 /* no paired-level launches (one level per launch, the round-4
                                     schedule): same levels */
-#define SGPU_DEBUG_DESC_DUAL 65536 /* detected features' descriptors through the round-4 dual-cell
-                                       kernel instead of the pixel-parallel k_descriptor_flat */
+#define SGPU_DEBUG_GAUSS_TILE_OFF 65536 /* no 2-D tile launches: every level through the
+                                           wave-streaming kernels (round 5): same levels */
+#define SGPU_DEBUG_DESC_WIDE_OFF 131072 /* descriptors one wave per feature for every count (the
+                                           shipped path gives few features a workgroup each):
+                                           same bits */
+#define SGPU_DEBUG_DESC_WIDE_ALWAYS 262144 /* descriptors one workgroup per feature for every
+                                              count: same bits */
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);

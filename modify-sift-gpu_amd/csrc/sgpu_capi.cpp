@@ -47,6 +47,19 @@ namespace {
 #define SGK_DUO_WIDE_MIN_MB 512
 #endif
 
+// 2-D tile launches (k_gauss_tile, sift_gauss_tile.hip) for levels of at most this many MB (one
+// 1080p image: 8.3 MB at octave 0), where the wave walk of k_gauss_lean is latency-bound
+#ifndef SGK_TILE_MB
+#define SGK_TILE_MB 16
+#endif
+
+// feature counts (of the previous call) up to which each descriptor gets a workgroup of 4 waves
+// (k_descriptor_wide): ~1,500 features of one 1080p image are ~1.5 waves per SIMD under one wave
+// each
+#ifndef SGK_WIDE_DESC_MAX
+#define SGK_WIDE_DESC_MAX 8192
+#endif
+
 // device and pinned-host allocations made by the library (sgpu_debug_alloc_count): a test hook
 // for sgpu_reserve, whose point is that the extract after it allocates nothing
 std::atomic<long long> g_allocs{0};
@@ -146,6 +159,11 @@ struct sgpu_ctx {
     bool duo_on = false;                   // SGPU_DUO=on: paired-level launches (size rule)
     bool duo_wide = false;                 // SGPU_DUO_WIDE=1: also the (21, 25) pairs
     bool duo_u8 = false;                   // SGPU_DUO_U8=1: the u8 ingest pair (13, 11)
+    size_t wide_desc_max = SGK_WIDE_DESC_MAX;   // feature counts (of the previous call) up to which
+                                           // descriptors run a workgroup per feature
+                                           // (SGPU_WIDE_DESC_MAX)
+    int tile_mb = SGK_TILE_MB;             // levels of at most this many MB: 2-D tile launches
+                                           // (SGPU_GAUSS_TILE_MB; k_gauss_tile)
     int env_flags = 0;                     // debug flags set from the environment at creation
     // sgpu_set_host_output: page-locked host buffers the next one-image extract fills in its own
     // stream (armed until that extract); done = the last extract filled them
@@ -432,8 +450,19 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     if (const char* ev = getenv("SGPU_STREAMS")) ctx->multi_stream = !strcmp(ev, "multi");
     if (const char* ev = getenv("SGPU_MATCH"))
         if (!strcmp(ev, "reg")) ctx->debug_flags |= SGPU_DEBUG_MATCH_REGSTAGE;
-    if (const char* ev = getenv("SGPU_DESC"))
+    if (const char* ev = getenv("SGPU_DESC")) {
         if (!strcmp(ev, "dual")) ctx->debug_flags |= SGPU_DEBUG_DESC_DUAL;
+        if (!strcmp(ev, "narrow")) ctx->debug_flags |= SGPU_DEBUG_DESC_WIDE_OFF;
+        if (!strcmp(ev, "wide")) ctx->debug_flags |= SGPU_DEBUG_DESC_WIDE_ALWAYS;
+    }
+    if (const char* ev = getenv("SGPU_GAUSS_TILE")) {   // A/B hook of the tile kernel
+        if (!strcmp(ev, "off")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_TILE_OFF;
+        if (!strcmp(ev, "always")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_TILE_ALWAYS;
+    }
+    if (const char* ev = getenv("SGPU_WIDE_DESC_MAX"))
+        if (atoll(ev) >= 0) ctx->wide_desc_max = (size_t)atoll(ev);
+    if (const char* ev = getenv("SGPU_GAUSS_TILE_MB"))
+        if (atoi(ev) >= 0) ctx->tile_mb = atoi(ev);
     ctx->env_flags = ctx->debug_flags;   // kept by sgpu_debug_set_flags (A/B runs of the probes)
     int rc = sgpu_ctx_set_options(ctx, opt);
     if (rc != SGPU_OK) {
@@ -610,8 +639,22 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     // 3.69-3.74 ms per 128 x 1080p), and the main stream waits for them before
     // the extremum kernel.  SGPU_DEBUG_PYR_SERIAL: one stream for the pyramid only.
     const bool side = noct > 1 && !pt.one_stream && !(ctx->debug_flags & SGPU_DEBUG_PYR_SERIAL);
-    const int wave_rows = (ctx->debug_flags & SGPU_DEBUG_GAUSS_BLOCK) ? -1 : (ctx->debug_flags >> 16);
+    const int wave_rows = (ctx->debug_flags & SGPU_DEBUG_GAUSS_BLOCK)
+                              ? -1 : ((ctx->debug_flags >> SGPU_DEBUG_BAND_SHIFT) & 0x7ff);
     const bool long_bands = (ctx->debug_flags & SGPU_DEBUG_GAUSS_LONG_BANDS) != 0;
+    // 2-D tiles for the cache-resident levels (sift_gauss_tile.hip): not with a forced kernel or
+    // band height (those test the wave kernels)
+    const bool tiles_on = wave_rows == 0 && !long_bands &&
+                          !(ctx->debug_flags & SGPU_DEBUG_GAUSS_TILE_OFF);
+    const bool tiles_all = tiles_on && (ctx->debug_flags & SGPU_DEBUG_GAUSS_TILE_ALWAYS);
+    auto tiled = [&](const sgk::LevelOp& op) {
+        return tiles_on && sgk::gauss_tile_supported(op) &&
+               (tiles_all || 4ll * op.w * op.h * op.batch <= ((long long)ctx->tile_mb << 20));
+    };
+    auto level = [&](const sgk::LevelOp& op, hipStream_t s_) {
+        return tiled(op) ? sgk::launch_gauss_tile(op, s_)
+                         : sgk::launch_gauss_op(op, s_, wave_rows, long_bands);
+    };
     // the level filters of every octave: op (o, k) filters level k-1 into level k (op (0, 0)
     // smooths the input into level 0); level kds of octave o also writes its decimation, level 0
     // of octave o+1
@@ -692,7 +735,7 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
             const hipStream_t so = side && e.o >= 1 ? pt.stream_oct : st;
             pt.gauss_launches++;
             if (side && e.o == 1 && e.k == 1) HIPCHK(ctx, hipStreamWaitEvent(so, pt.ev_ds, 0));
-            HIPCHK(ctx, sgk::launch_gauss_op(e.op, so, wave_rows, long_bands));
+            HIPCHK(ctx, level(e.op, so));
             if (side && e.o == 0 && e.k == kds && e.op.ds_dst) HIPCHK(ctx, hipEventRecord(pt.ev_ds, st));
         }
     } else {
@@ -752,12 +795,21 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
             int i = 0;
             for (; i + 1 < m; i += 2) {
                 int nl = 0;
-                HIPCHK(ctx, sgk::launch_gauss_two(*in_slot[i], *in_slot[i + 1], st, wave_rows,
-                                                  long_bands, &nl));
+                const bool ta = tiled(*in_slot[i]), tb = tiled(*in_slot[i + 1]);
+                if (ta && tb) {
+                    HIPCHK(ctx, sgk::launch_gauss_tile_two(*in_slot[i], *in_slot[i + 1], st, &nl));
+                } else if (!ta && !tb) {
+                    HIPCHK(ctx, sgk::launch_gauss_two(*in_slot[i], *in_slot[i + 1], st, wave_rows,
+                                                      long_bands, &nl));
+                } else {
+                    HIPCHK(ctx, level(*in_slot[i], st));
+                    HIPCHK(ctx, level(*in_slot[i + 1], st));
+                    nl = 2;
+                }
                 pt.gauss_launches += nl;
             }
             if (i < m) {
-                HIPCHK(ctx, sgk::launch_gauss_op(*in_slot[i], st, wave_rows, long_bands));
+                HIPCHK(ctx, level(*in_slot[i], st));
                 pt.gauss_launches++;
             }
         }
@@ -802,6 +854,11 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     const bool ori_wave = (ctx->debug_flags & SGPU_DEBUG_ORIENT_WAVE) ||
                           (pt.cand_hint > 0 && pt.cand_hint <= kWaveOrientationMax);
     const int feat_grid = (int)std::min(ne_cap, pt.feat_hint ? pt.feat_hint : ne_cap);
+    // few features (a single image): a workgroup of 4 waves per feature instead of one wave
+    // (k_descriptor_wide, same bits)
+    const bool desc_wide = !(ctx->debug_flags & SGPU_DEBUG_DESC_WIDE_OFF) &&
+                           ((ctx->debug_flags & SGPU_DEBUG_DESC_WIDE_ALWAYS) ||
+                            (pt.feat_hint > 0 && pt.feat_hint <= ctx->wide_desc_max));
     HIPCHK(ctx, sgk::launch_orientation(pyr, pt.mask.as<uint32_t>(), pt.row_base.as<uint32_t>(),
                                         pt.total_rows, n_cand_dev, (int)nc, cand_grid, fp,
                                         pt.cand.as<float4>(), pt.info.as<int2>(),
@@ -826,17 +883,31 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
                                    pt.feat.as<float4>(), pt.feat_info.as<int2>(),
                                    pt.keys.as<float4>(), st, &io));
     HIPCHK(ctx, rec(4, st));
+    // one image with registered host buffers: its keys, descriptors and count record go straight
+    // to the host (enqueue_readback then copies nothing) -- from the workgroup-per-feature
+    // descriptor kernel itself when it runs (written over the host link while it computes), else
+    // by k_copy_out after it
+    pt.copied_out = ctx->host_out.active && pt.one_stream && n == 1 && ctx->nparts == 1;
+    const bool exact_desc = ctx->debug_flags & SGPU_DEBUG_EXACT_DESCRIPTOR;
+    const bool dual_desc = ctx->debug_flags & SGPU_DEBUG_DESC_DUAL;
+    const bool host_in_desc = pt.copied_out && O.descriptors && desc_wide && !exact_desc && !dual_desc;
+    sgk::HostCopy hcopy;
+    if (host_in_desc) {
+        hcopy.keys = pt.keys.as<float4>();
+        hcopy.rec = pt.img_off_dev.as<int64_t>();
+        hcopy.rec_n = n + 2;
+        hcopy.cap = (uint32_t)ctx->host_out.cap;
+        hcopy.hkeys = reinterpret_cast<float4*>(ctx->host_out.keys);
+        hcopy.hdesc = ctx->host_out.desc;
+        hcopy.hrec = pt.h_read;
+    }
     if (O.descriptors)
         HIPCHK(ctx, sgk::launch_descriptor(pyr, pt.feat.as<float4>(), pt.feat_info.as<int2>(),
                                            n_feat_dev, feat_grid, fp, pt.desc.as<float>(), st,
-                                           nullptr, false,
-                                           ctx->debug_flags & SGPU_DEBUG_EXACT_DESCRIPTOR,
-                                           ctx->debug_flags & SGPU_DEBUG_DESC_DUAL));
+                                           nullptr, false, exact_desc, dual_desc, desc_wide,
+                                           host_in_desc ? &hcopy : nullptr));
     HIPCHK(ctx, rec(5, st));
-    // one image with registered host buffers: its keys, descriptors and count record go straight
-    // to the host (enqueue_readback then copies nothing)
-    pt.copied_out = ctx->host_out.active && pt.one_stream && n == 1 && ctx->nparts == 1;
-    if (pt.copied_out)
+    if (pt.copied_out && !host_in_desc)
         HIPCHK(ctx, sgk::launch_copy_out(pt.keys.as<float4>(), O.descriptors ? pt.desc.as<float>() : nullptr,
                                          n_feat_dev, ctx->host_out.cap, pt.img_off_dev.as<int64_t>(),
                                          n + 2, ctx->host_out.keys,
@@ -1065,12 +1136,14 @@ static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, i
 static int extract_impl(sgpu_ctx* ctx, const void* images, bool is_f32, int n, int w, int h,
                         int stride, int flags, int color = 0) {
     if (!ctx) return SGPU_EINVAL;
-    const int rc_args = check_extract_args(ctx, images, is_f32, n, w, h, stride, flags, color);
-    if (rc_args != SGPU_OK) return rc_args;
-    // a registered host output serves this extract only, and only one image
-    ctx->host_out.active = ctx->host_out.armed && n == 1;
+    // a registered host output serves this extract only (consumed even when the extract is
+    // rejected: ADVICE r05), and only one image
+    const bool armed = ctx->host_out.armed;
     ctx->host_out.armed = false;
     ctx->host_out.done = false;
+    const int rc_args = check_extract_args(ctx, images, is_f32, n, w, h, stride, flags, color);
+    if (rc_args != SGPU_OK) return rc_args;
+    ctx->host_out.active = armed && n == 1;
     const int rc = extract_body(ctx, images, is_f32, n, w, h, stride, flags, color);
     ctx->host_out.done = rc == SGPU_OK && ctx->host_out.active && ctx->nparts == 1 &&
                          ctx->part[0].copied_out;

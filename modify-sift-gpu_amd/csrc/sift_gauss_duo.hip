@@ -585,8 +585,9 @@ __global__ __launch_bounds__(64 * kDuoWaves) __attribute__((amdgpu_waves_per_eu(
     duo_wave<FWA, FWB, NIN, U8, DS>(J, gw, s_in_all[wave], s_mid_all[wave]);
 }
 
-// input row pairs in LDS: the DMA runs NIN - 1 steps ahead (compiled: 5 and 7; SGPU_DUO_NIN
-// picks one, A/B hook)
+// input row pairs in LDS: the DMA runs NIN - 1 steps ahead (compiled: 4, 5 and 7; SGPU_DUO_NIN
+// picks one, A/B hook).  NIN 7 and 5 (52,224 / 41,984 B per workgroup) leave 3 workgroups per
+// CU, NIN 4 (36,864 B) 4
 #ifndef SGK_DUO_NIN
 #define SGK_DUO_NIN 7
 #endif
@@ -595,7 +596,7 @@ static int duo_nin() {
         const char* e = getenv("SGPU_DUO_NIN");
         return e ? atoi(e) : SGK_DUO_NIN;
     }();
-    return v == 5 ? 5 : 7;
+    return v == 5 ? 5 : v == 4 ? 4 : 7;
 }
 static int duo_bands_env() {
     static const int v = [] {
@@ -662,6 +663,8 @@ hipError_t duo_launch(const LevelOp& a, const LevelOp& b, hipStream_t stream, in
         hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 2, true, DS>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
     else if (duo_nin() == 5)
         hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 5, false, DS>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
+    else if (duo_nin() == 4)   // 36,864 B of LDS per workgroup: 4 workgroups (16 waves) per CU
+        hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 4, false, DS>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
     else
         hipLaunchKernelGGL((k_gauss_duo<FWA, FWB, 7, false, DS>), dim3(nb), dim3(64 * kDuoWaves), 0, stream, J);
     return hipGetLastError();

@@ -99,6 +99,16 @@ bool gauss_duo_supported(const LevelOp& a, const LevelOp& b);
 hipError_t launch_gauss_duo(const LevelOp& a, const LevelOp& b, hipStream_t stream, int rows_hint,
                             float* trash);
 
+// One level in 2-D tiles (sift_gauss_tile.hip): a workgroup loads its 64 x 32 output tile's
+// whole input window at once, H pass into LDS, V pass from LDS -- for cache-resident levels (one
+// image: the wave walk of k_gauss_lean is a chain of load latencies there).  Bit-identical to
+// launch_gauss_op.  launch_gauss_tile_two: two independent levels in one launch (the diagonal
+// schedule's compiled width pairs), else two launches (*launches says which).
+bool gauss_tile_supported(const LevelOp& op);
+hipError_t launch_gauss_tile(const LevelOp& op, hipStream_t stream);
+hipError_t launch_gauss_tile_two(const LevelOp& a, const LevelOp& b, hipStream_t stream,
+                                 int* launches = nullptr);
+
 // First octave of -fo != 0 (BuildPyramid, PyramidCU.cpp:1011-1016): the batch's input
 // (u8 p/255 or f32; tw = w & ~3 columns used, rows `stride` apart) resampled into dst
 // (dw x dh per image, dst_img_stride apart): SampleImageD by 2^fo for fo > 0, UpsampleKernel
@@ -166,11 +176,25 @@ hipError_t launch_copy_out(const float4* keys, const float* desc, const uint32_t
 // keys_have_orientation == -1 (feat = (x, y, width, height) in octave coordinates).
 // exact: the reference's per-bin fma order and the oracle's transcendentals (bit-identical to the
 // oracle; the test mode); otherwise the relaxed-order pixel-parallel kernel k_descriptor_flat
-// (L2 ~1e-6 from the oracle), or with dual the round-4 dual-cell kernel (A/B).
+// (L2 ~1e-6 from the oracle), or with dual the round-4 dual-cell kernel (A/B).  wide: the
+// relaxed-order kernel with a workgroup of 4 waves per feature (k_descriptor_wide, for few
+// features; the grid is then one workgroup per feature up to n_feat_cap) -- the same bits.
+// host (wide only): keys[e], descriptor row e (e < cap) and the rec_n (<= 256) int64 words of rec
+// also to page-locked host memory, in place of a launch_copy_out after the kernel.
+struct HostCopy {
+    const float4* keys = nullptr;
+    const int64_t* rec = nullptr;
+    int rec_n = 0;
+    uint32_t cap = 0;
+    float4* hkeys = nullptr;
+    float* hdesc = nullptr;
+    int64_t* hrec = nullptr;
+};
 hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* feat_info,
                              const uint32_t* n_feat_dev, int n_feat_cap, const FeatureParams& fp,
                              float* desc, hipStream_t stream, const int* out_index = nullptr,
-                             bool rect = false, bool exact = false, bool dual = false);
+                             bool rect = false, bool exact = false, bool dual = false,
+                             bool wide = false, const HostCopy* host = nullptr);
 
 // Caller-supplied keypoints: strongest orientation into feat[e].w (num_orientation != 0, else
 // 0) and the image-coordinate key at keys_out[index[e]].

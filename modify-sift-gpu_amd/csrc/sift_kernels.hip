@@ -2480,11 +2480,13 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
     return v;
 }
 
-__device__ __forceinline__ void descriptor_flat(uint32_t e, int lane, const float* __restrict__ pyr,
+// The accumulation of feature e's window into the histogram at sh (kFlatWords floats): wave wv
+// of nwv takes the window's 64-pixel steps wv, wv + nwv, ... (every step when nwv = 1).
+__device__ __forceinline__ void flat_accumulate(uint32_t e, int lane, const float* __restrict__ pyr,
                                                 const float4* __restrict__ feat,
                                                 const int2* __restrict__ feat_info,
-                                                const FeatureParams& fp, float* __restrict__ desc,
-                                                uint32_t out, float* __restrict__ sh) {
+                                                const FeatureParams& fp, float* __restrict__ sh,
+                                                int wv, int nwv) {
     unsigned long long* hist = reinterpret_cast<unsigned long long*>(sh);   // kFlatHist
     // 36: (1 + ox', 1 - ox', 1 + oy', 1 - oy') of cell (i, j)
     float4* ctab = reinterpret_cast<float4*>(sh + 2 * kFlatHist);
@@ -2562,8 +2564,8 @@ __device__ __forceinline__ void descriptor_flat(uint32_t e, int lane, const floa
         const int incl = wave_incl_scan(len, lane);
         const int rs = incl - len;                                   // row L's first pixel index
         const int total = __builtin_amdgcn_readlane(incl, kFlatRows - 1);
-        int rcur = 0;   // the row of pixel `base` (uniform)
-        for (int base = 0; base < total; base += 64) {
+        int rcur = 0;   // a row at or before pixel `base`'s (uniform)
+        for (int base = 64 * wv; base < total; base += 64 * nwv) {
             const int p = base + lane;
             const bool valid = p < total;
             // pixel p's row: rcur + the rows after it starting at or before p (their starts read
@@ -2636,15 +2638,27 @@ __device__ __forceinline__ void descriptor_flat(uint32_t e, int lane, const floa
         }
         asm volatile("" ::: "memory");
     }
-    // cell (ix, iy) = lane >> 2, bins 2 sub, 2 sub + 1: the copies summed in order
+}
+
+// The descriptor from nh histograms (kFlatWords floats apart from sh on): cell (ix, iy) =
+// lane >> 2, bins 2 sub, 2 sub + 1, every copy of every histogram summed as 64-bit integers --
+// the same totals however the window's pixels were split over waves and copies -- then
+// normalised (NormalizeDescriptor, ProgramCU.cu:1173-1208) and stored as row `out`.
+__device__ __forceinline__ void flat_finish(int lane, const FeatureParams& fp,
+                                            float* __restrict__ desc, uint32_t out,
+                                            const float* __restrict__ sh, int nh,
+                                            float* __restrict__ hdesc = nullptr) {
     const int cell = lane >> 2, sub = lane & 3;
     const int ix = cell & 3, iy = cell >> 2;
-    const unsigned long long* hc = hist + ((iy * 4 + ix) * 8 + 2 * sub) * kFlatStride;
-    unsigned long long s0 = hc[0], s1 = hc[kFlatStride];
+    unsigned long long s0 = 0, s1 = 0;
+    for (int w = 0; w < nh; w++) {
+        const unsigned long long* hc = reinterpret_cast<const unsigned long long*>(sh + w * kFlatWords) +
+                                       ((iy * 4 + ix) * 8 + 2 * sub) * kFlatStride;
 #pragma unroll
-    for (int k = 1; k < kFlatCopies; k++) {
-        s0 += hc[k];
-        s1 += hc[kFlatStride + k];
+        for (int k = 0; k < kFlatCopies; k++) {
+            s0 += hc[k];
+            s1 += hc[kFlatStride + k];
+        }
     }
     float b0 = (float)((double)(long long)s0 * 0x1p-32), b1 = (float)((double)(long long)s1 * 0x1p-32);
     asm volatile("" ::: "memory");
@@ -2663,6 +2677,17 @@ __device__ __forceinline__ void descriptor_flat(uint32_t e, int lane, const floa
         b1 *= n2;
     }
     *reinterpret_cast<float2*>(desc + (size_t)out * 128 + cell * 8 + sub * 2) = make_float2(b0, b1);
+    if (hdesc)   // the row also to page-locked host memory (sgpu_set_host_output)
+        *reinterpret_cast<float2*>(hdesc + (size_t)out * 128 + cell * 8 + sub * 2) = make_float2(b0, b1);
+}
+
+__device__ __forceinline__ void descriptor_flat(uint32_t e, int lane, const float* __restrict__ pyr,
+                                                const float4* __restrict__ feat,
+                                                const int2* __restrict__ feat_info,
+                                                const FeatureParams& fp, float* __restrict__ desc,
+                                                uint32_t out, float* __restrict__ sh) {
+    flat_accumulate(e, lane, pyr, feat, feat_info, fp, sh, 0, 1);
+    flat_finish(lane, fp, desc, out, sh, 1);
 }
 
 // waves per SIMD the allocation must allow: 8 (64 VGPRs, no spills): 1.448-1.451 ms per
@@ -2690,6 +2715,39 @@ __global__ __launch_bounds__(256) SGK_FLAT_ATTR void k_descriptor_flat(const flo
     for (uint32_t e = blockIdx.x * 4 + wave; e < n; e += gridDim.x * 4)
         descriptor_flat(e, lane, pyr, feat, feat_info, fp, desc,
                         out_index ? (uint32_t)out_index[e] : e, s_flat[wave]);
+}
+
+// A workgroup of 4 waves per feature, for few features (one image: ~1,500 features are ~1.5 waves
+// per SIMD under one wave each, and each wave walks its window alone).  The waves take every
+// fourth 64-pixel step of the window into histograms of their own; wave 0 sums all of them.  The
+// sums are integers, so the descriptor is k_descriptor_flat's bit for bit, in any batch.
+__global__ __launch_bounds__(256) SGK_FLAT_ATTR void k_descriptor_wide(const float* __restrict__ pyr,
+                                                         const float4* __restrict__ feat,
+                                                         const int2* __restrict__ feat_info,
+                                                         const uint32_t* __restrict__ n_feat_dev,
+                                                         const FeatureParams fp,
+                                                         float* __restrict__ desc,
+                                                         const int* __restrict__ out_index,
+                                                         const HostCopy hc) {
+    __shared__ __attribute__((aligned(16))) float s_flat[4][kFlatWords];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t n = *n_feat_dev;
+    // host output (one image, sgpu_set_host_output): the count record, the first cap keys and
+    // descriptors also go to page-locked host memory from here -- written over the host link
+    // while the descriptors are computed, instead of by a k_copy_out launch after them
+    if (hc.hrec && blockIdx.x == 0 && threadIdx.x < (unsigned)hc.rec_n) hc.hrec[threadIdx.x] = hc.rec[threadIdx.x];
+    for (uint32_t e = blockIdx.x; e < n; e += gridDim.x) {   // uniform per workgroup
+        flat_accumulate(e, lane, pyr, feat, feat_info, fp, s_flat[wave], wave, 4);
+        __syncthreads();
+        const uint32_t out = out_index ? (uint32_t)out_index[e] : e;
+        const bool to_host = hc.hkeys && out < hc.cap;
+        if (wave == 0)
+            flat_finish(lane, fp, desc, out, &s_flat[0][0], 4, to_host ? hc.hdesc : nullptr);
+        else if (wave == 1 && lane == 0 && to_host)
+            hc.hkeys[out] = hc.keys[e];
+        __syncthreads();   // wave 0 has read every histogram before the next feature zeroes them
+    }
 }
 
 // One wave per feature, grid-stride over the features (count read on the device).
@@ -3185,8 +3243,11 @@ hipError_t launch_orient_keys(const float* pyr, float4* feat, const int2* feat_i
 hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* feat_info,
                              const uint32_t* n_feat_dev, int n_feat_cap, const FeatureParams& fp,
                              float* desc, hipStream_t stream, const int* out_index,
-                             bool rect, bool exact, bool dual) {
+                             bool rect, bool exact, bool dual, bool wide, const HostCopy* host) {
     if (n_feat_cap <= 0) return hipSuccess;
+    if (host && (!wide || exact || rect || dual || host->rec_n < 0 || host->rec_n > 256 ||
+                 !host->hkeys || !host->hrec || !host->keys || !host->rec))
+        return hipErrorInvalidValue;   // only the workgroup-per-feature kernel writes the host
     const unsigned grid = (unsigned)std::min(((long long)n_feat_cap + 3) / 4, 65536LL);
 #ifndef SGK_DESC_DUAL
 #define SGK_DESC_DUAL 1
@@ -3194,6 +3255,12 @@ hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* f
 #ifndef SGK_DESC_FLAT
 #define SGK_DESC_FLAT 1
 #endif
+    if (!exact && !rect && SGK_DESC_FLAT && !dual && wide) {
+        const unsigned wgrid = (unsigned)std::min((long long)n_feat_cap, 65536LL);
+        hipLaunchKernelGGL(k_descriptor_wide, dim3(wgrid), dim3(256), 0, stream, pyr, feat,
+                           feat_info, n_feat_dev, fp, desc, out_index, host ? *host : HostCopy{});
+        return hipGetLastError();
+    }
     if (!exact && !rect && SGK_DESC_FLAT && !dual) {
         hipLaunchKernelGGL(k_descriptor_flat, dim3(grid), dim3(256), 0, stream, pyr, feat,
                            feat_info, n_feat_dev, fp, desc, out_index);

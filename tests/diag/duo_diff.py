@@ -29,7 +29,7 @@ for (n, w, h, seed, rows) in [(1, 104, 33, 5, 0), (1, 640, 480, 1000, 0), (1, 10
     opts = default_options()
     ctx.set_options(opts)
     # the paired run first, on buffers laid out for the previous case's size
-    ctx.set_debug_flags((rows << 16) | DUO)
+    ctx.set_debug_flags((rows << sgpu.SiftContext.DEBUG_BAND_SHIFT) | DUO)
     ctx.extract(imgs)
     got = levels(0, opts)
     ctx.set_debug_flags(OFF)

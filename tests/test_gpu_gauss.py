@@ -62,7 +62,7 @@ def test_wave_levels_equal_block_kernel(gpu_ctx, rows, n, w, h):
     try:
         # the shipped k_gauss_lean with the forced band height
         for kernel in (0,):
-            gpu_ctx.set_debug_flags((rows << 16) | kernel)
+            gpu_ctx.set_debug_flags((rows << sgpu.SiftContext.DEBUG_BAND_SHIFT) | kernel)
             gpu_ctx.extract(imgs)
             got = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
             for a, b in zip(ref, got):
@@ -175,7 +175,7 @@ def test_duo_levels_equal_single_level(gpu_ctx, rows, n, w, h):
         gpu_ctx.extract(imgs)
         ref = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
         k_ref = [gpu_ctx.features(i)[0].copy() for i in range(n)]
-        gpu_ctx.set_debug_flags((rows << 16) | DUO)
+        gpu_ctx.set_debug_flags((rows << sgpu.SiftContext.DEBUG_BAND_SHIFT) | DUO)
         gpu_ctx.extract(imgs)
         got = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
         for a, b in zip(ref, got):
@@ -203,5 +203,117 @@ def test_duo_levels_vs_oracle(gpu_ctx, w, h, seed):
                 g = gpu_ctx.gaussian(0, o, lvl)
                 r = O.gaussian(img, o, lvl, opts)
                 assert np.array_equal(_bits(g), _bits(r)), (o, lvl)
+    finally:
+        gpu_ctx.set_debug_flags(0)
+
+
+TILE = sgpu.SiftContext.DEBUG_GAUSS_TILE_ALWAYS
+TILE_OFF = sgpu.SiftContext.DEBUG_GAUSS_TILE_OFF
+
+
+# sizes: tiny (one tile with every edge), ragged (width not a multiple of 64, height not of 32),
+# 1080p (C2's image: every level tiled by default), a tall ragged batch, C4's 4096^2 x 6 octaves
+@pytest.mark.parametrize("n,w,h,no", [(2, 16, 16, -1), (3, 203, 97, -1), (1, 1920, 1080, 4),
+                                      (2, 300, 1203, -1), (1, 4096, 4096, 6)])
+def test_tile_levels_equal_wave_kernel(gpu_ctx, n, w, h, no):
+    """The 2-D tile kernel (k_gauss_tile / k_gauss_tile_diag, sift_gauss_tile.hip: a workgroup's
+    whole input window loaded at once, H pass into LDS, V pass from LDS) for every level against
+    the wave-streaming kernels (SGPU_DEBUG_GAUSS_TILE_OFF): every level of every octave and every
+    keypoint, bit for bit -- including the u8 ingest level and the decimating levels."""
+    imgs = synth_batch(n, w, h, 170 + w % 13)
+    opts = default_options(octave_num=no) if no > 0 else default_options()
+    gpu_ctx.set_options(opts)
+    try:
+        gpu_ctx.set_debug_flags(TILE_OFF)
+        gpu_ctx.extract(imgs)
+        ref = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
+        k_ref = [gpu_ctx.features(i)[0].copy() for i in range(n)]
+        for flags in (TILE, TILE | gpu_ctx.DEBUG_PYR_SERIAL, 0):
+            gpu_ctx.set_debug_flags(flags)
+            gpu_ctx.extract(imgs)
+            got = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
+            for a, b in zip(ref, got):
+                for o, (la, lb) in enumerate(zip(a, b)):
+                    for lvl, (x, y) in enumerate(zip(la, lb)):
+                        assert np.array_equal(_bits(x), _bits(y)), (flags, o, lvl)
+            for i in range(n):
+                assert np.array_equal(_bits(gpu_ctx.features(i)[0]), _bits(k_ref[i])), flags
+    finally:
+        gpu_ctx.set_debug_flags(0)
+        gpu_ctx.set_options(default_options())
+
+
+# every filter width 5 .. 33 (as test_lean_levels_all_widths), first octaves -1 / 0 / 1 (the
+# float first level after the resampling), float input
+@pytest.mark.parametrize("over", [dict(dog_level_num=1), dict(dog_level_num=2),
+                                  dict(dog_level_num=5), dict(filter_width_factor=5.5),
+                                  dict(filter_width_factor=2.0), dict(octave_min=-1),
+                                  dict(octave_min=1)])
+def test_tile_levels_all_widths(gpu_ctx, over):
+    imgs = synth_batch(2, 517, 389, 77)
+    opts = default_options(**over)
+    gpu_ctx.set_options(opts)
+    try:
+        gpu_ctx.set_debug_flags(TILE_OFF)
+        gpu_ctx.extract(imgs)
+        ref = [_levels(gpu_ctx, i, opts) for i in (0, 1)]
+        gpu_ctx.set_debug_flags(TILE)
+        gpu_ctx.extract(imgs)
+        got = [_levels(gpu_ctx, i, opts) for i in (0, 1)]
+        for a, b in zip(ref, got):
+            for o, (la, lb) in enumerate(zip(a, b)):
+                for lvl, (x, y) in enumerate(zip(la, lb)):
+                    assert np.array_equal(_bits(x), _bits(y)), (o, lvl)
+        fimgs = (imgs.astype(np.float32) / np.float32(255.0)).astype(np.float32)
+        gpu_ctx.extract(fimgs[1])
+        got_f = [[gpu_ctx.gaussian(0, o, lvl).copy() for lvl in range(opts.dog_level_num + 3)]
+                 for o in range(len(gpu_ctx.geometry()))]
+        gpu_ctx.set_debug_flags(TILE_OFF)
+        gpu_ctx.extract(fimgs[1])
+        for o in range(len(got_f)):
+            for lvl in range(opts.dog_level_num + 3):
+                assert np.array_equal(_bits(gpu_ctx.gaussian(0, o, lvl)), _bits(got_f[o][lvl])), (o, lvl)
+    finally:
+        gpu_ctx.set_debug_flags(0)
+        gpu_ctx.set_options(default_options())
+
+
+@pytest.mark.parametrize("w,h,seed", [(640, 480, 1000), (1921, 1081, 5)])
+def test_tile_levels_vs_oracle(gpu_ctx, w, h, seed):
+    """k_gauss_tile's levels (the shipped single-image path) against the oracle (FilterH /
+    FilterV, ProgramCU.cu:115-222), every level of every octave."""
+    img = synth_image(w, h, seed)
+    opts = default_options()
+    gpu_ctx.set_options(opts)
+    gpu_ctx.set_debug_flags(TILE)
+    try:
+        gpu_ctx.extract(img)
+        for o in range(len(gpu_ctx.geometry())):
+            for lvl in range(opts.dog_level_num + 3):
+                g = gpu_ctx.gaussian(0, o, lvl)
+                r = O.gaussian(img, o, lvl, opts)
+                assert np.array_equal(_bits(g), _bits(r)), (o, lvl)
+    finally:
+        gpu_ctx.set_debug_flags(0)
+
+
+def test_debug_flags_do_not_alias_band_field(gpu_ctx):
+    """the descriptor-kernel flag used to share bit 16 with the band-height field.
+    Every flag bit now lies below SGPU_DEBUG_BAND_SHIFT, and a forced band height leaves the
+    descriptor kernel alone: same descriptors with and without (8 << shift)."""
+    C = sgpu.SiftContext
+    flags = [v for k, v in vars(C).items() if k.startswith("DEBUG_") and k != "DEBUG_BAND_SHIFT"]
+    assert all(0 < f < (1 << C.DEBUG_BAND_SHIFT) for f in flags)
+    assert len(set(flags)) == len(flags)
+    img = synth_image(640, 480, 31)
+    gpu_ctx.set_options(default_options())
+    try:
+        gpu_ctx.set_debug_flags(0)
+        gpu_ctx.extract(img)
+        k0, d0 = gpu_ctx.features(0)
+        gpu_ctx.set_debug_flags(8 << C.DEBUG_BAND_SHIFT)
+        gpu_ctx.extract(img)
+        k1, d1 = gpu_ctx.features(0)
+        assert np.array_equal(_bits(k0), _bits(k1)) and np.array_equal(_bits(d0), _bits(d1))
     finally:
         gpu_ctx.set_debug_flags(0)

@@ -703,6 +703,33 @@ def test_rect_keypoints_vs_oracle(gpu_ctx, over):
     gpu_ctx.set_options(default_options())
 
 
+@pytest.mark.parametrize("n,w,h", [(1, 1920, 1080), (6, 640, 480)])
+def test_wide_descriptor_equals_flat(gpu_ctx, n, w, h):
+    """k_descriptor_wide (a workgroup of 4 waves per feature, each wave every fourth 64-pixel step
+    of the window, the histograms' 64-bit integer sums merged by wave 0; the shipped form for few
+    features) against k_descriptor_flat (one wave per feature): every descriptor bit for bit, in
+    a single image and in a batch, normalised and -unn."""
+    imgs = synth_batch(n, w, h, 710 + n)
+    for opts in (default_options(), default_options(normalized=0)):
+        gpu_ctx.set_options(opts)
+        try:
+            gpu_ctx.set_debug_flags(gpu_ctx.DEBUG_DESC_WIDE_OFF)
+            gpu_ctx.extract(imgs)
+            ref = [gpu_ctx.features(i) for i in range(n)]
+            gpu_ctx.set_debug_flags(gpu_ctx.DEBUG_DESC_WIDE_ALWAYS)
+            gpu_ctx.extract(imgs)
+            got = [gpu_ctx.features(i) for i in range(n)]
+            total = 0
+            for (ka, da), (kb, db) in zip(ref, got):
+                assert np.array_equal(_bits(ka), _bits(kb))
+                assert np.array_equal(_bits(da), _bits(db))
+                total += len(ka)
+            assert total > 500
+        finally:
+            gpu_ctx.set_debug_flags(0)
+            gpu_ctx.set_options(default_options())
+
+
 @pytest.mark.parametrize("over", [{}, {"max_orientation": 1}, {"fixed_orientation": 1},
                                   {"circular_window": 1}, {"keep_extremum_sign": 1},
                                   {"subpixel": 0}, {"octave_min": -1}])
