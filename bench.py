@@ -80,6 +80,10 @@ def main():
                     help="skip the single-image drop-in API measurement (speed.cpp protocol)")
     ap.add_argument("--no-match", action="store_true")
     ap.add_argument("--match-n", type=int, default=50000)
+    ap.add_argument("--verify", action="store_true",
+                    help="after the timed steps: every rank all-gathers (feature count, 64-bit "
+                         "digest of keys + descriptors) per image, rank 0 recomputes a sample of "
+                         "the other ranks' images on its own GPU and compares (SURVEY.md 4 (vi))")
     ap.add_argument("--dist-backend", default="rccl", choices=["rccl", "gloo"],
                     help="rccl: the count all-gather runs on RCCL over xGMI inside libsiftgpu "
                          "(the real run); gloo: host all-gather (rehearsal: ranks may then "
@@ -193,6 +197,28 @@ def main():
         dist.all_reduce(f)
         feats = int(f.item())
 
+    verify = None
+    if args.verify:
+        # outside the timed region: the last step's results of every image of every rank, as
+        # (count, digest) records, one all-gather (RCCL over xGMI, or gloo in a rehearsal); rank
+        # 0 extracts a sample of the other ranks' images itself (a batch of its own: batch
+        # composition changes no bit, tests/test_gpu_parity.py) and compares the records
+        from sift_dist import image_digest, verify_sample, verify_records, gather_records
+        recs = np.array([image_digest(*ctx.features(i)) for i in range(B)], np.int32)
+        if rccl:
+            allrec = ctx.allgather_i32(recs.reshape(-1), world).reshape(-1, 3)
+        elif dist is not None:
+            allrec = gather_records(recs, dist)
+        else:
+            allrec = recs
+        if rank == 0:
+            sample = verify_sample(world, B, 2)
+            seed0 = 4000 if args.workload == "c4" else 3000
+            simgs = np.stack([synth_batch_fast(1, W, H, seed0 + g)[0] for g in sample])
+            ctx.extract(simgs)
+            verify = verify_records(allrec, {g: image_digest(*ctx.features(k))
+                                             for k, g in enumerate(sample)})
+
     # level filters and their kernel launches, as the library ran them (the diagonal schedule
     # shares launches between octaves, the paired-level kernel filters two levels per launch;
     # DESIGN.md 4.3-4.5)
@@ -289,6 +315,8 @@ def main():
             result["match_sharded"] = sm
     if c2 is not None:
         result["c2"] = c2
+    if verify is not None:
+        result["verify"] = verify
     if rank == 0 and not args.no_cpu_baseline:
         # rank 0 on the host cores beside its GPU work, for every N (the line is self-contained)
         result["cpu_baseline"] = cpu_baseline(imgs, opts)

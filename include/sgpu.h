@@ -284,7 +284,7 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
                                    (k_gauss_lean); both are bit-identical.  Bits
                                    SGPU_DEBUG_BAND_SHIFT.. of the flags, when not 0, force the
                                    wave kernel's band height in rows (test / tuning hook) */
-#define SGPU_DEBUG_BAND_SHIFT 20  /* band height field: (flags >> 20) & 0x7ff rows; the flag bits
+#define SGPU_DEBUG_BAND_SHIFT 20  /* band height field: (flags >> 20) & 0x7ff rows (< 2048); the flag bits
                                      below it never reach it (DESC_DUAL at 1 << 16
                                      used to share its bit with the band field) */
 #define SGPU_DEBUG_KEYED_MATCH 64 /* plain matching through the keyed epilogue (every value
@@ -297,9 +297,10 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
 #define SGPU_DEBUG_ORIENT_WAVE 512 /* orientation one wave per candidate for any count (the shipped
                                      path picks it for few candidates only): same bits */
 #define SGPU_DEBUG_GAUSS_TILE_ALWAYS 1024 /* every level through the 2-D tile kernel
-                                             (k_gauss_tile), whatever its size (the shipped path
+                                             (k_gauss_tile) and the extremum detection through
+                                             k_extrema_tile, whatever the size (the shipped path
                                              tiles levels of at most SGPU_GAUSS_TILE_MB, default
-                                             16 MB: a single image's): same levels */
+                                             16 MB: a single image's): same levels and keys */
 #define SGPU_DEBUG_MATCH_REGSTAGE 2048 /* keyless plain matching through the register-staged
                                           k_match_rows<..., RAW> instead of the LDS-DMA
                                           k_match_raw: same pairs */
@@ -323,6 +324,11 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
                                            same bits */
 #define SGPU_DEBUG_DESC_WIDE_ALWAYS 262144 /* descriptors one workgroup per feature for every
                                               count: same bits */
+#define SGPU_DEBUG_EXTREMA_TILE_OFF 524288 /* extremum detection always through the
+                                              wave-streaming k_extrema_wave2 (the shipped path
+                                              tiles cache-resident pyramids, k_extrema_tile;
+                                              SGPU_DEBUG_GAUSS_TILE_ALWAYS tiles every one) */
+
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);

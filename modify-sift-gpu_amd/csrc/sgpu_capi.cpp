@@ -162,6 +162,8 @@ struct sgpu_ctx {
     size_t wide_desc_max = SGK_WIDE_DESC_MAX;   // feature counts (of the previous call) up to which
                                            // descriptors run a workgroup per feature
                                            // (SGPU_WIDE_DESC_MAX)
+    bool tile_duo = false;                 // tile duos when every level is tiled (SGPU_TILE_DUO=on;
+                                           // measured slower)
     int tile_mb = SGK_TILE_MB;             // levels of at most this many MB: 2-D tile launches
                                            // (SGPU_GAUSS_TILE_MB; k_gauss_tile)
     int env_flags = 0;                     // debug flags set from the environment at creation
@@ -461,6 +463,11 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     }
     if (const char* ev = getenv("SGPU_WIDE_DESC_MAX"))
         if (atoll(ev) >= 0) ctx->wide_desc_max = (size_t)atoll(ev);
+    if (const char* ev = getenv("SGPU_EXTREMA")) {   // A/B hook of the tile extremum kernel
+        if (!strcmp(ev, "wave")) ctx->debug_flags |= SGPU_DEBUG_EXTREMA_TILE_OFF;
+    }
+    if (const char* ev = getenv("SGPU_TILE_DUO"))
+        ctx->tile_duo = !strcmp(ev, "on");
     if (const char* ev = getenv("SGPU_GAUSS_TILE_MB"))
         if (atoi(ev) >= 0) ctx->tile_mb = atoi(ev);
     ctx->env_flags = ctx->debug_flags;   // kept by sgpu_debug_set_flags (A/B runs of the probes)
@@ -728,7 +735,76 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
         }
     }
     pt.gauss_filters = (int)ops.size();
-    if (side || (ctx->debug_flags & SGPU_DEBUG_PYR_SERIAL) || kds < 1) {
+    // every level tiled (a cache-resident pyramid: one image, C2) and tile duos asked for
+    // (SGPU_TILE_DUO=on, or SGPU_DEBUG_DUO_ALWAYS with SGPU_DEBUG_GAUSS_TILE_ALWAYS): the tile-duo
+    // schedule -- octave
+    // 0 pairs levels (0, 1), (2, 3), (4, 5) into tile duos (two levels per launch from one load,
+    // sift_gauss_tile.hip), octaves >= 1 run level 1 alone and pair the rest; a job launches right
+    // after the job holding its input, and octave o+1's level 1 shares the launch of octave o's last
+    // duo (-no 4 -d 3: 9 launches instead of 15).  Measured slower than the single-level tiles of
+    // the diagonal schedule (C2 pyramid 115-119 vs 97-99 us: a duo tile's stage-1 halo region and
+    // its five barrier phases cost more than the launch and the level's round trip it saves,
+    // DESIGN.md 4.6), so not the default.
+    const bool want_duo = ctx->tile_duo || ((ctx->debug_flags & SGPU_DEBUG_DUO_ALWAYS) &&
+                                            (ctx->debug_flags & SGPU_DEBUG_GAUSS_TILE_ALWAYS));
+    bool all_tiled = want_duo && !side && !(ctx->debug_flags & SGPU_DEBUG_PYR_SERIAL) &&
+                     kds >= 1 && !ops.empty();
+    for (const Op& e : ops) all_tiled = all_tiled && tiled(e.op);
+    if (all_tiled) {
+        struct Job { size_t i0; int n, launch; };
+        std::vector<Job> jobs;
+        std::vector<int> job_of(ops.size(), -1);
+        auto op_index = [&](int o, int k) -> int {
+            for (size_t i = 0; i < ops.size(); i++)
+                if (ops[i].o == o && ops[i].k == k) return (int)i;
+            return -1;
+        };
+        for (size_t i = 0; i < ops.size();) {
+            const Op& e = ops[i];
+            const bool pair = e.k % 2 == 0 && i + 1 < ops.size() && ops[i + 1].o == e.o &&
+                              ops[i + 1].k == e.k + 1 &&
+                              sgk::gauss_tile_duo_supported(e.op, ops[i + 1].op);
+            jobs.push_back({i, pair ? 2 : 1, 0});
+            job_of[i] = (int)jobs.size() - 1;
+            if (pair) job_of[i + 1] = (int)jobs.size() - 1;
+            i += pair ? 2 : 1;
+        }
+        int last_launch = 0;
+        for (Job& jb : jobs) {
+            const Op& e = ops[jb.i0];
+            int dep = -1;   // the op writing this job's input level
+            if (e.k >= 2 || (e.k == 1 && e.o == 0)) dep = op_index(e.o, e.k - 1);
+            else if (e.k == 1) dep = op_index(e.o - 1, kds);
+            jb.launch = dep < 0 ? 0 : jobs[job_of[dep]].launch + 1;
+            last_launch = std::max(last_launch, jb.launch);
+        }
+        for (int L = 0; L <= last_launch; L++) {
+            std::vector<const Job*> in;
+            for (const Job& jb : jobs)
+                if (jb.launch == L) in.push_back(&jb);
+            size_t q = 0;
+            if (in.size() == 2 && in[0]->n != in[1]->n) {   // a duo beside a single level
+                const Job* d = in[0]->n == 2 ? in[0] : in[1];
+                const Job* o1 = in[0]->n == 2 ? in[1] : in[0];
+                int nl = 0;
+                HIPCHK(ctx, sgk::launch_gauss_tile_duo_one(ops[d->i0].op, ops[d->i0 + 1].op,
+                                                           ops[o1->i0].op, st, &nl));
+                pt.gauss_launches += nl;
+                q = 2;
+            } else if (in.size() == 2 && in[0]->n == 1 && in[1]->n == 1) {
+                int nl = 0;
+                HIPCHK(ctx, sgk::launch_gauss_tile_two(ops[in[0]->i0].op, ops[in[1]->i0].op, st, &nl));
+                pt.gauss_launches += nl;
+                q = 2;
+            }
+            for (; q < in.size(); q++) {
+                const Job& jb = *in[q];
+                if (jb.n == 2) HIPCHK(ctx, sgk::launch_gauss_tile_duo(ops[jb.i0].op, ops[jb.i0 + 1].op, st));
+                else HIPCHK(ctx, sgk::launch_gauss_tile(ops[jb.i0].op, st));
+                pt.gauss_launches++;
+            }
+        }
+    } else if (side || (ctx->debug_flags & SGPU_DEBUG_PYR_SERIAL) || kds < 1) {
         // octave by octave, one level per launch (octaves >= 1 on the side stream in the
         // stream layout)
         for (const Op& e : ops) {
@@ -827,8 +903,12 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
     if (!pt.one_stream)
         HIPCHK(ctx, sgk::launch_zero(pt.row_count.as<uint32_t>(), (size_t)pt.total_rows,
                                      pt.mask.as<uint32_t>(), (size_t)moff, nullptr, 0, st));
+    // a cache-resident pyramid (the same size rule as the level tiles): the tile extremum kernel
+    const bool ext_tiles = !(ctx->debug_flags & SGPU_DEBUG_EXTREMA_TILE_OFF) &&
+                           ((ctx->debug_flags & SGPU_DEBUG_GAUSS_TILE_ALWAYS) ||
+                            4ll * fp.oct[0].wa * fp.oct[0].h * n <= ((long long)ctx->tile_mb << 20));
     HIPCHK(ctx, sgk::launch_extrema(pyr, pt.mask.as<uint32_t>(), pt.row_count.as<uint32_t>(),
-                                    fp, st));
+                                    fp, st, ext_tiles));
     if (O.feature_count_threshold > 0)   // -tc: GenerateFeatureList skip + LimitFeatureCount(0)
         HIPCHK(ctx, sgk::launch_limit_rows(pt.row_count.as<uint32_t>(), fp,
                                            O.feature_count_threshold, O.truncate_method, st));

@@ -80,6 +80,8 @@ struct TileJob {
     float* ds;              // the next octave's level 0 (DS), rows dsw apart
     int dsw, dsh;
     long long ds_img;
+    float* dst2;            // tile duo: level k+2 (dst: level k+1; same geometry and strides)
+    Taps taps2;             // tile duo: the second filter
     int tx, ty;             // tiles per row / per column
     int nblocks;            // tx * ty * batch
     ZeroJob zero;           // buffers this launch zeroes besides filtering (the extract's first)
@@ -107,22 +109,15 @@ __device__ __forceinline__ void tile_zero(const ZeroJob& z) {
         }
 }
 
-// One 64 x 32 output tile (logical block lb of job J) with the workgroup's LDS `smem`.
-template <int FW, bool U8, bool DS>
-__device__ __forceinline__ void tile_block(const TileJob& J, int lb, char* smem) {
-    using G = TileGeom<FW>;
-    constexpr int HALF = G::HALF, OFF = G::OFF, NQ = G::NQ, SH = G::SH, IN_S = G::IN_S, HS = G::HS;
-    f2v* s_in = reinterpret_cast<f2v*>(smem);
-    float* s_h = reinterpret_cast<float*>(smem + G::IN_BYTES);
+// The input window of a tile into LDS row pairs: rows r0 .. r0 + 2 G::NPAIR - 1 and columns
+// a0 .. a0 + 4 G::NQ - 1 of the source (u8 -> p / 255), clamped to the image (clamp-to-edge);
+// column a0 + c lands at float2 index p G::IN_S + c + G::SH.  Every load is issued before any LDS
+// store (one round trip).
+template <class G, bool U8>
+__device__ __forceinline__ void tile_window(const TileJob& J, int b, int a0, int r0, f2v* s_in) {
+    constexpr int NQ = G::NQ, IN_S = G::IN_S, SH = G::SH;
     const int tid = threadIdx.x;
     const int W = J.W, H = J.H;
-    const int sx = lb % J.tx, rest = lb / J.tx;
-    const int ty = rest % J.ty, b = rest / J.ty;
-    const int x0 = sx * kTW, y0 = ty * kTH;
-    const int a0 = x0 - HALF - OFF;   // input column of LDS column SH (16-B aligned)
-    const int r0 = y0 - HALF;         // input row of window row 0
-
-    // ---- the window: every load issued before any LDS store (one round trip)
     struct Raw { float4 v0, v1; };   // rows 2p, 2p+1 of one quad (u8: .x holds the 4 bytes)
     Raw raw[G::LITEMS];
     const float* sf = U8 ? nullptr : J.src + (long long)b * J.src_img;
@@ -181,18 +176,25 @@ __device__ __forceinline__ void tile_block(const TileJob& J, int lb, char* smem)
             for (int t = 0; t < 4; t++) q[t] = pr[t];
         }
     }
-    __syncthreads();
+}
 
-    // ---- H pass: window rows 2 hp, 2 hp + 1, tile columns hc .. hc + 3, taps t = 0 .. FW-1
+// The H pass of a width-FW filter over LDS row pairs s_in (stride IN_S float2, window column
+// c at c + SH, output column j reading window columns j + OFF + t): NP row pairs x NC columns
+// into s_h (rows HS floats apart), 2 rows x 4 columns per item, taps t = 0 .. FW-1 in order.
+template <int FW, int NP, int NC, int IN_S, int OFF, int SH, int HS>
+__device__ __forceinline__ void tile_hpass(const Taps& taps, const f2v* s_in, float* s_h) {
+    constexpr int NG = NC / 4, NH = NP * NG, ITEMS = (NH + kTT - 1) / kTT, NRD = (FW + 3) / 2;
+    static_assert(NC % 4 == 0 && (OFF + SH) % 2 == 0 && IN_S % 2 == 0, "16-B aligned reads");
+    const int tid = threadIdx.x;
 #pragma unroll
-    for (int i = 0; i < G::HITEMS; i++) {
+    for (int i = 0; i < ITEMS; i++) {
         const int item = tid + kTT * i;
-        if (G::NH % kTT != 0 && item >= G::NH) break;
-        const int hp = item >> 4, hc = (item & 15) * 4;
+        if (NH % kTT != 0 && item >= NH) break;
+        const int hp = item / NG, hc = (item - hp * NG) * 4;
         const f2v* h_rd = s_in + hp * IN_S + hc + OFF + SH;
         f2v a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
-        for (int q = 0; q < G::NRD; q++) {
+        for (int q = 0; q < NRD; q++) {
             const float4 v = reinterpret_cast<const float4*>(h_rd)[q];
             const f2v e[2] = {f2v{v.x, v.y}, f2v{v.z, v.w}};
 #pragma unroll
@@ -200,16 +202,28 @@ __device__ __forceinline__ void tile_block(const TileJob& J, int lb, char* smem)
                 const int m = 2 * q + u;
 #pragma unroll
                 for (int c = 0; c < 4; c++)
-                    if (m - c >= 0 && m - c < FW) a[c] = tpk(e[u], ttap<FW>(J.taps, m - c), a[c]);
+                    if (m - c >= 0 && m - c < FW) a[c] = tpk(e[u], ttap<FW>(taps, m - c), a[c]);
             }
         }
         float* h_wr = s_h + 2 * hp * HS + hc;
         *reinterpret_cast<float4*>(h_wr) = make_float4(a[0].x, a[1].x, a[2].x, a[3].x);
         *reinterpret_cast<float4*>(h_wr + HS) = make_float4(a[0].y, a[1].y, a[2].y, a[3].y);
     }
-    __syncthreads();
+}
 
-    // ---- V pass: tile rows vr .. vr + 3, columns vc, vc + 1
+// The output tile from a window already in LDS (s_in, TileGeom<FW>'s layout, window column c =
+// image column x0 - HALF - OFF + c): H pass into s_h, V pass, stores of level rows y0 .. y0 + 31
+// (and the decimation into the next octave's level 0).
+template <int FW, bool DS>
+__device__ __forceinline__ void tile_hv(const TileJob& J, const Taps& taps, float* dst, int b,
+                                        int x0, int y0, const f2v* s_in, float* s_h) {
+    using G = TileGeom<FW>;
+    constexpr int HS = G::HS;
+    tile_hpass<FW, G::NPAIR, kTW, G::IN_S, G::OFF, G::SH, HS>(taps, s_in, s_h);
+    __syncthreads();
+    // V pass: tile rows vr .. vr + 3, columns vc, vc + 1
+    const int tid = threadIdx.x;
+    const int W = J.W, H = J.H;
     const int vc = (tid & 31) * 2, vr = (tid >> 5) * 4;
     f2v acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
@@ -217,11 +231,11 @@ __device__ __forceinline__ void tile_block(const TileJob& J, int lb, char* smem)
         const f2v v = *reinterpret_cast<const f2v*>(s_h + (vr + m) * HS + vc);
 #pragma unroll
         for (int j = 0; j < 4; j++)
-            if (m - j >= 0 && m - j < FW) acc[j] = tpk(v, ttap<FW>(J.taps, m - j), acc[j]);
+            if (m - j >= 0 && m - j < FW) acc[j] = tpk(v, ttap<FW>(taps, m - j), acc[j]);
     }
     const int x = x0 + vc;
     if (x >= W) return;
-    float* d = J.dst + (long long)b * J.dst_img;
+    float* d = dst + (long long)b * J.dst_img;
     float* dd = DS ? J.ds + (long long)b * J.ds_img : nullptr;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -236,6 +250,135 @@ __device__ __forceinline__ void tile_block(const TileJob& J, int lb, char* smem)
                 for (int cc = W >> 1; cc < J.dsw; cc++) drow[cc] = acc[j].y;
         }
     }
+}
+
+// One 64 x 32 output tile (logical block lb of job J) with the workgroup's LDS `smem`.
+template <int FW, bool U8, bool DS>
+__device__ __forceinline__ void tile_block(const TileJob& J, int lb, char* smem) {
+    using G = TileGeom<FW>;
+    f2v* s_in = reinterpret_cast<f2v*>(smem);
+    float* s_h = reinterpret_cast<float*>(smem + G::IN_BYTES);
+    const int sx = lb % J.tx, rest = lb / J.tx;
+    const int ty = rest % J.ty, b = rest / J.ty;
+    const int x0 = sx * kTW, y0 = ty * kTH;
+    tile_window<G, U8>(J, b, x0 - G::HALF - G::OFF, y0 - G::HALF, s_in);
+    __syncthreads();
+    tile_hv<FW, DS>(J, J.taps, J.dst, b, x0, y0, s_in, s_h);
+}
+
+// ------------------------------------------------------------------------------------------
+// Two consecutive levels per tile ("tile duo"): levels k+1 = V(H(level k)) and k+2 from one load
+// of level k's window -- half the launches of a single image's pyramid and one level's HBM round
+// trip less.  Stage 1 filters level k into level k+1 over the region the FWB filter of stage 2
+// needs (the tile plus RB halo rows and columns, TileGeom<FWB>'s window), straight into LDS in
+// stage 2's row-pair layout, and stores the tile's own 64 x 32 of level k+1; stage 2 is the
+// single-level tile_hv on that region.  Clamp-to-edge of level k+1: its values at positions
+// outside the image are recomputed as copies of the edge row / column (in the edge tiles only),
+// exactly what stage 2 of a separate launch reads there.  Bit-identical to two launches: every
+// output is the same fma sequence of the same values.
+template <int FWA, int FWB>
+struct TileDuoGeom {
+    using GB = TileGeom<FWB>;
+    static constexpr int RA = FWA >> 1, RB = FWB >> 1;
+    static constexpr int MROWS = GB::ROWS;              // level k+1 rows y0 - RB .. (stage 2 window)
+    static constexpr int MC = 4 * GB::NQ;               // level k+1 columns aB .., aB = x0 - RB - GB::OFF
+    // the level-k window of stage 1: rows from y0 - RB - RA, columns from aB - RA - OFF
+    struct Win {
+        static constexpr int OFF = (-RA) & 3;
+        static constexpr int SH = OFF & 1;
+        static constexpr int NQ = (MC + FWA - 1 + OFF + 3) / 4;
+        static constexpr int IN_S0 = (4 * NQ + SH + 3) & ~3;
+        static constexpr int IN_S = IN_S0 + ((2 - IN_S0) & 31);
+        static constexpr int NPAIR = (MROWS + FWA - 1) / 2;
+        static constexpr int NLOAD = NPAIR * NQ;
+        static constexpr int LITEMS = (NLOAD + kTT - 1) / kTT;
+    };
+    static constexpr int H1S = MC + 4;                  // stage-1 H rows (floats)
+    static constexpr int R0 = Win::NPAIR * Win::IN_S * 8 > GB::IN_BYTES ? Win::NPAIR * Win::IN_S * 8
+                                                                         : GB::IN_BYTES;
+    static constexpr int H1B = 2 * Win::NPAIR * H1S * 4, H2B = GB::ROWS * GB::HS * 4;
+    static constexpr int LDS_BYTES = R0 + (H1B > H2B ? H1B : H2B);
+    static_assert(MROWS % 2 == 0 && MC % 4 == 0, "row pairs, quads");
+};
+
+template <int FWA, int FWB, bool U8, bool DSB>
+__device__ __forceinline__ void tile_duo_block(const TileJob& J, int lb, char* smem) {
+    using D = TileDuoGeom<FWA, FWB>;
+    using GB = typename D::GB;
+    using WG = typename D::Win;
+    constexpr int RB = D::RB, MC = D::MC, MROWS = D::MROWS, H1S = D::H1S;
+    f2v* s_w = reinterpret_cast<f2v*>(smem);             // level-k window, then level k+1 (GB layout)
+    float* s_h = reinterpret_cast<float*>(smem + D::R0);  // stage-1 H rows, then stage-2 H rows
+    const int tid = threadIdx.x;
+    const int W = J.W, H = J.H;
+    const int sx = lb % J.tx, rest = lb / J.tx;
+    const int ty = rest % J.ty, b = rest / J.ty;
+    const int x0 = sx * kTW, y0 = ty * kTH;
+    const int aB = x0 - RB - GB::OFF;   // level k+1 column of stage-2 window column 0
+    const int mr0 = y0 - RB;            // level k+1 row of stage-2 window row 0
+    tile_window<WG, U8>(J, b, aB - D::RA - WG::OFF, mr0 - D::RA, s_w);
+    __syncthreads();
+    // stage 1, H: every window row, level k+1 columns aB .. aB + MC - 1
+    tile_hpass<FWA, WG::NPAIR, MC, WG::IN_S, WG::OFF, WG::SH, H1S>(J.taps, s_w, s_h);
+    __syncthreads();
+    // stage 1, V: level k+1 rows 2 rp, 2 rp + 1 (stage-2 window rows), columns 2 cp, 2 cp + 1, into
+    // stage 2's row pairs; the tile's own 64 x 32 also to HBM
+    {
+        constexpr int NCP = MC / 2, NV = NCP * (MROWS / 2), ITEMS = (NV + kTT - 1) / kTT;
+        float* d1 = J.dst + (long long)b * J.dst_img;
+#pragma unroll 1
+        for (int i = 0; i < ITEMS; i++) {
+            const int item = tid + kTT * i;
+            if (item >= NV) break;
+            const int rp = item / NCP, cp = item - rp * NCP;
+            const int j = 2 * cp;
+            const float* h_rd = s_h + 2 * rp * H1S + j;
+            f2v a0{0.f, 0.f}, a1{0.f, 0.f};   // rows 2 rp, 2 rp + 1 (columns j, j + 1)
+#pragma unroll
+            for (int m = 0; m <= FWA; m++) {
+                const f2v v = *reinterpret_cast<const f2v*>(h_rd + m * H1S);
+                if (m < FWA) a0 = tpk(v, ttap<FWA>(J.taps, m), a0);
+                if (m >= 1) a1 = tpk(v, ttap<FWA>(J.taps, m - 1), a1);
+            }
+            f2v* q = s_w + rp * GB::IN_S + j + GB::SH;
+            q[0] = f2v{a0.x, a1.x};
+            q[1] = f2v{a0.y, a1.y};
+            // (RB may be odd: the pair's rows can straddle the tile's first / last row)
+            const int y = mr0 + 2 * rp, x = aB + j;
+            if (x >= x0 && x < x0 + kTW && x < W) {
+                if (y >= y0 && y < y0 + kTH && y < H) *reinterpret_cast<f2v*>(d1 + (long long)y * W + x) = a0;
+                if (y + 1 >= y0 && y + 1 < y0 + kTH && y + 1 < H)
+                    *reinterpret_cast<f2v*>(d1 + (long long)(y + 1) * W + x) = a1;
+            }
+        }
+    }
+    __syncthreads();
+    // clamp-to-edge of level k+1 (edge tiles): columns outside the image take the edge column,
+    // then rows outside take the edge row
+    float* sm = reinterpret_cast<float*>(s_w);
+    auto at = [&](int r, int c) -> float& {   // stage-2 window row r, column c (= aB + c)
+        return sm[2 * ((r >> 1) * GB::IN_S + c + GB::SH) + (r & 1)];
+    };
+    const int cl = aB < 0 ? -aB : 0, cr = aB + MC > W ? aB + MC - W : 0;
+    if (cl | cr) {
+        for (int i = tid; i < MROWS * (cl + cr); i += kTT) {
+            const int r = i / (cl + cr), k = i - r * (cl + cr);
+            const int c = k < cl ? k : MC - cr + (k - cl);
+            at(r, c) = at(r, k < cl ? cl : W - 1 - aB);
+        }
+        __syncthreads();
+    }
+    const int rt = mr0 < 0 ? -mr0 : 0, rbt = mr0 + MROWS > H ? mr0 + MROWS - H : 0;
+    if (rt | rbt) {
+        for (int i = tid; i < (rt + rbt) * MC; i += kTT) {
+            const int k = i / MC, c = i - k * MC;
+            const int r = k < rt ? k : MROWS - rbt + (k - rt);
+            at(r, c) = at(k < rt ? rt : H - 1 - mr0, c);
+        }
+        __syncthreads();
+    }
+    // stage 2: level k+2 (and its decimation)
+    tile_hv<FWB, DSB>(J, J.taps2, J.dst2, b, x0, y0, s_w, s_h);
 }
 
 template <int FW, bool U8, bool DS>
@@ -258,6 +401,28 @@ __global__ __launch_bounds__(kTT) void k_gauss_tile_diag(const TileJob A, const 
         if (lb < B.nblocks) tile_block<FWB, false, false>(B, lb, smem);
     } else {
         tile_block<FWA, false, false>(A, tile_order(bid - nbB, (int)gridDim.x - nbB), smem);
+    }
+}
+
+template <int FWA, int FWB, bool U8, bool DSB>
+__global__ __launch_bounds__(kTT) void k_gauss_tile_duo(const TileJob J) {
+    __shared__ __attribute__((aligned(16))) char smem[TileDuoGeom<FWA, FWB>::LDS_BYTES];
+    if (J.zero.n[0] | J.zero.n[1] | J.zero.n[2]) tile_zero(J.zero);
+    tile_duo_block<FWA, FWB, U8, DSB>(J, tile_order(blockIdx.x, gridDim.x), smem);
+}
+
+// A tile duo of octave o (job A) beside octave o+1's first level (job B, single, FWC) in one
+// launch: blocks [0, nbB) job B, the rest job A (as k_gauss_tile_diag).
+template <int FWA, int FWB, int FWC>
+__global__ __launch_bounds__(kTT) void k_gauss_tile_duo_diag(const TileJob A, const TileJob B, int nbB) {
+    constexpr int LA = TileDuoGeom<FWA, FWB>::LDS_BYTES, LB = TileGeom<FWC>::LDS_BYTES;
+    __shared__ __attribute__((aligned(16))) char smem[LA > LB ? LA : LB];
+    const int bid = blockIdx.x;
+    if (bid < nbB) {
+        const int lb = tile_order(bid, nbB);
+        if (lb < B.nblocks) tile_block<FWC, false, false>(B, lb, smem);
+    } else {
+        tile_duo_block<FWA, FWB, false, false>(A, tile_order(bid - nbB, (int)gridDim.x - nbB), smem);
     }
 }
 
@@ -306,6 +471,35 @@ hipError_t tile_diag_launch(const LevelOp& a, const LevelOp& b, hipStream_t stre
     return hipGetLastError();
 }
 
+TileJob make_duo_job(const LevelOp& a, const LevelOp& b) {
+    TileJob J = make_job(a);
+    J.dst2 = b.dst;
+    J.taps2 = b.taps;
+    J.ds = b.ds_dst;
+    J.dsw = b.ds_w;
+    J.dsh = b.ds_h;
+    J.ds_img = b.ds_img_stride;
+    return J;
+}
+
+template <int FWA, int FWB, bool U8, bool DSB>
+hipError_t tile_duo_launch(const LevelOp& a, const LevelOp& b, hipStream_t stream) {
+    const TileJob J = make_duo_job(a, b);
+    hipLaunchKernelGGL((k_gauss_tile_duo<FWA, FWB, U8, DSB>), dim3((unsigned)J.nblocks), dim3(kTT), 0,
+                       stream, J);
+    return hipGetLastError();
+}
+
+template <int FWA, int FWB, int FWC>
+hipError_t tile_duo_diag_launch(const LevelOp& a, const LevelOp& b, const LevelOp& c,
+                                hipStream_t stream) {
+    const TileJob A = make_duo_job(a, b), B = make_job(c);
+    const int nbBp = (B.nblocks + 7) / 8 * 8;
+    hipLaunchKernelGGL((k_gauss_tile_duo_diag<FWA, FWB, FWC>), dim3((unsigned)(nbBp + A.nblocks)),
+                       dim3(kTT), 0, stream, A, B, nbBp);
+    return hipGetLastError();
+}
+
 bool tile_diag_ok(const LevelOp& op) {
     return !op.src_u8 && !op.ds_dst && !(op.zero.n[0] | op.zero.n[1] | op.zero.n[2]);
 }
@@ -351,6 +545,52 @@ hipError_t launch_gauss_tile_two(const LevelOp& a, const LevelOp& b, hipStream_t
     const hipError_t e = launch_gauss_tile(a, stream);
     if (e != hipSuccess) return e;
     return launch_gauss_tile(b, stream);
+}
+
+}  // namespace sgk
+
+namespace sgk {
+
+// The compiled tile duos (the default -d 3 schedule: octave 0's (13 u8, 11), (13, 17 + decimation),
+// (21, 25); octaves >= 1: (13, 17 [+ decimation]), (21, 25); (13, 11) from a float first level,
+// (11, 13) and (17, 21) for other pairings).
+bool gauss_tile_duo_supported(const LevelOp& a, const LevelOp& b) {
+    if (!gauss_tile_supported(a) || !gauss_tile_supported(b)) return false;
+    if (a.ds_dst || b.src_u8 || (b.zero.n[0] | b.zero.n[1] | b.zero.n[2])) return false;
+    if (a.src_u8 && b.ds_dst) return false;
+    const bool geo = b.src == a.dst && a.w == b.w && a.h == b.h && a.batch == b.batch &&
+                     b.src_stride == a.w && a.dst_img_stride == b.dst_img_stride &&
+                     b.src_img_stride == a.dst_img_stride && a.dst_img_stride >= (long long)a.w * a.h;
+    if (!geo) return false;
+    const int fa = a.fw, fb = b.fw;
+    if (b.ds_dst) return fa == 13 && fb == 17;
+    return (fa == 13 && fb == 11) || (fa == 13 && fb == 17) || (fa == 21 && fb == 25) ||
+           (fa == 11 && fb == 13) || (fa == 17 && fb == 21);
+}
+
+hipError_t launch_gauss_tile_duo(const LevelOp& a, const LevelOp& b, hipStream_t stream) {
+    if (!gauss_tile_duo_supported(a, b)) return hipErrorInvalidValue;
+    const int fa = a.fw, fb = b.fw;
+    if (a.src_u8) return fa == 13 && fb == 11 ? tile_duo_launch<13, 11, true, false>(a, b, stream)
+                                              : tile_duo_launch<11, 13, true, false>(a, b, stream);
+    if (b.ds_dst) return tile_duo_launch<13, 17, false, true>(a, b, stream);
+#define SGK_TDUO(A, B) if (fa == A && fb == B) return tile_duo_launch<A, B, false, false>(a, b, stream);
+    SGK_TDUO(13, 11) SGK_TDUO(13, 17) SGK_TDUO(21, 25) SGK_TDUO(11, 13) SGK_TDUO(17, 21)
+#undef SGK_TDUO
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_gauss_tile_duo_one(const LevelOp& a, const LevelOp& b, const LevelOp& c,
+                                     hipStream_t stream, int* launches) {
+    if (launches) *launches = 1;
+    if (gauss_tile_duo_supported(a, b) && !a.src_u8 && !b.ds_dst && gauss_tile_supported(c) &&
+        tile_diag_ok(c) && !(a.zero.n[0] | a.zero.n[1] | a.zero.n[2])) {
+        if (a.fw == 21 && b.fw == 25 && c.fw == 11) return tile_duo_diag_launch<21, 25, 11>(a, b, c, stream);
+    }
+    if (launches) *launches = 2;
+    const hipError_t e = launch_gauss_tile_duo(a, b, stream);
+    if (e != hipSuccess) return e;
+    return launch_gauss_tile(c, stream);
 }
 
 }  // namespace sgk

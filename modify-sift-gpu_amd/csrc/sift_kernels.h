@@ -108,6 +108,15 @@ bool gauss_tile_supported(const LevelOp& op);
 hipError_t launch_gauss_tile(const LevelOp& op, hipStream_t stream);
 hipError_t launch_gauss_tile_two(const LevelOp& a, const LevelOp& b, hipStream_t stream,
                                  int* launches = nullptr);
+// Two consecutive levels per tile (a = level k -> k+1, b = level k+1 -> k+2, b.src == a.dst): one
+// load of level k's window, level k+1 filtered into LDS over the region b's filter needs, its
+// tile stored, then level k+2 (and b's decimation) -- bit-identical to two launch_gauss_tile calls.
+// launch_gauss_tile_duo_one: that duo beside an independent single level c in one launch (the
+// compiled combination (21, 25) + 11: octave o's last levels with octave o+1's first), else two.
+bool gauss_tile_duo_supported(const LevelOp& a, const LevelOp& b);
+hipError_t launch_gauss_tile_duo(const LevelOp& a, const LevelOp& b, hipStream_t stream);
+hipError_t launch_gauss_tile_duo_one(const LevelOp& a, const LevelOp& b, const LevelOp& c,
+                                     hipStream_t stream, int* launches = nullptr);
 
 // First octave of -fo != 0 (BuildPyramid, PyramidCU.cpp:1011-1016): the batch's input
 // (u8 p/255 or f32; tw = w & ~3 columns used, rows `stride` apart) resampled into dst
@@ -126,9 +135,11 @@ hipError_t launch_color_to_gray(const uint8_t* src, int n, int w, int h, int str
 
 // Extremum detection for all octaves, all d levels and all images (one launch): sets the
 // keypoint bits in the zeroed mask and adds per-row keypoint counts into the zeroed row_count
-// (rows ordered image, octave, level, row).
+// (rows ordered image, octave, level, row).  tiles: the 2-D tile kernel (k_extrema_tile: each
+// workgroup loads its 64 x 16-pixel window of every plane at once; for cache-resident pyramids),
+// else the wave-streaming k_extrema_wave2 -- the same bits and counts.
 hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
-                          const FeatureParams& fp, hipStream_t stream);
+                          const FeatureParams& fp, hipStream_t stream, bool tiles = false);
 
 // Exclusive scan of n uint32 values into out[0..n]; out[n] = total.  tmp needs
 // scan_tmp_words(n) words.

@@ -1015,6 +1015,126 @@ __global__ __launch_bounds__(256, SGK_EXT2_WAVES) void k_extrema_wave2(const flo
 }
 
 // ------------------------------------------------------------------------------------------
+// Extremum detection in 2-D tiles, for cache-resident pyramids (one image: C2).  The wave kernel's
+// walk of a strip segment is a chain of row loads; a single 1080p image gives it ~2,700 waves
+// that each wait for ~5 dependent row fetches (29 us, profiles/r06a).  Here a workgroup owns 64
+// tested columns x 16 rows of one octave and image for all d levels: it issues the loads of the
+// d + 3 Gaussian planes' window (18 rows x 72 columns, aligned quads) at once, stores the d + 2
+// DoG planes D_m = G_{m+1} - G_m into LDS, and each wave tests 4 rows (a lane per column): the
+// same branch-free 3x3x3 pre-filter superset as k_extrema_wave2, then ComputeKEY's exact state
+// machine (key_test) on the LDS values for every candidate.  The tested pixels (1 .. W-2 x
+// 1 .. H-2 per octave), the mask bits and the row counts are the wave kernel's; only the order of
+// the commutative atomics differs.
+struct ExtremaTileGrid {
+    int tile0[kMaxOctaves + 1];   // first workgroup of octave o
+    int tx[kMaxOctaves];          // tiles per row of octave o
+    int ty[kMaxOctaves];          // tiles per column
+};
+constexpr int kEtW = 64, kEtH = 16, kEtLW = 72;   // tile columns / rows, LDS row (18 quads)
+
+template <int ND>
+__global__ __launch_bounds__(256) void k_extrema_tile(const float* __restrict__ pyr,
+                                                      uint32_t* __restrict__ mask,
+                                                      uint32_t* __restrict__ row_count,
+                                                      const FeatureParams fp,
+                                                      const ExtremaTileGrid eg) {
+    constexpr int NJ = ND - 2, R = kEtH + 2, NQ = kEtLW / 4, NIT = R * NQ;
+    constexpr int LITEMS = (NIT + 255) / 256;
+    __shared__ __attribute__((aligned(16))) float s_d[ND][R][kEtLW];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int bid = blockIdx.x;
+    int o = 0;
+    while (o + 1 < fp.n_octaves && bid >= eg.tile0[o + 1]) o++;
+    o = __builtin_amdgcn_readfirstlane(o);
+    const OctaveDesc& od = fp.oct[o];
+    const int W = od.wa, H = od.h;
+    const int id = bid - eg.tile0[o];
+    const int sx = id % eg.tx[o], rest = id / eg.tx[o];
+    const int sy = rest % eg.ty[o], b = rest / eg.ty[o];
+    const int x0 = sx * kEtW, y0 = sy * kEtH;
+    const long long lstride = od.level_stride;
+    const float* g0 = pyr + od.gauss_off + (long long)b * W * H;
+    // the window: rows y0 - 1 .. y0 + 16 (clamped), columns x0 - 4 .. x0 + 67 as aligned quads
+    // (clamped: the tested columns' neighbours x0 - 1 .. x0 + 64 are inside the plane wherever a
+    // tested column exists)
+    float4 gq[LITEMS][ND + 1];
+#pragma unroll
+    for (int i = 0; i < LITEMS; i++) {
+        const int it = min(tid + 256 * i, NIT - 1);
+        const int rr = it / NQ, q = it - rr * NQ;
+        const int y = clampi(y0 - 1 + rr, 0, H - 1);
+        const int xq = clampi(x0 - 4 + 4 * q, 0, W - 4);
+        const float* p = g0 + (long long)y * W + xq;
+#pragma unroll
+        for (int m = 0; m <= ND; m++) gq[i][m] = *reinterpret_cast<const float4*>(p + m * lstride);
+    }
+#pragma unroll
+    for (int i = 0; i < LITEMS; i++) {
+        const int it = tid + 256 * i;
+        if (NIT % 256 != 0 && it >= NIT) break;
+        const int rr = it / NQ, q = it - rr * NQ;
+#pragma unroll
+        for (int m = 0; m < ND; m++) {
+            const float4 a = gq[i][m], c = gq[i][m + 1];
+            *reinterpret_cast<float4*>(&s_d[m][rr][4 * q]) =
+                make_float4(c.x - a.x, c.y - a.y, c.z - a.z, c.w - a.w);
+        }
+    }
+    __syncthreads();
+    // wave w: tile rows 4 w .. 4 w + 3 (LDS rows 4 w + 1 .. 4 w + 4), lane = column x0 + lane
+    // (LDS column lane + 4)
+    const int x = x0 + lane;
+    const bool col_ok = x > 0 && x < W - 1;
+    const int lc = lane + 4;
+    float hx[ND][6], hn[ND][6];   // 3-wide row max / min of LDS rows 4 w .. 4 w + 5
+#pragma unroll
+    for (int m = 0; m < ND; m++)
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+            const float* row = &s_d[m][4 * wave + r][lc];
+            const float a = row[-1], c = row[0], e = row[1];
+            hx[m][r] = fmax_(fmax_(a, c), e);
+            hn[m][r] = fmin_(fmin_(a, c), e);
+        }
+    uint32_t pend = 0;   // bit i * NJ + j: row i, level j passed the pre-filter
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int y = y0 + 4 * wave + i;
+        const bool row_ok = y > 0 && y < H - 1;
+#pragma unroll
+        for (int j = 0; j < NJ; j++) {
+            const float v = s_d[j + 1][4 * wave + 1 + i][lc];
+            float mx = hx[j][i], mn = hn[j][i];
+#pragma unroll
+            for (int m = j; m < j + 3; m++) {
+                mx = fmax_(mx, fmax_(fmax_(hx[m][i], hx[m][i + 1]), hx[m][i + 2]));
+                mn = fmin_(mn, fmin_(fmin_(hn[m][i], hn[m][i + 1]), hn[m][i + 2]));
+            }
+            if (row_ok && col_ok && fabs_(v) > fp.t0 && (v >= mx || v <= mn)) pend |= 1u << (i * NJ + j);
+        }
+    }
+    // every lane works through its candidates one per iteration (the wave loops while any lane
+    // has one left): ComputeKEY on the LDS values, accepted pixels set their mask bit and count
+    while (__ballot(pend != 0)) {
+        if (pend) {
+            const int bit = __ffs(pend) - 1;
+            pend &= pend - 1;
+            const int i = bit / NJ, j = bit - i * NJ;
+            const int lr = 4 * wave + 1 + i;
+            auto get = [&](int m, int r, int c) { return s_d[j + m][lr + r - 1][lc + c - 1]; };
+            if (key_test(get, fp.t0, fp.t, fp.edge, fp.subpixel).result != 0.f) {
+                const int y = y0 + 4 * wave + i;
+                uint32_t* mrow = mask + od.mask_off + j * od.mask_level_stride +
+                                 ((long long)b * H + y) * od.nwords;
+                atomicOr(&mrow[x >> 5], 1u << (x & 31));
+                atomicAdd(&row_count[(long long)b * fp.rows_per_image + fp.row_off[o] + j * H + y], 1u);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Exclusive scan (uint32), 1024 elements per block.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     const int lane = threadIdx.x & 63;
@@ -1061,33 +1181,37 @@ __global__ __launch_bounds__(256) void k_scan_block(const uint32_t* __restrict__
 // the block scan (each a few microseconds of launch latency at these sizes).
 __global__ __launch_bounds__(1024) void k_scan_single(const uint32_t* __restrict__ in,
                                                       uint32_t* __restrict__ out, size_t n) {
+    // one pass: thread t owns the contiguous run [t c, t c + c), c = ceil(n / 1024) <= 32, loaded
+    // at once (one round trip; round 5 walked 4,096-element tiles one after the other: a single
+    // image's two scans took 6-7 us each)
     __shared__ uint32_t s_w[16];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t carry = 0;
-    for (size_t t0 = 0; t0 < n; t0 += 4096) {
-        const size_t base = t0 + (size_t)threadIdx.x * 4;
-        uint32_t v[4];
+    const size_t c = (n + 1023) / 1024;
+    const size_t base = (size_t)threadIdx.x * c;
+    uint32_t v[32];
+    uint32_t tsum = 0;
 #pragma unroll
-        for (int i = 0; i < 4; i++) v[i] = (base + i < n) ? in[base + i] : 0u;
-        const uint32_t tsum = v[0] + v[1] + v[2] + v[3];
-        const uint32_t incl = wave_incl_scan(tsum);
-        if (lane == 63) s_w[wave] = incl;
-        __syncthreads();
-        uint32_t wofs = 0, total = 0;
-        for (int w = 0; w < 16; w++) {
-            if (w < wave) wofs += s_w[w];
-            total += s_w[w];
-        }
-        uint32_t run = carry + wofs + incl - tsum;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            if (base + i < n) out[base + i] = run;
-            run += v[i];
-        }
-        carry += total;
-        __syncthreads();   // s_w is rewritten by the next tile
+    for (int i = 0; i < 32; i++) {
+        v[i] = ((size_t)i < c && base + i < n) ? in[base + i] : 0u;
+        tsum += v[i];
     }
-    if (threadIdx.x == 0) out[n] = carry;
+    const uint32_t incl = wave_incl_scan(tsum);
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t wofs = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+        const uint32_t sw = s_w[w];
+        wofs += w < wave ? sw : 0u;
+        total += sw;
+    }
+    uint32_t run = wofs + incl - tsum;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+        if ((size_t)i < c && base + i < n) out[base + i] = run;
+        run += v[i];
+    }
+    if (threadIdx.x == 0) out[n] = total;
 }
 
 __global__ __launch_bounds__(256) void k_scan_add(uint32_t* __restrict__ out, size_t n,
@@ -1259,6 +1383,61 @@ __device__ __forceinline__ float strongest_orientation(const float (&vote)[37]) 
 // 838-851) and its info record; false when no orientation is computed (num_orientation == 0:
 // the keypoint is written with orientation 0 here).
 struct OriKey { float kx, ky, kz; const float* g; int W, H; };
+// locate() by a whole wave (the one-wave-per-candidate orientation form): the same (image,
+// octave, level, row, column) from 3 dependent loads instead of ~13 binary-search steps plus a
+// serial scan over the mask row's words (up to 60 for a 1080p row) -- the latency chain of a
+// single image's orientation launch.
+//   * row: a 64-ary search for the last row whose scanned base is <= f -- the lanes probe 64
+//     evenly spaced rows of the remaining range, the highest lane whose probe passes narrows it;
+//   * column: lane l loads mask word l (64 at a time), a wave prefix sum of their popcounts picks
+//     the word holding the k-th set bit, that lane finds the bit.
+__device__ __forceinline__ KeyLoc locate_wave(uint32_t f, int lane, const uint32_t* __restrict__ row_base,
+                                              int total_rows, const uint32_t* __restrict__ mask,
+                                              const FeatureParams& fp) {
+    int lo = 0, n = total_rows;   // the answer lies in [lo, lo + n); row_base[lo] <= f
+    uint32_t base_lo = 0;         // row_base[lo] (row_base[0] = 0)
+    while (n > 1) {
+        const int step = (n + 63) / 64;
+        const int i = lo + lane * step;
+        const bool in = lane * step < n;
+        const uint32_t v = in ? row_base[i] : 0xffffffffu;
+        const unsigned long long bal = __ballot(in && v <= f);   // lane 0 always passes
+        const int k = 63 - __clzll(bal);
+        base_lo = (uint32_t)__builtin_amdgcn_readlane((int)v, k);
+        const int end = lo + n;
+        lo += k * step;
+        n = min(step, end - lo);
+    }
+    KeyLoc L = row_loc(lo, fp);
+    uint32_t k = f - base_lo;
+    const OctaveDesc& od = fp.oct[L.o];
+    const uint32_t* mrow = mask + od.mask_off + L.j * od.mask_level_stride +
+                           ((long long)L.b * od.h + L.row) * od.nwords;
+    int col = 0;
+    for (int w0 = 0; w0 < od.nwords; w0 += 64) {
+        const int w = w0 + lane;
+        uint32_t m = w < od.nwords ? mrow[w] : 0u;
+        const int c = __popc(m);
+        int incl = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int u = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += u;
+        }
+        const int excl = incl - c;
+        const unsigned long long hit = __ballot((uint32_t)excl <= k && k < (uint32_t)incl);
+        if (hit) {
+            const int hl = __ffsll((long long)hit) - 1;
+            for (uint32_t q = 0; q < k - (uint32_t)excl && lane == hl; q++) m &= m - 1;
+            col = __builtin_amdgcn_readlane(w * 32 + (__ffs(m) - 1), hl);
+            break;
+        }
+        k -= (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+    }
+    L.col = col;
+    return L;
+}
+
 __device__ __forceinline__ bool orientation_key(uint32_t f, bool writer,
                                                 const float* __restrict__ pyr,
                                                 const uint32_t* __restrict__ mask,
@@ -1266,8 +1445,11 @@ __device__ __forceinline__ bool orientation_key(uint32_t f, bool writer,
                                                 int total_rows, const FeatureParams& fp,
                                                 float4* __restrict__ out4,
                                                 int2* __restrict__ info,
-                                                uint32_t* __restrict__ ocount, OriKey& K) {
-    const KeyLoc L = locate(f, row_base, total_rows, mask, fp);
+                                                uint32_t* __restrict__ ocount, OriKey& K,
+                                                int wave_lane = -1) {
+    // wave_lane >= 0: called by a whole wave for one candidate (locate_wave), else per lane
+    const KeyLoc L = wave_lane >= 0 ? locate_wave(f, wave_lane, row_base, total_rows, mask, fp)
+                                    : locate(f, row_base, total_rows, mask, fp);
     const KeyOut kv = key_at(pyr, fp, L);
     const OctaveDesc& od = fp.oct[L.o];
 
@@ -1473,7 +1655,7 @@ __global__ __launch_bounds__(256) void k_orientation_wave(const float* __restric
     for (uint32_t f = blockIdx.x * 4 + wave; f < n; f += gridDim.x * 4) {   // uniform per wave
         OriKey K;
         if (!orientation_key(f, lane == 0, pyr, mask, row_base, total_rows, fp, out4, info,
-                             ocount, K))
+                             ocount, K, lane))
             continue;
         float vote[37];
         orientation_hist_wave(K, fp, lane, s_vote[wave], s_pair[wave], vote);
@@ -2438,11 +2620,12 @@ __global__ __launch_bounds__(256) SGK_DUAL_ATTR void k_descriptor_dual(const flo
 // neighbouring lanes on neighbouring pixels (coalesced loads).  A pixel's dual cell (a, b) and
 // its weights are those of descriptor_dual (the same dnx, dny, the reference's rounded cell
 // centres, ProgramCU.cu:1044-1094, from a 6 x 6 per-feature table), its 4 cells x 2 orientation
-// bins are 8 no-return LDS float adds into the wave's histogram, kept in kFlatCopies copies
-// (lane mod kFlatCopies) against same-address serialisation and summed at the end.  Within a
-// wave the adds of one instruction to one address serialise in a fixed order, so a feature's
-// descriptor does not depend on the batch around it; against the exact kernel the sums' order
-// differs (L2 ~1e-6, tests/test_gpu_parity.py::test_shipped_descriptor_vs_exact).
+// bins are 8 no-return 64-bit integer LDS adds (ds_add_u64 of a fixed-point word, to_fix32) into
+// the wave's histogram, kept in kFlatCopies copies (lane mod kFlatCopies) against same-address
+// serialisation and summed at the end.  Integer sums do not depend on their order, so a
+// feature's descriptor does not depend on the batch around it or on how its pixels are split
+// over waves (k_descriptor_wide); against the exact kernel the sums differ by the float order
+// (L2 ~1e-6, tests/test_gpu_parity.py::test_shipped_descriptor_vs_exact).
 #ifndef SGK_FLAT_COPIES
 #define SGK_FLAT_COPIES 4
 #endif
@@ -2465,10 +2648,39 @@ constexpr int kFlatWords = 2 * kFlatHist + 144;
 // 2^-32).  LDS integer adds are full rate where float adds (ds_add_f32) serialise their lanes
 // (~4 cycles per lane, 7.8 ms per 128 x 1080p step against 1.37 with integer adds,
 // tests/diag/r05l.sh), and integer sums do not depend on their order.
+typedef __attribute__((address_space(3))) unsigned long long lds_u64;
+
 __device__ __forceinline__ unsigned long long to_fix32(float v) {
     const float fl = floor_(v);
     const uint32_t lo = (uint32_t)((v - fl) * 4294967296.0f);
     return ((unsigned long long)(uint32_t)(int)fl << 32) | lo;
+}
+
+// Inclusive wave scan by DPP (row_shr 1 / 2 / 4 / 8 within each row of 16 lanes, then
+// row_bcast:15 and row_bcast:31 carry the row totals into the rows above): 6 VALU with DPP
+// operands instead of 6 ds_bpermute round trips through the LDS crossbar.
+__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 (rows 1, 3)
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 (rows 2, 3)
+    return v;
+}
+
+// Sum over the wave, in every lane: DPP within each row of 16 (quad_perm swaps, row_ror 4 / 8),
+// then the four row sums read as scalars (v_readlane) and added in row order.
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xb1, 0xf, 0xf, false));  // quad_perm [1,0,3,2]
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4e, 0xf, 0xf, false));  // quad_perm [2,3,0,1]
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false)); // row_ror:4
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false)); // row_ror:8
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return (r0 + r1) + (r2 + r3);
 }
 
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
@@ -2487,7 +2699,11 @@ __device__ __forceinline__ void flat_accumulate(uint32_t e, int lane, const floa
                                                 const int2* __restrict__ feat_info,
                                                 const FeatureParams& fp, float* __restrict__ sh,
                                                 int wv, int nwv) {
-    unsigned long long* hist = reinterpret_cast<unsigned long long*>(sh);   // kFlatHist
+    // the histogram as an LDS-space pointer, stated: its adds can only be ds_add_u64 (an LDS
+    // offset outside the allocation is dropped by the LDS), never flat atomics through a generic
+    // address, which the compiler would have to fall back to if the LDS origin of `sh` were lost
+    // (round 5's fi64 variant faulted with an aperture violation)
+    lds_u64* hist = (lds_u64*)sh;   // kFlatHist
     // 36: (1 + ox', 1 - ox', 1 + oy', 1 - oy') of cell (i, j)
     float4* ctab = reinterpret_cast<float4*>(sh + 2 * kFlatHist);
     const float4 key = feat[e];
@@ -2510,7 +2726,7 @@ __device__ __forceinline__ void flat_accumulate(uint32_t e, int lane, const floa
     // (descriptor_dual's oxl / oyl)
 #pragma unroll
     for (int i = lane; i < kFlatHist / 2; i += 64)
-        reinterpret_cast<float4*>(hist)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        reinterpret_cast<float4*>(sh)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (lane < 36) {
         const float ox = (float)(lane % 6 - 1) - 1.5f, oy = (float)(lane / 6 - 1) - 1.5f;
         const float ptx = fma_(cspt, ox, -(sspt * oy)) + key.x;
@@ -2561,7 +2777,7 @@ __device__ __forceinline__ void flat_accumulate(uint32_t e, int lane, const floa
                 len = ih >= il ? ih - il + 1 : 0;
             }
         }
-        const int incl = wave_incl_scan(len, lane);
+        const int incl = wave_incl_scan_dpp(len);
         const int rs = incl - len;                                   // row L's first pixel index
         const int total = __builtin_amdgcn_readlane(incl, kFlatRows - 1);
         int rcur = 0;   // a row at or before pixel `base`'s (uniform)
@@ -2580,15 +2796,30 @@ __device__ __forceinline__ void flat_accumulate(uint32_t e, int lane, const floa
             const int y = rb + r;
             // (the shuffles with every lane active: a lane outside the valid ones may be the
             // source; the asm keeps the compiler from moving them under the valid test)
-            int xr = __shfl(lo, r, 64) + (p - __shfl(rs, r, 64));
+            const int rsr = __shfl(rs, r, 64);        // row r's first pixel
+            const int rnx = __shfl(incl, r, 64);      // the next row's first pixel
+            int xr = __shfl(lo, r, 64) + (p - rsr);
             asm volatile("" : "+v"(xr));
             const int x = valid ? xr : bx0;
             const int yc = valid ? y : y0;
             // 32-bit byte offsets from the level image's base (an image plane is < 4 GB)
             const char* gp = reinterpret_cast<const char*>(g) + 4u * (uint32_t)(yc * W + x);
             const uint32_t W4 = 4u * (uint32_t)W;
-            const float gx = *reinterpret_cast<const float*>(gp + 4) - *reinterpret_cast<const float*>(gp - 4);
-            const float gy = *reinterpret_cast<const float*>(gp + W4) - *reinterpret_cast<const float*>(gp - W4);
+            // the gradient's 4 neighbours: the row above and below are gathered, the left and right
+            // ones are the neighbouring lanes' centre pixels (lanes hold consecutive pixels of a
+            // row: p - 1 and p + 1) taken by DPP wave shifts; only the lanes at a row's or the
+            // step's ends load them -- 3 gathers per pixel instead of 4, the same values
+            const float cen = *reinterpret_cast<const float*>(gp);
+            const float gup = *reinterpret_cast<const float*>(gp - W4);
+            const float gdn = *reinterpret_cast<const float*>(gp + W4);
+            float grt = __int_as_float(__builtin_amdgcn_update_dpp(
+                0, __float_as_int(cen), 0x130, 0xf, 0xf, false));   // wave_shl:1: lane + 1
+            float glt = __int_as_float(__builtin_amdgcn_update_dpp(
+                0, __float_as_int(cen), 0x138, 0xf, 0xf, false));   // wave_shr:1: lane - 1
+            if (!(valid && lane < 63 && p + 1 < rnx)) grt = *reinterpret_cast<const float*>(gp + 4);
+            if (!(valid && lane > 0 && p > rsr)) glt = *reinterpret_cast<const float*>(gp - 4);
+            const float gx = grt - glt;
+            const float gy = gdn - gup;
             const float m2 = fma_(gx, gx, gy * gy);
             float rot = atan2_relaxed(gy, gx);
             const float dd = fabs_(anglef - rot);
@@ -2621,7 +2852,7 @@ __device__ __forceinline__ void flat_accumulate(uint32_t e, int lane, const floa
                 // the 4 cells (a - 1 + dx, b - 1 + dy); cells outside 0 .. 3 (the dual cells on the
                 // window's border) are not descriptor cells and take nothing
                 const bool x0in = a >= 1, x1in = a <= 3, y0in = b >= 1, y1in = b <= 3;
-                unsigned long long* hp = hist + (((b - 1) * 4 + (a - 1)) * 8) * kFlatStride + copy;
+                lds_u64* hp = hist + (((b - 1) * 4 + (a - 1)) * 8) * kFlatStride + copy;
                 const int o0 = b0 * kFlatStride, o1 = b1 * kFlatStride;
                 constexpr int CX = 8 * kFlatStride, CY = 4 * 8 * kFlatStride;
                 auto add2 = [&](bool in, int off, float wc) {
@@ -2652,7 +2883,7 @@ __device__ __forceinline__ void flat_finish(int lane, const FeatureParams& fp,
     const int ix = cell & 3, iy = cell >> 2;
     unsigned long long s0 = 0, s1 = 0;
     for (int w = 0; w < nh; w++) {
-        const unsigned long long* hc = reinterpret_cast<const unsigned long long*>(sh + w * kFlatWords) +
+        const lds_u64* hc = (const lds_u64*)(sh + w * kFlatWords) +
                                        ((iy * 4 + ix) * 8 + 2 * sub) * kFlatStride;
 #pragma unroll
         for (int k = 0; k < kFlatCopies; k++) {
@@ -2663,15 +2894,11 @@ __device__ __forceinline__ void flat_finish(int lane, const FeatureParams& fp,
     float b0 = (float)((double)(long long)s0 * 0x1p-32), b1 = (float)((double)(long long)s1 * 0x1p-32);
     asm volatile("" ::: "memory");
     if (fp.normalize) {
-        float sn = fma_(b0, b0, b1 * b1);
-#pragma unroll
-        for (int k = 32; k >= 1; k >>= 1) sn += __shfl_xor(sn, k, 64);
+        float sn = wave_sum_dpp(fma_(b0, b0, b1 * b1));
         const float n1 = __builtin_amdgcn_rsqf(sn);
         b0 = fmin_(0.2f, b0 * n1);
         b1 = fmin_(0.2f, b1 * n1);
-        sn = fma_(b0, b0, b1 * b1);
-#pragma unroll
-        for (int k = 32; k >= 1; k >>= 1) sn += __shfl_xor(sn, k, 64);
+        sn = wave_sum_dpp(fma_(b0, b0, b1 * b1));
         const float n2 = __builtin_amdgcn_rsqf(sn);
         b0 *= n2;
         b1 *= n2;
@@ -2717,11 +2944,12 @@ __global__ __launch_bounds__(256) SGK_FLAT_ATTR void k_descriptor_flat(const flo
                         out_index ? (uint32_t)out_index[e] : e, s_flat[wave]);
 }
 
-// A workgroup of 4 waves per feature, for few features (one image: ~1,500 features are ~1.5 waves
-// per SIMD under one wave each, and each wave walks its window alone).  The waves take every
-// fourth 64-pixel step of the window into histograms of their own; wave 0 sums all of them.  The
+// A workgroup of NWV (4) waves per feature, for few features (one image: ~1,500 features are ~1.5
+// waves per SIMD under one wave each, and each wave walks its window alone).  The waves take every
+// NWV-th 64-pixel step of the window into histograms of their own; wave 0 sums all of them.  The
 // sums are integers, so the descriptor is k_descriptor_flat's bit for bit, in any batch.
-__global__ __launch_bounds__(256) SGK_FLAT_ATTR void k_descriptor_wide(const float* __restrict__ pyr,
+template <int NWV>
+__global__ __launch_bounds__(64 * NWV) SGK_FLAT_ATTR void k_descriptor_wide(const float* __restrict__ pyr,
                                                          const float4* __restrict__ feat,
                                                          const int2* __restrict__ feat_info,
                                                          const uint32_t* __restrict__ n_feat_dev,
@@ -2729,7 +2957,7 @@ __global__ __launch_bounds__(256) SGK_FLAT_ATTR void k_descriptor_wide(const flo
                                                          float* __restrict__ desc,
                                                          const int* __restrict__ out_index,
                                                          const HostCopy hc) {
-    __shared__ __attribute__((aligned(16))) float s_flat[4][kFlatWords];
+    __shared__ __attribute__((aligned(16))) float s_flat[NWV][kFlatWords];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t n = *n_feat_dev;
@@ -2738,12 +2966,12 @@ __global__ __launch_bounds__(256) SGK_FLAT_ATTR void k_descriptor_wide(const flo
     // while the descriptors are computed, instead of by a k_copy_out launch after them
     if (hc.hrec && blockIdx.x == 0 && threadIdx.x < (unsigned)hc.rec_n) hc.hrec[threadIdx.x] = hc.rec[threadIdx.x];
     for (uint32_t e = blockIdx.x; e < n; e += gridDim.x) {   // uniform per workgroup
-        flat_accumulate(e, lane, pyr, feat, feat_info, fp, s_flat[wave], wave, 4);
+        flat_accumulate(e, lane, pyr, feat, feat_info, fp, s_flat[wave], wave, NWV);
         __syncthreads();
         const uint32_t out = out_index ? (uint32_t)out_index[e] : e;
         const bool to_host = hc.hkeys && out < hc.cap;
         if (wave == 0)
-            flat_finish(lane, fp, desc, out, &s_flat[0][0], 4, to_host ? hc.hdesc : nullptr);
+            flat_finish(lane, fp, desc, out, &s_flat[0][0], NWV, to_host ? hc.hdesc : nullptr);
         else if (wave == 1 && lane == 0 && to_host)
             hc.hkeys[out] = hc.keys[e];
         __syncthreads();   // wave 0 has read every histogram before the next feature zeroes them
@@ -3048,7 +3276,31 @@ hipError_t launch_first_octave_input(const float* src, const uint8_t* src_u8, in
 }
 
 hipError_t launch_extrema(const float* pyr, uint32_t* mask, uint32_t* row_count,
-                          const FeatureParams& fp, hipStream_t stream) {
+                          const FeatureParams& fp, hipStream_t stream, bool tiles) {
+    bool tile_ok = tiles && ((uintptr_t)pyr % 16) == 0;
+    for (int o = 0; o < fp.n_octaves; o++)
+        tile_ok = tile_ok && fp.oct[o].wa % 4 == 0 && fp.oct[o].wa >= 4 && fp.oct[o].gauss_off % 4 == 0 &&
+                  fp.oct[o].level_stride % 4 == 0;
+    if (tile_ok) {
+        ExtremaTileGrid tg{};
+        long long nb = 0;
+        for (int o = 0; o < fp.n_octaves; o++) {
+            tg.tile0[o] = (int)nb;
+            tg.tx[o] = (fp.oct[o].wa + kEtW - 1) / kEtW;
+            tg.ty[o] = (fp.oct[o].h + kEtH - 1) / kEtH;
+            nb += (long long)tg.tx[o] * tg.ty[o] * fp.batch;
+        }
+        tg.tile0[fp.n_octaves] = (int)nb;
+        if (nb <= 0 || nb >= (1ll << 31)) return hipErrorInvalidValue;
+        switch (fp.d + 2) {
+#define SGK_EXTT(ND) \
+    case ND: hipLaunchKernelGGL((k_extrema_tile<ND>), dim3((unsigned)nb), dim3(256), 0, stream, pyr, mask, \
+                                row_count, fp, tg); return hipGetLastError();
+            SGK_EXTT(3) SGK_EXTT(4) SGK_EXTT(5) SGK_EXTT(6) SGK_EXTT(7) SGK_EXTT(8)
+#undef SGK_EXTT
+            default: return hipErrorInvalidValue;
+        }
+    }
     // one wave per (image, strip of tested columns, row segment); ~32k waves in all.  Two
     // columns per lane when every plane is 8-byte aligned (always, for pyramid levels: widths
     // are multiples of 4)
@@ -3152,7 +3404,7 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tm
                            (uint32_t*)nullptr);
         return hipGetLastError();
     }
-    if (n <= 32768) {   // one workgroup, <= 8 tiles
+    if (n <= 32768) {   // one workgroup, <= 32 elements per thread
         hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(1024), 0, stream, in, out, n);
         return hipGetLastError();
     }
@@ -3256,9 +3508,24 @@ hipError_t launch_descriptor(const float* pyr, const float4* feat, const int2* f
 #define SGK_DESC_FLAT 1
 #endif
     if (!exact && !rect && SGK_DESC_FLAT && !dual && wide) {
-        const unsigned wgrid = (unsigned)std::min((long long)n_feat_cap, 65536LL);
-        hipLaunchKernelGGL(k_descriptor_wide, dim3(wgrid), dim3(256), 0, stream, pyr, feat,
-                           feat_info, n_feat_dev, fp, desc, out_index, host ? *host : HostCopy{});
+        // A/B knobs: SGPU_WIDE_DESC_WAVES (4 or 8 waves per feature), SGPU_WIDE_DESC_GRID (at most
+        // this many workgroups, each taking every grid-th feature)
+        static const int nwv = [] {
+            const char* e = getenv("SGPU_WIDE_DESC_WAVES");
+            return e && atoi(e) == 8 ? 8 : 4;
+        }();
+        static const long long gmax = [] {
+            const char* e = getenv("SGPU_WIDE_DESC_GRID");
+            return e && atoll(e) > 0 ? atoll(e) : 65536LL;
+        }();
+        const unsigned wgrid = (unsigned)std::min((long long)n_feat_cap, gmax);
+        const HostCopy hc = host ? *host : HostCopy{};
+        if (nwv == 8)
+            hipLaunchKernelGGL(k_descriptor_wide<8>, dim3(wgrid), dim3(512), 0, stream, pyr, feat,
+                               feat_info, n_feat_dev, fp, desc, out_index, hc);
+        else
+            hipLaunchKernelGGL(k_descriptor_wide<4>, dim3(wgrid), dim3(256), 0, stream, pyr, feat,
+                               feat_info, n_feat_dev, fp, desc, out_index, hc);
         return hipGetLastError();
     }
     if (!exact && !rect && SGK_DESC_FLAT && !dual) {

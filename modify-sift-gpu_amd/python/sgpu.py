@@ -463,12 +463,12 @@ class SiftContext:
     DEBUG_PARTS2, DEBUG_PARTS4, DEBUG_TINY_CAP, DEBUG_FUSED_MATCH = 1, 2, 4, 8
     DEBUG_EXACT_DESCRIPTOR = 16
     DEBUG_GAUSS_BLOCK = 32    # workgroup strip Gaussian (k_gauss_pk2)
-    DEBUG_BAND_SHIFT = 20     # (rows << 20): the wave kernels' forced band height (0: automatic)
+    DEBUG_BAND_SHIFT = 20     # (rows << 20), rows < 2048: the wave kernels' forced band height (0: automatic)
     DEBUG_KEYED_MATCH = 64    # keyed matcher epilogue even when ratiomax <= 1
     DEBUG_FULL_COLUMNS = 128  # mutual matching decides every column, not only the matched ones
     DEBUG_DESC_DUAL = 256     # descriptors through the round-4 dual-cell kernel
     DEBUG_ORIENT_WAVE = 512   # orientation one wave per candidate for any candidate count
-    DEBUG_GAUSS_TILE_ALWAYS = 1024  # every level through the 2-D tile kernel (k_gauss_tile)
+    DEBUG_GAUSS_TILE_ALWAYS = 1024  # every level (k_gauss_tile) and the extrema (k_extrema_tile) in tiles
     DEBUG_MATCH_REGSTAGE = 2048  # keyless matcher with register staging (k_match_rows<RAW>)
     DEBUG_PYR_SERIAL = 4096    # all pyramid octaves on one stream
     DEBUG_GAUSS_LONG_BANDS = 8192  # Gaussian bands of >= 4 chunks on every level
@@ -477,6 +477,7 @@ class SiftContext:
     DEBUG_GAUSS_TILE_OFF = 65536       # no tile launches (the wave-streaming level kernels)
     DEBUG_DESC_WIDE_OFF = 131072       # descriptors one wave per feature for every count
     DEBUG_DESC_WIDE_ALWAYS = 262144    # descriptors one workgroup per feature for every count
+    DEBUG_EXTREMA_TILE_OFF = 524288    # extremum detection always through k_extrema_wave2
 
     def set_debug_flags(self, flags: int):
         """Per-context debug flags (sgpu_debug_set_flags; 0 = shipped configuration)."""

@@ -49,7 +49,7 @@ def test_wave_levels_vs_oracle(gpu_ctx, w, h, seed):
 
 # band heights: auto, one chunk, bands not a multiple of the lag span, a band taller than the
 # image; sizes: tiny, ragged (width not a multiple of 64, odd height), 1080p
-@pytest.mark.parametrize("rows", [0, 8, 24, 40, 4096])
+@pytest.mark.parametrize("rows", [0, 8, 24, 40, 2040])
 @pytest.mark.parametrize("n,w,h", [(2, 16, 16), (3, 203, 97), (2, 1920, 1080), (5, 300, 1203)])
 def test_wave_levels_equal_block_kernel(gpu_ctx, rows, n, w, h):
     imgs = synth_batch(n, w, h, 40 + w % 7)
@@ -160,7 +160,7 @@ DUO_OFF = sgpu.SiftContext.DEBUG_DUO_OFF
 # band heights: auto, one chunk (each band re-walks 2 (RA + RB) halo rows), not a multiple of
 # 8, taller than the image; sizes: tiny (one strip with both edges), ragged widths (not a
 # multiple of the 104- / 116-column strips), odd heights (the (H-1, H-1) bottom pair), 1080p
-@pytest.mark.parametrize("rows", [0, 8, 36, 4096])
+@pytest.mark.parametrize("rows", [0, 8, 36, 2040])
 @pytest.mark.parametrize("n,w,h", [(2, 16, 16), (3, 203, 97), (2, 1920, 1080), (2, 300, 1203),
                                    (1, 104, 33)])
 def test_duo_levels_equal_single_level(gpu_ctx, rows, n, w, h):
@@ -228,7 +228,8 @@ def test_tile_levels_equal_wave_kernel(gpu_ctx, n, w, h, no):
         gpu_ctx.extract(imgs)
         ref = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
         k_ref = [gpu_ctx.features(i)[0].copy() for i in range(n)]
-        for flags in (TILE, TILE | gpu_ctx.DEBUG_PYR_SERIAL, 0):
+        # TILE | DUO: the tile-duo schedule (two levels per tile launch, SGPU_TILE_DUO)
+        for flags in (TILE, TILE | DUO, TILE | gpu_ctx.DEBUG_PYR_SERIAL, 0):
             gpu_ctx.set_debug_flags(flags)
             gpu_ctx.extract(imgs)
             got = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
@@ -257,13 +258,15 @@ def test_tile_levels_all_widths(gpu_ctx, over):
         gpu_ctx.set_debug_flags(TILE_OFF)
         gpu_ctx.extract(imgs)
         ref = [_levels(gpu_ctx, i, opts) for i in (0, 1)]
+        for flags in (TILE, TILE | DUO):
+            gpu_ctx.set_debug_flags(flags)
+            gpu_ctx.extract(imgs)
+            got = [_levels(gpu_ctx, i, opts) for i in (0, 1)]
+            for a, b in zip(ref, got):
+                for o, (la, lb) in enumerate(zip(a, b)):
+                    for lvl, (x, y) in enumerate(zip(la, lb)):
+                        assert np.array_equal(_bits(x), _bits(y)), (flags, o, lvl)
         gpu_ctx.set_debug_flags(TILE)
-        gpu_ctx.extract(imgs)
-        got = [_levels(gpu_ctx, i, opts) for i in (0, 1)]
-        for a, b in zip(ref, got):
-            for o, (la, lb) in enumerate(zip(a, b)):
-                for lvl, (x, y) in enumerate(zip(la, lb)):
-                    assert np.array_equal(_bits(x), _bits(y)), (o, lvl)
         fimgs = (imgs.astype(np.float32) / np.float32(255.0)).astype(np.float32)
         gpu_ctx.extract(fimgs[1])
         got_f = [[gpu_ctx.gaussian(0, o, lvl).copy() for lvl in range(opts.dog_level_num + 3)]

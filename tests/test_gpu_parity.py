@@ -703,6 +703,39 @@ def test_rect_keypoints_vs_oracle(gpu_ctx, over):
     gpu_ctx.set_options(default_options())
 
 
+@pytest.mark.parametrize("n,w,h,over", [(1, 1920, 1080, {}), (3, 640, 480, {}), (2, 203, 97, {}),
+                                        (1, 4096, 4096, dict(octave_num=6)),
+                                        (2, 517, 389, dict(dog_level_num=1)),
+                                        (2, 517, 389, dict(dog_level_num=2)),
+                                        (2, 517, 389, dict(dog_level_num=5)),
+                                        (1, 641, 479, dict(octave_min=-1)),
+                                        (1, 641, 479, dict(octave_min=1)),
+                                        (2, 640, 480, dict(subpixel=0))])
+def test_extrema_tile_equals_wave(gpu_ctx, n, w, h, over):
+    """The tile extremum kernel (k_extrema_tile: a workgroup's 64 x 16-pixel window of every
+    Gaussian plane loaded at once, DoG planes in LDS, the pre-filter and ComputeKEY per lane)
+    against the wave-streaming k_extrema_wave2 (SGPU_DEBUG_EXTREMA_TILE_OFF): the same
+    candidates in the same order and every key bit for bit, for 1 .. 6 DoG levels per octave."""
+    imgs = synth_batch(n, w, h, 820 + w % 17)
+    opts = default_options(**over)
+    gpu_ctx.set_options(opts)
+    try:
+        gpu_ctx.set_debug_flags(gpu_ctx.DEBUG_EXTREMA_TILE_OFF)
+        gpu_ctx.extract(imgs)
+        ci, cf = gpu_ctx.candidates()
+        ref = [gpu_ctx.features(i, descriptors=False)[0] for i in range(n)]
+        gpu_ctx.set_debug_flags(gpu_ctx.DEBUG_GAUSS_TILE_ALWAYS)
+        gpu_ctx.extract(imgs)
+        ti, tf = gpu_ctx.candidates()
+        assert len(ci) > 0 and np.array_equal(ci, ti) and np.array_equal(_bits(cf), _bits(tf))
+        for i in range(n):
+            k = gpu_ctx.features(i, descriptors=False)[0]
+            assert k.shape == ref[i].shape and np.array_equal(_bits(k), _bits(ref[i])), i
+    finally:
+        gpu_ctx.set_debug_flags(0)
+        gpu_ctx.set_options(default_options())
+
+
 @pytest.mark.parametrize("n,w,h", [(1, 1920, 1080), (6, 640, 480)])
 def test_wide_descriptor_equals_flat(gpu_ctx, n, w, h):
     """k_descriptor_wide (a workgroup of 4 waves per feature, each wave every fourth 64-pixel step
