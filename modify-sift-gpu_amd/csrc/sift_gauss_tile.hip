@@ -45,7 +45,7 @@ __device__ __forceinline__ float ttap(const Taps& k, int t) {
     return k.k[t < FW - 1 - t ? t : FW - 1 - t];
 }
 
-template <int FW>
+template <int FW, int TH = kTH>
 struct TileGeom {
     static constexpr int HALF = FW >> 1;
     static constexpr int OFF = (-HALF) & 3;                  // LDS column of the window's first input
@@ -54,7 +54,7 @@ struct TileGeom {
     static constexpr int SH = OFF & 1;                       // keeps the H-pass reads 16-B aligned
     static constexpr int IN_S0 = (4 * NQ + SH + 3) & ~3;
     static constexpr int IN_S = IN_S0 + ((2 - IN_S0) & 31);  // float2 per row pair (= 2 mod 32)
-    static constexpr int ROWS = kTH + FW - 1;                // window rows (even: FW is odd)
+    static constexpr int ROWS = TH + FW - 1;                 // window rows (even: FW is odd)
     static constexpr int NPAIR = ROWS / 2;
     static constexpr int HS = kTW + 4;                       // H-result row stride (floats)
     static constexpr int IN_BYTES = NPAIR * IN_S * 8;
@@ -65,6 +65,7 @@ struct TileGeom {
     static constexpr int HITEMS = (NH + kTT - 1) / kTT;
     static constexpr int NRD = (FW + 3) / 2;                 // ds_read_b128 per H item
     static_assert(FW % 2 == 1 && FW <= 33, "odd widths up to 33");
+    static_assert(TH == 16 || TH == 32, "tile heights 16 and 32 (V pass: TH / 8 rows per thread)");
     static_assert(IN_S % 32 == 2 && 4 * NQ + SH <= IN_S, "row-pair stride");
 };
 
@@ -214,23 +215,26 @@ __device__ __forceinline__ void tile_hpass(const Taps& taps, const f2v* s_in, fl
 // The output tile from a window already in LDS (s_in, TileGeom<FW>'s layout, window column c =
 // image column x0 - HALF - OFF + c): H pass into s_h, V pass, stores of level rows y0 .. y0 + 31
 // (and the decimation into the next octave's level 0).
-template <int FW, bool DS>
+template <int FW, bool DS, int TH = kTH>
 __device__ __forceinline__ void tile_hv(const TileJob& J, const Taps& taps, float* dst, int b,
                                         int x0, int y0, const f2v* s_in, float* s_h) {
-    using G = TileGeom<FW>;
+    using G = TileGeom<FW, TH>;
+    constexpr int RT = TH / 8;   // V-pass rows per thread
     constexpr int HS = G::HS;
     tile_hpass<FW, G::NPAIR, kTW, G::IN_S, G::OFF, G::SH, HS>(taps, s_in, s_h);
     __syncthreads();
-    // V pass: tile rows vr .. vr + 3, columns vc, vc + 1
+    // V pass: tile rows vr .. vr + RT - 1, columns vc, vc + 1
     const int tid = threadIdx.x;
     const int W = J.W, H = J.H;
-    const int vc = (tid & 31) * 2, vr = (tid >> 5) * 4;
-    f2v acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+    const int vc = (tid & 31) * 2, vr = (tid >> 5) * RT;
+    f2v acc[RT];
 #pragma unroll
-    for (int m = 0; m < FW + 3; m++) {
+    for (int j = 0; j < RT; j++) acc[j] = f2v{0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < FW + RT - 1; m++) {
         const f2v v = *reinterpret_cast<const f2v*>(s_h + (vr + m) * HS + vc);
 #pragma unroll
-        for (int j = 0; j < 4; j++)
+        for (int j = 0; j < RT; j++)
             if (m - j >= 0 && m - j < FW) acc[j] = tpk(v, ttap<FW>(taps, m - j), acc[j]);
     }
     const int x = x0 + vc;
@@ -238,7 +242,7 @@ __device__ __forceinline__ void tile_hv(const TileJob& J, const Taps& taps, floa
     float* d = dst + (long long)b * J.dst_img;
     float* dd = DS ? J.ds + (long long)b * J.ds_img : nullptr;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
+    for (int j = 0; j < RT; j++) {
         const int y = y0 + vr + j;
         if (y >= H) break;
         *reinterpret_cast<f2v*>(d + (long long)y * W + x) = acc[j];
@@ -252,18 +256,18 @@ __device__ __forceinline__ void tile_hv(const TileJob& J, const Taps& taps, floa
     }
 }
 
-// One 64 x 32 output tile (logical block lb of job J) with the workgroup's LDS `smem`.
-template <int FW, bool U8, bool DS>
+// One 64 x TH output tile (logical block lb of job J) with the workgroup's LDS `smem`.
+template <int FW, bool U8, bool DS, int TH = kTH>
 __device__ __forceinline__ void tile_block(const TileJob& J, int lb, char* smem) {
-    using G = TileGeom<FW>;
+    using G = TileGeom<FW, TH>;
     f2v* s_in = reinterpret_cast<f2v*>(smem);
     float* s_h = reinterpret_cast<float*>(smem + G::IN_BYTES);
     const int sx = lb % J.tx, rest = lb / J.tx;
     const int ty = rest % J.ty, b = rest / J.ty;
-    const int x0 = sx * kTW, y0 = ty * kTH;
+    const int x0 = sx * kTW, y0 = ty * TH;
     tile_window<G, U8>(J, b, x0 - G::HALF - G::OFF, y0 - G::HALF, s_in);
     __syncthreads();
-    tile_hv<FW, DS>(J, J.taps, J.dst, b, x0, y0, s_in, s_h);
+    tile_hv<FW, DS, TH>(J, J.taps, J.dst, b, x0, y0, s_in, s_h);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -381,26 +385,26 @@ __device__ __forceinline__ void tile_duo_block(const TileJob& J, int lb, char* s
     tile_hv<FWB, DSB>(J, J.taps2, J.dst2, b, x0, y0, s_w, s_h);
 }
 
-template <int FW, bool U8, bool DS>
+template <int FW, bool U8, bool DS, int TH>
 __global__ __launch_bounds__(kTT) void k_gauss_tile(const TileJob J) {
-    __shared__ __attribute__((aligned(16))) char smem[TileGeom<FW>::LDS_BYTES];
+    __shared__ __attribute__((aligned(16))) char smem[TileGeom<FW, TH>::LDS_BYTES];
     if (J.zero.n[0] | J.zero.n[1] | J.zero.n[2]) tile_zero(J.zero);
-    tile_block<FW, U8, DS>(J, tile_order(blockIdx.x, gridDim.x), smem);
+    tile_block<FW, U8, DS, TH>(J, tile_order(blockIdx.x, gridDim.x), smem);
 }
 
 // Two independent level jobs in one launch (the diagonal schedule, DESIGN.md 4.4: octave o+1's
 // level k beside octave o's level k + kds): blocks [0, nbB) job B (dispatched first), the rest job
 // A; nbB is a multiple of 8, so both keep the XCD-aware order.  f32 levels without decimation.
-template <int FWA, int FWB>
+template <int FWA, int FWB, int TH>
 __global__ __launch_bounds__(kTT) void k_gauss_tile_diag(const TileJob A, const TileJob B, int nbB) {
-    constexpr int LA = TileGeom<FWA>::LDS_BYTES, LB = TileGeom<FWB>::LDS_BYTES;
+    constexpr int LA = TileGeom<FWA, TH>::LDS_BYTES, LB = TileGeom<FWB, TH>::LDS_BYTES;
     __shared__ __attribute__((aligned(16))) char smem[LA > LB ? LA : LB];
     const int bid = blockIdx.x;
     if (bid < nbB) {
         const int lb = tile_order(bid, nbB);
-        if (lb < B.nblocks) tile_block<FWB, false, false>(B, lb, smem);
+        if (lb < B.nblocks) tile_block<FWB, false, false, TH>(B, lb, smem);
     } else {
-        tile_block<FWA, false, false>(A, tile_order(bid - nbB, (int)gridDim.x - nbB), smem);
+        tile_block<FWA, false, false, TH>(A, tile_order(bid - nbB, (int)gridDim.x - nbB), smem);
     }
 }
 
@@ -426,7 +430,7 @@ __global__ __launch_bounds__(kTT) void k_gauss_tile_duo_diag(const TileJob A, co
     }
 }
 
-TileJob make_job(const LevelOp& op) {
+TileJob make_job(const LevelOp& op, int th = kTH) {
     TileJob J{};
     J.src = op.src;
     J.src8 = op.src_u8;
@@ -442,17 +446,17 @@ TileJob make_job(const LevelOp& op) {
     J.dsh = op.ds_h;
     J.ds_img = op.ds_img_stride;
     J.tx = (op.w + kTW - 1) / kTW;
-    J.ty = (op.h + kTH - 1) / kTH;
+    J.ty = (op.h + th - 1) / th;
     J.nblocks = J.tx * J.ty * op.batch;
     J.zero = op.zero;
     return J;
 }
 
-template <int FW>
-hipError_t tile_launch(const LevelOp& op, hipStream_t stream) {
-    const TileJob J = make_job(op);
+template <int FW, int TH>
+hipError_t tile_launch_th(const LevelOp& op, hipStream_t stream) {
+    const TileJob J = make_job(op, TH);
 #define SGK_TILE(U8, DS) \
-    hipLaunchKernelGGL((k_gauss_tile<FW, U8, DS>), dim3((unsigned)J.nblocks), dim3(kTT), 0, stream, J)
+    hipLaunchKernelGGL((k_gauss_tile<FW, U8, DS, TH>), dim3((unsigned)J.nblocks), dim3(kTT), 0, stream, J)
     if (op.src_u8) {
         if (op.ds_dst) SGK_TILE(true, true); else SGK_TILE(true, false);
     } else {
@@ -462,12 +466,19 @@ hipError_t tile_launch(const LevelOp& op, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// (16-row tiles for the larger levels measured slower: C2 0.225-0.229 vs 0.220-0.224 ms with 32,
+// alternating processes, tests/diag/r06e.sh; TileGeom / tile_hv keep the height as a parameter)
+template <int FW>
+hipError_t tile_launch(const LevelOp& op, hipStream_t stream) {
+    return tile_launch_th<FW, kTH>(op, stream);
+}
+
 template <int FWA, int FWB>
 hipError_t tile_diag_launch(const LevelOp& a, const LevelOp& b, hipStream_t stream) {
-    const TileJob A = make_job(a), B = make_job(b);
+    const TileJob A = make_job(a, kTH), B = make_job(b, kTH);
     const int nbBp = (B.nblocks + 7) / 8 * 8;
-    hipLaunchKernelGGL((k_gauss_tile_diag<FWA, FWB>), dim3((unsigned)(nbBp + A.nblocks)), dim3(kTT),
-                       0, stream, A, B, nbBp);
+    hipLaunchKernelGGL((k_gauss_tile_diag<FWA, FWB, kTH>), dim3((unsigned)(nbBp + A.nblocks)),
+                       dim3(kTT), 0, stream, A, B, nbBp);
     return hipGetLastError();
 }
 

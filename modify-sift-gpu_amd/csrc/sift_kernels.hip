@@ -2650,6 +2650,12 @@ constexpr int kFlatWords = 2 * kFlatHist + 144;
 // tests/diag/r05l.sh), and integer sums do not depend on their order.
 typedef __attribute__((address_space(3))) unsigned long long lds_u64;
 
+// 1: the gradient's left / right neighbours from the neighbouring lanes' centre pixels by DPP
+// (3 gathers per pixel); 0: the 4 gathers of round 5 (A/B, build variant)
+#ifndef SGK_DESC_DPP_NB
+#define SGK_DESC_DPP_NB 1
+#endif
+
 __device__ __forceinline__ unsigned long long to_fix32(float v) {
     const float fl = floor_(v);
     const uint32_t lo = (uint32_t)((v - fl) * 4294967296.0f);
@@ -2805,21 +2811,31 @@ __device__ __forceinline__ void flat_accumulate(uint32_t e, int lane, const floa
             // 32-bit byte offsets from the level image's base (an image plane is < 4 GB)
             const char* gp = reinterpret_cast<const char*>(g) + 4u * (uint32_t)(yc * W + x);
             const uint32_t W4 = 4u * (uint32_t)W;
+#if SGK_DESC_DPP_NB
             // the gradient's 4 neighbours: the row above and below are gathered, the left and right
             // ones are the neighbouring lanes' centre pixels (lanes hold consecutive pixels of a
             // row: p - 1 and p + 1) taken by DPP wave shifts; only the lanes at a row's or the
             // step's ends load them -- 3 gathers per pixel instead of 4, the same values
+            // (every load is issued before the shifts wait for the centre: one round trip)
+            const bool from_r = valid && lane < 63 && p + 1 < rnx;   // lane + 1 holds x + 1
+            const bool from_l = valid && lane > 0 && p > rsr;        // lane - 1 holds x - 1
             const float cen = *reinterpret_cast<const float*>(gp);
             const float gup = *reinterpret_cast<const float*>(gp - W4);
             const float gdn = *reinterpret_cast<const float*>(gp + W4);
-            float grt = __int_as_float(__builtin_amdgcn_update_dpp(
+            float lrt = 0.0f, llt = 0.0f;
+            if (!from_r) lrt = *reinterpret_cast<const float*>(gp + 4);
+            if (!from_l) llt = *reinterpret_cast<const float*>(gp - 4);
+            const float srt = __int_as_float(__builtin_amdgcn_update_dpp(
                 0, __float_as_int(cen), 0x130, 0xf, 0xf, false));   // wave_shl:1: lane + 1
-            float glt = __int_as_float(__builtin_amdgcn_update_dpp(
+            const float slt = __int_as_float(__builtin_amdgcn_update_dpp(
                 0, __float_as_int(cen), 0x138, 0xf, 0xf, false));   // wave_shr:1: lane - 1
-            if (!(valid && lane < 63 && p + 1 < rnx)) grt = *reinterpret_cast<const float*>(gp + 4);
-            if (!(valid && lane > 0 && p > rsr)) glt = *reinterpret_cast<const float*>(gp - 4);
-            const float gx = grt - glt;
+            const float gx = (from_r ? srt : lrt) - (from_l ? slt : llt);
             const float gy = gdn - gup;
+#else
+            (void)rnx;
+            const float gx = *reinterpret_cast<const float*>(gp + 4) - *reinterpret_cast<const float*>(gp - 4);
+            const float gy = *reinterpret_cast<const float*>(gp + W4) - *reinterpret_cast<const float*>(gp - W4);
+#endif
             const float m2 = fma_(gx, gx, gy * gy);
             float rot = atan2_relaxed(gy, gx);
             const float dd = fabs_(anglef - rot);

@@ -152,9 +152,9 @@ def test_speed_replica_timing_slots(tmp_path):
     non-negative time, the pyramid and descriptor slots are positive, and the slots add up to no
     more than the wall time per RunSIFT of that second (stage-timed, SetVerbose(-2)) loop, plus a
     small allowance for event rounding.  The first loop runs with the stage timing off
-    (SetVerbose(0) -> _timingS 0, SiftGPU.cpp:426-427), so it is no slower than the second.  The
-    relative sizes of the slots are wall-clock properties and go to bench.py's report, not here
-    (one C2 run once read 0.53 ms against 0.38-0.41 for its neighbours)."""
+    (SetVerbose(0) -> _timingS 0, SiftGPU.cpp:426-427).  Wall-clock ratios between the two loops
+    and the relative sizes of the slots go to bench.py's report, not here (one C2 run once read
+    0.53 ms against 0.38-0.41 for its neighbours)."""
     exe = os.path.join(ROOT, "modify-sift-gpu_amd", "bin", "speed_replica")
     img = synth_image(1920, 1080, 2000)      # the C2 image of bench.py
     pgm = tmp_path / "c2.pgm"
@@ -171,8 +171,11 @@ def test_speed_replica_timing_slots(tmp_path):
     assert all(np.isfinite(t[s]) and t[s] >= 0 for s in slots), t
     assert t["descriptor"] > 0 and t["build_pyramid"] > 0, t
     total = sum(t[s] for s in slots)
-    assert total <= 1.10 * sp["timed_avg_ms"] + 0.02, (total, sp["timed_avg_ms"], t)
-    assert sp["avg_ms"] <= 1.10 * sp["timed_avg_ms"] + 0.02, sp
+    # the stage events lie inside each RunSIFT of the timed loop, so their sum is bounded by its
+    # wall time per call (plus event rounding), and the slots are not lost or zeroed: they cover
+    # at least half of it (the rest is host work between the events)
+    assert 0.5 * sp["timed_avg_ms"] <= total <= 1.10 * sp["timed_avg_ms"] + 0.02, \
+        (total, sp["timed_avg_ms"], t)
 
 
 def test_allocate_pyramid_then_runsift_allocates_nothing(tmp_path):
@@ -213,16 +216,20 @@ def test_reserve_then_extract_allocates_nothing(gpu_ctx):
 
 
 @pytest.mark.parametrize("cap", [4096, 16])
-def test_host_output_equals_copy_features(gpu_ctx, cap):
+@pytest.mark.parametrize("wide", [True, False])
+def test_host_output_equals_copy_features(gpu_ctx, cap, wide):
     """sgpu_set_host_output: the next one-image extract writes image 0's keys and descriptors
     from the GPU into the registered page-locked buffers (k_copy_out, in the extract's stream);
     they equal sgpu_copy_features' copies bit for bit, sgpu_copy_features on those pointers copies
-    nothing more, and with a capacity below the count (16) the GPU writes only that many and
-sgpu_copy_features into buffers of the image's size does the work.  The
-    registration serves one extract: the one after it writes nothing there."""
+    nothing more, and with a capacity below the count (16) the GPU writes exactly the first 16
+    keys and descriptors and nothing past them, and sgpu_copy_features into buffers of the image's
+    size does the work.  Both writers: the workgroup-per-feature descriptor kernel itself (wide,
+    the single-image default) and k_copy_out after the one-wave kernel.  The registration serves
+    one extract: the one after it writes nothing there."""
     import sgpu
     img = synth_image(640, 480, 77)
     gpu_ctx.set_options(default_options())
+    gpu_ctx.set_debug_flags(gpu_ctx.DEBUG_DESC_WIDE_ALWAYS if wide else gpu_ctx.DEBUG_DESC_WIDE_OFF)
     hk = sgpu.PinnedArray((cap, 4), np.float32)
     hd = sgpu.PinnedArray((cap, 128), np.float32)
     try:
@@ -238,7 +245,8 @@ sgpu_copy_features into buffers of the image's size does the work.  The
             assert np.array_equal(hd.array[:n].view(np.uint32), d.view(np.uint32))
             assert np.all(hk.array[n:] == -1.0)
         else:
-            assert np.all(hk.array[:] == -1.0) or np.array_equal(hk.array.view(np.uint32), k[:cap].view(np.uint32))
+            assert np.array_equal(hk.array.view(np.uint32), k[:cap].view(np.uint32))
+            assert np.array_equal(hd.array.view(np.uint32), d[:cap].view(np.uint32))
         # through the registered pointers (when they hold the image): the fast path
         if n <= cap:
             gpu_ctx.copy_features_into(hk.array, hd.array)
@@ -249,6 +257,32 @@ sgpu_copy_features into buffers of the image's size does the work.  The
         assert np.all(hk.array == -2.0)
         k2, _ = gpu_ctx.features(0)
         assert np.array_equal(k2.view(np.uint32), k.view(np.uint32))
+    finally:
+        gpu_ctx.set_debug_flags(0)
+        hk.free()
+        hd.free()
+
+
+def test_rejected_extract_consumes_host_output(gpu_ctx):
+    """an extract rejected for its arguments still consumes a registered host output
+    (sgpu_set_host_output), so a later good extract does not write into buffers the caller may
+    have freed since: the buffers keep their sentinel values."""
+    import ctypes
+    import sgpu
+    img = synth_image(320, 240, 6)
+    gpu_ctx.set_options(default_options())
+    hk = sgpu.PinnedArray((4096, 4), np.float32)
+    hd = sgpu.PinnedArray((4096, 128), np.float32)
+    try:
+        hk.array[:] = -3.0
+        hd.array[:] = -3.0
+        gpu_ctx.set_host_output(hk.array, hd.array, 4096)
+        buf = np.zeros((8, 8), np.uint8)
+        rc = sgpu.lib().sgpu_extract(gpu_ctx._ctx, buf.ctypes.data_as(ctypes.c_void_p), 1, 8, 8, 4, 0)
+        assert rc != 0   # stride < width: rejected
+        gpu_ctx.extract(img)
+        assert gpu_ctx.total() > 0
+        assert np.all(hk.array == -3.0) and np.all(hd.array == -3.0)
     finally:
         hk.free()
         hd.free()

@@ -345,8 +345,10 @@ def test_full_hd_batch_properties(gpu_ctx):
     assert np.array_equal(_bits(k), _bits(first[0][0]))
 
 
-def test_full_hd_single_vs_oracle(gpu_ctx):
-    img = synth_image(1920, 1080, 4242)
+@pytest.mark.parametrize("seed", [4242, 2000])
+def test_full_hd_single_vs_oracle(gpu_ctx, seed):
+    """One 1080p image (-no 4) against the oracle key by key; seed 2000 is bench.py's C2 image."""
+    img = synth_image(1920, 1080, seed)
     opts = default_options(octave_num=4)
     gpu_ctx.set_options(opts)
     gpu_ctx.extract(img)
@@ -734,6 +736,36 @@ def test_extrema_tile_equals_wave(gpu_ctx, n, w, h, over):
     finally:
         gpu_ctx.set_debug_flags(0)
         gpu_ctx.set_options(default_options())
+
+
+@pytest.mark.parametrize("normalized", [1, 0])
+def test_dual_descriptor_vs_exact(gpu_ctx, normalized):
+    """The round-4 dual-cell descriptor kernel (SGPU_DEBUG_DESC_DUAL, kept for A/B) against the
+    bit-exact kernel: same keys, descriptors within L2 1e-5 (relative for -unn) -- the bound the
+    shipped kernel meets (test_shipped_descriptor_vs_exact)."""
+    from sift_synth import synth_batch_fast
+    imgs = synth_batch_fast(4, 1280, 720, 515)
+    opts = default_options(normalized=normalized)
+    gpu_ctx.set_options(opts)
+    try:
+        gpu_ctx.set_debug_flags(gpu_ctx.DEBUG_DESC_DUAL)
+        gpu_ctx.extract(imgs)
+        dual = [gpu_ctx.features(i) for i in range(4)]
+        gpu_ctx.set_debug_flags(gpu_ctx.DEBUG_EXACT_DESCRIPTOR)
+        gpu_ctx.extract(imgs)
+        exact = [gpu_ctx.features(i) for i in range(4)]
+    finally:
+        gpu_ctx.set_debug_flags(0)
+        gpu_ctx.set_options(default_options())
+    kd = np.concatenate([f[0] for f in dual])
+    ke = np.concatenate([f[0] for f in exact])
+    assert len(kd) > 3000 and np.array_equal(_bits(kd), _bits(ke))
+    dd = np.concatenate([f[1] for f in dual]).astype(np.float64)
+    de = np.concatenate([f[1] for f in exact]).astype(np.float64)
+    l2 = np.linalg.norm(dd - de, axis=1)
+    if not normalized:
+        l2 = l2 / np.maximum(np.linalg.norm(de, axis=1), 1e-30)
+    assert l2.max() < 1e-5, l2.max()
 
 
 @pytest.mark.parametrize("n,w,h", [(1, 1920, 1080), (6, 640, 480)])
