@@ -1562,7 +1562,10 @@ __device__ __forceinline__ void orientation_hist_wave(const OriKey& K, const Fea
     const float ymax = fmin_(K.H - 1.5f, floor_(K.ky + win) + 0.5f);
     const int ncols = xmax >= xmin ? (int)(xmax - xmin) + 1 : 0;
     const int nrows = ymax >= ymin ? (int)(ymax - ymin) + 1 : 0;
-    const int total = ncols * nrows;
+#ifndef SGK_ORI_EXP
+#define SGK_ORI_EXP 0   // timing experiment only (wrong orientations): 1 = no window samples
+#endif
+    const int total = SGK_ORI_EXP == 1 ? 0 : ncols * nrows;
     float acc = 0.0f;   // bin `lane`
     // sample base + lane: its pixel and the 4 gradient neighbours, fetched one batch ahead (the
     // loads are unconditional, at a clamped in-plane pixel, so the compiler waits only for the
@@ -1772,6 +1775,38 @@ __global__ __launch_bounds__(256) void k_color_gray(const uint8_t* __restrict__ 
 // (io.off != nullptr: the grid's last block writes the readback record instead -- off[0] = the
 // candidate count, off[1 + b] = image b's first feature for b in [0, batch] -- which one more
 // launch after the descriptors wrote before; a single image's extract pays per launch)
+// Candidate f's 0, 1 or 2 features at slots e0 .. e0 + n - 1 (ReshapeFeatureListCPU,
+// PyramidCU.cpp:560-578): the orientations unpacked, the image-coordinate keys
+// (PyramidCU.cpp:701-751).
+__device__ __forceinline__ void expand_one(uint32_t f, uint32_t e0, uint32_t n,
+                                           const float4* __restrict__ cand,
+                                           const int2* __restrict__ info, const FeatureParams& fp,
+                                           float4* __restrict__ feat, int2* __restrict__ feat_info,
+                                           float4* __restrict__ keys) {
+    const float4 c = cand[f];
+    const int2 in = info[f];
+    const int o = in.y / fp.d;
+    const float oss = ldexpf(1.0f, o + fp.octave_min);   // os * 2^o, os = 2^octave_min
+    const double twopi = 2.0 * 3.14159265358979323846;
+    float ang[2];
+    if (fp.num_orientation >= 2) {
+        const double factor = 2.0 * 3.14159265358979323846 / 65535.0;
+        const uint32_t pk = as_uint(c.w);
+        ang[0] = (float)(factor * (double)(pk & 0xffffu));
+        ang[1] = (float)(factor * (double)(pk >> 16));
+    } else {
+        ang[0] = ang[1] = c.w;
+    }
+    for (uint32_t q = 0; q < n; q++) {
+        const uint32_t e = e0 + q;
+        feat[e] = make_float4(c.x, c.y, c.z, ang[q]);
+        feat_info[e] = in;
+        keys[e] = make_float4(oss * (c.x - 0.5f) + fp.origin_offset,
+                              oss * (c.y - 0.5f) + fp.origin_offset, oss * c.z,
+                              (float)fmod(twopi - (double)ang[q], twopi));
+    }
+}
+
 __global__ __launch_bounds__(256) void k_expand(const float4* __restrict__ cand,
                                                 const int2* __restrict__ info,
                                                 const uint32_t* __restrict__ eoff,
@@ -1797,30 +1832,8 @@ __global__ __launch_bounds__(256) void k_expand(const float4* __restrict__ cand,
     }
     const uint32_t ncand = min(*n_cand_dev, cap);
     for (uint32_t f = blockIdx.x * 256 + threadIdx.x; f < ncand; f += (uint32_t)nblk * 256) {
-    const uint32_t e0 = eoff[f], n = eoff[f + 1] - e0;
-    if (n == 0) continue;
-    const float4 c = cand[f];
-    const int2 in = info[f];
-    const int o = in.y / fp.d;
-    const float oss = ldexpf(1.0f, o + fp.octave_min);   // os * 2^o, os = 2^octave_min
-    const double twopi = 2.0 * 3.14159265358979323846;
-    float ang[2];
-    if (fp.num_orientation >= 2) {
-        const double factor = 2.0 * 3.14159265358979323846 / 65535.0;
-        const uint32_t pk = as_uint(c.w);
-        ang[0] = (float)(factor * (double)(pk & 0xffffu));
-        ang[1] = (float)(factor * (double)(pk >> 16));
-    } else {
-        ang[0] = ang[1] = c.w;
-    }
-    for (uint32_t q = 0; q < n; q++) {
-        const uint32_t e = e0 + q;
-        feat[e] = make_float4(c.x, c.y, c.z, ang[q]);
-        feat_info[e] = in;
-        keys[e] = make_float4(oss * (c.x - 0.5f) + fp.origin_offset,
-                              oss * (c.y - 0.5f) + fp.origin_offset, oss * c.z,
-                              (float)fmod(twopi - (double)ang[q], twopi));
-    }
+        const uint32_t e0 = eoff[f], n = eoff[f + 1] - e0;
+        if (n != 0) expand_one(f, e0, n, cand, info, fp, feat, feat_info, keys);
     }
 }
 
@@ -2651,9 +2664,12 @@ constexpr int kFlatWords = 2 * kFlatHist + 144;
 typedef __attribute__((address_space(3))) unsigned long long lds_u64;
 
 // 1: the gradient's left / right neighbours from the neighbouring lanes' centre pixels by DPP
-// (3 gathers per pixel); 0: the 4 gathers of round 5 (A/B, build variant)
+// (3 gathers per pixel; build variant); 0 (shipped): the 4 gathers -- the DPP form measured
+// 1.492-1.493 against 1.425-1.430 ms per 128 x 1080p step (three alternating pairs, r06f): the
+// shifts wait for the centre load, and the row-end lanes' loads are exec-masked instructions of
+// their own
 #ifndef SGK_DESC_DPP_NB
-#define SGK_DESC_DPP_NB 1
+#define SGK_DESC_DPP_NB 0
 #endif
 
 __device__ __forceinline__ unsigned long long to_fix32(float v) {
