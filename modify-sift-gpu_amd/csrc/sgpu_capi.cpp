@@ -162,6 +162,7 @@ struct sgpu_ctx {
     size_t wide_desc_max = SGK_WIDE_DESC_MAX;   // feature counts (of the previous call) up to which
                                            // descriptors run a workgroup per feature
                                            // (SGPU_WIDE_DESC_MAX)
+    bool unit_input = true;                // the last extract's input lies in [0, 1] (not a caller's f32)
     bool tile_duo = false;                 // tile duos when every level is tiled (SGPU_TILE_DUO=on;
                                            // measured slower)
     int tile_mb = SGK_TILE_MB;             // levels of at most this many MB: 2-D tile launches
@@ -564,6 +565,7 @@ static int layout_part(sgpu_ctx* ctx, Part& pt) {
     fp.keep_sign = O.keep_extremum_sign;
     fp.circular = O.circular_window;
     fp.normalize = O.normalized;
+    fp.unit_input = ctx->unit_input ? 1 : 0;
     fp.origin_offset = O.lowe_origin ? 0.0f : 0.5f;
     fp.octave_min = ctx->plan.octave_min + ctx->plan.ds;   // coordinate scale 2^(om + ds)
 
@@ -1074,6 +1076,9 @@ static int check_extract_args(sgpu_ctx* ctx, const void* images, bool is_f32, in
 
 static int extract_body(sgpu_ctx* ctx, const void* images, bool is_f32, int n, int w, int h,
                         int stride, int flags, int color) {
+    // a caller's float image may hold any range; u8, colour and the library's own conversions of
+    // them lie in [0, 1] (the descriptor's 32-bit sums rely on it, sift_kernels.hip flat_narrow)
+    ctx->unit_input = !is_f32;
     const bool staged = (flags & SGPU_INPUT_STAGED) != 0;
     const int channels = color == SGPU_RGB || color == SGPU_BGR ? 3 : color ? 4 : 1;
     HIPCHK(ctx, hipSetDevice(ctx->device));

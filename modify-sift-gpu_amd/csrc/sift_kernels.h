@@ -35,6 +35,7 @@ struct FeatureParams {
     int subpixel, num_orientation, keep_sign, circular, normalize;
     float origin_offset;                 // 0.5 (or 0 with -loweo)
     int octave_min;                      // -fo: octave o of the pyramid is octave o + octave_min
+    int unit_input;                      // the image's values lie in [0, 1] (u8 / 255, colour, -prep)
     OctaveDesc oct[kMaxOctaves];
 };
 

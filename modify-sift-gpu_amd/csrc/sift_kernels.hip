@@ -2662,6 +2662,20 @@ constexpr int kFlatWords = 2 * kFlatHist + 144;
 // (~4 cycles per lane, 7.8 ms per 128 x 1080p step against 1.37 with integer adds,
 // tests/diag/r05l.sh), and integer sums do not depend on their order.
 typedef __attribute__((address_space(3))) unsigned long long lds_u64;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// 1: features whose window cannot overflow it (unit-range input, <= kNarrowPix window pixels)
+// sum their contributions as 32-bit fixed point (20 fraction bits, ds_add_u32: half the LDS
+// traffic, 2 VALU per conversion instead of ~6) -- A/B build switch; 0: 64-bit for all
+#ifndef SGK_FLAT_U32
+#define SGK_FLAT_U32 0
+#endif
+// a contribution is <= 0.75 on unit-range images (m <= 0.5 sqrt(2), every weight <= 1 + rounding)
+// and each pixel adds at most its own contribution to a bin: window pixels * 0.75 < 2^12
+constexpr float kNarrowPix = 5000.0f;
+__device__ __forceinline__ uint32_t to_fix20(float v) {   // v >= 0
+    return (uint32_t)fma_(v, 1048576.0f, 0.5f);
+}
 
 // 1: the gradient's left / right neighbours from the neighbouring lanes' centre pixels by DPP
 // (3 gathers per pixel; build variant); 0 (shipped): the 4 gathers -- the DPP form measured
@@ -2712,6 +2726,18 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
         if (lane >= k) v += u;
     }
     return v;
+}
+
+// the window's half side hb (feature frame: the rotated 5 x 5-cell square) -- flat_accumulate's
+__device__ __forceinline__ float flat_half_box(const float4 key, const FeatureParams& fp) {
+    const float spt = fabs_(key.z * fp.window_factor);
+    float s, c;
+    sincos_(key.w, &s, &c);
+    return 2.5f * (fabs_(c * spt) + fabs_(s * spt)) + 0.01f;
+}
+// 32-bit sums for this feature (SGK_FLAT_U32, unit-range input, a window that cannot overflow)
+__device__ __forceinline__ bool flat_narrow(const FeatureParams& fp, float hb) {
+    return SGK_FLAT_U32 && fp.unit_input && (2.0f * hb + 2.0f) * (2.0f * hb + 2.0f) <= kNarrowPix;
 }
 
 // The accumulation of feature e's window into the histogram at sh (kFlatWords floats): wave wv
@@ -2765,6 +2791,8 @@ __device__ __forceinline__ void flat_accumulate(uint32_t e, int lane, const floa
     int y1 = (int)fmin_(fH - 2.0f, fmax_(-1.0f, floor_(key.y + hb - 0.5f)));
     const int bx0 = (int)fmax_(1.0f, fmin_(fW, ceilf(key.x - hb - 0.5f)));
     const int bx1 = (int)fmin_(fW - 2.0f, fmax_(-1.0f, floor_(key.x + hb - 0.5f)));
+    const bool narrow = flat_narrow(fp, hb);
+    lds_u32* hist32 = (lds_u32*)sh;
     if (!(spt > 0.0f)) y1 = y0 - 1;
     // a row's span: the columns whose dnx, dny can lie in [-2.5, 2.5) (0.05-pixel margin; the
     // per-pixel test decides)
@@ -2887,8 +2915,12 @@ __device__ __forceinline__ void flat_accumulate(uint32_t e, int lane, const floa
                 lds_u64* hp = hist + (((b - 1) * 4 + (a - 1)) * 8) * kFlatStride + copy;
                 const int o0 = b0 * kFlatStride, o1 = b1 * kFlatStride;
                 constexpr int CX = 8 * kFlatStride, CY = 4 * 8 * kFlatStride;
+                const int hoff = (((b - 1) * 4 + (a - 1)) * 8) * kFlatStride + copy;
                 auto add2 = [&](bool in, int off, float wc) {
-                    if (in) {
+                    if (in && narrow) {
+                        __hip_atomic_fetch_add(hist32 + hoff + off + o0, to_fix20(wc * tk0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_add(hist32 + hoff + off + o1, to_fix20(wc * tk1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else if (in) {
                         __hip_atomic_fetch_add(hp + off + o0, to_fix32(wc * tk0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         __hip_atomic_fetch_add(hp + off + o1, to_fix32(wc * tk1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
@@ -2909,21 +2941,31 @@ __device__ __forceinline__ void flat_accumulate(uint32_t e, int lane, const floa
 // normalised (NormalizeDescriptor, ProgramCU.cu:1173-1208) and stored as row `out`.
 __device__ __forceinline__ void flat_finish(int lane, const FeatureParams& fp,
                                             float* __restrict__ desc, uint32_t out,
-                                            const float* __restrict__ sh, int nh,
+                                            const float* __restrict__ sh, int nh, bool narrow,
                                             float* __restrict__ hdesc = nullptr) {
     const int cell = lane >> 2, sub = lane & 3;
     const int ix = cell & 3, iy = cell >> 2;
     unsigned long long s0 = 0, s1 = 0;
+    const int hi = ((iy * 4 + ix) * 8 + 2 * sub) * kFlatStride;
     for (int w = 0; w < nh; w++) {
-        const lds_u64* hc = (const lds_u64*)(sh + w * kFlatWords) +
-                                       ((iy * 4 + ix) * 8 + 2 * sub) * kFlatStride;
+        if (narrow) {
+            const lds_u32* hc = (const lds_u32*)(sh + w * kFlatWords) + hi;
 #pragma unroll
-        for (int k = 0; k < kFlatCopies; k++) {
-            s0 += hc[k];
-            s1 += hc[kFlatStride + k];
+            for (int k = 0; k < kFlatCopies; k++) {
+                s0 += hc[k];
+                s1 += hc[kFlatStride + k];
+            }
+        } else {
+            const lds_u64* hc = (const lds_u64*)(sh + w * kFlatWords) + hi;
+#pragma unroll
+            for (int k = 0; k < kFlatCopies; k++) {
+                s0 += hc[k];
+                s1 += hc[kFlatStride + k];
+            }
         }
     }
-    float b0 = (float)((double)(long long)s0 * 0x1p-32), b1 = (float)((double)(long long)s1 * 0x1p-32);
+    const double scale = narrow ? 0x1p-20 : 0x1p-32;
+    float b0 = (float)((double)(long long)s0 * scale), b1 = (float)((double)(long long)s1 * scale);
     asm volatile("" ::: "memory");
     if (fp.normalize) {
         float sn = wave_sum_dpp(fma_(b0, b0, b1 * b1));
@@ -2946,7 +2988,7 @@ __device__ __forceinline__ void descriptor_flat(uint32_t e, int lane, const floa
                                                 const FeatureParams& fp, float* __restrict__ desc,
                                                 uint32_t out, float* __restrict__ sh) {
     flat_accumulate(e, lane, pyr, feat, feat_info, fp, sh, 0, 1);
-    flat_finish(lane, fp, desc, out, sh, 1);
+    flat_finish(lane, fp, desc, out, sh, 1, flat_narrow(fp, flat_half_box(feat[e], fp)));
 }
 
 // waves per SIMD the allocation must allow: 8 (64 VGPRs, no spills): 1.448-1.451 ms per
@@ -3003,7 +3045,8 @@ __global__ __launch_bounds__(64 * NWV) SGK_FLAT_ATTR void k_descriptor_wide(cons
         const uint32_t out = out_index ? (uint32_t)out_index[e] : e;
         const bool to_host = hc.hkeys && out < hc.cap;
         if (wave == 0)
-            flat_finish(lane, fp, desc, out, &s_flat[0][0], NWV, to_host ? hc.hdesc : nullptr);
+            flat_finish(lane, fp, desc, out, &s_flat[0][0], NWV,
+                        flat_narrow(fp, flat_half_box(feat[e], fp)), to_host ? hc.hdesc : nullptr);
         else if (wave == 1 && lane == 0 && to_host)
             hc.hkeys[out] = hc.keys[e];
         __syncthreads();   // wave 0 has read every histogram before the next feature zeroes them
