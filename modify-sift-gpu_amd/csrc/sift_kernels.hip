@@ -320,6 +320,9 @@ struct GaussWaveGrid {
 #ifndef SGK_GW_HSPAD
 #define SGK_GW_HSPAD 4
 #endif
+#ifndef SGK_GW_STMAP
+#define SGK_GW_STMAP 0   // 1: conflict-free row-pair stores in k_gauss_lean (lane map, no pad slot)
+#endif
 constexpr int kGwWaves = SGK_GW_WPB;   // waves per workgroup of k_gauss_lean
 
 // band height of the level kernel: rows_hint > 0 forces it (test / tuning hook), else bands of
@@ -485,8 +488,17 @@ __device__ __forceinline__ void gauss_lean_wave(const GaussJob& J, int gw, f2v* 
     const int a0 = x0 - HALF - OFF;
     // loader lane: half-wave g, quad j (lanes past the row's last quad re-load the last quad and
     // store into a pad slot)
+#if SGK_GW_STMAP
+    // lane = 8 k + 4 g + i -> quad 4 k + i of row pair g: an 8-lane ds_write_b128 group covers
+    // all 32 banks (rows 2p and 2p + 2's pairs are 2 IN_S = 4 mod 32 floats apart), and the lanes
+    // past the row's last quad skip the row-pair store instead of sharing one pad slot
+    const int lj0 = (lane & 3) | ((lane >> 3) << 2);
+    const int lg = (lane >> 2) & 1, lj = min(lj0, NQ - 1);
+    const bool lreal = lj0 < NQ;
+#else
     const int lg = lane >> 5, lj = min(lane & 31, NQ - 1);
     const bool lreal = (lane & 31) < NQ;
+#endif
     const int gq = a0 + 4 * lj;
     const int lq = clampi(gq, 0, W - 4);
     const bool left = gq < 0, right = gq > W - 4;
@@ -562,6 +574,7 @@ __device__ __forceinline__ void gauss_lean_wave(const GaussJob& J, int gw, f2v* 
                 for (int t = 0; t < 4; t++) pr[t] = left ? e0 : (right ? e3 : pr[t]);
             }
             f2v* q = s_in + (m ? s_off1 : s_off0);
+            if (SGK_GW_STMAP && !lreal) continue;
             if (SH == 0) {
                 reinterpret_cast<float4*>(q)[0] = make_float4(pr[0].x, pr[0].y, pr[1].x, pr[1].y);
                 reinterpret_cast<float4*>(q)[1] = make_float4(pr[2].x, pr[2].y, pr[3].x, pr[3].y);

@@ -13,5 +13,5 @@ tail -2 gpurun_out/smoke.log
 timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err && echo bench ok && \
 timeout -k 10 900 bash tests/profile_kernels.sh "$TAG" && echo profile ok && \
 timeout -k 10 300 bash tests/pmc_match.sh "gpurun_out/pmc_match_$TAG" && \
-python3 tests/pmc_match_summary.py "gpurun_out/pmc_match_$TAG" k_match_raw "gpurun_out/${TAG}_match_sq_counters.json" && echo pmc match ok && \
+python3 tests/pmc_match_summary.py "gpurun_out/pmc_match_$TAG" "gpurun_out/${TAG}_match_sq_counters.json" && echo pmc match ok && \
 timeout -k 10 300 bash tests/profile_c2.sh "$TAG" > gpurun_out/prof_c2.log 2>&1 && echo c2 ok
