@@ -330,6 +330,17 @@ int sgpu_comm_allreduce_f64(sgpu_ctx* ctx, double* v, int n, int op_max);
                                               SGPU_DEBUG_GAUSS_TILE_ALWAYS tiles every one) */
 
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags);
+/* The batch pyramid's launch plan, a test / A-B hook -- the levels are the same
+ * bits in every plan.  trio: three-level launches (k_gauss_trio): none (shipped), on levels of
+ * >= 512 MB, or wherever the widths and the decimation allow (SGPU_TRIO=off / on / always at
+ * context creation).  pairs: the octave's paired-level launches taken from its end, (4, 5),
+ * (2, 3) with the decimation, (0, 1) (shipped), or from its front (SGPU_DUO_PLAN=end / front). */
+#define SGPU_TRIO_OFF 0
+#define SGPU_TRIO_ON 1
+#define SGPU_TRIO_ALWAYS 2
+#define SGPU_PAIRS_FRONT 0
+#define SGPU_PAIRS_END 1
+int sgpu_debug_set_schedule(sgpu_ctx* ctx, int trio, int pairs);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);
 /* Gaussian level (image, octave, level 0..level_num-1) as wa*h floats. */

@@ -46,6 +46,23 @@ namespace {
 #ifndef SGK_DUO_WIDE_MIN_MB
 #define SGK_DUO_WIDE_MIN_MB 512
 #endif
+// three levels per launch (k_gauss_trio: widths (11, 13, 17), the third decimated into the next
+// octave) for levels of at least this many MB; the octave's remaining (21, 25) pair then runs as a
+// paired-level launch
+// the octave's level pairs taken from its end ((4, 5), (2, 3) with the decimation, (0, 1)): 1,
+// or from its front: 0 (sgpu_ctx::duo_plan); from the end only on levels of at most
+// SGK_DUO_PLAN_MAXW columns (128 x 1080p: octave 0 2.575 vs 2.613 ms; 16 x 4096^2 (C4): 2.87 vs
+// 2.80 ms -- every paired-level launch of the 4096-column levels runs ~10 % slower than on 1920
+// columns)
+#ifndef SGK_DUO_PLAN
+#define SGK_DUO_PLAN 1
+#endif
+#ifndef SGK_DUO_PLAN_MAXW
+#define SGK_DUO_PLAN_MAXW 2048
+#endif
+#ifndef SGK_TRIO_MIN_MB
+#define SGK_TRIO_MIN_MB 512
+#endif
 
 // 2-D tile launches (k_gauss_tile, sift_gauss_tile.hip) for levels of at most this many MB (one
 // 1080p image: 8.3 MB at octave 0), where the wave walk of k_gauss_lean is latency-bound
@@ -159,6 +176,10 @@ struct sgpu_ctx {
     bool duo_on = false;                   // SGPU_DUO=on: paired-level launches (size rule)
     bool duo_wide = false;                 // SGPU_DUO_WIDE=1: also the (21, 25) pairs
     bool duo_u8 = false;                   // SGPU_DUO_U8=1: the u8 ingest pair (13, 11)
+    int trio_mode = SGPU_TRIO_OFF;         // three-level launches: SGPU_TRIO_* (SGPU_TRIO=off / on /
+                                           // always; sgpu_debug_set_schedule)
+    int duo_plan = SGK_DUO_PLAN;           // SGPU_PAIRS_END: pairs from the octave's end
+                                           // (SGPU_DUO_PLAN=end), SGPU_PAIRS_FRONT: from its front
     size_t wide_desc_max = SGK_WIDE_DESC_MAX;   // feature counts (of the previous call) up to which
                                            // descriptors run a workgroup per feature
                                            // (SGPU_WIDE_DESC_MAX)
@@ -193,7 +214,7 @@ struct sgpu_ctx {
                                                   // pre: the 2^ds-sampled input (-fo > 0)
     // sgpu_extract_stream: second input slot, copy-engine streams, slot events
     DevBuf input2;
-    DevBuf duo_trash;                      // k_gauss_duo's scratch stores (kGaussDuoTrashBytes)
+    DevBuf duo_trash;                      // k_gauss_duo's / k_gauss_trio's scratch stores
     hipStream_t h2d = nullptr, d2h = nullptr;
     hipEvent_t up_ev[2] = {}, down_ev[2] = {};
     bool gathered = false;
@@ -444,6 +465,15 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     }
     if (const char* ev = getenv("SGPU_DUO_U8")) {
         if (ev[0] == '1') ctx->duo_u8 = true;
+    }
+    if (const char* ev = getenv("SGPU_DUO_PLAN")) {   // A/B hook of the octave pairing
+        if (!strcmp(ev, "end")) ctx->duo_plan = SGPU_PAIRS_END;
+        if (!strcmp(ev, "front")) ctx->duo_plan = SGPU_PAIRS_FRONT;
+    }
+    if (const char* ev = getenv("SGPU_TRIO")) {   // A/B hook of the three-level kernel
+        if (!strcmp(ev, "off")) ctx->trio_mode = SGPU_TRIO_OFF;
+        if (!strcmp(ev, "always")) ctx->trio_mode = SGPU_TRIO_ALWAYS;
+        if (!strcmp(ev, "on")) ctx->trio_mode = SGPU_TRIO_ON;
     }
     if (const char* ev = getenv("SGPU_GAUSS_BANDS"))
         if (!strcmp(ev, "long")) ctx->debug_flags |= SGPU_DEBUG_GAUSS_LONG_BANDS;
@@ -829,32 +859,86 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
         const bool duo_all = (ctx->debug_flags & SGPU_DEBUG_DUO_ALWAYS) != 0;
         const bool duo_off = (ctx->debug_flags & SGPU_DEBUG_DUO_OFF) != 0 ||
                              (!SGK_DUO_DEFAULT && !duo_all && !ctx->duo_on);
+        // Three levels: ops (o, k), (o, k+1), (o, k+2) with the widths (11, 13,
+        // 17) and the third decimated into octave o+1 run as one k_gauss_trio launch in slot
+        // o * kds + k + 2 (level k read once, levels k+1 .. k+3 and the decimation written:
+        // 17 instead of 25 B per pixel), on levels >= SGK_TRIO_MIN_MB (any size with
+        // SGPU_TRIO_ALWAYS); the octave's (21, 25) pair after it then pairs too.
+        std::vector<char> trio_third(ops.size(), 0), in_trio(ops.size(), 0);
+        std::vector<char> trio_octave(sgk::kMaxOctaves, 0);
+        if (!duo_off && wave_rows >= 0 && ctx->trio_mode != SGPU_TRIO_OFF) {
+            for (size_t i = 0; i + 2 < ops.size(); i++) {
+                const Op& a = ops[i];
+                const Op& b = ops[i + 1];
+                const Op& c = ops[i + 2];
+                if (in_trio[i] || a.o != b.o || a.o != c.o || b.k != a.k + 1 || c.k != a.k + 2) continue;
+                const long long bytes = 4ll * a.op.w * a.op.h * a.op.batch;
+                if (ctx->trio_mode != SGPU_TRIO_ALWAYS && bytes < ((long long)SGK_TRIO_MIN_MB << 20))
+                    continue;
+                if (!sgk::gauss_trio_supported(a.op, b.op, c.op)) continue;
+                in_trio[i] = in_trio[i + 1] = in_trio[i + 2] = 1;
+                trio_third[i + 2] = 1;
+                trio_octave[a.o] = 1;
+            }
+        }
         std::vector<int> duo_next(ops.size(), -1);   // op i pairs with op duo_next[i]
         std::vector<char> duo_second(ops.size(), 0);
+        // Pairs from the octave's end: on a level of >= SGK_DUO_WIDE_MIN_MB (any
+        // size with SGPU_DEBUG_DUO_ALWAYS), octave o's levels pair as (4, 5) = (21, 25), (2, 3) =
+        // (13, 17) with level 3's decimation, (0, 1) = the u8 ingest pair (13, 11) -- three
+        // launches for octave 0 instead of four (level 0, (1, 2), (3, 4), level 5), 34 instead of
+        // 38 B per pixel -- when the (2, 3) pair is supported; otherwise the pairs from the front.
+        if (!duo_off && wave_rows >= 0 && ctx->duo_plan == SGPU_PAIRS_END) {
+            for (size_t j = ops.size(); j >= 2; j--) {
+                const size_t i = j - 2;   // candidate pair (i, i + 1)
+                const Op& a = ops[i];
+                const Op& b = ops[i + 1];
+                if (a.o != b.o || b.k != a.k + 1 || (b.k % 2) != 1) continue;
+                if (in_trio[i] || in_trio[i + 1] || duo_second[i] || duo_next[i + 1] >= 0) continue;
+                const long long bytes = 4ll * a.op.w * a.op.h * a.op.batch;
+                if (!duo_all && (bytes < ((long long)SGK_DUO_WIDE_MIN_MB << 20) ||
+                                 a.op.w > SGK_DUO_PLAN_MAXW))
+                    continue;
+                // the octave takes the plan only with its (2, 3) pair: look it up first
+                bool mid_ok = false;
+                for (size_t q = 0; q + 1 < ops.size(); q++)
+                    if (ops[q].o == a.o && ops[q].k == 2 && ops[q + 1].k == 3 && ops[q + 1].o == a.o)
+                        mid_ok = sgk::gauss_duo_supported(ops[q].op, ops[q + 1].op) &&
+                                 ops[q + 1].op.ds_dst != nullptr;
+                if (!mid_ok || !sgk::gauss_duo_supported(a.op, b.op)) continue;
+                duo_next[i] = (int)(i + 1);
+                duo_second[i + 1] = 1;
+            }
+        }
         if (!duo_off && wave_rows >= 0) {
             for (size_t i = 0; i + 1 < ops.size(); i++) {
                 const Op& a = ops[i];
                 const Op& b = ops[i + 1];
-                if (duo_second[i] || a.o != b.o || b.k != a.k + 1) continue;
+                if (in_trio[i] || in_trio[i + 1]) continue;
+                if (duo_second[i] || duo_next[i] >= 0 || duo_second[i + 1] || duo_next[i + 1] >= 0) continue;
+                if (a.o != b.o || b.k != a.k + 1) continue;
                 const long long bytes = 4ll * a.op.w * a.op.h * a.op.batch;
                 if (!duo_all && bytes < ((long long)SGK_DUO_MIN_MB << 20)) continue;
                 if (!duo_all && a.op.fw + b.op.fw > 24) {
                     const bool ds_pair = a.op.ds_dst != nullptr;
-                    if (!ds_pair && !ctx->duo_wide) continue;
+                    if (!ds_pair && !ctx->duo_wide && !trio_octave[a.o]) continue;
                     if (bytes < ((long long)SGK_DUO_WIDE_MIN_MB << 20)) continue;
                 }
                 // the u8 ingest pair (levels 0, 1: 725 us) displaces the (11, 13) pair of levels
                 // 1, 2 (750 us, level 0 alone 390): opt-in
                 if (!duo_all && !ctx->duo_u8 && a.op.src_u8) continue;
-                if (!sgk::gauss_duo_supported(a.op, b.op)) continue;
+                // (a pair that decimates its second level only in the plan from the octave's end)
+                if (b.op.ds_dst || !sgk::gauss_duo_supported(a.op, b.op)) continue;
                 duo_next[i] = (int)(i + 1);
                 duo_second[i + 1] = 1;
             }
         }
-        bool any_duo = false;
+        bool any_duo = false, any_trio = false;
         for (int v : duo_next) any_duo |= v >= 0;
-        if (any_duo)
-            ALLOCCHK(ctx, ctx->duo_trash.ensure(sgk::kGaussDuoTrashBytes));
+        for (char v : trio_third) any_trio |= v != 0;
+        if (any_duo || any_trio)
+            ALLOCCHK(ctx, ctx->duo_trash.ensure(std::max(sgk::kGaussDuoTrashBytes,
+                                                         sgk::kGaussTrioTrashBytes)));
         int last = 0;
         for (const Op& e : ops) last = std::max(last, e.o * kds + e.k);
         for (int slot = 0; slot <= last; slot++) {
@@ -862,11 +946,15 @@ static int enqueue_part(sgpu_ctx* ctx, Part& pt, const void* src_in, bool is_f32
             int m = 0;
             for (size_t i = 0; i < ops.size(); i++) {
                 const Op& e = ops[i];
-                if (duo_second[i] && e.o * kds + e.k == slot) {   // the pair ends in this slot
+                if (trio_third[i] && e.o * kds + e.k == slot) {   // the trio ends in this slot
+                    HIPCHK(ctx, sgk::launch_gauss_trio(ops[i - 2].op, ops[i - 1].op, e.op, st,
+                                                       wave_rows, ctx->duo_trash.as<float>()));
+                    pt.gauss_launches++;
+                } else if (duo_second[i] && e.o * kds + e.k == slot) {   // the pair ends in this slot
                     HIPCHK(ctx, sgk::launch_gauss_duo(ops[i - 1].op, e.op, st, wave_rows,
                                                       ctx->duo_trash.as<float>()));
                     pt.gauss_launches++;
-                } else if (duo_next[i] < 0 && !duo_second[i] && e.o * kds + e.k == slot) {
+                } else if (!in_trio[i] && duo_next[i] < 0 && !duo_second[i] && e.o * kds + e.k == slot) {
                     in_slot[m++] = &e.op;
                 }
             }
@@ -2105,6 +2193,15 @@ int sgpu_last_timing(const sgpu_ctx* ctx, float* times, int n) {
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags) {
     if (!ctx) return SGPU_EINVAL;
     ctx->debug_flags = flags | ctx->env_flags;
+    return SGPU_OK;
+}
+
+int sgpu_debug_set_schedule(sgpu_ctx* ctx, int trio, int pairs) {
+    if (!ctx || trio < SGPU_TRIO_OFF || trio > SGPU_TRIO_ALWAYS || pairs < SGPU_PAIRS_FRONT ||
+        pairs > SGPU_PAIRS_END)
+        return SGPU_EINVAL;
+    ctx->trio_mode = trio;
+    ctx->duo_plan = pairs;
     return SGPU_OK;
 }
 

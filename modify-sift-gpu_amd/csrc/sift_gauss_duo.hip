@@ -38,6 +38,7 @@
 #include <cstring>
 #include <utility>
 
+#include "sift_gauss_ring.h"
 #include "sift_kernels.h"
 
 // the DMA asm names M0 as clobbered: clang warns that M0 is reserved; nothing else in this file
@@ -47,43 +48,7 @@
 namespace sgk {
 namespace {
 
-typedef float f2v __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) void* lds_ptr;
-
-__device__ __forceinline__ f2v pkf(f2v a, float k, f2v c) {
-    return __builtin_elementwise_fma(a, f2v{k, k}, c);
-}
-__device__ __forceinline__ int clampd(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
-
-// tap i of a width-FW filter (make_filter's taps are symmetric bit for bit: half the SGPRs)
-template <int FW>
-__device__ __forceinline__ float tapk(const Taps& t, int i) {
-    return t.k[i < FW - 1 - i ? i : FW - 1 - i];
-}
-
-template <int... I, class F>
-__device__ __forceinline__ void unroll_seq(std::integer_sequence<int, I...>, F&& f) {
-    (f(std::integral_constant<int, I>{}), ...);
-}
-
-// a wave-uniform pointer as one (the asm's "s" operand needs an SGPR pair)
-__device__ __forceinline__ const char* uniform_ptr(const void* p) {
-    const uint64_t v = reinterpret_cast<uint64_t>(p);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
-    return reinterpret_cast<const char*>(((uint64_t)hi << 32) | lo);
-}
-
-__device__ __forceinline__ float readlane_f(float v, int l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-
-// workgroup order: blocks dealt round-robin over the 8 XCDs (observed, speed only), so logical
-// block xcd * q + k runs on XCD xcd and neighbouring strips share one L2 (as k_gauss_lean)
-__device__ __forceinline__ int duo_block(int bid, int nb) {
-    const int q = nb / 8, r = nb % 8, xcd = bid % 8, k = bid / 8;
-    return xcd < r ? xcd * (q + 1) + k : r * (q + 1) + (xcd - r) * q + k;
-}
+using namespace gring;
 
 // the two H passes of a step in one scheduling region (their fma chains interleave) or kept
 // apart by a compiler barrier (SGK_DUO_INTERLEAVE=0)
@@ -134,8 +99,8 @@ struct DuoJob {
     long long dst_img;
     int W, H;
     Taps ta, tb;                 // the two filters (widths FWA, FWB)
-    float* ds;                   // level k + 1 decimated into the next octave's level 0 (DS)
-    int dsw;
+    float* ds;                   // level k + 1 (DS 1) or k + 2 (DS 2) decimated into the next
+    int dsw, dsh;                // octave's level 0
     long long ds_img;
     int strips, nsy, rows_per_band, total_waves;
     float* trash;                // 3,072 B per wave slot (1024 slots): stores of rows outside
@@ -159,27 +124,9 @@ __device__ __forceinline__ void duo_zero(const ZeroJob& z) {
         }
 }
 
-// p / 255 correctly rounded on a pair (u8_to_unit of sift_kernels.hip, packed: the same three
-// IEEE operations per element)
-__device__ __forceinline__ f2v u8_pair_to_unit(uint32_t a, uint32_t b) {
-    const float c = 1.0f / 255.0f;
-    const f2v x{(float)a, (float)b};
-    const f2v q = x * f2v{c, c};
-    const f2v r = __builtin_elementwise_fma(-q, f2v{255.0f, 255.0f}, x);
-    return __builtin_elementwise_fma(r, f2v{c, c}, q);
-}
-
-// s_waitcnt with vmcnt = n (0 .. 63), expcnt and lgkmcnt not waited for
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-    static_assert(N >= 0 && N < 64, "vmcnt field");
-    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-}
-__device__ __forceinline__ void wait_lgkm0() {
-    __builtin_amdgcn_s_waitcnt((15) | (3 << 14) | (7 << 4) | (0 << 8));   // lgkmcnt(0) only
-}
-
-template <int FWA, int FWB, int NIN, bool U8, bool DS>
+// DS: 0 no decimation, 1 level k + 1 (stage A) into the next octave's level 0, 2 level k + 2
+// (stage B)
+template <int FWA, int FWB, int NIN, bool U8, int DS>
 __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, float* s_mid) {
     using G = DuoGeom<FWA, FWB>;
     constexpr int RA = G::RA, RB = G::RB, SW = G::SW, NDMA = G::NDMA, IN_SLOT = G::IN_SLOT;
@@ -210,13 +157,9 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
     for (int q = 0; q < NDMA; q++)
         coff[q] = 4u * (uint32_t)clampd(a0 + 32 * q + (SGK_DUO_EXP == 1 ? (lane & 31) : (lane >> 1)), 0, W - 1);
     const uint32_t rsel = ((SGK_DUO_EXP == 1 ? lane >> 5 : lane) & 1) ? 4u * (uint32_t)J.src_stride : 0u;
-    // The DMAs are inline asm, not __builtin_amdgcn_global_load_lds: the compiler's wait
-    // insertion treats every later LDS read as possibly aliasing a pending LDS-DMA and puts an
-    // s_waitcnt vmcnt(0) before it (seen in the ISA), which would drain the whole DMA ring every
-    // step.  Hidden from the compiler, the DMAs are waited for by the explicit counted waits below
-    // only; every LDS access of the wave stays inside its own slots.  M0 holds the LDS address
-    // (nothing else in this kernel uses M0).
-    static_assert(NDMA == 5, "the asm below issues 5 DMAs per row pair");
+    // the DMAs: gring::dma_pair5 (inline asm, waited for by the counted waits below only; every
+    // LDS access of the wave stays inside its own slots)
+    static_assert(NDMA == 5, "dma_pair5 issues 5 DMAs per row pair");
     auto dma = [&](int rho, float* slot) __attribute__((always_inline)) {
         const int r0 = clampd(rho, 0, H - 1), r1 = clampd(rho + 1, 0, H - 1);
         const char* base = uniform_ptr(reinterpret_cast<const char*>(src) +
@@ -224,21 +167,7 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
         const uint32_t ro = r1 != r0 ? rsel : 0u;
         const uint32_t lds = __builtin_amdgcn_readfirstlane(
             (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)slot);
-        asm volatile(
-            "s_mov_b32 m0, %[l]\n\ts_nop 0\n\t"
-            "global_load_lds_dword %[o0], %[b]\n\t"
-            "s_add_u32 m0, m0, 0x100\n\ts_nop 0\n\t"
-            "global_load_lds_dword %[o1], %[b]\n\t"
-            "s_add_u32 m0, m0, 0x100\n\ts_nop 0\n\t"
-            "global_load_lds_dword %[o2], %[b]\n\t"
-            "s_add_u32 m0, m0, 0x100\n\ts_nop 0\n\t"
-            "global_load_lds_dword %[o3], %[b]\n\t"
-            "s_add_u32 m0, m0, 0x100\n\ts_nop 0\n\t"
-            "global_load_lds_dword %[o4], %[b]"
-            :
-            : [l] "s"(lds), [b] "s"(base), [o0] "v"(coff[0] + ro), [o1] "v"(coff[1] + ro),
-              [o2] "v"(coff[2] + ro), [o3] "v"(coff[3] + ro), [o4] "v"(coff[4] + ro)
-            : "memory", "m0", "scc");
+        dma_pair5(base, lds, coff, ro);
     };
     // u8 input (stage A of the ingest pair): lane j < NQ loads quad j (columns a0 + 4 j ..
     // + 3, whole quads: W % 4 == 0 and a0 % 4 == 0) of both rows of a pair into registers; the
@@ -447,14 +376,16 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
     char* const bA = reinterpret_cast<char*>(d1);
     char* const bB = reinterpret_cast<char*>(d2);
     char* const bT = reinterpret_cast<char*>(trash);
-    // DS: the even row of stage A's pair (mc + DSR; mc's parity is RB's, yb being even) decimated
-    // into the next octave's level 0 -- DownsampleKernel<1> (ProgramCU.cu:287-298): ds(r, cc) =
-    // level(2 r, 2 cc), stored by the lanes that own column c = 2 cc
+    // DS 1: the even row of stage A's pair (mc + DSR; mc's parity is RB's, yb being even)
+    // decimated into the next octave's level 0 -- DownsampleKernel<1> (ProgramCU.cu:287-298):
+    // ds(r, cc) = level(2 r, 2 cc), stored by the lanes that own column c = 2 cc; DS 2: stage B's
+    // row y (even: y - yb is a multiple of 2), by the lanes that own column e = 2 cc
     constexpr int DSR = RB & 1;
     char* const bD = DS ? reinterpret_cast<char*>(J.ds + (long long)b * J.ds_img) : nullptr;
     const uint32_t DW4 = DS ? 4u * (uint32_t)J.dsw : 0u;
-    uint32_t rowD = DS ? (uint32_t)((rho0 - RA + DSR) / 2) * DW4 : 0u;   // (rho0 - RA + DSR even)
-    const uint32_t voffD = 2u * (uint32_t)c;
+    uint32_t rowD = DS == 1 ? (uint32_t)((rho0 - RA + DSR) / 2) * DW4            // (even)
+                  : DS == 2 ? (uint32_t)((rho0 - RA - 2 - RB) / 2) * DW4 : 0u;   // (row y, even)
+    const uint32_t voffD = 2u * (uint32_t)(DS == 2 ? e : c);
     int slot_use = 0;                 // input slot of step t (t mod NIN)
     int mid_cur = 0;                  // mid slot of step t's stage A (t & 1; U may be odd)
     int slot_dma = NIN - 1;           // input slot of step t + NIN - 1
@@ -542,7 +473,7 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
                 if (own1) {
                     *reinterpret_cast<f2v*>((a0ok ? bA : bT) + (a0ok ? rowA + voffA : vtr)) = A0;
                     *reinterpret_cast<f2v*>((a1ok ? bA : bT) + (a1ok ? rowA + W4 + voffA : vtr)) = A1;
-                    if constexpr (DS) {
+                    if constexpr (DS == 1) {
                         const int yd = mc + DSR;
                         const bool dok = yd >= yb && yd < ye;
                         *reinterpret_cast<float*>((dok ? bD : bT) + (dok ? rowD + voffD : vtr)) =
@@ -552,6 +483,10 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
                 if (own2) {
                     *reinterpret_cast<f2v*>((b0ok ? bB : bT) + (b0ok ? rowB + voffB : vtr)) = B0;
                     *reinterpret_cast<f2v*>((b1ok ? bB : bT) + (b1ok ? rowB + W4 + voffB : vtr)) = B1;
+                    if constexpr (DS == 2) {   // (an odd H's last row decimates into no row when dsh = H / 2)
+                        const bool dok = b0ok && (y >> 1) < J.dsh;
+                        *reinterpret_cast<float*>((dok ? bD : bT) + (dok ? rowD + voffD : vtr)) = B0.x;
+                    }
                 }
                 rowA += 2 * W4;
                 rowB += 2 * W4;
@@ -564,23 +499,23 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
 }
 
 // waves per SIMD the register allocation must allow: 3 (<= 168 VGPRs) for (21, 25), whose
-// scheduler otherwise hoists both H passes' LDS reads (255 VGPRs, one wave per SIMD); 4 (<= 128)
-// for the narrower pairs
+// scheduler otherwise hoists both H passes' LDS reads (255 VGPRs, one wave per SIMD), and the
+// other pairs of >= 30 taps; 4 (<= 128) for the narrower pairs
 #ifndef SGK_DUO_WPE_WIDE
 #define SGK_DUO_WPE_WIDE 3
 #endif
 #ifndef SGK_DUO_WPE_NARROW
 #define SGK_DUO_WPE_NARROW 4
 #endif
-template <int FWA, int FWB, int NIN, bool U8, bool DS>
-__global__ __launch_bounds__(64 * kDuoWaves) __attribute__((amdgpu_waves_per_eu(FWA + FWB > 30 ? SGK_DUO_WPE_WIDE : SGK_DUO_WPE_NARROW))) void k_gauss_duo(const DuoJob J) {
+template <int FWA, int FWB, int NIN, bool U8, int DS>
+__global__ __launch_bounds__(64 * kDuoWaves) __attribute__((amdgpu_waves_per_eu(FWA + FWB >= 30 ? SGK_DUO_WPE_WIDE : SGK_DUO_WPE_NARROW))) void k_gauss_duo(const DuoJob J) {
     using G = DuoGeom<FWA, FWB>;
     // u8 input: one input slot (the registers hold the prefetched rows)
     __shared__ __attribute__((aligned(16))) float s_in_all[kDuoWaves][(U8 ? 1 : NIN) * G::IN_SLOT];
     __shared__ __attribute__((aligned(16))) float s_mid_all[kDuoWaves][4 * kMidSlot];
     if (J.zero.n[0] | J.zero.n[1] | J.zero.n[2]) duo_zero(J.zero);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int gw = duo_block(blockIdx.x, gridDim.x) * kDuoWaves + wave;
+    const int gw = ring_block(blockIdx.x, gridDim.x) * kDuoWaves + wave;
     if (gw >= J.total_waves) return;   // uniform per wave
     duo_wave<FWA, FWB, NIN, U8, DS>(J, gw, s_in_all[wave], s_mid_all[wave]);
 }
@@ -619,7 +554,7 @@ static long long duo_waves_target() {
     return v;
 }
 
-template <int FWA, int FWB, bool U8, bool DS>
+template <int FWA, int FWB, bool U8, int DS>
 hipError_t duo_launch(const LevelOp& a, const LevelOp& b, hipStream_t stream, int rows_hint,
                       float* trash) {
     using G = DuoGeom<FWA, FWB>;
@@ -636,9 +571,11 @@ hipError_t duo_launch(const LevelOp& a, const LevelOp& b, hipStream_t stream, in
     J.H = a.h;
     J.ta = a.taps;
     J.tb = b.taps;
-    J.ds = a.ds_dst;
-    J.dsw = a.ds_w;
-    J.ds_img = a.ds_img_stride;
+    const LevelOp& dl = DS == 2 ? b : a;   // the level op that decimates
+    J.ds = dl.ds_dst;
+    J.dsw = dl.ds_w;
+    J.dsh = dl.ds_h;
+    J.ds_img = dl.ds_img_stride;
     J.strips = (a.w + G::SW - 1) / G::SW;
     const long long per_band = (long long)J.strips * a.batch;
     // bands: as many as the grid needs for duo_waves_target() waves; each band re-walks
@@ -673,11 +610,16 @@ hipError_t duo_launch(const LevelOp& a, const LevelOp& b, hipStream_t stream, in
 }  // namespace
 
 bool gauss_duo_supported(const LevelOp& a, const LevelOp& b) {
-    // f32 pairs (11, 13), (21, 25), (17, 21) with level k + 1 decimated into the next octave; the
-    // u8 ingest pair (13, 11) (level 0 from the image, level 1)
+    // f32 pairs (11, 13), (21, 25), (17, 21) with level k + 1 decimated into the next octave,
+    // (13, 17) with level k + 2 decimated; the u8 ingest pair (13, 11) (level 0 from the image,
+    // level 1)
     const bool u8 = a.src_u8 != nullptr;
-    const bool ds = a.ds_dst != nullptr;
-    const bool pair = u8 ? (a.fw == 13 && b.fw == 11 && !ds)
+    const bool ds = a.ds_dst != nullptr, dsb = b.ds_dst != nullptr;
+    const bool dsb_ok = dsb && a.fw == 13 && b.fw == 17 && (b.w % 2) == 0 && b.ds_w * 2 == b.w &&
+                        (b.ds_h == (b.h + 1) / 2 || b.ds_h == b.h / 2) &&
+                        b.ds_img_stride >= (long long)b.ds_w * b.ds_h;
+    const bool pair = u8 ? (a.fw == 13 && b.fw == 11 && !ds && !dsb)
+                    : dsb ? (dsb_ok && !ds)
                     : ds ? (a.fw == 17 && b.fw == 21 && (a.w % 2) == 0 && a.ds_w * 2 == a.w &&
                             a.ds_h == (a.h + 1) / 2 && a.ds_img_stride >= (long long)a.ds_w * a.ds_h)
                          : ((a.fw == 11 && b.fw == 13) || (a.fw == 21 && b.fw == 25));
@@ -686,7 +628,7 @@ bool gauss_duo_supported(const LevelOp& a, const LevelOp& b) {
                            : (a.src && a.src_stride >= a.w);
     const bool b_zeroes = (b.zero.n[0] | b.zero.n[1] | b.zero.n[2]) != 0;
     const bool a_zeroes = (a.zero.n[0] | a.zero.n[1] | a.zero.n[2]) != 0;
-    return pair && src_ok && !b_zeroes && (u8 || !a_zeroes) && !b.ds_dst &&
+    return pair && src_ok && !b_zeroes && (u8 || !a_zeroes) && (!b.ds_dst || dsb_ok) &&
            b.src == a.dst && !b.src_u8 && a.w == b.w && a.h == b.h && a.batch == b.batch &&
            a.w >= 8 && a.h >= 8 && (a.w % 4) == 0 && b.src_stride == a.w &&
            a.dst_img_stride == b.dst_img_stride && b.src_img_stride == a.dst_img_stride &&
@@ -696,10 +638,11 @@ bool gauss_duo_supported(const LevelOp& a, const LevelOp& b) {
 hipError_t launch_gauss_duo(const LevelOp& a, const LevelOp& b, hipStream_t stream, int rows_hint,
                             float* trash) {
     if (!trash || !gauss_duo_supported(a, b)) return hipErrorInvalidValue;
-    if (a.src_u8) return duo_launch<13, 11, true, false>(a, b, stream, rows_hint, trash);
-    if (a.ds_dst) return duo_launch<17, 21, false, true>(a, b, stream, rows_hint, trash);
+    if (a.src_u8) return duo_launch<13, 11, true, 0>(a, b, stream, rows_hint, trash);
+    if (a.ds_dst) return duo_launch<17, 21, false, 1>(a, b, stream, rows_hint, trash);
+    if (b.ds_dst) return duo_launch<13, 17, false, 2>(a, b, stream, rows_hint, trash);
 #define SGK_DUO(A, B) \
-    if (a.fw == A && b.fw == B) return duo_launch<A, B, false, false>(a, b, stream, rows_hint, trash);
+    if (a.fw == A && b.fw == B) return duo_launch<A, B, false, 0>(a, b, stream, rows_hint, trash);
     SGK_DUO(11, 13) SGK_DUO(21, 25)
 #undef SGK_DUO
     return hipErrorInvalidValue;

@@ -100,6 +100,16 @@ bool gauss_duo_supported(const LevelOp& a, const LevelOp& b);
 hipError_t launch_gauss_duo(const LevelOp& a, const LevelOp& b, hipStream_t stream, int rows_hint,
                             float* trash);
 
+// Three consecutive levels in one launch (sift_gauss_trio.hip): a = level k -> k+1, b = k+1 ->
+// k+2, c = k+2 -> k+3 (b.src == a.dst, c.src == b.dst) with level k+3 decimated into the next
+// octave's level 0 (c.ds_dst); f32 widths (11, 13, 17): 17 B of HBM traffic per pixel for the
+// three levels instead of 25 for a paired-level launch plus one level.  Bit-identical to three
+// launch_gauss_op calls.  trash: kGaussTrioTrashBytes of device scratch.
+constexpr size_t kGaussTrioTrashBytes = 1024 * 4096;
+bool gauss_trio_supported(const LevelOp& a, const LevelOp& b, const LevelOp& c);
+hipError_t launch_gauss_trio(const LevelOp& a, const LevelOp& b, const LevelOp& c,
+                             hipStream_t stream, int rows_hint, float* trash);
+
 // One level in 2-D tiles (sift_gauss_tile.hip): a workgroup loads its 64 x 32 output tile's
 // whole input window at once, H pass into LDS, V pass from LDS -- for cache-resident levels (one
 // image: the wave walk of k_gauss_lean is a chain of load latencies there).  Bit-identical to

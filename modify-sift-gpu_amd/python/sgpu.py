@@ -33,7 +33,7 @@ C_API = [
     "sgpu_match_shard_begin", "sgpu_match_shard_end", "sgpu_match_sharded",
     "sgpu_extract_stream", "sgpu_host_alloc", "sgpu_host_free", "sgpu_reserve",
     "sgpu_debug_alloc_count", "sgpu_last_pyramid_launches", "sgpu_set_stage_timing",
-    "sgpu_set_host_output",
+    "sgpu_set_host_output", "sgpu_debug_set_schedule",
 ]
 
 _LIB = None
@@ -81,6 +81,7 @@ def lib():
         L.sgpu_quantize_descriptors.argtypes = [vp, c.c_size_t, vp]
         L.sgpu_last_timing.argtypes = [vp, vp, c.c_int]
         L.sgpu_debug_set_flags.argtypes = [vp, c.c_int]
+        L.sgpu_debug_set_schedule.argtypes = [vp, c.c_int, c.c_int]
         L.sgpu_debug_geometry.argtypes = [vp, P(c.c_int), vp, c.c_int]
         L.sgpu_debug_gaussian.argtypes = [vp, c.c_int, c.c_int, c.c_int, vp]
         L.sgpu_debug_candidates.argtypes = [vp, vp, vp, c.c_int, P(c.c_int)]
@@ -482,6 +483,16 @@ class SiftContext:
     def set_debug_flags(self, flags: int):
         """Per-context debug flags (sgpu_debug_set_flags; 0 = shipped configuration)."""
         self._check(lib().sgpu_debug_set_flags(self._ctx, flags), "sgpu_debug_set_flags")
+
+    TRIO_OFF, TRIO_ON, TRIO_ALWAYS = 0, 1, 2
+    PAIRS_FRONT, PAIRS_END = 0, 1
+
+    def set_schedule(self, trio: int = 0, pairs: int = 1):
+        """The batch pyramid's launch plan (sgpu_debug_set_schedule): three-level launches
+        (TRIO_OFF, shipped; TRIO_ON: the size rule; TRIO_ALWAYS: wherever the widths and the
+        decimation allow) and the octave's level pairs from its end (PAIRS_END, shipped) or its
+        front (PAIRS_FRONT)."""
+        self._check(lib().sgpu_debug_set_schedule(self._ctx, trio, pairs), "sgpu_debug_set_schedule")
 
     @contextlib.contextmanager
     def exact_descriptors(self):

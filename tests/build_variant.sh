@@ -14,11 +14,12 @@ H=/opt/rocm/bin/hipcc
 $H $CX -c -o "$OUT/k.o" $PKG/csrc/sift_kernels.hip &
 $H $CX -c -o "$OUT/d.o" $PKG/csrc/sift_gauss_duo.hip &
 $H $CX -c -o "$OUT/t.o" $PKG/csrc/sift_gauss_tile.hip &
+$H $CX -c -o "$OUT/r.o" $PKG/csrc/sift_gauss_trio.hip &
 $H $CX -mllvm -amdgpu-mfma-vgpr-form=1 -c -o "$OUT/m.o" $PKG/csrc/sift_match.hip &
 $H $CX -x hip -c -o "$OUT/c.o" $PKG/csrc/sgpu_capi.cpp &
 $H $CX -x hip -c -o "$OUT/a.o" $PKG/csrc/siftgpu_api.cpp &
 wait
-$H --offload-arch=gfx950 -shared -o "$OUT/libsiftgpu.so" "$OUT"/{k,d,t,m,c,a}.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+$H --offload-arch=gfx950 -shared -o "$OUT/libsiftgpu.so" "$OUT"/{k,d,t,r,m,c,a}.o -L/opt/rocm/lib -lrccl -ldl -Wl,-rpath,/opt/rocm/lib
 rm -f "$OUT"/*.o
 # the test-hook library is loaded from beside the product library (sgpu_debug_candidates)
 cp "$PKG/lib/libsiftgpu_debug.so" "$OUT/"

@@ -160,13 +160,16 @@ DUO_OFF = sgpu.SiftContext.DEBUG_DUO_OFF
 # band heights: auto, one chunk (each band re-walks 2 (RA + RB) halo rows), not a multiple of
 # 8, taller than the image; sizes: tiny (one strip with both edges), ragged widths (not a
 # multiple of the 104- / 116-column strips), odd heights (the (H-1, H-1) bottom pair), 1080p
+@pytest.mark.parametrize("pairs", [sgpu.SiftContext.PAIRS_END, sgpu.SiftContext.PAIRS_FRONT])
 @pytest.mark.parametrize("rows", [0, 8, 36, 2040])
 @pytest.mark.parametrize("n,w,h", [(2, 16, 16), (3, 203, 97), (2, 1920, 1080), (2, 300, 1203),
                                    (1, 104, 33)])
-def test_duo_levels_equal_single_level(gpu_ctx, rows, n, w, h):
+def test_duo_levels_equal_single_level(gpu_ctx, pairs, rows, n, w, h):
     """The paired-level kernel (k_gauss_duo: levels k+1, k+2 from level k in one pass, both
     vertical passes pushed into register accumulators) against one level per launch
-    (SGPU_DEBUG_DUO_OFF): every level of every octave and every keypoint, bit for bit."""
+    (SGPU_DEBUG_DUO_OFF): every level of every octave and every keypoint, bit for bit.  The pairs
+    from the octave's end take the u8 ingest pair (13, 11), (13, 17) with the second level
+    decimated and (21, 25); from its front (11, 13) and (17, 21) with the first decimated."""
     imgs = synth_batch(n, w, h, 140 + w % 11)
     opts = default_options()
     gpu_ctx.set_options(opts)
@@ -175,6 +178,7 @@ def test_duo_levels_equal_single_level(gpu_ctx, rows, n, w, h):
         gpu_ctx.extract(imgs)
         ref = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
         k_ref = [gpu_ctx.features(i)[0].copy() for i in range(n)]
+        gpu_ctx.set_schedule(gpu_ctx.TRIO_OFF, pairs)
         gpu_ctx.set_debug_flags((rows << sgpu.SiftContext.DEBUG_BAND_SHIFT) | DUO)
         gpu_ctx.extract(imgs)
         got = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
@@ -185,6 +189,7 @@ def test_duo_levels_equal_single_level(gpu_ctx, rows, n, w, h):
         for i in range(n):
             assert np.array_equal(_bits(gpu_ctx.features(i)[0]), _bits(k_ref[i]))
     finally:
+        gpu_ctx.set_schedule()
         gpu_ctx.set_debug_flags(0)
 
 
@@ -205,6 +210,70 @@ def test_duo_levels_vs_oracle(gpu_ctx, w, h, seed):
                 assert np.array_equal(_bits(g), _bits(r)), (o, lvl)
     finally:
         gpu_ctx.set_debug_flags(0)
+
+
+# sizes: ragged (odd heights: the (H-1, H-1) bottom pairs and a last row that decimates into
+# no row; octave 1's padded width takes no trio), 1080p (the shipped case: two bands), a tall
+# ragged batch (three strips), a narrow one (one strip with both edges, 2 octaves), a small
+# square; band heights as the duo's
+@pytest.mark.parametrize("rows", [0, 8, 36, 2040])
+@pytest.mark.parametrize("n,w,h", [(3, 203, 97), (2, 1920, 1080), (2, 296, 1203), (1, 104, 33),
+                                   (2, 64, 64)])
+def test_trio_levels_equal_single_level(gpu_ctx, rows, n, w, h):
+    """The three-level kernel (k_gauss_trio: levels k+1 .. k+3 and the decimation from level k in
+    one pass, three vertical passes pushed into register accumulators, sgpu_debug_set_schedule
+    ALWAYS) against one level per launch (SGPU_DEBUG_DUO_OFF): every level of every octave and
+    every keypoint, bit for bit; and it ran (fewer launches than one level per launch)."""
+    imgs = synth_batch(n, w, h, 170 + w % 13)
+    opts = default_options()
+    gpu_ctx.set_options(opts)
+    try:
+        gpu_ctx.set_debug_flags(DUO_OFF)
+        gpu_ctx.extract(imgs)
+        ref = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
+        k_ref = [gpu_ctx.features(i)[0].copy() for i in range(n)]
+        band = rows << sgpu.SiftContext.DEBUG_BAND_SHIFT
+        gpu_ctx.set_schedule(gpu_ctx.TRIO_OFF)
+        gpu_ctx.set_debug_flags(band)
+        gpu_ctx.extract(imgs)
+        single_launches = gpu_ctx.pyramid_launches()[0]
+        # the trio alone (levels too small for pairs), then beside the paired levels
+        for flags in (band, band | DUO):
+            gpu_ctx.set_schedule(gpu_ctx.TRIO_ALWAYS)
+            gpu_ctx.set_debug_flags(flags)
+            gpu_ctx.extract(imgs)
+            if flags == band:
+                assert gpu_ctx.pyramid_launches()[0] < single_launches
+            got = [_levels(gpu_ctx, i, opts) for i in (0, n - 1)]
+            for a, b in zip(ref, got):
+                for o, (la, lb) in enumerate(zip(a, b)):
+                    for lvl, (x, y) in enumerate(zip(la, lb)):
+                        assert np.array_equal(_bits(x), _bits(y)), (flags, o, lvl)
+            for i in range(n):
+                assert np.array_equal(_bits(gpu_ctx.features(i)[0]), _bits(k_ref[i]))
+    finally:
+        gpu_ctx.set_schedule()
+        gpu_ctx.set_debug_flags(0)
+
+
+@pytest.mark.parametrize("w,h,seed", [(640, 480, 1000), (1921, 1081, 5)])
+def test_trio_levels_vs_oracle(gpu_ctx, w, h, seed):
+    """k_gauss_trio's levels (and the decimated next-octave bases) against the oracle
+    (FilterH / FilterV, ProgramCU.cu:115-222; DownsampleKernel, :287-298), every level of every
+    octave."""
+    img = synth_image(w, h, seed)
+    opts = default_options()
+    gpu_ctx.set_options(opts)
+    gpu_ctx.set_schedule(gpu_ctx.TRIO_ALWAYS)
+    try:
+        gpu_ctx.extract(img)
+        for o in range(len(gpu_ctx.geometry())):
+            for lvl in range(opts.dog_level_num + 3):
+                g = gpu_ctx.gaussian(0, o, lvl)
+                r = O.gaussian(img, o, lvl, opts)
+                assert np.array_equal(_bits(g), _bits(r)), (o, lvl)
+    finally:
+        gpu_ctx.set_schedule()
 
 
 TILE = sgpu.SiftContext.DEBUG_GAUSS_TILE_ALWAYS
