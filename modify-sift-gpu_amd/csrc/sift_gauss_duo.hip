@@ -57,9 +57,17 @@ using namespace gring;
 #endif
 constexpr bool kDuoInterleave = SGK_DUO_INTERLEAVE != 0;
 // timing experiments only (wrong levels, tests/diag): 1 = DMA lanes row-contiguous (lanes 0-31 row
-// 2p, 32-63 row 2p+1), 2 = no H / V arithmetic (one LDS read per pass), 0 = the kernel
+// 2p, 32-63 row 2p+1), 2 = no H / V arithmetic (one LDS read per pass), 3 = the row pair as two
+// 16-B-per-lane DMAs (global_load_lds_dwordx4, 128 lane addresses instead of 320), 4 = the same
+// with the second on 8 lanes (72 lane addresses), 0 = the kernel
 #ifndef SGK_DUO_EXP
 #define SGK_DUO_EXP 0
+#endif
+// f32 input rows by 16-B-per-lane DMA (global_load_lds_dwordx4: 2 instructions, ~74 lane
+// addresses per row pair instead of 5 x 64) into row-major slots, read by a column-packed H1: 1;
+// the per-column dword DMA into (row 2p, row 2p+1)-interleaved slots (round 5): 0
+#ifndef SGK_DUO_X4
+#define SGK_DUO_X4 1
 #endif
 constexpr int kDuoWaves = 4;      // waves per workgroup (each wave works alone: no barriers)
 constexpr int kMidSlot = 256;     // floats of one mid row pair: 128 columns x (row, row + 1)
@@ -82,11 +90,16 @@ struct DuoGeom {
     static constexpr int SW = (128 - 2 * MOFF) / SGK_DUO_SWALIGN * SGK_DUO_SWALIGN;
     static constexpr int IN_W = 128 + 2 * RA;         // input columns of stage A
     static constexpr int NDMA = (IN_W + 31) / 32;     // dword DMAs per row pair (32 columns each)
-    static constexpr int IN_SLOT = NDMA * 64;         // floats of one input row pair
+    static constexpr int IN_SLOT = (SGK_DUO_EXP == 3 ? 8 : NDMA) * 64;   // floats of one input row pair
     static constexpr int PMAX = FWA > FWB ? FWA : FWB;
     static constexpr int P = (PMAX + 1) & ~1;         // accumulator ring period (rows), even
     static constexpr int U = P / 2;                   // steps per unrolled iteration
     static constexpr int NQ = IN_W / 4;               // u8 input: dword quads per row
+    // X4 slots: a row's quads start at column c0 = a0 - D (16-B aligned: x0 is a multiple of 32),
+    // NQ4 per row (lane l's H1 reads floats D + 2 l .. D + 2 l + FWA of each row), row 2p + 1
+    // 4 NQ4 floats after row 2p
+    static constexpr int D = (-(MOFF + RA)) & 3;
+    static constexpr int NQ4 = (D + 128 + FWA + 3) / 4;
 };
 
 struct DuoJob {
@@ -134,8 +147,16 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
     static_assert(!U8 || ((MOFF + RA) % 4 == 0 && G::IN_W % 4 == 0 && NQ <= 64),
                   "u8 input: the strip's input quads are 4-column aligned");
     // VMEM instructions per step: the DMAs, 2 + 2 stores, the decimated row's store
-    constexpr int OPS = NDMA + 4 + (DS ? 1 : 0);
-    static_assert(NIN >= 2 && OPS * (NIN - 1) < 64, "DMA ring (vmcnt field)");
+    constexpr bool kX4 = SGK_DUO_EXP == 3 || SGK_DUO_EXP == 4;
+    // the shipped 16-B DMA, for the pairs of < 40 taps: (21, 25)'s register budget (168 VGPRs at
+    // 3 waves per SIMD) does not take the second walk copy (a VGPR spill, 1,265 vs 987 us)
+    constexpr bool kRowX4 = SGK_DUO_X4 && !U8 && SGK_DUO_EXP == 0 && FWA + FWB < 40;
+    constexpr int D = G::D, NQ4 = G::NQ4;
+    static_assert(!kRowX4 || (8 * NQ4 <= IN_SLOT && 2 * NQ4 > 64 && 2 * NQ4 <= 128), "X4 slot");
+    // (X4: the interior strips' 2 DMAs; the edge strips keep 5 per-column DMAs, OPSE)
+    constexpr int OPS = (kX4 || kRowX4 ? 2 : NDMA) + 4 + (DS ? 1 : 0);
+    constexpr int OPSE = (kX4 ? 2 : NDMA) + 4 + (DS ? 1 : 0);
+    static_assert(NIN >= 2 && OPSE * (NIN - 1) < 64, "DMA ring (vmcnt field)");
     const int lane = threadIdx.x & 63;
     const int W = J.W, H = J.H;
     const int sx = gw % J.strips, rest = gw / J.strips;
@@ -157,17 +178,53 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
     for (int q = 0; q < NDMA; q++)
         coff[q] = 4u * (uint32_t)clampd(a0 + 32 * q + (SGK_DUO_EXP == 1 ? (lane & 31) : (lane >> 1)), 0, W - 1);
     const uint32_t rsel = ((SGK_DUO_EXP == 1 ? lane >> 5 : lane) & 1) ? 4u * (uint32_t)J.src_stride : 0u;
-    // the DMAs: gring::dma_pair5 (inline asm, waited for by the counted waits below only; every
-    // LDS access of the wave stays inside its own slots)
+    // the DMAs: gring::dma_pair5 / dma_pair_x4 (inline asm, waited for by the counted waits below
+    // only; every LDS access of the wave stays inside its own slots)
     static_assert(NDMA == 5, "dma_pair5 issues 5 DMAs per row pair");
-    auto dma = [&](int rho, float* slot) __attribute__((always_inline)) {
+    const int c0 = a0 - D;         // X4: column of the slot rows' float 0
+    const uint32_t qoff0 = 4u * (uint32_t)clampd(c0 + 4 * (lane < NQ4 ? lane : lane - NQ4), 0, W - 4);
+    const uint32_t qoff1 = 4u * (uint32_t)clampd(c0 + 4 * min(64 - NQ4 + lane, NQ4 - 1), 0, W - 4);
+    // X4 edge strips (a slot column outside the image, uniform): the row-major slot filled by 5
+    // per-column dword DMAs, each column clamped to the image (lane i of instruction q: slot
+    // float 64 q + i, row 2p + 1 from float 4 NQ4 on)
+    const bool xedge = kRowX4 && (c0 < 0 || c0 + 4 * NQ4 > W);
+    uint32_t ecoff[NDMA], erow[NDMA];
+#pragma unroll
+    for (int q = 0; q < NDMA; q++) {
+        const int f = 64 * q + lane, r = f >= 4 * NQ4 ? 1 : 0;
+        ecoff[q] = 4u * (uint32_t)clampd(c0 + f - 4 * NQ4 * r, 0, W - 1);
+        erow[q] = r ? 4u * (uint32_t)J.src_stride : 0u;
+    }
+    auto dma = [&](int rho, float* slot, auto EDGE) __attribute__((always_inline)) {
         const int r0 = clampd(rho, 0, H - 1), r1 = clampd(rho + 1, 0, H - 1);
         const char* base = uniform_ptr(reinterpret_cast<const char*>(src) +
                                        (uint32_t)r0 * (4u * (uint32_t)J.src_stride));
         const uint32_t ro = r1 != r0 ? rsel : 0u;
         const uint32_t lds = __builtin_amdgcn_readfirstlane(
             (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)slot);
-        dma_pair5(base, lds, coff, ro);
+        if constexpr (kRowX4 && decltype(EDGE)::value) {
+            const uint32_t rm = r1 != r0 ? ~0u : 0u;
+            const uint32_t eo[NDMA] = {ecoff[0] + (erow[0] & rm), ecoff[1] + (erow[1] & rm),
+                                       ecoff[2] + (erow[2] & rm), ecoff[3] + (erow[3] & rm),
+                                       ecoff[4] + (erow[4] & rm)};
+            dma_pair5(base, lds, eo, 0u);
+        } else if constexpr (kRowX4) {
+            // instruction 0: lanes < NQ4 quads of row 2p, the rest row 2p + 1's first quads;
+            // instruction 1 (lanes < 2 NQ4 - 64): row 2p + 1's last quads (interior strips: every
+            // quad inside the image)
+            const uint32_t rr = r1 != r0 ? 4u * (uint32_t)J.src_stride : 0u;
+            dma_pair_x4(base, lds, qoff0 + (lane < NQ4 ? 0u : rr), qoff1 + rr, true, lane,
+                        2 * NQ4 - 64);
+        } else if constexpr (kX4) {   // (timing only) quads of the aligned window: 36 per row
+            const uint32_t rr = r1 != r0 ? 4u * (uint32_t)J.src_stride : 0u;
+            const int a4 = a0 & ~3;
+            const uint32_t o0 = 4u * (uint32_t)clampd(a4 + 4 * (lane < 36 ? lane : lane - 36), 0, W - 4) +
+                                (lane < 36 ? 0u : rr);
+            const uint32_t o1 = 4u * (uint32_t)clampd(a4 + 4 * min(28 + lane, 35), 0, W - 4) + rr;
+            dma_pair_x4(base, lds, o0, o1, SGK_DUO_EXP == 4, lane, 8);
+        } else {
+            dma_pair5(base, lds, coff, ro);
+        }
     };
     // u8 input (stage A of the ingest pair): lane j < NQ loads quad j (columns a0 + 4 j ..
     // + 3, whole quads: W % 4 == 0 and a0 % 4 == 0) of both rows of a pair into registers; the
@@ -249,6 +306,29 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
             }
         }
     };
+    // H1 of an X4 slot, column-packed: row 2p's (c, c + 1) and row 2p + 1's, each the sum over
+    // taps m = 0 .. FWA-1 of tap m times the columns (c - RA + m, c + 1 - RA + m), in tap order;
+    // lane l's inputs are floats D + 2 l .. D + 2 l + FWA of each row, read as 8-B-aligned pairs,
+    // the odd-offset operands formed from two neighbouring pairs
+    auto h1rows = [&](int off, f2v& r0, f2v& r1) __attribute__((always_inline)) {
+        constexpr int O = D & 1;                      // x[m] sits at pair float m + O
+        constexpr int NP = (FWA + O) / 2 + 1;         // pairs read per row
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const f2v* pp = reinterpret_cast<const f2v*>(s_in + off + r * 4 * NQ4 + D - O + 2 * lane);
+            f2v pr[NP];
+#pragma unroll
+            for (int i = 0; i < NP; i++) pr[i] = pp[i];
+            f2v o{0.f, 0.f};
+#pragma unroll
+            for (int m = 0; m < FWA; m++) {
+                const int idx = m + O;
+                const f2v op = (idx & 1) ? f2v{pr[idx >> 1].y, pr[(idx >> 1) + 1].x} : pr[idx >> 1];
+                o = pkf(op, tapa(m), o);
+            }
+            (r ? r1 : r0) = o;
+        }
+    };
     // H2 of a mid slot: output columns e, e + 1 from mid float2 2 le + OB + m, m = 0 .. FWB
     auto h2 = [&](const float* slot, f2v& o0, f2v& o1) __attribute__((always_inline)) {
         o0 = f2v{0.f, 0.f};
@@ -313,13 +393,20 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
                 fetch8(2 * p, r);
                 stage8(r, s_in);
             } else {
-                dma(2 * p, s_in);
+                if (xedge) dma(2 * p, s_in, std::true_type{});
+                else dma(2 * p, s_in, std::false_type{});
                 wait_vm<0>();
             }
             asm volatile("" ::: "memory");
-            f2v o0, o1;
-            h1(s_in, o0, o1);
-            const f2v r0{o0.x, o1.x}, r1{o0.y, o1.y};   // rows 2p, 2p + 1: columns (c, c + 1)
+            f2v r0, r1;   // rows 2p, 2p + 1: columns (c, c + 1)
+            if constexpr (kRowX4) {
+                h1rows(0, r0, r1);
+            } else {
+                f2v o0, o1;
+                h1(s_in, o0, o1);
+                r0 = f2v{o0.x, o1.x};
+                r1 = f2v{o0.y, o1.y};
+            }
             if (p == 0) {
 #pragma unroll
                 for (int i = 0; i <= RA; i++) mz = pkf(r0, tapa(i), i == 0 ? f2v{0.f, 0.f} : mz);
@@ -355,16 +442,8 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
     if constexpr (U8) {
 #pragma unroll
         for (int k = 0; k < U; k++) fetch8(rho0 + 2 * k, rg[k]);
-    } else {
-#pragma unroll
-        for (int k = 0; k < NIN - 1; k++) {
-            dma(rho0 + 2 * k, s_in + k * IN_SLOT);
-#pragma unroll
-            for (int j = 0; j < 4 + (DS ? 1 : 0); j++)
-                *reinterpret_cast<f2v*>(trash + 128 * (j + 1) + 2 * lane) = f2v{0.f, 0.f};
-        }
     }
-    asm volatile("" ::: "memory");
+    // (f32: issued at the start of the walk, whose copy fixes the DMA form)
     // stores: uniform row pointers (the level's image base + row * W, updated per step) plus a
     // lane byte offset; rows outside the band go to the wave's scratch block at lane * 8
     const uint32_t voffA = 4u * (uint32_t)c, voffB = 4u * (uint32_t)e, vtr = 8u * (uint32_t)lane;
@@ -389,111 +468,135 @@ __device__ __forceinline__ void duo_wave(const DuoJob& J, int gw, float* s_in, f
     int slot_use = 0;                 // input slot of step t (t mod NIN)
     int mid_cur = 0;                  // mid slot of step t's stage A (t & 1; U may be odd)
     int slot_dma = NIN - 1;           // input slot of step t + NIN - 1
-    for (int it = 0; it < niter; it++) {
-        unroll_seq(std::make_integer_sequence<int, U>{}, [&](auto KI) __attribute__((always_inline)) {
-            constexpr int k = decltype(KI)::value;
-            const int t = it * U + k;
-            const int rho = rho0 + 2 * t;
-            const int mc = rho - RA;          // stage A's completed pair
-            const int mu = mc - 2;            // stage B's pair
-            asm volatile("" ::: "memory");
-            if constexpr (U8) {
-                // step t's quads (loaded U steps ago) into the one input slot, then step t + U's
-                // loads into the same registers
-                stage8(rg[k], s_in);
-                fetch8(rho + 2 * U, rg[k]);
-            } else {
-                dma(rho + 2 * (NIN - 1), s_in + slot_dma * IN_SLOT);
-                slot_dma = slot_dma == NIN - 1 ? 0 : slot_dma + 1;
-                // every older VMEM instruction but the OPS (NIN - 1) youngest -- this step's DMA,
-                // the previous NIN - 2 steps' DMAs and stores, and the stores of the step that
-                // issued step t's DMA -- has completed: step t's DMA has landed
-                wait_vm<OPS * (NIN - 1)>();
-            }
-            asm volatile("" ::: "memory");
-            // both H passes: stage A on the input slot, stage B on the previous step's mid pair
-            // (an offset from one base: a select between the slot pointers made the compiler
-            // lose their LDS address space -- flat accesses through the lambdas' closure)
-            const int mb_off = mu <= -1 ? 2 * kMidSlot : (mu >= H - 1 ? 3 * kMidSlot
-                                                                      : (mid_cur ^ 1) * kMidSlot);
-            const float* mb = s_mid + mb_off;
-            f2v o0, o1, q0, q1;
-            h1(s_in + (U8 ? 0 : slot_use * IN_SLOT), o0, o1);
-            slot_use = slot_use == NIN - 1 ? 0 : slot_use + 1;
-            // V1 push of rows rho (ring row 2k) and rho + 1 (2k + 1)
-            const f2v r0{o0.x, o1.x}, r1{o0.y, o1.y};
+    // the walk, in two copies: edge strips (X4: the slot columns outside the image replicated
+    // after each DMA lands) and the rest (fewer live scalars)
+    auto walk = [&](auto EDGE) __attribute__((always_inline)) {
+        constexpr bool kEdge = decltype(EDGE)::value;
+        constexpr int OPSW = kEdge ? OPSE : OPS;   // VMEM instructions per step of this copy
+        if constexpr (!U8) {
 #pragma unroll
-            for (int i = 0; i < (SGK_DUO_EXP == 2 ? 1 : FWA); i++) {
-                const int s = ((2 * k - i) % P + P) % P;
-                accA[s] = pkf(r0, tapa(i), i == 0 ? f2v{0.f, 0.f} : accA[s]);
-            }
-            f2v A0 = accA[((2 * k - (FWA - 1)) % P + P) % P];
+            for (int k = 0; k < NIN - 1; k++) {
+                dma(rho0 + 2 * k, s_in + k * IN_SLOT, EDGE);
 #pragma unroll
-            for (int i = 0; i < (SGK_DUO_EXP == 2 ? 1 : FWA); i++) {
-                const int s = ((2 * k + 1 - i) % P + P) % P;
-                accA[s] = pkf(r1, tapa(i), i == 0 ? f2v{0.f, 0.f} : accA[s]);
+                for (int j = 0; j < 4 + (DS ? 1 : 0); j++)
+                    *reinterpret_cast<f2v*>(trash + 128 * (j + 1) + 2 * lane) = f2v{0.f, 0.f};
             }
-            f2v A1 = accA[((2 * k + 1 - (FWA - 1)) % P + P) % P];
-            if constexpr (!kDuoInterleave) asm volatile("" ::: "memory");
-            h2(mb, q0, q1);
-            // V2 push of mid rows mu (ring row 2k) and mu + 1
-            const f2v g0{q0.x, q1.x}, g1{q0.y, q1.y};
-#pragma unroll
-            for (int i = 0; i < (SGK_DUO_EXP == 2 ? 1 : FWB); i++) {
-                const int s = ((2 * k - i) % P + P) % P;
-                accB[s] = pkf(g0, tapb(i), i == 0 ? f2v{0.f, 0.f} : accB[s]);
-            }
-            const f2v B0 = accB[((2 * k - (FWB - 1)) % P + P) % P];
-#pragma unroll
-            for (int i = 0; i < (SGK_DUO_EXP == 2 ? 1 : FWB); i++) {
-                const int s = ((2 * k + 1 - i) % P + P) % P;
-                accB[s] = pkf(g1, tapb(i), i == 0 ? f2v{0.f, 0.f} : accB[s]);
-            }
-            const f2v B1 = accB[((2 * k + 1 - (FWB - 1)) % P + P) % P];
-            // stage A's pair into mid slot t & 1 (and the bottom pair): edge columns clamped
-            if (mc == H - 1) A1 = A0;   // odd H: the pair (H-1, H) is (H-1, H-1)
-            if (left || right) {
-                fix_edges(A0);
-                fix_edges(A1);
-            }
-            put_mid(s_mid + mid_cur * kMidSlot, A0, A1);
-            mid_cur ^= 1;
-            if (mc <= H - 1 && mc + 1 >= H - 1) {
-                const f2v Bv = mc == H - 1 ? A0 : A1;
-                put_mid(mid_bot, Bv, Bv);
-            }
-            asm volatile("" ::: "memory");
-            // level k + 1 rows mc, mc + 1 and level k + 2 rows y = mu - RB, y + 1: the wave's
-            // own columns; rows outside the band into the scratch block
-            {
-                const int y = mu - RB;
-                // (mc is odd for an odd RA + RB, as in the u8 pair: each row of a pair is tested)
-                const bool a0ok = mc >= yb && mc < ye, a1ok = mc + 1 >= yb && mc + 1 < ye;
-                const bool b0ok = y >= yb && y < ye, b1ok = y + 1 >= yb && y + 1 < ye;
-                if (own1) {
-                    *reinterpret_cast<f2v*>((a0ok ? bA : bT) + (a0ok ? rowA + voffA : vtr)) = A0;
-                    *reinterpret_cast<f2v*>((a1ok ? bA : bT) + (a1ok ? rowA + W4 + voffA : vtr)) = A1;
-                    if constexpr (DS == 1) {
-                        const int yd = mc + DSR;
-                        const bool dok = yd >= yb && yd < ye;
-                        *reinterpret_cast<float*>((dok ? bD : bT) + (dok ? rowD + voffD : vtr)) =
-                            DSR ? A1.x : A0.x;
-                    }
+        }
+        asm volatile("" ::: "memory");
+        for (int it = 0; it < niter; it++) {
+            unroll_seq(std::make_integer_sequence<int, U>{}, [&](auto KI) __attribute__((always_inline)) {
+                constexpr int k = decltype(KI)::value;
+                const int t = it * U + k;
+                const int rho = rho0 + 2 * t;
+                const int mc = rho - RA;          // stage A's completed pair
+                const int mu = mc - 2;            // stage B's pair
+                asm volatile("" ::: "memory");
+                if constexpr (U8) {
+                    // step t's quads (loaded U steps ago) into the one input slot, then step t + U's
+                    // loads into the same registers
+                    stage8(rg[k], s_in);
+                    fetch8(rho + 2 * U, rg[k]);
+                } else {
+                    dma(rho + 2 * (NIN - 1), s_in + slot_dma * IN_SLOT, EDGE);
+                    slot_dma = slot_dma == NIN - 1 ? 0 : slot_dma + 1;
+                    // every older VMEM instruction but the OPS (NIN - 1) youngest -- this step's DMA,
+                    // the previous NIN - 2 steps' DMAs and stores, and the stores of the step that
+                    // issued step t's DMA -- has completed: step t's DMA has landed
+                    wait_vm<OPSW * (NIN - 1)>();
                 }
-                if (own2) {
-                    *reinterpret_cast<f2v*>((b0ok ? bB : bT) + (b0ok ? rowB + voffB : vtr)) = B0;
-                    *reinterpret_cast<f2v*>((b1ok ? bB : bT) + (b1ok ? rowB + W4 + voffB : vtr)) = B1;
-                    if constexpr (DS == 2) {   // (an odd H's last row decimates into no row when dsh = H / 2)
-                        const bool dok = b0ok && (y >> 1) < J.dsh;
-                        *reinterpret_cast<float*>((dok ? bD : bT) + (dok ? rowD + voffD : vtr)) = B0.x;
-                    }
+                asm volatile("" ::: "memory");
+                // both H passes: stage A on the input slot, stage B on the previous step's mid pair
+                // (an offset from one base: a select between the slot pointers made the compiler
+                // lose their LDS address space -- flat accesses through the lambdas' closure)
+                const int mb_off = mu <= -1 ? 2 * kMidSlot : (mu >= H - 1 ? 3 * kMidSlot
+                                                                          : (mid_cur ^ 1) * kMidSlot);
+                const float* mb = s_mid + mb_off;
+                f2v q0, q1, r0, r1;
+                if constexpr (kRowX4) {
+                    h1rows(slot_use * IN_SLOT, r0, r1);
+                } else {
+                    f2v o0, o1;
+                    h1(s_in + (U8 ? 0 : slot_use * IN_SLOT), o0, o1);
+                    r0 = f2v{o0.x, o1.x};
+                    r1 = f2v{o0.y, o1.y};
                 }
-                rowA += 2 * W4;
-                rowB += 2 * W4;
-                if constexpr (DS) rowD += DW4;
-            }
-        });
-    }
+                slot_use = slot_use == NIN - 1 ? 0 : slot_use + 1;
+                // V1 push of rows rho (ring row 2k) and rho + 1 (2k + 1)
+    #pragma unroll
+                for (int i = 0; i < (SGK_DUO_EXP == 2 ? 1 : FWA); i++) {
+                    const int s = ((2 * k - i) % P + P) % P;
+                    accA[s] = pkf(r0, tapa(i), i == 0 ? f2v{0.f, 0.f} : accA[s]);
+                }
+                f2v A0 = accA[((2 * k - (FWA - 1)) % P + P) % P];
+    #pragma unroll
+                for (int i = 0; i < (SGK_DUO_EXP == 2 ? 1 : FWA); i++) {
+                    const int s = ((2 * k + 1 - i) % P + P) % P;
+                    accA[s] = pkf(r1, tapa(i), i == 0 ? f2v{0.f, 0.f} : accA[s]);
+                }
+                f2v A1 = accA[((2 * k + 1 - (FWA - 1)) % P + P) % P];
+                if constexpr (!kDuoInterleave) asm volatile("" ::: "memory");
+                h2(mb, q0, q1);
+                // V2 push of mid rows mu (ring row 2k) and mu + 1
+                const f2v g0{q0.x, q1.x}, g1{q0.y, q1.y};
+    #pragma unroll
+                for (int i = 0; i < (SGK_DUO_EXP == 2 ? 1 : FWB); i++) {
+                    const int s = ((2 * k - i) % P + P) % P;
+                    accB[s] = pkf(g0, tapb(i), i == 0 ? f2v{0.f, 0.f} : accB[s]);
+                }
+                const f2v B0 = accB[((2 * k - (FWB - 1)) % P + P) % P];
+    #pragma unroll
+                for (int i = 0; i < (SGK_DUO_EXP == 2 ? 1 : FWB); i++) {
+                    const int s = ((2 * k + 1 - i) % P + P) % P;
+                    accB[s] = pkf(g1, tapb(i), i == 0 ? f2v{0.f, 0.f} : accB[s]);
+                }
+                const f2v B1 = accB[((2 * k + 1 - (FWB - 1)) % P + P) % P];
+                // stage A's pair into mid slot t & 1 (and the bottom pair): edge columns clamped
+                if (mc == H - 1) A1 = A0;   // odd H: the pair (H-1, H) is (H-1, H-1)
+                if (left || right) {
+                    fix_edges(A0);
+                    fix_edges(A1);
+                }
+                put_mid(s_mid + mid_cur * kMidSlot, A0, A1);
+                mid_cur ^= 1;
+                if (mc <= H - 1 && mc + 1 >= H - 1) {
+                    const f2v Bv = mc == H - 1 ? A0 : A1;
+                    put_mid(mid_bot, Bv, Bv);
+                }
+                asm volatile("" ::: "memory");
+                // level k + 1 rows mc, mc + 1 and level k + 2 rows y = mu - RB, y + 1: the wave's
+                // own columns; rows outside the band into the scratch block
+                {
+                    const int y = mu - RB;
+                    // (mc is odd for an odd RA + RB, as in the u8 pair: each row of a pair is tested)
+                    const bool a0ok = mc >= yb && mc < ye, a1ok = mc + 1 >= yb && mc + 1 < ye;
+                    const bool b0ok = y >= yb && y < ye, b1ok = y + 1 >= yb && y + 1 < ye;
+                    if (own1) {
+                        *reinterpret_cast<f2v*>((a0ok ? bA : bT) + (a0ok ? rowA + voffA : vtr)) = A0;
+                        *reinterpret_cast<f2v*>((a1ok ? bA : bT) + (a1ok ? rowA + W4 + voffA : vtr)) = A1;
+                        if constexpr (DS == 1) {
+                            const int yd = mc + DSR;
+                            const bool dok = yd >= yb && yd < ye;
+                            *reinterpret_cast<float*>((dok ? bD : bT) + (dok ? rowD + voffD : vtr)) =
+                                DSR ? A1.x : A0.x;
+                        }
+                    }
+                    if (own2) {
+                        *reinterpret_cast<f2v*>((b0ok ? bB : bT) + (b0ok ? rowB + voffB : vtr)) = B0;
+                        *reinterpret_cast<f2v*>((b1ok ? bB : bT) + (b1ok ? rowB + W4 + voffB : vtr)) = B1;
+                        if constexpr (DS == 2) {   // (an odd H's last row decimates into no row when dsh = H / 2)
+                            const bool dok = b0ok && (y >> 1) < J.dsh;
+                            *reinterpret_cast<float*>((dok ? bD : bT) + (dok ? rowD + voffD : vtr)) = B0.x;
+                        }
+                    }
+                    rowA += 2 * W4;
+                    rowB += 2 * W4;
+                    if constexpr (DS) rowD += DW4;
+                }
+            });
+        }
+    };
+    if (xedge) walk(std::true_type{});
+    else walk(std::false_type{});
     // no DMA may land after the workgroup's LDS is handed to another workgroup
     wait_vm<0>();
 }

@@ -89,6 +89,27 @@ __device__ __forceinline__ void dma_pair5(const char* base, uint32_t lds, const 
           [o2] "v"(off[2] + ro), [o3] "v"(off[3] + ro), [o4] "v"(off[4] + ro)
         : "memory", "m0", "scc");
 }
+// One row pair as two global_load_lds_dwordx4 (16 B per lane, 1 KB per instruction, lane-linear
+// in LDS): lanes' byte offsets off0 / off1 from the uniform base; with `masked` the second
+// instruction runs on lanes 0 .. n1 - 1 only (1 <= n1: it is always issued, for the counted
+// waits).
+__device__ __forceinline__ void dma_pair_x4(const char* base, uint32_t lds, uint32_t off0,
+                                            uint32_t off1, bool masked, int lane, int n1) {
+    asm volatile(
+        "s_mov_b32 m0, %[l]\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %[o0], %[b]"
+        :
+        : [l] "s"(lds), [b] "s"(base), [o0] "v"(off0)
+        : "memory", "m0");
+    if (!masked || lane < n1) {
+        asm volatile(
+            "s_mov_b32 m0, %[l]\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %[o1], %[b]"
+            :
+            : [l] "s"(lds + 1024u), [b] "s"(base), [o1] "v"(off1)
+            : "memory", "m0");
+    }
+}
 #pragma clang diagnostic pop
 
 }  // namespace gring
