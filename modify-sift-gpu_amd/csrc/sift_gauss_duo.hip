@@ -11,9 +11,13 @@
 //   * a wave owns SW = 128 - 2 RB output columns of both levels (RB = FWB / 2) and walks a band
 //     of rows top to bottom, two rows (one row pair) per step;
 //   * stage A: the input row pair (128 + 2 RA columns, clamped to the image) arrives in LDS by
-//     LDS-DMA (global_load_lds_dword, one float per lane, laid out as (row 2p, row 2p+1) pairs),
-//     NIN - 1 steps ahead of its use -- no staging registers;  H1 (lane l: mid columns
-//     m0 + 2l, m0 + 2l + 1, packed over the row pair) reads it with ds_read_b128;
+//     LDS-DMA NIN - 1 steps ahead of its use -- no staging registers.  Pairs of < 40 taps
+//     (SGK_DUO_X4): two global_load_lds_dwordx4 (16 B per lane) into a row-major slot, H1 (lane
+//     l: mid columns m0 + 2l, m0 + 2l + 1 of each row, packed over the column pair) reads
+//     8-B pairs; the edge strips, whose slots hold columns outside the image, keep 5 per-column
+//     clamped dword DMAs into the same layout (a second copy of the walk with its own counted
+//     wait).  (21, 25): 5 dword DMAs into (row 2p, row 2p+1) pairs, H1 packed over the row pair
+//     reads ds_read_b128;
 //   * the V1 pass is pushed: each H1 row is multiplied into the FWA accumulators of the mid rows
 //     it contributes to, so mid row m receives input rows m - RA .. m + RA in that order -- the
 //     reference's tap order i = 0 .. FW-1, one fma each, bit for bit the pull form's sum.  The
@@ -32,7 +36,9 @@
 // Every VMEM instruction of a step is issued unconditionally (rows outside the band store to a
 // per-wave scratch area), so the count of memory operations younger than a step's DMA is a
 // constant and one `s_waitcnt vmcnt(OPS (NIN - 1))` waits for exactly that DMA.  Levels are
-// bit-identical to two k_gauss_lean launches (tests/test_gpu_gauss.py).
+// bit-identical to two k_gauss_lean launches (tests/test_gpu_gauss.py).  Pairs: (11, 13),
+// (21, 25), (17, 21) decimating its first level, (13, 17) decimating its second, the u8 ingest
+// pair (13, 11).
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>

@@ -482,6 +482,8 @@ __device__ __forceinline__ void trio_wave(const TrioJob& J, int gw, float* s_in,
     wait_vm<0>();
 }
 
+// waves per SIMD the register allocation must allow: 2 (173 VGPRs, no spill); at 3 (168) the
+// allocator spilled 5 VGPRs and 63 SGPRs and the launch took 1,921 against ~1,360 us
 #ifndef SGK_TRIO_WPE
 #define SGK_TRIO_WPE 2
 #endif
@@ -498,7 +500,7 @@ __global__ __launch_bounds__(64 * kTrioWaves) __attribute__((amdgpu_waves_per_eu
 }
 
 // input row pairs in LDS: the DMA runs NIN - 1 steps ahead; NIN 4 leaves 13,312 B of LDS per
-// wave, 3 workgroups (12 waves) per CU
+// wave, 3 workgroups per CU (the registers allow 2 waves per SIMD)
 #ifndef SGK_TRIO_NIN
 #define SGK_TRIO_NIN 4
 #endif

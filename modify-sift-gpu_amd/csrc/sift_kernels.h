@@ -91,8 +91,8 @@ hipError_t launch_gauss_two(const LevelOp& a, const LevelOp& b, hipStream_t stre
 // Two consecutive levels in one launch (sift_gauss_duo.hip): a = level k -> k+1, b = level
 // k+1 -> k+2 (b.src == a.dst); f32 widths (11, 13) or (21, 25): 12 B of HBM
 // traffic per pixel for the two levels instead of 16 (and (17, 21) with level k+1 decimated into
-// the next octave's level 0); or the u8 ingest pair (13, 11), level 0
-// from the image and level 1 (with a's ZeroJob): 9 B instead of 13.  Bit-identical to two
+// the next octave's level 0, (13, 17) with level k+2 decimated); or the u8 ingest pair (13, 11),
+// level 0 from the image and level 1 (with a's ZeroJob): 9 B instead of 13.  Bit-identical to two
 // launch_gauss_op calls.  trash: kGaussDuoTrashBytes of device scratch.  rows_hint > 0 forces
 // the band height.
 constexpr size_t kGaussDuoTrashBytes = 1024 * 3072;

@@ -320,8 +320,11 @@ struct GaussWaveGrid {
 #ifndef SGK_GW_HSPAD
 #define SGK_GW_HSPAD 4
 #endif
+// 1: conflict-free row-pair stores in k_gauss_lean (lane map, no pad slot):
+// 128 x 1080p pyramid 3.402 / 3.434 vs 3.440 / 3.441 ms per step, C4 3.75 / 3.76 vs 3.77 / 3.73
+// (two alternating pairs, tests/diag/g6.sh); 0: round 5's lane map
 #ifndef SGK_GW_STMAP
-#define SGK_GW_STMAP 0   // 1: conflict-free row-pair stores in k_gauss_lean (lane map, no pad slot)
+#define SGK_GW_STMAP 1
 #endif
 constexpr int kGwWaves = SGK_GW_WPB;   // waves per workgroup of k_gauss_lean
 
