@@ -341,6 +341,12 @@ int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags);
 #define SGPU_PAIRS_FRONT 0
 #define SGPU_PAIRS_END 1
 int sgpu_debug_set_schedule(sgpu_ctx* ctx, int trio, int pairs);
+/* Plain mutual matching (ratiomax <= 1) decides the listed columns over the rows of set 1 that can
+ * change a decision -- those with some dot at or above the smallest second value that fails the
+ * ratio test against the weakest passing row maximum -- instead of all of set 1 (on != 0, the
+ * shipped default; SGPU_MATCH_PRUNE=off at context creation turns it off): the same pairs
+ * (DESIGN.md 4.8), a test / A-B hook. */
+int sgpu_debug_set_match_prune(sgpu_ctx* ctx, int on);
 /* Octave geometry of the last extract: n_octaves, and (w, h, wa) per octave. */
 int sgpu_debug_geometry(const sgpu_ctx* ctx, int* n_octaves, int* dims /* 3*max */, int max);
 /* Gaussian level (image, octave, level 0..level_num-1) as wa*h floats. */

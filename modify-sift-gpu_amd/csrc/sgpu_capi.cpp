@@ -222,6 +222,9 @@ struct sgpu_ctx {
     float timing[T_N] = {};
     // matcher
     DevBuf m_d1, m_d2, m_s1, m_s2, m_part, m_terms, m_match, m_dist, m_mask, m_loc, m_colpart, m_cols;
+    DevBuf m_prune, m_s1c;                 // pruned column side: [rmax n1][map n1][ct n1 + pad], s8 rows
+    bool match_prune = true;               // plain mutual matching prunes set 1 for the column side
+                                           // (sgpu_debug_set_match_prune; SGPU_MATCH_PRUNE=off)
     std::vector<int> h_match;
     bool dist_ready = false;
     // multi-GPU: RCCL communicator of this context's device (sgpu_comm_*)
@@ -499,6 +502,8 @@ int sgpu_ctx_create(int device, const sgpu_options* opt, sgpu_ctx** out) {
     }
     if (const char* ev = getenv("SGPU_TILE_DUO"))
         ctx->tile_duo = !strcmp(ev, "on");
+    if (const char* ev = getenv("SGPU_MATCH_PRUNE"))   // A/B hook of the pruned column side
+        ctx->match_prune = strcmp(ev, "off") != 0;
     if (const char* ev = getenv("SGPU_GAUSS_TILE_MB"))
         if (atoi(ev) >= 0) ctx->tile_mb = atoi(ev);
     ctx->env_flags = ctx->debug_flags;   // kept by sgpu_debug_set_flags (A/B runs of the probes)
@@ -533,7 +538,7 @@ int sgpu_ctx_destroy(sgpu_ctx* ctx) {
     if (ctx->d2h) (void)hipStreamDestroy(ctx->d2h);
     DevBuf* bufs[] = {&ctx->input, &ctx->input2, &ctx->duo_trash, &ctx->all_keys, &ctx->all_desc, &ctx->gray, &ctx->pre, &ctx->m_d1, &ctx->m_d2, &ctx->m_s1, &ctx->m_s2,
                       &ctx->m_part, &ctx->m_terms, &ctx->m_match, &ctx->m_dist, &ctx->m_mask, &ctx->m_loc,
-                      &ctx->m_colpart, &ctx->m_cols,
+                      &ctx->m_colpart, &ctx->m_cols, &ctx->m_prune, &ctx->m_s1c,
                       &ctx->c_buf};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i <= T_N; i++)
@@ -1641,9 +1646,16 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     // count is known on the device only, so the partials are sized for any count
     const bool compact = mbm && !fused && !(ctx->debug_flags & SGPU_DEBUG_FULL_COLUMNS);
     const size_t part_b = compact ? sgk::match_part_bound(n2, n1, dma) : (size_t)cb * n2;
+    // ... over the rows of set 1 that can change a listed column's decision (the LDS-DMA kernel
+    // only: its B count may live on the device)
+    const bool prune = compact && dma && ctx->match_prune;
     ALLOCCHK(ctx, ctx->m_part.ensure(std::max((size_t)ca * n1, part_b) * sizeof(sgk::Top2)));
     if (fused) ALLOCCHK(ctx, ctx->m_colpart.ensure((size_t)panels * n2 * sizeof(sgk::Top2)));
-    if (compact) ALLOCCHK(ctx, ctx->m_cols.ensure((size_t)(2 * n2 + 1) * sizeof(int)));
+    if (compact) ALLOCCHK(ctx, ctx->m_cols.ensure((size_t)(2 * n2 + 3) * sizeof(int)));
+    if (prune) {
+        ALLOCCHK(ctx, ctx->m_prune.ensure(((size_t)3 * n1 + sgk::match_ct_pad()) * sizeof(int)));
+        ALLOCCHK(ctx, ctx->m_s1c.ensure((size_t)n1 * 128));
+    }
     ALLOCCHK(ctx, ctx->m_terms.ensure(((size_t)2 * (n1 + n2) + 2 * sgk::match_ct_pad()) * sizeof(int)));
     ALLOCCHK(ctx, ctx->m_match.ensure((size_t)(n1 + n2) * sizeof(int)));
     int* row1 = ctx->m_terms.as<int>();          // row terms 128 * sum(d1), column terms
@@ -1665,14 +1677,18 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
     // ... with the row terms 128 * sum(d1) and, for mutual matching, the column side's terms
     // (two GEMMs: 128 * sum(d2), the row terms of the swapped launch; fused: the column terms
     // 128 * sum(d2) - 2^21, guided: 0) and the matched-column flags cleared
-    int* cw = compact ? ctx->m_cols.as<int>() : nullptr;   // [flag n2][count][list n2]
+    // [flag n2][count][ntau][pruned count][list n2]
+    int* cw = compact ? ctx->m_cols.as<int>() : nullptr;
+    int* rmax1 = prune ? ctx->m_prune.as<int>() : nullptr;   // pruning: row maxima of set 1,
+    int* map1c = prune ? rmax1 + n1 : nullptr;                // the kept rows' indices,
+    int* ct1c = prune ? map1c + n1 : nullptr;                 // their column terms
     HIPCHK(ctx, sgk::launch_prep_set(a, n1, ctx->m_s1.as<uint8_t>(), row1, 128, 0, nullptr, 0, st,
-                                     dma && mbm && !fused ? ct1 : nullptr));
+                                     dma && mbm && !fused ? ct1 : nullptr, ct1c));
     if (mbm || dma)
         HIPCHK(ctx, sgk::launch_prep_set(b, n2, ctx->m_s2.as<uint8_t>(), mbm ? col2 : nullptr,
                                          guided && fused ? 0 : 128,
                                          fused && !guided ? -2097152 : 0,
-                                         cw, compact ? n2 + 1 : 0, st, dma ? ct2 : nullptr));
+                                         cw, compact ? n2 + 3 : 0, st, dma ? ct2 : nullptr));
     else
         HIPCHK(ctx, sgk::launch_to_s8(b, n2, ctx->m_s2.as<uint8_t>(), st));
     if (mbm && !fused) {
@@ -1683,23 +1699,41 @@ static int match_impl(sgpu_ctx* ctx, const uint8_t* d1, int n1, const uint8_t* d
         // scans all of set 1, so its decision is the reference's (SGPU_DEBUG_FULL_COLUMNS:
         // every column, as ColMatch_Kernel does).  The flags and the count were cleared with
         // the s8 conversion.
+        //
+        // Pruning (plain mutual matching with ratiomax <= 1): a listed column's decision depends
+        // only on rows of set 1 with some dot >= tau, the smallest second value that fails the
+        // ratio test against the weakest passing row maximum (k_match_finish).
+        // The row finish records every row's maximum and that bound, k_prune_set compacts the
+        // rows at or above it, and the column GEMM runs over them (count on the device): the
+        // same decisions, the same pairs.
         sgk::ColumnList claim, cols;
         if (compact) {
             claim.flag = cw;
             claim.count = cw + n2;
-            claim.list = cw + n2 + 1;
+            claim.list = cw + n2 + 3;
             cols.count = claim.count;
             cols.map = claim.list;
             cols.dma = dma ? 1 : 0;
+        }
+        if (prune) {
+            claim.rmax = rmax1;
+            claim.ntau = cw + n2 + 1;
+            cols.bmap = map1c;
+            cols.bn = cw + n2 + 2;
         }
         HIPCHK(ctx, sgk::launch_match_rows(s1, n1, s2, n2, ca, part, st, nullptr, true, nullptr,
                                            nullptr, raw, nullptr, nullptr, dma ? ct2 : nullptr));
         HIPCHK(ctx, sgk::launch_match_finish(part, n1, ca, row1, ctx->m_dist.as<float>(), distmax,
                                              ratiomax, match1, nullptr, st, true,
                                              raw ? a : nullptr, raw ? b : nullptr, n2, claim));
-        HIPCHK(ctx, sgk::launch_match_rows(s2, n2, s1, n1, cb, part, st, nullptr, false, nullptr,
-                                           nullptr, raw, cols.map, cols.count,
-                                           dma ? ct1 : nullptr));
+        if (prune)
+            HIPCHK(ctx, sgk::launch_prune_set(rmax1, claim.ntau, n1, s1, ct1,
+                                              ctx->m_s1c.as<uint8_t>(), ct1c, map1c,
+                                              cw + n2 + 2, st));
+        HIPCHK(ctx, sgk::launch_match_rows(s2, n2, prune ? ctx->m_s1c.as<uint8_t>() : s1, n1, cb,
+                                           part, st, nullptr, false, nullptr, nullptr, raw,
+                                           cols.map, cols.count,
+                                           prune ? ct1c : dma ? ct1 : nullptr, cols.bn));
         HIPCHK(ctx, sgk::launch_match_finish(part, n2, cb, col2, ctx->m_dist.as<float>(), distmax,
                                              ratiomax, match2, nullptr, st, false,
                                              raw ? b : nullptr, raw ? a : nullptr, n1, cols));
@@ -2193,6 +2227,12 @@ int sgpu_last_timing(const sgpu_ctx* ctx, float* times, int n) {
 int sgpu_debug_set_flags(sgpu_ctx* ctx, int flags) {
     if (!ctx) return SGPU_EINVAL;
     ctx->debug_flags = flags | ctx->env_flags;
+    return SGPU_OK;
+}
+
+int sgpu_debug_set_match_prune(sgpu_ctx* ctx, int on) {
+    if (!ctx) return SGPU_EINVAL;
+    ctx->match_prune = on != 0;
     return SGPU_OK;
 }
 

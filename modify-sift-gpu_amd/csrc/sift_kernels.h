@@ -255,9 +255,11 @@ hipError_t launch_rowsums(const uint8_t* d, int n, int* s, int scale, int bias, 
 // both at once, for one set: dst = s8 form, sums[i] = scale * sum_k src[i][k] + bias (sums may
 // be null), zero[0 .. nzero) = 0, and ctp (optional, n + match_ct_pad() entries) the biased
 // column terms of a raw launch_match_rows with this set as B
+// ctfill (optional, n + match_ct_pad() entries): set to the column term of a missing column, so
+// that a launch_prune_set output over it reads as padded past its device-side count
 hipError_t launch_prep_set(const uint8_t* src, int n, uint8_t* dst, int* sums, int scale,
                            int bias, int* zero, int nzero, hipStream_t stream,
-                           int* ctp = nullptr);
+                           int* ctp = nullptr, int* ctfill = nullptr);
 int match_ct_pad();
 // column chunks of a row launch: dma = the launch runs k_match_raw (raw with ctp), whose split
 // is its own cost model (sift_match.hip chunks_for)
@@ -283,7 +285,7 @@ hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
                              const uint8_t* mask, bool row_side, const int* row_term = nullptr,
                              Top2* colpart = nullptr, bool raw = false,
                              const int* amap = nullptr, const int* an = nullptr,
-                             const int* ctp = nullptr);
+                             const int* ctp = nullptr, const int* bn = nullptr);
 size_t match_part_bound(int nA, int nB, bool dma = false);
 int match_panels(int nA);
 // Column decisions from the panels' partials: col_term[j] = 128 * sum(B_j) - 2^21 (guided: 0).
@@ -307,13 +309,30 @@ hipError_t launch_guided_mask(const float* loc1, int n1, const float* loc2, int 
 // reads match2[j] only for j = match1[i] >= 0).  ColumnList, row side: flag (nB ints, zeroed)
 // and count (zeroed) set -> each matched column is appended once to list.  Column side: map =
 // that list and count -> the launch covers rows map[0 .. *count) (n = the upper bound).
+// Pruning of the column side (row side: rmax, ntau set): rmax[i] = row i's largest dot over set 2
+// (an upper bound of every dot of row i), ntau (zeroed) = INT_MAX - the smallest second value
+// tau that would fail the ratio test of a column whose maximum is a passing row's maximum; rows
+// with rmax < tau cannot change any listed column's decision (launch_prune_set).  Column side:
+// bmap / bn = the kept rows of set 1 (original row of each, count on the device) that B holds.
 struct ColumnList {
     int* flag = nullptr;
     int* list = nullptr;
     int* count = nullptr;
     const int* map = nullptr;
     int dma = 0;   // map launches: the rows ran through k_match_raw (its chunk split)
+    int* rmax = nullptr;
+    int* ntau = nullptr;
+    const int* bmap = nullptr;
+    const int* bn = nullptr;
 };
+// The rows of set 1 that a listed column's decision can depend on (rmax[i] >= INT_MAX - *ntau),
+// compacted: s8c / ctc / mapc [slot] = s8 row, k_match_raw column term, original index, in
+// workgroup order (the order changes no decision: a passing column maximum is unique), *countc =
+// their number (zeroed before).  ctc must hold the missing-column term past the count
+// (launch_prep_set's ctfill).
+hipError_t launch_prune_set(const int* rmax, const int* ntau, int n, const uint8_t* s8,
+                            const int* ct, uint8_t* s8c, int* ctc, int* mapc, int* countc,
+                            hipStream_t stream);
 hipError_t launch_match_finish(const Top2* part, int n, int chunks, const int* row_term,
                                const float* dist, float distmax, float ratiomax, int* out,
                                Top2* best, hipStream_t stream, bool row_side,

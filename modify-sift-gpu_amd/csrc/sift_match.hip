@@ -27,6 +27,7 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr int kPanel = 128;      // A rows per workgroup (4 waves x 32)
 constexpr int kTile = 128;       // B columns per LDS tile
 constexpr int kCtPad = kTile;    // k_match_raw: zero column terms past nB (launch_prep_set)
+constexpr int kCtMissing = -6291456;   // k_match_raw's column term of a column past nB (-2^22 - 2^21)
 #ifndef SGK_MATCH_LDSROW
 #define SGK_MATCH_LDSROW 144
 #endif
@@ -142,7 +143,8 @@ __global__ __launch_bounds__(256) void k_to_s8(const uint4* __restrict__ src, si
 __global__ __launch_bounds__(256) void k_prep_set(const uint4* __restrict__ src, size_t n16,
                                                   uint4* __restrict__ dst, int* __restrict__ sums,
                                                   int scale, int bias, int* __restrict__ zero,
-                                                  int nzero, int* __restrict__ ctp, int n) {
+                                                  int nzero, int* __restrict__ ctp, int n,
+                                                  int* __restrict__ ctfill) {
     const size_t stride = (size_t)gridDim.x * 256;
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) {
         uint4 v = src[i];
@@ -158,11 +160,14 @@ __global__ __launch_bounds__(256) void k_prep_set(const uint4* __restrict__ src,
         if ((i & 7) == 0) {
             if (sums) sums[i >> 3] = scale * t + bias;
             if (ctp) ctp[i >> 3] = 128 * t - 2097152;   // k_match_raw's biased column term
+            if (ctfill) ctfill[i >> 3] = kCtMissing;
         }
     }
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < (size_t)nzero; i += stride) zero[i] = 0;
     if (ctp)
-        for (int i = blockIdx.x * 256 + threadIdx.x; i < kCtPad; i += (int)stride) ctp[n + i] = -6291456;
+        for (int i = blockIdx.x * 256 + threadIdx.x; i < kCtPad; i += (int)stride) ctp[n + i] = kCtMissing;
+    if (ctfill)
+        for (int i = blockIdx.x * 256 + threadIdx.x; i < kCtPad; i += (int)stride) ctfill[n + i] = kCtMissing;
 }
 
 // Equal-dot order of the two decisions: does column a come before column b (-1 = none)?
@@ -644,7 +649,8 @@ __global__ __launch_bounds__(64 * kRawWaves) SGK_RAW_ATTR void k_match_raw(const
                                                    const int* __restrict__ ctp, int cols_per_chunk,
                                                    Top2* __restrict__ part,
                                                    const int* __restrict__ amap,
-                                                   const int* __restrict__ an) {
+                                                   const int* __restrict__ an,
+                                                   const int* __restrict__ bn) {
     constexpr int NW = kRawWaves;
     constexpr int kRows = 32 * NW;        // panel rows
     constexpr int kDmaB = 16 / NW;        // 1-KB image runs per wave and tile
@@ -655,6 +661,7 @@ __global__ __launch_bounds__(64 * kRawWaves) SGK_RAW_ATTR void k_match_raw(const
     constexpr int kBuf = kTile * 128 + NW * 256;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int panel = blockIdx.x, chunk = blockIdx.y;
+    if (bn) nB = *bn;   // a pruned B (launch_prune_set): its count on the device, B's bound at most
     if (an) {
         nA = *an;
         if (nA <= 0) return;
@@ -912,6 +919,7 @@ __global__ __launch_bounds__(kFinishThreads) void k_match_finish(const Top2* __r
                                                       const uint8_t* __restrict__ raw_A,
                                                       const uint8_t* __restrict__ raw_B,
                                                       int nB, ColumnList cl) {
+    if (cl.bn) nB = *cl.bn;   // the column side over a pruned set 1 (launch_prune_set)
     if (cl.map) {
         n = *cl.count;
         chunks = chunks_for(n, nB, cl.dma != 0);
@@ -951,7 +959,8 @@ __global__ __launch_bounds__(kFinishThreads) void k_match_finish(const Top2* __r
         // (there is one: a passing maximum is unique)
         const int c = (idx & ~127) + 16 * sub + (idx & 15);
         const uint4* a = reinterpret_cast<const uint4*>(raw_A + (size_t)g * 128);
-        const uint4* b = reinterpret_cast<const uint4*>(raw_B + (size_t)min(c, nB - 1) * 128);
+        const int cb = max(min(c, nB - 1), 0);
+        const uint4* b = reinterpret_cast<const uint4*>(raw_B + (size_t)(cl.bmap ? cl.bmap[cb] : cb) * 128);
         uint4 av[8], bv[8];
 #pragma unroll
         for (int q = 0; q < 8; q++) { av[q] = a[q]; bv[q] = b[q]; }
@@ -978,10 +987,28 @@ __global__ __launch_bounds__(kFinishThreads) void k_match_finish(const Top2* __r
         sc = max(sc, s8);
         ok = ok && d1 < dist[min(sc, 262144)] * ratiomax;
     }
-    const int res = ok ? idx : -1;
+    // pruned column side: B's index -> the row of set 1 (a passing maximum has idx >= 0)
+    const int res = ok ? (cl.bmap ? cl.bmap[idx] : idx) : -1;
     if (valid && sub == 0) {
         out[g] = res;
         if (best) best[g] = Top2{mx, idx, sc};
+        if (cl.rmax) cl.rmax[g] = mx;   // >= every dot of the row (mx is its largest, clamped at 0)
+    }
+    if (cl.ntau && valid && sub == 0 && res >= 0) {
+        // Column j = res will be decided with a maximum M >= mx (row g's dot with it) and fails
+        // the ratio test exactly when its second s satisfies dist[M] >= dist[s] * ratiomax; that
+        // predicate is monotone in s (dist does not increase), so every s below the smallest
+        // failing value tau(mx) <= tau(M) passes, whichever row it comes from.  A row whose dots
+        // are all below min tau can neither be a listed column's maximum (tau <= mx <= M) nor
+        // decide its test: the column side skips it (launch_prune_set).  tau by bisection over
+        // the same table and comparison as the test above.
+        const float dm = dist[min(mx, 262144)];
+        int lo = 0, hi = 262145;   // the smallest s in [0, 262145) that fails, or 262145
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (dm >= dist[mid] * ratiomax) hi = mid; else lo = mid + 1;
+        }
+        atomicMax(cl.ntau, INT_MAX - lo);
     }
     if (cl.flag) {
         // the first claim of a column appends it: slots per wave (ballot), per workgroup
@@ -1001,6 +1028,43 @@ __global__ __launch_bounds__(kFinishThreads) void k_match_finish(const Top2* __r
         }
         __syncthreads();
         if (first) cl.list[s_base + s_cnt[wave] + __popcll(bal & ((1ull << lane) - 1))] = res;
+    }
+}
+
+// The rows of set 1 that the column side of a plain mutual match still needs (ColumnList rmax /
+// ntau): 8 lanes per row copy its s8 descriptor (16 B each) to the next free slot; slots per wave
+// by ballot, per workgroup by an LDS prefix and one atomic add.
+__global__ __launch_bounds__(256) void k_prune_set(const int* __restrict__ rmax,
+                                                   const int* __restrict__ ntau, int n,
+                                                   const uint4* __restrict__ s8,
+                                                   const int* __restrict__ ct,
+                                                   uint4* __restrict__ s8c, int* __restrict__ ctc,
+                                                   int* __restrict__ mapc, int* __restrict__ countc) {
+    __shared__ int s_cnt[4], s_base;
+    const int tau = INT_MAX - *ntau;   // no passing row: INT_MAX, nothing kept (no listed column)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sub = lane & 7;
+    const int r = blockIdx.x * 32 + (threadIdx.x >> 3);
+    const bool keep = r < n && rmax[r] >= tau;
+    const unsigned long long bal = __ballot(keep && sub == 0);
+    if (lane == 0) s_cnt[wave] = __popcll(bal);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < 4; w++) {
+            const int c = s_cnt[w];
+            s_cnt[w] = tot;
+            tot += c;
+        }
+        s_base = tot ? atomicAdd(countc, tot) : 0;
+    }
+    __syncthreads();
+    if (keep) {
+        const int slot = s_base + s_cnt[wave] + __popcll(bal & ((1ull << (lane & ~7)) - 1));
+        s8c[(size_t)slot * 8 + sub] = s8[(size_t)r * 8 + sub];
+        if (sub == 0) {
+            ctc[slot] = ct[r];
+            mapc[slot] = r;
+        }
     }
 }
 
@@ -1209,14 +1273,15 @@ hipError_t launch_to_s8(const uint8_t* src, int n, uint8_t* dst, hipStream_t str
 }
 
 hipError_t launch_prep_set(const uint8_t* src, int n, uint8_t* dst, int* sums, int scale,
-                           int bias, int* zero, int nzero, hipStream_t stream, int* ctp) {
+                           int bias, int* zero, int nzero, hipStream_t stream, int* ctp,
+                           int* ctfill) {
     if (n <= 0 && nzero <= 0) return hipSuccess;
     const size_t n16 = (size_t)std::max(n, 0) * 8;
     const size_t work = std::max(n16, (size_t)std::max(nzero, 0));
     const unsigned grid = (unsigned)std::min<size_t>((work + 255) / 256, 4096);
     hipLaunchKernelGGL(k_prep_set, dim3(grid), dim3(256), 0, stream,
                        reinterpret_cast<const uint4*>(src), n16, reinterpret_cast<uint4*>(dst),
-                       sums, scale, bias, zero, nzero, ctp, std::max(n, 0));
+                       sums, scale, bias, zero, nzero, ctp, std::max(n, 0), ctfill);
     return hipGetLastError();
 }
 
@@ -1260,11 +1325,12 @@ hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
                              int chunks, Top2* part, hipStream_t stream,
                              const uint8_t* mask, bool row_side, const int* row_term,
                              Top2* colpart, bool raw, const int* amap, const int* an,
-                             const int* ctp) {
+                             const int* ctp, const int* bn) {
     if (raw && (mask || colpart)) return hipErrorInvalidValue;
     if (nA <= 0 || nB <= 0) return hipSuccess;
     if (colpart && (!row_term || !row_side)) return hipErrorInvalidValue;
     if ((amap != nullptr) != (an != nullptr) || (an && (mask || colpart))) return hipErrorInvalidValue;
+    if (bn && !(raw && ctp && an)) return hipErrorInvalidValue;   // a device-side B count: k_match_raw, 1-D grid
     int per = (nB + chunks - 1) / chunks;
     per = (per + kTile - 1) / kTile * kTile;
     // compacted rows (at most nA of them): a 1-D grid large enough for any count
@@ -1283,7 +1349,7 @@ hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
         constexpr int rows = kRawRows;
         const dim3 rgrid = an ? grid : dim3((nA + rows - 1) / rows, chunks);
         hipLaunchKernelGGL(k_match_raw, rgrid, dim3(64 * kRawWaves), 0, stream, A, nA,
-                           B, nB, ctp, per, part, amap, an);
+                           B, nB, ctp, per, part, amap, an, bn);
     } else if (raw) {
         if (row_side) SGK_MRR(true); else SGK_MRR(false);
     } else if (an) {
@@ -1297,6 +1363,16 @@ hipError_t launch_match_rows(const uint8_t* A, int nA, const uint8_t* B, int nB,
     }
 #undef SGK_MR
 #undef SGK_MRR
+    return hipGetLastError();
+}
+
+hipError_t launch_prune_set(const int* rmax, const int* ntau, int n, const uint8_t* s8,
+                            const int* ct, uint8_t* s8c, int* ctc, int* mapc, int* countc,
+                            hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prune_set, dim3((n + 31) / 32), dim3(256), 0, stream, rmax, ntau, n,
+                       reinterpret_cast<const uint4*>(s8), ct, reinterpret_cast<uint4*>(s8c), ctc,
+                       mapc, countc);
     return hipGetLastError();
 }
 
@@ -1317,6 +1393,9 @@ hipError_t launch_match_finish(const Top2* part, int n, int chunks, const int* r
                                ColumnList cl) {
     if (n <= 0) return hipSuccess;
     if ((cl.map && !cl.count) || (cl.flag && (!cl.list || !cl.count || cl.map))) return hipErrorInvalidValue;
+    if ((cl.rmax != nullptr) != (cl.ntau != nullptr) || (cl.ntau && (!cl.flag || !raw_A)) ||
+        (cl.bmap != nullptr) != (cl.bn != nullptr) || (cl.bn && (!cl.map || !raw_A)))
+        return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_match_finish, dim3((n + kFinishRows - 1) / kFinishRows), dim3(kFinishThreads), 0,
                        stream, part, n,
                        chunks, row_term, dist, distmax, ratiomax, out, best, row_side ? 1 : 0,

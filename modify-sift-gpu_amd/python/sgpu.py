@@ -33,7 +33,7 @@ C_API = [
     "sgpu_match_shard_begin", "sgpu_match_shard_end", "sgpu_match_sharded",
     "sgpu_extract_stream", "sgpu_host_alloc", "sgpu_host_free", "sgpu_reserve",
     "sgpu_debug_alloc_count", "sgpu_last_pyramid_launches", "sgpu_set_stage_timing",
-    "sgpu_set_host_output", "sgpu_debug_set_schedule",
+    "sgpu_set_host_output", "sgpu_debug_set_schedule", "sgpu_debug_set_match_prune",
 ]
 
 _LIB = None
@@ -82,6 +82,7 @@ def lib():
         L.sgpu_last_timing.argtypes = [vp, vp, c.c_int]
         L.sgpu_debug_set_flags.argtypes = [vp, c.c_int]
         L.sgpu_debug_set_schedule.argtypes = [vp, c.c_int, c.c_int]
+        L.sgpu_debug_set_match_prune.argtypes = [vp, c.c_int]
         L.sgpu_debug_geometry.argtypes = [vp, P(c.c_int), vp, c.c_int]
         L.sgpu_debug_gaussian.argtypes = [vp, c.c_int, c.c_int, c.c_int, vp]
         L.sgpu_debug_candidates.argtypes = [vp, vp, vp, c.c_int, P(c.c_int)]
@@ -493,6 +494,12 @@ class SiftContext:
         decimation allow) and the octave's level pairs from its end (PAIRS_END, shipped) or its
         front (PAIRS_FRONT)."""
         self._check(lib().sgpu_debug_set_schedule(self._ctx, trio, pairs), "sgpu_debug_set_schedule")
+
+    def set_match_prune(self, on: bool = True):
+        """Plain mutual matching's column side over the rows of set 1 that can change a listed
+        column's decision (sgpu_debug_set_match_prune; on = shipped): the same pairs."""
+        self._check(lib().sgpu_debug_set_match_prune(self._ctx, int(bool(on))),
+                    "sgpu_debug_set_match_prune")
 
     @contextlib.contextmanager
     def exact_descriptors(self):

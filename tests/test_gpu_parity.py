@@ -509,7 +509,41 @@ def test_matched_columns_equal_full_columns(gpu_ctx):
         assert len(got[0]) > 5000 and len(got[3]) == 130, (flags, ratiomax)
 
 
-@pytest.mark.parametrize("n1,n2,dup", [(1, 700, 0), (700, 1, 0), (257, 1000, 100),
+def test_pruned_column_side_equals_unpruned(gpu_ctx):
+    """Plain mutual matching with ratiomax <= 1 decides the listed columns over the rows of set 1
+    whose largest dot reaches tau, the smallest second value that fails the ratio test against
+    the weakest passing row maximum (k_match_finish bisects the distance table; k_prune_set
+    compacts the rows; the column GEMM takes their count from the device).  Pairs must equal the
+    unpruned column side (sgpu_debug_set_match_prune(0)) and the oracle: planted duplicates among
+    random rows (most rows pruned), distmax / ratiomax that let weak rows pass (tau low, nothing
+    pruned), exact copies (dots above 2^18), tie scenes, many rows on one column, no row and
+    every row matching, ragged sizes."""
+    d1 = synth_descriptors(20000, 6000)
+    d2 = synth_descriptors(20000, 6001, base=d1, n_dup=8000)
+    q1t, q2t, _ = synth_tie_scene(3000, 9000, 29, [(200, 129), (130, 2), (4000, 33), (8999, 1)],
+                                  [(60, 61), (1, 2995)])
+    g1, g2, _, _, _, _ = synth_guided_scene(3000, 2000, 31)
+    base = quantize(synth_descriptors(400, 5))
+    cases = [(quantize(d1), quantize(d2)), (q1t, q2t), (g1, g2),
+             (base, np.concatenate([base, base[:200]])),
+             (base[:130], base[:130].copy()),
+             (quantize(synth_descriptors(700, 8)), quantize(synth_descriptors(129, 9))),
+             (base[:1], base.copy()), (base.copy(), base[:1])]
+    for distmax, ratiomax in ((0.7, 0.8), (0.9, 1.0), (2.0, 1.0), (0.9, 0.5), (2.0, 0.99)):
+        got = [gpu_ctx.match(a, b, distmax, ratiomax, 1) for a, b in cases]
+        try:
+            gpu_ctx.set_match_prune(False)
+            full = [gpu_ctx.match(a, b, distmax, ratiomax, 1) for a, b in cases]
+        finally:
+            gpu_ctx.set_match_prune(True)
+        for i, (g, f) in enumerate(zip(got, full)):
+            assert np.array_equal(g, f), (distmax, ratiomax, i)
+        assert len(got[0]) > 5000 and len(got[4]) == 130, (distmax, ratiomax)
+        for i in (2, 5):
+            assert np.array_equal(got[i], O.match(*cases[i], distmax, ratiomax, 1)), (distmax, ratiomax, i)
+
+
+@pytest.mark.parametrize("n1,n2,dup",[(1, 700, 0), (700, 1, 0), (257, 1000, 100),
                                        (3000, 2500, 1000), (4096, 4096, 2000), (5000, 129, 50)])
 def test_fused_match_vs_oracle(gpu_ctx, n1, n2, dup):
     """The one-GEMM mutual matcher (row decisions and per-panel column partials from the same

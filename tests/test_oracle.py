@@ -157,6 +157,46 @@ def test_matcher_oracle_vs_numpy(mbm):
     np.testing.assert_array_equal(got, want)
 
 
+@pytest.mark.parametrize("distmax,ratiomax,dup", [(0.7, 0.8, 150), (0.9, 1.0, 150),
+                                                  (2.0, 1.0, 0), (0.9, 0.5, 300), (2.0, 0.99, 40)])
+def test_row_bound_pruning_is_exact(distmax, ratiomax, dup):
+    """The pruned column side of the library's plain mutual matcher (k_match_finish /
+    k_prune_set), restated with NumPy: tau = the smallest second value s with
+    dist[M] >= dist[s] * ratiomax for a passing row maximum M (bisection over the distance
+    table), tau_min over the passing rows; the listed columns decided over the rows whose largest
+    dot reaches tau_min give the same pairs as over every row (ratiomax <= 1)."""
+    d1 = synth_descriptors(400, 7000 + dup)
+    d2 = synth_descriptors(350, 7001 + dup, base=d1, n_dup=dup)
+    q1, q2 = quantize(d1), quantize(d2)
+    q2[:3] = q1[:3]                                 # exact copies: dots above 2^18
+    dot = q1.astype(np.int64) @ q2.astype(np.int64).T
+    rows = _np_top(dot, distmax, ratiomax, True)
+    full = _np_pairs(rows, _np_top(dot.T, distmax, ratiomax), 1)
+    table = np.arccos(np.minimum((np.arange(262145).astype(np.float32) * np.float32(2 ** -18))
+                                 .astype(np.float64), 1.0)).astype(np.float32)
+    rmax = np.maximum(dot.max(axis=1), 0)
+    taus = []
+    for i in np.nonzero(rows >= 0)[0]:
+        dm, lo, hi = table[min(rmax[i], 262144)], 0, 262145
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if dm >= table[mid] * np.float32(ratiomax):
+                hi = mid
+            else:
+                lo = mid + 1
+        taus.append(lo)
+    keep = np.nonzero(rmax >= min(taus))[0] if taus else np.zeros(0, np.int64)
+    cols = np.full(q2.shape[0], -1)
+    if len(keep):
+        c = _np_top(dot[keep].T, distmax, ratiomax)
+        cols = np.where(c >= 0, keep[np.maximum(c, 0)], -1)
+    pruned = _np_pairs(rows, cols, 1)
+    np.testing.assert_array_equal(pruned, full)
+    assert len(full) > 0
+    if (distmax, ratiomax) == (0.7, 0.8):
+        assert len(keep) < q1.shape[0] // 2   # planted duplicates among random rows: most pruned
+
+
 def np_shard_state(q1s, row_begin, q2, distmax=0.7, ratiomax=0.8):
     """What a rank computes for rows [row_begin, row_begin + len(q1s)) of set 1 (restated with
     NumPy): its rows' decisions (RowMatch_Kernel, local) and, per set-2 row, the clamped column
