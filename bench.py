@@ -416,7 +416,8 @@ def bench_match(ctx, n, cpu=True):
     out = {"workload": f"C5 {n}x{n} u8 descriptors, mutual best match",
             "ms": ms, "matches": int(len(m)),
             "path": "i8-MFMA GEMM with a keyless top-2 fold (ratiomax <= 1) for the row side, "
-                    "then the sets swapped for the columns some row matched",
+                    "then the sets swapped for the columns some row matched, over the rows of "
+                    "set 1 whose largest dot reaches the passing rows' ratio-test bound",
             "ops": ops, "ops_note": "F = 2*128*N1*N2 counted once (SURVEY.md 8d)",
             "tops": ops / (ms * 1e-3) / 1e12,
             "mfma_util": ops / (ms * 1e-3) / 1e12 / I8_MFMA_PEAK_TOPS,

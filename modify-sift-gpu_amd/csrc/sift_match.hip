@@ -988,7 +988,7 @@ __global__ __launch_bounds__(kFinishThreads) void k_match_finish(const Top2* __r
         ok = ok && d1 < dist[min(sc, 262144)] * ratiomax;
     }
     // pruned column side: B's index -> the row of set 1 (a passing maximum has idx >= 0)
-    const int res = ok ? (cl.bmap ? cl.bmap[idx] : idx) : -1;
+    const int res = ok && idx >= 0 ? (cl.bmap ? cl.bmap[idx] : idx) : -1;
     if (valid && sub == 0) {
         out[g] = res;
         if (best) best[g] = Top2{mx, idx, sc};
