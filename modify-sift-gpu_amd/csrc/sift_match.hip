@@ -1000,14 +1000,16 @@ __global__ __launch_bounds__(kFinishThreads) void k_match_finish(const Top2* __r
         // predicate is monotone in s (dist does not increase), so every s below the smallest
         // failing value tau(mx) <= tau(M) passes, whichever row it comes from.  A row whose dots
         // are all below min tau can neither be a listed column's maximum (tau <= mx <= M) nor
-        // decide its test: the column side skips it (launch_prune_set).  tau by bisection over
-        // the same table and comparison as the test above.
+        // decide its test: the column side skips it (launch_prune_set).  Any lower bound of tau
+        // keeps that true (it only keeps more rows): tau ~ cos(dist[mx] / ratiomax) * 2^18 less
+        // a margin of 64 (far above the float error of cos and of the table), checked with the
+        // test's own comparison at the value below it -- if that one already fails, the bound
+        // falls back to 0 (nothing pruned).  An 18-step bisection of the table measured 42 vs
+        // 12 us for this finish at C5 (dependent loads per row); the check is one load.
         const float dm = dist[min(mx, 262144)];
-        int lo = 0, hi = 262145;   // the smallest s in [0, 262145) that fails, or 262145
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (dm >= dist[mid] * ratiomax) hi = mid; else lo = mid + 1;
-        }
+        int lo = (int)floorf(cosf(dm / ratiomax) * 262144.f) - 64;
+        lo = min(max(lo, 0), 262144);
+        if (lo > 0 && dm >= dist[lo - 1] * ratiomax) lo = 0;
         atomicMax(cl.ntau, INT_MAX - lo);
     }
     if (cl.flag) {

@@ -164,7 +164,9 @@ def test_row_bound_pruning_is_exact(distmax, ratiomax, dup):
     k_prune_set), restated with NumPy: tau = the smallest second value s with
     dist[M] >= dist[s] * ratiomax for a passing row maximum M (bisection over the distance
     table), tau_min over the passing rows; the listed columns decided over the rows whose largest
-    dot reaches tau_min give the same pairs as over every row (ratiomax <= 1)."""
+    dot reaches tau_min give the same pairs as over every row (ratiomax <= 1).  The library takes
+    the lower bound cos(dist[M] / ratiomax) * 2^18 - 64 (checked one below) instead of the
+    bisection; it must not exceed the bisected tau, and lie within 80 of it."""
     d1 = synth_descriptors(400, 7000 + dup)
     d2 = synth_descriptors(350, 7001 + dup, base=d1, n_dup=dup)
     q1, q2 = quantize(d1), quantize(d2)
@@ -184,7 +186,13 @@ def test_row_bound_pruning_is_exact(distmax, ratiomax, dup):
                 hi = mid
             else:
                 lo = mid + 1
-        taus.append(lo)
+        # the library's bound (k_match_finish): cos estimate less 64, checked one below
+        est = int(np.floor(np.float32(np.cos(np.float32(dm / np.float32(ratiomax)))) * np.float32(262144))) - 64
+        est = min(max(est, 0), 262144)
+        if est > 0 and dm >= table[est - 1] * np.float32(ratiomax):
+            est = 0
+        assert est <= lo and lo - est <= 80, (est, lo)
+        taus.append(est)
     keep = np.nonzero(rmax >= min(taus))[0] if taus else np.zeros(0, np.int64)
     cols = np.full(q2.shape[0], -1)
     if len(keep):
