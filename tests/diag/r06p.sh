@@ -3,7 +3,7 @@
 # summary the bench line's traffic reads), the bench line, smoke, matcher SQ counters.
 set -o pipefail
 mkdir -p gpurun_out/r06p
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "match" > gpurun_out/r06p/pytest_match.log 2>&1; rc=$?; tail -2 gpurun_out/r06p/pytest_match.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r06p/pytest_gpu.log 2>&1; rc=$?; tail -2 gpurun_out/r06p/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 for r in 1 2 3; do timeout -k 10 120 python -u tests/diag/match_time.py 50000 plain,plain_noprune,rows_only >> gpurun_out/r06p/match_time.log 2>&1 || exit 1; done
 cat gpurun_out/r06p/match_time.log
 timeout -k 10 900 bash tests/profile_kernels.sh r06p && echo profile ok || exit 1
